@@ -1,0 +1,182 @@
+"""Training-throughput benchmark: BASELINE.json metric "training images/sec at 1280x720 bf16".
+
+Workload (config.workload): one REFINE training step of the reference's train.py hot loop
+(train.py:250-327) on synthetic BDD100K-shaped batches resident in HBM — normalise,
+anchor matching, MobileNet-v2 + refine heads forward, smooth-L1 loss, backward, SGD+clip —
+at 720x1280, batch 8 per GPU (configs[1] on one GPU; configs[2] = batch 64 on 8 GPUs is
+the same per-GPU work, weak scaling).  Every kernel is librod (HIP, gfx950).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  N>1: launched by torch.distributed.run, one rank per GPU, RCCL all-reduce of the flat
+  gradient buffer (sum, global-batch normalisation), clip after reduce.
+
+Prints one JSON line (rank 0) with roofline (live HIP-event timing of the dominant
+kernel over the timed region) and cpu_baseline (the oracle — a PyTorch-CPU restatement
+of the same step — on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'road-object-detection-for-bdd100k_amd')
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=8, help='images per GPU')
+    ap.add_argument('--height', type=int, default=720)
+    ap.add_argument('--width', type=int, default=1280)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--train_range', default='REFINE', choices=['REFINE', 'ALL'])
+    ap.add_argument('--probe', default='rod_conv_fwd', help='kernel reported in "roofline"')
+    ap.add_argument('--cpu-baseline', dest='cpu_baseline', action='store_true', default=True)
+    ap.add_argument('--no-cpu-baseline', dest='cpu_baseline', action='store_false')
+    return ap.parse_args()
+
+
+def cpu_baseline(H, W):
+    """Oracle (PyTorch-CPU fp32 restatement of the reference step) on ONE image."""
+    import config
+    from oracle import anchors as oa
+    from oracle import net as onet
+    from oracle import targets as ot
+    from nets.catch_net import CatchNet
+    from rod.data import synthetic_boxes
+    threads = min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    cfg = {'train_range': config.train_range.REFINE, 'process_backbone_method': config.process_backbone_method.NONE,
+           'deconv_method': config.deconv_method.LEARN_HALF, 'merge_method': config.merge_method.ADD}
+    net = CatchNet('mobilenet_v2', cfg, 'cpu', 0)   # parameters only (host copy)
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in net.store.params.items()}
+    Bf = {k: v.detach().clone() for k, v in net.store.buffers.items()}
+    g = torch.Generator().manual_seed(0)
+    img = torch.randint(0, 256, (1, H, W, 3), dtype=torch.uint8, generator=g)
+    corner, labels, n = synthetic_boxes(1)
+    init = oa.init_anchor(6, (H, W))
+    chain = oa.feat_sizes((H, W), [s for (_, s, _, _, _) in onet.SPEC])
+    anchors = [oa.anchors_one_layer((H, W), chain[t - 1], init[i]) for i, t in enumerate(onet.TAPS)]
+    t0 = time.perf_counter()
+    x = torch.from_numpy(np.float32(2.0 / 255.0) * img.numpy().astype(np.float32) - np.float32(1.0))
+    center = ot.corner_to_center(corner[0, :n[0]])
+    gts, _, _, pms = ot.refine_groundtruth(anchors, center, labels[0, :n[0]], config.refine_pos_jac_val_all_layers)
+    refine = onet.forward(x, P, Bf, True, moving={})
+    loss = 0.
+    for l in range(6):
+        d = (torch.from_numpy(gts[l][None]) - refine[l]) * torch.from_numpy(pms[l][None]).float()
+        ad = d.abs()
+        loss = loss + (0.5 * ((ad - 1) * torch.clamp(ad, max=1.0) + ad)).sum()
+    loss.backward()
+    with torch.no_grad():
+        for p in P.values():
+            if p.grad is not None:
+                p -= 1e-3 * p.grad.clamp(-5, 5)
+    dt = time.perf_counter() - t0
+    return {'value': round(1.0 / dt, 5), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
+            'sample': f'1 image {H}x{W}, one full REFINE train step (targets+fwd+bwd+SGD), oracle fp32 PyTorch-CPU, '
+                      f'{dt:.1f} s'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    import config
+    from rod import _abi, roofline
+    from rod.data import SEED, synthetic_batch
+    from rod.trainer import Trainer
+
+    dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    tr_range = config.train_range.REFINE if args.train_range == 'REFINE' else config.train_range.ALL
+    reducer = None
+    if world > 1:
+        def reducer(flat_grad):
+            torch.distributed.all_reduce(flat_grad)  # RCCL ring/tree over xGMI, one 22 MB buffer
+    tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
+                 world_size=world, reducer=reducer)
+    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED + rank)
+
+    for _ in range(args.warmup):
+        tr.step(*batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    _abi.PROBE.arm(args.probe)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = tr.step(*batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _abi.PROBE.disarm()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    recs = _abi.PROBE.records
+    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in recs)
+    byts = sum(c[0] for _, _, c in recs)
+    flops = sum(c[1] for _, _, c in recs)
+    n_launch = len(recs)
+    loss_val = float(losses[0].item())
+
+    if rank == 0:
+        per_launch_ms = ms / max(n_launch, 1)
+        achieved_gbs = byts / max(ms, 1e-9) / 1e6
+        achieved_tf = flops / max(ms, 1e-9) / 1e9
+        peak_tf = roofline.MI355X_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else roofline.MI355X_F32_PEAK_TFLOPS
+        # bound: whichever roof the kernel's aggregate arithmetic intensity meets first
+        ai = flops / max(byts, 1)
+        ridge = peak_tf * 1e12 / (roofline.MI355X_HBM_PEAK_GBS * 1e9)
+        if ai < ridge:
+            rl = {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': roofline.MI355X_HBM_PEAK_GBS,
+                  'unit': 'GB/s', 'frac': round(achieved_gbs / roofline.MI355X_HBM_PEAK_GBS, 4)}
+        else:
+            rl = {'bound': 'mfma', 'achieved': round(achieved_tf, 2), 'peak': peak_tf, 'unit': 'TFLOP/s',
+                  'frac': round(achieved_tf / peak_tf, 4)}
+        rl.update({'traffic': None, 'kernel': args.probe, 'launches_per_step': n_launch // max(args.steps, 1),
+                   'avg_launch_us': round(per_launch_ms * 1e3, 2), 'alg_bytes_per_step': byts // max(args.steps, 1),
+                   'alg_flops_per_step': flops // max(args.steps, 1)})
+        imgs = args.batch * world * args.steps
+        out = {
+            'metric': 'training images/sec at 1280x720 bf16' if dtype == torch.bfloat16 else
+                      'training images/sec at 1280x720 fp32',
+            'value': round(imgs / elapsed, 3), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic',
+            'config': {'workload': f'{args.train_range} train step (train.py), MobileNet-v2 RefineDet, '
+                                   f'{args.height}x{args.width}, {args.batch} images/GPU',
+                       'global_batch': args.batch * world, 'img_hw': [args.height, args.width],
+                       'train_range': args.train_range, 'parallelism': f'dp{world}'},
+            'loss': round(loss_val, 5),
+            'roofline': rl,
+        }
+        if args.cpu_baseline and world == 1:
+            out['cpu_baseline'] = cpu_baseline(args.height, args.width)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

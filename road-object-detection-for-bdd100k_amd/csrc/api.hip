@@ -1,0 +1,125 @@
+// api.hip — error reporting, version, and small elementwise entry points.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "rod_common.h"
+
+namespace rod {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- kernels
+template <typename T>
+__global__ void normalize_image_kernel(const uint8_t* __restrict__ img, T* __restrict__ out, long n) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const float k = 2.0f / 255.0f;  // (2.0 / 255.0) * imgs - 1.0, train.py:126 (f32 graph)
+  if (i + 3 < n) {
+    uchar4 v = *(const uchar4*)(img + i);
+    out[i + 0] = from_f32<T>(k * (float)v.x - 1.0f);
+    out[i + 1] = from_f32<T>(k * (float)v.y - 1.0f);
+    out[i + 2] = from_f32<T>(k * (float)v.z - 1.0f);
+    out[i + 3] = from_f32<T>(k * (float)v.w - 1.0f);
+  } else {
+    for (; i < n; ++i) out[i] = from_f32<T>(k * (float)img[i] - 1.0f);
+  }
+}
+
+template <typename S, typename D>
+__global__ void cast_kernel(const S* __restrict__ src, D* __restrict__ dst, long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) dst[i] = from_f32<D>(to_f32(src[i]));
+}
+
+__global__ void sgd_clip_kernel(float* __restrict__ p, const float* __restrict__ g, long n, float lr,
+                                float clip) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  long stride = (long)gridDim.x * blockDim.x * 4;
+  for (; i < n; i += stride) {
+    if (i + 3 < n) {
+      f32x4 pv = *(f32x4*)(p + i);
+      f32x4 gv = *(const f32x4*)(g + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float c = fminf(fmaxf(gv[j], -clip), clip);  // tf.clip_by_value
+        pv[j] = pv[j] - lr * c;                       // ApplyGradientDescent: var -= alpha * delta
+      }
+      *(f32x4*)(p + i) = pv;
+    } else {
+      for (long k = i; k < n; ++k) p[k] = p[k] - lr * fminf(fmaxf(g[k], -clip), clip);
+    }
+  }
+}
+
+}  // namespace rod
+
+using namespace rod;
+
+extern "C" {
+
+int rod_abi_version(void) { return ROD_ABI_VERSION; }
+const char* rod_last_error(void) { return rod::g_err; }
+
+int rod_normalize_image(const void* img_u8, void* out, long n, int out_dtype, void* stream) {
+  ROD_CHECK_ARG(n >= 0, "rod_normalize_image: n < 0");
+  if (n == 0) return 0;
+  ROD_CHECK_ARG(((uintptr_t)img_u8 & 3) == 0, "rod_normalize_image: input must be 4-byte aligned");
+  int blocks = cdiv(cdivl(n, 4), 256);
+  ROD_DISPATCH_DTYPE(out_dtype, hipLaunchKernelGGL(normalize_image_kernel<T>, dim3(blocks), dim3(256),
+                                                   0, ROD_STREAM(stream), (const uint8_t*)img_u8,
+                                                   (T*)out, n));
+  return check_launch("rod_normalize_image");
+}
+
+int rod_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, void* stream) {
+  ROD_CHECK_ARG(n >= 0, "rod_cast: n < 0");
+  if (n == 0) return 0;
+  int blocks = (int)std::min<long>(cdivl(n, 256), 8192);
+  hipStream_t s = ROD_STREAM(stream);
+  if (src_dtype == ROD_F32 && dst_dtype == ROD_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), dim3(blocks), dim3(256), 0, s, (const float*)src,
+                       (bf16_t*)dst, n);
+  else if (src_dtype == ROD_BF16 && dst_dtype == ROD_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)src,
+                       (float*)dst, n);
+  else if (src_dtype == ROD_F32 && dst_dtype == ROD_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(blocks), dim3(256), 0, s, (const float*)src,
+                       (float*)dst, n);
+  else if (src_dtype == ROD_BF16 && dst_dtype == ROD_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), dim3(blocks), dim3(256), 0, s,
+                       (const bf16_t*)src, (bf16_t*)dst, n);
+  else {
+    set_error("rod_cast: bad dtype pair %d -> %d", src_dtype, dst_dtype);
+    return ROD_EINVAL;
+  }
+  return check_launch("rod_cast");
+}
+
+int rod_sgd_clip(float* param, const float* grad, long n, float lr, float clip, void* stream) {
+  ROD_CHECK_ARG(n >= 0, "rod_sgd_clip: n < 0");
+  ROD_CHECK_ARG(((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0,
+                "rod_sgd_clip: buffers must be 16-byte aligned");
+  if (n == 0) return 0;
+  int blocks = (int)std::min<long>(cdivl(cdivl(n, 4), 256), 4096);
+  hipLaunchKernelGGL(sgd_clip_kernel, dim3(blocks), dim3(256), 0, ROD_STREAM(stream), param, grad, n,
+                     lr, clip);
+  return check_launch("rod_sgd_clip");
+}
+
+}  // extern "C"

@@ -1,0 +1,487 @@
+// batchnorm.hip — slim.batch_norm (fused, NHWC) forward statistics, apply(+activation
+// +residual) and backward.  Reference semantics: nets/backbone/mobilenet/mobilenet.py:417-420
+// (decay 0.997, center+scale in the backbone) and slim defaults in the heads
+// (nets/catch_net.py:302: decay 0.999, center, no scale); epsilon 1e-3.
+//
+// Statistics are computed on x - k where k = x[row 0, c] (a per-channel pivot taken
+// from the data), so E[(x-k)^2] - E[x-k]^2 does not cancel catastrophically; per-block
+// partial sums go to a slab [nblk][2][C] and are combined in f64 by a finalize kernel
+// (deterministic, no atomics).
+#include "rod_common.h"
+
+namespace rod {
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  if (act == ROD_ACT_RELU6) return fminf(fmaxf(z, 0.f), 6.f);   // tf.nn.relu6
+  if (act == ROD_ACT_LEAKY) return z > 0.f ? z : z * 0.2f;       // tf.nn.leaky_relu(alpha=0.2)
+  return z;
+}
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == ROD_ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;  // Relu6Grad
+  if (act == ROD_ACT_LEAKY) return z > 0.f ? 1.f : 0.2f;               // LeakyReluGrad
+  return 1.f;
+}
+
+struct RedPlan {
+  int V, CV, CVp, cgroups, nbx;
+  long chunk;
+};
+
+static int p2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+template <typename T>
+static RedPlan red_plan(long M, int C, bool vec) {
+  RedPlan r;
+  r.V = vec ? Vec16<T>::N : 1;
+  r.CV = C / r.V;
+  r.CVp = std::min(p2(r.CV), 256);
+  r.cgroups = cdiv(r.CV, r.CVp);
+  long want = std::max<long>(1, 1024 / r.cgroups);
+  long lanes = 256 / r.CVp;
+  long chunk = std::max<long>(cdivl(M, want), lanes * 16);
+  r.chunk = chunk;
+  r.nbx = (int)cdivl(M, chunk);
+  return r;
+}
+
+// ---------------------------------------------------------------- statistics
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, long M, int C, int ldx, int CVp,
+                                                       long chunk, float* __restrict__ slab) {
+  constexpr int V = VEC ? Vec16<T>::N : 1;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][256][V]
+  const int tid = threadIdx.x;
+  const int lanes = 256 / CVp;
+  const int cvl = tid % CVp, pln = tid / CVp;
+  const int CV = C / V;
+  const int cv = blockIdx.y * CVp + cvl;
+  const bool active = cv < CV;
+  const int c = cv * V;
+  const long r0 = (long)blockIdx.x * chunk;
+  const long r1 = r0 + chunk < M ? r0 + chunk : M;
+  float s1[V], s2[V], k[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) s1[v] = s2[v] = 0.f;
+  if (active) {
+    if constexpr (VEC) {
+      Vec16<T> kv;
+      kv.load(x + c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) k[v] = kv.get(v);
+    } else {
+      k[0] = to_f32(x[c]);
+    }
+    for (long r = r0 + pln; r < r1; r += lanes) {
+      const T* p = x + r * ldx + c;
+      if constexpr (VEC) {
+        Vec16<T> vv;
+        vv.load(p);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          float d = vv.get(v) - k[v];
+          s1[v] += d;
+          s2[v] = fmaf(d, d, s2[v]);
+        }
+      } else {
+        float d = to_f32(p[0]) - k[0];
+        s1[0] += d;
+        s2[0] = fmaf(d, d, s2[0]);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    red[tid * V + v] = s1[v];
+    red[(256 + tid) * V + v] = s2[v];
+  }
+  __syncthreads();
+  for (int s = lanes >> 1; s > 0; s >>= 1) {
+    if (pln < s) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        red[tid * V + v] += red[(tid + s * CVp) * V + v];
+        red[(256 + tid) * V + v] += red[(256 + tid + s * CVp) * V + v];
+      }
+    }
+    __syncthreads();
+  }
+  if (pln == 0 && active) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      slab[((long)blockIdx.x * 2 + 0) * C + c + v] = red[tid * V + v];
+      slab[((long)blockIdx.x * 2 + 1) * C + c + v] = red[(256 + tid) * V + v];
+    }
+  }
+}
+
+template <typename T>
+__global__ void bn_stats_finalize_kernel(const T* __restrict__ x, const float* __restrict__ slab, int nblk, long M,
+                                         int C, float eps, float decay, float* __restrict__ mean,
+                                         float* __restrict__ rstd, float* __restrict__ mmean,
+                                         float* __restrict__ mvar) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s1 += (double)slab[((long)b * 2 + 0) * C + c];
+    s2 += (double)slab[((long)b * 2 + 1) * C + c];
+  }
+  const double k = (double)to_f32(x[c]);
+  const double m = s1 / (double)M;
+  double var = s2 / (double)M - m * m;
+  if (var < 0.0) var = 0.0;
+  const float mu = (float)(k + m);
+  const float vf = (float)var;
+  mean[c] = mu;
+  rstd[c] = (float)(1.0 / sqrt((double)vf + (double)eps));
+  if (mmean != nullptr) {
+    // slim: assign_moving_average(zero_debias=False): v -= (v - value) * (1 - decay)
+    const float one_m = 1.0f - decay;
+    const float unbiased = M > 1 ? (float)(var * (double)M / (double)(M - 1)) : vf;
+    mmean[c] = mmean[c] - (mmean[c] - mu) * one_m;
+    mvar[c] = mvar[c] - (mvar[c] - unbiased) * one_m;
+  }
+}
+
+__global__ void bn_eval_stats_kernel(const float* __restrict__ mm, const float* __restrict__ mv, float eps,
+                                     float* __restrict__ mean, float* __restrict__ rstd, int C) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = mm[c];
+  rstd[c] = (float)(1.0 / sqrt((double)mv[c] + (double)eps));
+}
+
+// ---------------------------------------------------------------- apply
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, const T* __restrict__ res,
+                                                       T* __restrict__ y, long M, int C, int ldx, int ldr, int ldy,
+                                                       int act) {
+  constexpr int V = VEC ? Vec16<T>::N : 1;
+  const int CV = C / V;
+  const long total = M * CV;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long r = t / CV;
+    const int c = (int)(t - r * CV) * V;
+    float xv[V], rv[V];
+    if constexpr (VEC) {
+      Vec16<T> a;
+      a.load(x + r * ldx + c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) xv[v] = a.get(v);
+      if (res) {
+        Vec16<T> b;
+        b.load(res + r * ldr + c);
+#pragma unroll
+        for (int v = 0; v < V; ++v) rv[v] = b.get(v);
+      }
+    } else {
+      xv[0] = to_f32(x[r * ldx + c]);
+      if (res) rv[0] = to_f32(res[r * ldr + c]);
+    }
+    Vec16<T> o;
+    float ov[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float sc = gamma ? rstd[c + v] * gamma[c + v] : rstd[c + v];  // rsqrt(var+eps)*scale
+      const float b = beta ? beta[c + v] : 0.f;
+      float z = (xv[v] - mean[c + v]) * sc + b;
+      z = act_fwd(z, act);
+      if (res) z = z + rv[v];
+      ov[v] = z;
+    }
+    if constexpr (VEC) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) o.set(v, ov[v]);
+      o.store(y + r * ldy + c);
+    } else {
+      y[r * ldy + c] = from_f32<T>(ov[0]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- backward
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, long M, int C, int lddy,
+                                                            int ldx, int act, int CVp, long chunk,
+                                                            float* __restrict__ slab) {
+  constexpr int V = VEC ? Vec16<T>::N : 1;
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int tid = threadIdx.x;
+  const int lanes = 256 / CVp;
+  const int cvl = tid % CVp, pln = tid / CVp;
+  const int CV = C / V;
+  const int cv = blockIdx.y * CVp + cvl;
+  const bool active = cv < CV;
+  const int c = cv * V;
+  const long r0 = (long)blockIdx.x * chunk;
+  const long r1 = r0 + chunk < M ? r0 + chunk : M;
+  float sg[V], sgx[V], mu[V], rs[V], sc[V], be[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) sg[v] = sgx[v] = 0.f;
+  if (active) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      mu[v] = mean[c + v];
+      rs[v] = rstd[c + v];
+      sc[v] = gamma ? rs[v] * gamma[c + v] : rs[v];
+      be[v] = beta ? beta[c + v] : 0.f;
+    }
+    for (long r = r0 + pln; r < r1; r += lanes) {
+      float xv[V], gv[V];
+      if constexpr (VEC) {
+        Vec16<T> a, b;
+        a.load(x + r * ldx + c);
+        b.load(dy + r * lddy + c);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          xv[v] = a.get(v);
+          gv[v] = b.get(v);
+        }
+      } else {
+        xv[0] = to_f32(x[r * ldx + c]);
+        gv[0] = to_f32(dy[r * lddy + c]);
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float d = xv[v] - mu[v];
+        const float z = d * sc[v] + be[v];
+        const float g = gv[v] * act_grad(z, act);
+        sg[v] += g;
+        sgx[v] = fmaf(g, d * rs[v], sgx[v]);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    red[tid * V + v] = sg[v];
+    red[(256 + tid) * V + v] = sgx[v];
+  }
+  __syncthreads();
+  for (int s = lanes >> 1; s > 0; s >>= 1) {
+    if (pln < s) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        red[tid * V + v] += red[(tid + s * CVp) * V + v];
+        red[(256 + tid) * V + v] += red[(256 + tid + s * CVp) * V + v];
+      }
+    }
+    __syncthreads();
+  }
+  if (pln == 0 && active) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      slab[((long)blockIdx.x * 2 + 0) * C + c + v] = red[tid * V + v];
+      slab[((long)blockIdx.x * 2 + 1) * C + c + v] = red[(256 + tid) * V + v];
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ slab, int nblk, long M, int C,
+                                       const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ coef) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    sg += (double)slab[((long)b * 2 + 0) * C + c];
+    sgx += (double)slab[((long)b * 2 + 1) * C + c];
+  }
+  if (dbeta) dbeta[c] = (float)sg;
+  if (dgamma) dgamma[c] = (float)sgx;
+  coef[c] = gamma ? rstd[c] * gamma[c] : rstd[c];
+  coef[C + c] = (float)(sg / (double)M);
+  coef[2 * C + c] = (float)(sgx / (double)M);
+}
+
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ coef, T* __restrict__ dx,
+                                                           long M, int C, int lddy, int ldx, int lddx, int act) {
+  constexpr int V = VEC ? Vec16<T>::N : 1;
+  const int CV = C / V;
+  const long total = M * CV;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long r = t / CV;
+    const int c = (int)(t - r * CV) * V;
+    float xv[V], gv[V];
+    if constexpr (VEC) {
+      Vec16<T> a, b;
+      a.load(x + r * ldx + c);
+      b.load(dy + r * lddy + c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        xv[v] = a.get(v);
+        gv[v] = b.get(v);
+      }
+    } else {
+      xv[0] = to_f32(x[r * ldx + c]);
+      gv[0] = to_f32(dy[r * lddy + c]);
+    }
+    float ov[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float rs = rstd[c + v];
+      const float sc = gamma ? rs * gamma[c + v] : rs;
+      const float d = xv[v] - mean[c + v];
+      const float z = d * sc + (beta ? beta[c + v] : 0.f);
+      const float g = gv[v] * act_grad(z, act);
+      const float xh = d * rs;
+      ov[v] = coef[c + v] * (g - coef[C + c + v] - xh * coef[2 * C + c + v]);
+    }
+    if constexpr (VEC) {
+      Vec16<T> o;
+#pragma unroll
+      for (int v = 0; v < V; ++v) o.set(v, ov[v]);
+      o.store(dx + r * lddx + c);
+    } else {
+      dx[r * lddx + c] = from_f32<T>(ov[0]);
+    }
+  }
+}
+
+template <typename T>
+static bool vec_ok(int C, std::initializer_list<std::pair<const void*, int>> bufs) {
+  const int V = Vec16<T>::N;
+  if (C % V) return false;
+  for (auto& b : bufs) {
+    if (b.first == nullptr) continue;
+    if (((uintptr_t)b.first & 15) != 0) return false;
+    if (b.second % V) return false;
+  }
+  return true;
+}
+
+static int max_nbx(long M, int C) {
+  int a = red_plan<float>(M, C, false).nbx;
+  int b = red_plan<float>(M, C, C % 4 == 0).nbx;
+  int c = red_plan<bf16_t>(M, C, C % 8 == 0).nbx;
+  return std::max(a, std::max(b, c));
+}
+
+static int ew_blocks(long vecs) { return (int)std::min<long>(cdivl(vecs, 256), 256L * 16); }
+
+}  // namespace rod
+
+using namespace rod;
+
+extern "C" {
+
+size_t rod_bn_stats_workspace(long M, int C) {
+  return (size_t)max_nbx(M, C) * 2 * C * sizeof(float);
+}
+
+int rod_bn_stats(const void* x, long M, int C, int ldx, float eps, float decay, float* mean, float* rstd,
+                 float* moving_mean, float* moving_var, void* workspace, int dtype, void* stream) {
+  ROD_CHECK_ARG(M > 0 && C > 0, "rod_bn_stats: bad shape M=%ld C=%d", M, C);
+  if (ldx == 0) ldx = C;
+  ROD_CHECK_ARG(ldx >= C, "rod_bn_stats: ldx < C");
+  ROD_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr), "rod_bn_stats: moving stats mismatch");
+  ROD_CHECK_ARG(workspace != nullptr, "rod_bn_stats: workspace is NULL");
+  hipStream_t s = ROD_STREAM(stream);
+  ROD_DISPATCH_DTYPE(dtype, {
+    const bool vec = vec_ok<T>(C, {{x, ldx}});
+    RedPlan pl = red_plan<T>(M, C, vec);
+    dim3 grid(pl.nbx, pl.cgroups);
+    size_t lds = 2 * 256 * pl.V * sizeof(float);
+    if (vec)
+      hipLaunchKernelGGL((bn_stats_kernel<T, true>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp,
+                         pl.chunk, (float*)workspace);
+    else
+      hipLaunchKernelGGL((bn_stats_kernel<T, false>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp,
+                         pl.chunk, (float*)workspace);
+    hipLaunchKernelGGL(bn_stats_finalize_kernel<T>, dim3(cdiv(C, 256)), dim3(256), 0, s, (const T*)x,
+                       (const float*)workspace, pl.nbx, M, C, eps, decay, mean, rstd, moving_mean, moving_var);
+  });
+  return check_launch("rod_bn_stats");
+}
+
+int rod_bn_eval_stats(const float* moving_mean, const float* moving_var, float eps, float* mean, float* rstd, int C,
+                      void* stream) {
+  ROD_CHECK_ARG(C > 0, "rod_bn_eval_stats: C <= 0");
+  hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(cdiv(C, 256)), dim3(256), 0, ROD_STREAM(stream), moving_mean,
+                     moving_var, eps, mean, rstd, C);
+  return check_launch("rod_bn_eval_stats");
+}
+
+int rod_bn_apply(const void* x, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                 const void* residual, void* y, long M, int C, int ldx, int ldr, int ldy, int act, int dtype,
+                 void* stream) {
+  ROD_CHECK_ARG(M > 0 && C > 0, "rod_bn_apply: bad shape");
+  ROD_CHECK_ARG(act >= ROD_ACT_NONE && act <= ROD_ACT_LEAKY, "rod_bn_apply: bad act %d", act);
+  if (ldx == 0) ldx = C;
+  if (ldy == 0) ldy = C;
+  if (ldr == 0) ldr = C;
+  ROD_CHECK_ARG(ldx >= C && ldy >= C && ldr >= C, "rod_bn_apply: leading dim < C");
+  hipStream_t s = ROD_STREAM(stream);
+  ROD_DISPATCH_DTYPE(dtype, {
+    const bool vec = vec_ok<T>(C, {{x, ldx}, {y, ldy}, {residual, ldr}});
+    const int V = vec ? Vec16<T>::N : 1;
+    int blocks = ew_blocks(M * (C / V));
+    if (vec)
+      hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)x, mean, rstd, gamma,
+                         beta, (const T*)residual, (T*)y, M, C, ldx, ldr, ldy, act);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(blocks), dim3(256), 0, s, (const T*)x, mean, rstd,
+                         gamma, beta, (const T*)residual, (T*)y, M, C, ldx, ldr, ldy, act);
+  });
+  return check_launch("rod_bn_apply");
+}
+
+size_t rod_bn_bwd_workspace(long M, int C) {
+  return (size_t)max_nbx(M, C) * 2 * C * sizeof(float) + (size_t)3 * C * sizeof(float) + 16;
+}
+
+int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma,
+               const float* beta, void* dx, float* dgamma, float* dbeta, void* workspace, long M, int C, int lddy,
+               int ldx, int lddx, int act, int dtype, void* stream) {
+  ROD_CHECK_ARG(M > 0 && C > 0, "rod_bn_bwd: bad shape");
+  ROD_CHECK_ARG(workspace != nullptr, "rod_bn_bwd: workspace is NULL");
+  if (lddy == 0) lddy = C;
+  if (ldx == 0) ldx = C;
+  if (lddx == 0) lddx = C;
+  ROD_CHECK_ARG(lddy >= C && ldx >= C && lddx >= C, "rod_bn_bwd: leading dim < C");
+  hipStream_t s = ROD_STREAM(stream);
+  ROD_DISPATCH_DTYPE(dtype, {
+    const bool vec = vec_ok<T>(C, {{dy, lddy}, {x, ldx}, {dx, lddx}});
+    RedPlan pl = red_plan<T>(M, C, vec);
+    float* slab = (float*)workspace;
+    float* coef = slab + (size_t)max_nbx(M, C) * 2 * C;  // after the largest slab
+    dim3 grid(pl.nbx, pl.cgroups);
+    size_t lds = 2 * 256 * pl.V * sizeof(float);
+    if (vec)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x, mean,
+                         rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x,
+                         mean, rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, slab, pl.nbx, M, C, rstd, gamma,
+                       dgamma, dbeta, coef);
+    const int V = pl.V;
+    int blocks = ew_blocks(M * (C / V));
+    if (vec)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dy, (const T*)x,
+                         mean, rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false>), dim3(blocks), dim3(256), 0, s, (const T*)dy,
+                         (const T*)x, mean, rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
+  });
+  return check_launch("rod_bn_bwd");
+}
+
+}  // extern "C"

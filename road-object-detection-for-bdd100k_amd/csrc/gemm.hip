@@ -1,0 +1,536 @@
+// gemm.hip — dense convolutions as MFMA implicit GEMMs on gfx950.
+//
+//   rod_conv_fwd   : y[m, co] = sum_k A[m, k] * wt[co, k] (+ bias)          ("NT": k contiguous)
+//   rod_conv_wgrad : dw[co, k] = sum_m dy[m, co] * A[m, k]                  ("TN": reduction over rows)
+//
+// A is either the activation rows (1x1 conv) or the 3x3 / stride-1 / TF-SAME im2col of x,
+// gathered on the fly (no im2col buffer ever touches HBM).  bf16 storage uses
+// v_mfma_f32_16x16x32_bf16; fp32 storage uses the exact-f32 v_mfma_f32_16x16x4_f32 (no
+// reduced-precision path exists on gfx950), so fp32 parity runs are genuine fp32.
+//
+// Fragment maps (cdna_hip_programming.md §3): for 16x16x32 bf16 lane l holds
+// A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15], j=0..7; C/D col = l&15, row = 4(l>>4)+r.
+// The f32 16x16x4 form is issued 8 times per 32-deep k-step with lane l contributing
+// k = 8(l>>4)+j in issue j, so both dtypes read the same 8-element k-runs from LDS.
+#include "rod_common.h"
+
+namespace rod {
+
+constexpr int BK = 32;
+
+template <typename T> struct LdsPad;                       // row padding (elements)
+template <> struct LdsPad<bf16_t> { static constexpr int v = 8; };   // 80-byte rows
+template <> struct LdsPad<float> { static constexpr int v = 4; };    // 144-byte rows
+
+// ---- 8-element chunk of T held in registers ------------------------------------
+template <typename T> struct Chunk8;
+template <> struct Chunk8<bf16_t> {
+  bf16x8 v;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16_t)0.f;
+  }
+  __device__ __forceinline__ void load_vec(const bf16_t* p) { v = *(const bf16x8*)p; }
+  __device__ __forceinline__ void set(int j, bf16_t x) { v[j] = x; }
+  __device__ __forceinline__ void store_lds(bf16_t* p) const { *(bf16x8*)p = v; }
+};
+template <> struct Chunk8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = b[j] = 0.f;
+  }
+  __device__ __forceinline__ void load_vec(const float* p) {
+    a = *(const f32x4*)p;
+    b = *(const f32x4*)(p + 4);
+  }
+  __device__ __forceinline__ void set(int j, float x) {
+    if (j < 4) a[j] = x; else b[j - 4] = x;
+  }
+  __device__ __forceinline__ void store_lds(float* p) const {
+    *(f32x4*)p = a;
+    *(f32x4*)(p + 4) = b;
+  }
+};
+
+// ---- A-row source: one output pixel of the conv (fixed for the whole K loop) --------
+template <typename T, int KS>
+struct RowSrc {
+  const T* base;  // KS==1: &x[m*ldx]; KS==3: &x[pixel (n,0,0)]
+  int y, x;       // KS==3 only
+  bool valid;
+  __device__ __forceinline__ void init(const T* X, long m, long M, int H, int W, int ldx) {
+    valid = m < M;
+    if (!valid) { base = X; y = x = 0; return; }
+    if constexpr (KS == 1) {
+      base = X + m * ldx;
+    } else {
+      const int xx = (int)(m % W);
+      const long t = m / W;
+      y = (int)(t % H);
+      x = xx;
+      const long n = t / H;
+      base = X + n * (long)H * W * ldx;
+    }
+  }
+  // load A[m, k..k+7]; K = KS*KS*Cin
+  template <bool VEC>
+  __device__ __forceinline__ void load(Chunk8<T>& c, int k, int K, int Cin, int H, int W, int ldx) const {
+    if (!valid || k >= K) { c.zero(); return; }
+    if constexpr (KS == 1) {
+      if (VEC && k + 8 <= K) {
+        c.load_vec(base + k);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c.set(j, (k + j < K) ? base[k + j] : (T)0.f);
+      }
+    } else {
+      if (VEC) {  // Cin % 8 == 0 : the chunk lies inside one tap
+        const int tap = k / Cin, ci = k - tap * Cin;
+        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          c.load_vec(base + ((long)yy * W + xx) * ldx + ci);
+        else
+          c.zero();
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int kk = k + j;
+          T v = (T)0.f;
+          if (kk < K) {
+            const int tap = kk / Cin, ci = kk - tap * Cin;
+            const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+            if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = base[((long)yy * W + xx) * ldx + ci];
+          }
+          c.set(j, v);
+        }
+      }
+    }
+  }
+};
+
+// ---- MFMA over one 32-deep k step for one 16x16 tile ---------------------------------
+__device__ __forceinline__ void mma32(f32x4& acc, const bf16_t* a, const bf16_t* b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)a, *(const bf16x8*)b, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b) {
+  const f32x4 a0 = *(const f32x4*)a, a1 = *(const f32x4*)(a + 4);
+  const f32x4 b0 = *(const f32x4*)b, b1 = *(const f32x4*)(b + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b0[j], acc, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b1[j], acc, 0, 0, 0);
+}
+
+// =====================================================================================
+// forward: y[m, co] = sum_k A[m,k] wt[co,k] + bias[co]
+// block 256 threads = 4 waves laid out WM x WN; tile BM x BN; wave tile (BM/WM) x (BN/WN)
+// =====================================================================================
+template <typename T, int KS, int BN, bool VA, bool VB>
+__global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
+                                                       const float* __restrict__ bias, T* __restrict__ Y, long M,
+                                                       int H, int W, int Cin, int Cout, int ldx, int ldy) {
+  constexpr int BM = 128;
+  constexpr int WN = BN >= 64 ? 2 : 1;
+  constexpr int WM = 4 / WN;
+  constexpr int MT = BM / WM / 16;
+  constexpr int NT = BN / WN / 16;
+  constexpr int LD = BK + LdsPad<T>::v;
+  constexpr int ACH = BM * BK / 8 / 256;          // A chunks per thread (=2)
+  constexpr int BCH = (BN * BK / 8 + 255) / 256;  // B chunks per thread
+  __shared__ __attribute__((aligned(16))) T As[BM * LD];
+  __shared__ __attribute__((aligned(16))) T Bs[BN * LD];
+
+  const int K = KS * KS * Cin;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const long m0 = (long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int kc = (tid & 3) * 8;
+
+  RowSrc<T, KS> rows[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) rows[i].init(X, m0 + (tid >> 2) + i * 64, M, H, W, ldx);
+
+  Chunk8<T> ra[ACH], rb[BCH];
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) rows[i].template load<VA>(ra[i], k0 + kc, K, Cin, H, W, ldx);
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int cid = tid + i * 256;
+      const int r = cid >> 2;
+      const int co = n0 + r;
+      const int k = k0 + kc;
+      if (cid >= BN * BK / 8) continue;
+      if (co >= Cout || k >= K) {
+        rb[i].zero();
+      } else if (VB && k + 8 <= K) {
+        rb[i].load_vec(Wt + (long)co * K + k);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rb[i].set(j, (k + j < K) ? Wt[(long)co * K + k + j] : (T)0.f);
+      }
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.f;
+
+  load_tiles(0);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) ra[i].store_lds(As + ((tid >> 2) + i * 64) * LD + kc);
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int cid = tid + i * 256;
+      if (cid < BN * BK / 8) rb[i].store_lds(Bs + (cid >> 2) * LD + kc);
+    }
+    __syncthreads();
+    if (k0 + BK < K) load_tiles(k0 + BK);  // next tile in flight under the MFMAs
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      const T* pa = As + (wm * (BM / WM) + a * 16 + fr) * LD + fk;
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const T* pb = Bs + (wn * (BN / WN) + b * 16 + fr) * LD + fk;
+        mma32(acc[a][b], pa, pb);
+      }
+    }
+  }
+
+  // epilogue: bias + store (row = 4(l>>4)+r, col = l&15)
+#pragma unroll
+  for (int b = 0; b < NT; ++b) {
+    const int col = n0 + wn * (BN / WN) + b * 16 + (lane & 15);
+    if (col >= Cout) continue;
+    const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long row = m0 + wm * (BM / WM) + a * 16 + (lane >> 4) * 4 + r;
+        if (row < M) Y[row * ldy + col] = from_f32<T>(acc[a][b][r] + bv);
+      }
+    }
+  }
+}
+
+// =====================================================================================
+// weight gradient: part[s][co][k] = sum_{m in split s} dy[m, co] * A[m, k]
+// tile 64 (co) x 64 (k); rows staged m-major in LDS and read transposed
+// (ds_read_b64_tr_b16 for bf16, plain b32 lane-per-column reads for f32).
+// =====================================================================================
+constexpr int WG_T = 64;            // co / k tile
+constexpr int WG_LD = WG_T + 4;     // LDS row (elements): 136 B bf16 / 272 B f32
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
+  s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+  return __builtin_bit_cast(bf16x4, r);
+}
+
+template <typename T, int KS, bool VA, bool VD>
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X, const T* __restrict__ DY,
+                                                         float* __restrict__ part, long M, int H, int W, int Cin,
+                                                         int Cout, int ldx, int lddy, long chunk, int ktiles) {
+  __shared__ __attribute__((aligned(16))) T Ds[BK * WG_LD];  // [m][co]
+  __shared__ __attribute__((aligned(16))) T Xs[BK * WG_LD];  // [m][k]
+  const int K = KS * KS * Cin;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves of 32x32
+  const int co0 = (blockIdx.x / ktiles) * WG_T;
+  const int k0 = (blockIdx.x % ktiles) * WG_T;
+  const long mb = (long)blockIdx.y * chunk;
+  const long me = mb + chunk < M ? mb + chunk : M;
+
+  // each thread stages one 8-wide chunk of a Ds row and one of an Xs row per step
+  const int lr = tid >> 3;       // row within the 32-row step
+  const int lc = (tid & 7) * 8;  // column chunk within the 64-wide tile
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.f;
+
+  Chunk8<T> rd, rx;
+  auto load_step = [&](long m) {
+    const long row = m + lr;
+    // dy[row, co0+lc .. +7]
+    if (row >= me || co0 + lc >= Cout) {
+      rd.zero();
+    } else if (VD && co0 + lc + 8 <= Cout) {
+      rd.load_vec(DY + row * lddy + co0 + lc);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rd.set(j, (co0 + lc + j < Cout) ? DY[row * lddy + co0 + lc + j] : (T)0.f);
+    }
+    RowSrc<T, KS> rs;
+    rs.init(X, row < me ? row : M, M, H, W, ldx);
+    rs.template load<VA>(rx, k0 + lc, K, Cin, H, W, ldx);
+  };
+
+  if (mb < me) load_step(mb);
+  for (long m = mb; m < me; m += BK) {
+    __syncthreads();
+    rd.store_lds(Ds + lr * WG_LD + lc);
+    rx.store_lds(Xs + lr * WG_LD + lc);
+    __syncthreads();
+    if (m + BK < me) load_step(m + BK);
+    if constexpr (sizeof(T) == 2) {
+      // A operand (rows = co): lane needs Ds[8g+j][co]; B (cols = k): Xs[8g+j][k]
+      const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int cb = wm * 32 + a * 16;
+        const bf16x4 lo = tr_read((const bf16_t*)Ds + (8 * g + q) * WG_LD + cb + 4 * p);
+        const bf16x4 hi = tr_read((const bf16_t*)Ds + (8 * g + 4 + q) * WG_LD + cb + 4 * p);
+        bf16x8 fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int kb = wn * 32 + b * 16;
+          const bf16x4 l2 = tr_read((const bf16_t*)Xs + (8 * g + q) * WG_LD + kb + 4 * p);
+          const bf16x4 h2 = tr_read((const bf16_t*)Xs + (8 * g + 4 + q) * WG_LD + kb + 4 * p);
+          bf16x8 fb = {l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[a][b], 0, 0, 0);
+        }
+      }
+    } else {
+      // f32 16x16x4: lane l contributes A[i=l&15][k=l>>4] = Ds[kk*4 + (l>>4)][co]
+      const int i = lane & 15, q = lane >> 4;
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        const int mr = kk * 4 + q;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const float av = ((const float*)Ds)[mr * WG_LD + wm * 32 + a * 16 + i];
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const float bv = ((const float*)Xs)[mr * WG_LD + wn * 32 + b * 16 + i];
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[a][b], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  // write the partial tile: rows co, cols k
+  float* out = part + (long)blockIdx.y * Cout * K;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int k = k0 + wn * 32 + b * 16 + (lane & 15);
+      if (k >= K) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
+        if (co < Cout) out[(long)co * K + k] = acc[a][b][r];
+      }
+    }
+}
+
+__global__ void split_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int splits, long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int b = 0; b < splits; ++b) s += part[(long)b * n + i];
+  out[i] = s;
+}
+
+// column sums of dy[M, C] (row stride ld): slab [nblk][C] then reduce
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ dy, long M, int C, int ld, long chunk,
+                                                     float* __restrict__ slab) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const long r0 = (long)blockIdx.x * chunk;
+  const long r1 = r0 + chunk < M ? r0 + chunk : M;
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += to_f32(dy[r * ld + c]);
+  slab[(long)blockIdx.x * C + c] = s;
+}
+
+template <typename T>
+__global__ void weight_prep_kernel(const float* __restrict__ w, T* __restrict__ wt, int Cout, int Cin, int ks,
+                                   int mode) {
+  const long n = (long)Cout * ks * ks * Cin;
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  if (mode == 0) {
+    wt[idx] = from_f32<T>(w[idx]);
+    return;
+  }
+  // destination index -> [ci][i][j][co]
+  const int co = (int)(idx % Cout);
+  long t = idx / Cout;
+  const int j = (int)(t % ks);
+  t /= ks;
+  const int i = (int)(t % ks);
+  const int ci = (int)(t / ks);
+  const int si = ks - 1 - i, sj = ks - 1 - j;
+  wt[idx] = from_f32<T>(w[(((long)co * ks + si) * ks + sj) * Cin + ci]);
+}
+
+struct WgradPlan {
+  int ctiles, ktiles, splits;
+  long chunk;
+};
+static WgradPlan wgrad_plan(long M, int Cin, int Cout, int ks) {
+  WgradPlan p;
+  const int K = ks * ks * Cin;
+  p.ctiles = cdiv(Cout, WG_T);
+  p.ktiles = cdiv(K, WG_T);
+  const int tiles = p.ctiles * p.ktiles;
+  long splits = std::max<long>(1, std::min<long>(cdivl(2048, tiles), cdivl(M, 512)));
+  long chunk = cdivl(M, splits);
+  chunk = cdivl(chunk, BK) * BK;
+  p.chunk = chunk;
+  p.splits = (int)cdivl(M, chunk);
+  return p;
+}
+
+template <typename T>
+static bool aligned16(const void* p) {
+  return ((uintptr_t)p & 15) == 0;
+}
+
+template <typename T, int KS, int BN, bool VA, bool VB>
+static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
+                            int Cout, int ldx, int ldy, hipStream_t s) {
+  dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
+  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB>), grid, dim3(256), 0, s, (const T*)x, (const T*)wt, bias,
+                     (T*)y, M, H, W, Cin, Cout, ldx, ldy);
+}
+
+template <typename T, int KS, int BN>
+static void conv_fwd_va_vb(bool va, bool vb, const void* x, const void* wt, const float* bias, void* y, long M, int H,
+                           int W, int Cin, int Cout, int ldx, int ldy, hipStream_t s) {
+  if (va && vb) conv_fwd_launch<T, KS, BN, true, true>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  else if (va) conv_fwd_launch<T, KS, BN, true, false>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  else if (vb) conv_fwd_launch<T, KS, BN, false, true>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  else conv_fwd_launch<T, KS, BN, false, false>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+}
+
+template <typename T, int KS>
+static void conv_fwd_bn(bool va, bool vb, const void* x, const void* wt, const float* bias, void* y, long M, int H,
+                        int W, int Cin, int Cout, int ldx, int ldy, hipStream_t s) {
+  if (Cout <= 32) conv_fwd_va_vb<T, KS, 32>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  else if (Cout <= 64) conv_fwd_va_vb<T, KS, 64>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  else conv_fwd_va_vb<T, KS, 128>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+}
+
+template <typename T>
+static void conv_fwd_typed(const void* x, const void* wt, const float* bias, void* y, int N, int H, int W, int Cin,
+                           int Cout, int ksize, int ldx, int ldy, hipStream_t s) {
+  const long M = (long)N * H * W;
+  const int K = ksize * ksize * Cin;
+  const int eV = Vec16<T>::N;
+  const bool va = aligned16<T>(x) && (ldx % eV == 0) && (ksize == 1 ? true : (Cin % 8 == 0));
+  const bool vb = aligned16<T>(wt) && (K % eV == 0);
+  if (ksize == 1) conv_fwd_bn<T, 1>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  else conv_fwd_bn<T, 3>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+}
+
+template <typename T, int KS, bool VA, bool VD>
+static void wgrad_launch(const WgradPlan& p, const void* x, const void* dy, float* part, long M, int H, int W,
+                         int Cin, int Cout, int ldx, int lddy, hipStream_t s) {
+  dim3 grid(p.ctiles * p.ktiles, p.splits);
+  hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, VA, VD>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, part, M,
+                     H, W, Cin, Cout, ldx, lddy, p.chunk, p.ktiles);
+}
+
+template <typename T, int KS>
+static void wgrad_va_vd(bool va, bool vd, const WgradPlan& p, const void* x, const void* dy, float* part, long M,
+                        int H, int W, int Cin, int Cout, int ldx, int lddy, hipStream_t s) {
+  if (va && vd) wgrad_launch<T, KS, true, true>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  else if (va) wgrad_launch<T, KS, true, false>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  else if (vd) wgrad_launch<T, KS, false, true>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  else wgrad_launch<T, KS, false, false>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+}
+
+template <typename T>
+static void wgrad_typed(const void* x, const void* dy, float* dw, float* db, float* part, int N, int H, int W, int Cin,
+                        int Cout, int ksize, int ldx, int lddy, hipStream_t s) {
+  const long M = (long)N * H * W;
+  const long K = (long)ksize * ksize * Cin;
+  WgradPlan p = wgrad_plan(M, Cin, Cout, ksize);
+  const int eV = Vec16<T>::N;
+  const bool va = aligned16<T>(x) && (ldx % eV == 0) && (ksize == 1 ? true : (Cin % 8 == 0));
+  const bool vd = aligned16<T>(dy) && (lddy % eV == 0);
+  if (ksize == 1) wgrad_va_vd<T, 1>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  else wgrad_va_vd<T, 3>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  const long n = (long)Cout * K;
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(cdivl(n, 256)), dim3(256), 0, s, part, dw, p.splits, n);
+  if (db) {
+    long cchunk = std::max<long>(64, cdivl(M, 512));
+    int nb = (int)cdivl(M, cchunk);
+    hipLaunchKernelGGL(colsum_kernel<T>, dim3(nb, cdiv(Cout, 256)), dim3(256), 0, s, (const T*)dy, M, Cout, lddy,
+                       cchunk, part);
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(cdiv(Cout, 256)), dim3(256), 0, s, part, db, nb, (long)Cout);
+  }
+}
+
+}  // namespace rod
+
+using namespace rod;
+
+extern "C" {
+
+int rod_conv_fwd(const void* x, const void* wt, const float* bias, void* y, int N, int H, int W, int Cin, int Cout,
+                 int ksize, int ldx, int ldy, int dtype, void* stream) {
+  ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "rod_conv_fwd: bad shape");
+  ROD_CHECK_ARG(ksize == 1 || ksize == 3, "rod_conv_fwd: ksize must be 1 or 3");
+  if (ldx == 0) ldx = Cin;
+  if (ldy == 0) ldy = Cout;
+  ROD_CHECK_ARG(ldx >= Cin && ldy >= Cout, "rod_conv_fwd: leading dim too small");
+  ROD_DISPATCH_DTYPE(dtype, conv_fwd_typed<T>(x, wt, bias, y, N, H, W, Cin, Cout, ksize, ldx, ldy,
+                                              ROD_STREAM(stream)));
+  return check_launch("rod_conv_fwd");
+}
+
+int rod_conv_weight_prep(const float* w, void* wt, int Cout, int Cin, int ksize, int mode, int dtype,
+                         void* stream) {
+  ROD_CHECK_ARG(Cout > 0 && Cin > 0 && (ksize == 1 || ksize == 3), "rod_conv_weight_prep: bad shape");
+  ROD_CHECK_ARG(mode == 0 || mode == 1, "rod_conv_weight_prep: bad mode %d", mode);
+  const long n = (long)Cout * ksize * ksize * Cin;
+  ROD_DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(weight_prep_kernel<T>, dim3(cdivl(n, 256)), dim3(256), 0,
+                                               ROD_STREAM(stream), w, (T*)wt, Cout, Cin, ksize, mode));
+  return check_launch("rod_conv_weight_prep");
+}
+
+size_t rod_conv_wgrad_workspace(int N, int H, int W, int Cin, int Cout, int ksize) {
+  const long M = (long)N * H * W;
+  WgradPlan p = wgrad_plan(M, Cin, Cout, ksize);
+  const long K = (long)ksize * ksize * Cin;
+  size_t part = (size_t)p.splits * Cout * K * sizeof(float);
+  long cchunk = std::max<long>(64, cdivl(M, 512));
+  size_t cs = (size_t)cdivl(M, cchunk) * Cout * sizeof(float);
+  return std::max(part, cs);
+}
+
+int rod_conv_wgrad(const void* x, const void* dy, float* dw, float* db, void* workspace, int N, int H, int W,
+                   int Cin, int Cout, int ksize, int ldx, int lddy, int dtype, void* stream) {
+  ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "rod_conv_wgrad: bad shape");
+  ROD_CHECK_ARG(ksize == 1 || ksize == 3, "rod_conv_wgrad: ksize must be 1 or 3");
+  ROD_CHECK_ARG(workspace != nullptr, "rod_conv_wgrad: workspace is NULL");
+  if (ldx == 0) ldx = Cin;
+  if (lddy == 0) lddy = Cout;
+  ROD_CHECK_ARG(ldx >= Cin && lddy >= Cout, "rod_conv_wgrad: leading dim too small");
+  ROD_DISPATCH_DTYPE(dtype, wgrad_typed<T>(x, dy, dw, db, (float*)workspace, N, H, W, Cin, Cout, ksize, ldx, lddy,
+                                           ROD_STREAM(stream)));
+  return check_launch("rod_conv_wgrad");
+}
+
+}  // extern "C"

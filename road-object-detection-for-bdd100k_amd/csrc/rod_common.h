@@ -1,0 +1,91 @@
+// rod_common.h — shared device/host helpers for librod (gfx950 / CDNA4 only).
+//
+// Conventions (see include/rod.h):
+//   * every tensor is NHWC, row-major, C innermost;
+//   * dtype codes: ROD_F32 = 0, ROD_BF16 = 1 (storage type; arithmetic is fp32);
+//   * every entry point returns 0 or an error code and records a message in
+//     rod_last_error(); launches are stream-ordered on the caller's hipStream_t.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/rod.h"
+
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace rod {
+
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+// ---- scalar conversions -------------------------------------------------
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16_t v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) { return (bf16_t)v; }
+
+// 16-byte vector of T: 4 x f32 or 8 x bf16.
+template <typename T> struct Vec16;
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  f32x4 v;
+  __device__ __forceinline__ void load(const float* p) { v = *(const f32x4*)p; }
+  __device__ __forceinline__ void store(float* p) const { *(f32x4*)p = v; }
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = x; }
+};
+template <> struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x8*)p; }
+  __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x8*)p = v; }
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = (bf16_t)x; }
+};
+
+// Correctly-rounded f32 transcendental functions (evaluated in f64 and
+// rounded once).  The oracle uses the same definition (np.float64 then cast),
+// so integer decisions downstream of exp/log are reproducible bit for bit.
+__device__ __forceinline__ float exp_cr(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float log_cr(float x) { return (float)log((double)x); }
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+inline long cdivl(long a, long b) { return (a + b - 1) / b; }
+
+}  // namespace rod
+
+#define ROD_CHECK_ARG(cond, ...)             \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::rod::set_error(__VA_ARGS__);         \
+      return ROD_EINVAL;                     \
+    }                                        \
+  } while (0)
+
+#define ROD_STREAM(s) ((hipStream_t)(s))
+
+// dispatch on storage dtype: defines `T` inside the body
+#define ROD_DISPATCH_DTYPE(dt, ...)                                   \
+  do {                                                                \
+    if ((dt) == ROD_F32) {                                            \
+      typedef float T;                                                \
+      __VA_ARGS__;                                                    \
+    } else if ((dt) == ROD_BF16) {                                    \
+      typedef bf16_t T;                                               \
+      __VA_ARGS__;                                                    \
+    } else {                                                          \
+      ::rod::set_error("unsupported dtype code %d", (int)(dt));        \
+      return ROD_EINVAL;                                              \
+    }                                                                 \
+  } while (0)

@@ -1,0 +1,111 @@
+"""Modified MobileNet-v2 backbone (reference nets/backbone/mobilenet/mobilenet_v2.py:41-87,
+built by mobilenet.py:149-294 from conv_blocks.expanded_conv, conv_blocks.py:163-312).
+
+Spec differences from stock MobileNet-v2, kept as in the reference: the stem conv has
+stride 1, layers 19-20 have 320 outputs, and four x2-expansion blocks (256 outputs) are
+appended.  Every conv is followed by BatchNorm (center+scale, decay 0.997, eps 1e-3)
+and ReLU6, except the linear projection; no conv has a bias.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from rod import ops
+from rod.params import trunc_normal
+
+
+def make_divisible(v, divisor, min_value=None):
+    """Channel rounding of conv_blocks._make_divisible (conv_blocks.py:50-57)."""
+    if min_value is None:
+        min_value = divisor
+    new_v = max(min_value, int(v + divisor / 2) // divisor * divisor)
+    if new_v < 0.9 * v:
+        new_v += divisor
+    return new_v
+
+
+# (kind, stride, num_outputs, expansion factor, divisible_by); kind 'conv' = 3x3 stem
+V2_SPEC = [('conv', 1, 32, None, None), ('ir', 1, 16, 1, 1)] + \
+    [('ir', s, c, 6, 8) for s, c in [(2, 24), (1, 24), (2, 32), (1, 32), (1, 32), (2, 64), (1, 64), (1, 64),
+                                     (1, 64), (2, 96), (1, 96), (1, 96), (1, 96), (2, 160), (1, 160), (1, 160),
+                                     (2, 320), (1, 320)]] + \
+    [('ir', s, 256, 2, 8) for s in (2, 1, 2, 1)]
+
+BN_DECAY = 0.997   # mobilenet.training_scope bn_decay (mobilenet.py:390)
+BN_EPS = 1e-3      # slim.batch_norm default
+W_STD = 0.09       # trunc-normal stddev (mobilenet.py:388)
+
+
+def layer_plan(in_ch=3):
+    """[(index, kind, stride, cin, inner, cout, residual, scope)] for the 24 spec entries."""
+    plan, cin, n_ir = [], in_ch, 0
+    for i, (kind, s, cout, exp, div) in enumerate(V2_SPEC):
+        if kind == 'conv':
+            plan.append((i + 1, 'conv', s, cin, None, cout, False, 'Conv'))
+        else:
+            inner = make_divisible(cin * exp, div)
+            scope = 'expanded_conv' if n_ir == 0 else 'expanded_conv_%d' % n_ir
+            n_ir += 1
+            plan.append((i + 1, 'ir', s, cin, inner, cout, s == 1 and cin == cout, scope))
+        cin = cout
+    return plan
+
+
+class MobilenetV2:
+    def __init__(self, store, rng, scope='backbone/MobilenetV2'):
+        self.store = store
+        self.plan = layer_plan()
+        self.scope = scope
+        for (idx, kind, s, cin, inner, cout, res, sc) in self.plan:
+            base = '%s/%s' % (scope, sc)
+            if kind == 'conv':
+                store.add(base + '/weights', trunc_normal(rng, (cout, 3, 3, cin), W_STD))
+                self._bn(base + '/BatchNorm', cout)
+                continue
+            if inner > cin:  # conv_blocks.py:263
+                store.add(base + '/expand/weights', trunc_normal(rng, (inner, 1, 1, cin), W_STD))
+                self._bn(base + '/expand/BatchNorm', inner)
+            store.add(base + '/depthwise/depthwise_weights', trunc_normal(rng, (3, 3, inner), W_STD))
+            self._bn(base + '/depthwise/BatchNorm', inner)
+            store.add(base + '/project/weights', trunc_normal(rng, (cout, 1, 1, inner), W_STD))
+            self._bn(base + '/project/BatchNorm', cout)
+
+    def _bn(self, name, c):
+        self.store.add(name + '/gamma', np.ones(c, np.float32))
+        self.store.add(name + '/beta', np.zeros(c, np.float32))
+        self.store.add_buffer(name + '/moving_mean', np.zeros(c, np.float32))
+        self.store.add_buffer(name + '/moving_variance', np.ones(c, np.float32))
+
+    def _bn_act(self, x, name, act, training, residual=None):
+        P, B = self.store.params, self.store.buffers
+        return ops.bn_act(x, P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'],
+                          B[name + '/moving_variance'], act, training, BN_DECAY, BN_EPS, residual)
+
+    def __call__(self, x, is_training, final_endpoint=None):
+        """Returns the endpoint dict {'layer_1': ..., 'layer_24': ...} (mobilenet.py:275-281)."""
+        P = self.store.params
+        end_points = {}
+        for (idx, kind, s, cin, inner, cout, res, sc) in self.plan:
+            base = '%s/%s' % (self.scope, sc)
+            if kind == 'conv':
+                x = ops.conv2d(x, P[base + '/weights'], None, 3)
+                x = self._bn_act(x, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training)
+            else:
+                inp = x
+                if inner > cin:
+                    x = ops.conv2d(x, P[base + '/expand/weights'], None, 1)
+                    x = self._bn_act(x, base + '/expand/BatchNorm', ops.ROD_ACT_RELU6, is_training)
+                x = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s)
+                x = self._bn_act(x, base + '/depthwise/BatchNorm', ops.ROD_ACT_RELU6, is_training)
+                x = ops.conv2d(x, P[base + '/project/weights'], None, 1)
+                x = self._bn_act(x, base + '/project/BatchNorm', ops.ROD_ACT_NONE, is_training,
+                                 residual=inp if res else None)
+            end_points['layer_%d' % idx] = x
+            if final_endpoint is not None and final_endpoint == 'layer_%d' % idx:
+                break
+        return end_points
+
+
+def mobilenet_v2(inputs, is_training, net):
+    """Functional form mirroring mobilenet_v2(inputs, is_training=...) -> end_points."""
+    return net(inputs, is_training)

@@ -1,0 +1,205 @@
+"""Detector assembly — drop-in for the reference's nets/catch_net.py (factory, 37-363).
+
+``factory(inputs, backbone_name, is_training, config_dict, dtype)`` builds (once, cached
+per configuration) and runs the network on NHWC `inputs` and exposes ``get_output()``
+exactly as the reference: REFINE -> refine_out; ALL -> (refine_out, det_out, clf_out),
+each a list of six [B, fh, fw, A, 4 | 11] tensors.
+
+Structure (reference line numbers):
+  backbone endpoints layer_11/15/18/20/22/24 (__feats_aug_block NONE, 111-114)
+  ALL: deconv pyramid LEARN_HALF (160-212) + ADD merge (237-273)
+  heads: per level, for ch in [128, k*A]: conv1x1(+bias) -> BN -> leaky(0.2) ->
+         conv3x3(+bias) -> BN -> leaky (276-342); head BN is slim's default
+         (center, no scale, decay 0.999, eps 1e-3); weights xavier, biases zero.
+"""
+from __future__ import annotations
+
+import collections
+
+import numpy as np
+import torch
+
+import config
+from nets.backbone.mobilenet_v2 import MobilenetV2
+from rod import ops
+from rod.params import ParamStore, trunc_normal, xavier_uniform
+
+HEAD_BN_DECAY = 0.999
+HEAD_BN_EPS = 1e-3
+
+
+def n_anchor_each_layer(backbone_name):
+    import utils.net_tools as net_tools
+    return net_tools.n_anchor_each_layer(backbone_name)
+
+
+class CatchNet:
+    """Parameters + forward of the whole detector for one configuration."""
+
+    def __init__(self, backbone_name, config_dict, device, seed=0, build_all=None):
+        if backbone_name != 'mobilenet_v2':
+            raise ValueError('backbone %r is not built by this framework (see DESIGN.md)' % backbone_name)
+        if config_dict['process_backbone_method'] is not config.process_backbone_method.NONE:
+            raise ValueError('Not support the method(%s) now' % str(config_dict['process_backbone_method']))
+        self.backbone_name = backbone_name
+        self.config_dict = dict(config_dict)
+        self.train_range = config_dict['train_range']
+        all_mode = self.train_range is config.train_range.ALL if build_all is None else build_all
+        self.all_mode = all_mode
+        rng = np.random.default_rng(seed)
+        self.store = ParamStore()
+        self.backbone = MobilenetV2(self.store, rng)
+        self.feat_ch = self._endpoint_channels()
+        self.n_anchor = n_anchor_each_layer(backbone_name)
+        self._head('refine', self.feat_ch, 4, rng)
+        if all_mode:
+            if config_dict['deconv_method'] is not config.deconv_method.LEARN_HALF:
+                raise ValueError('Parameter "method(%s)" wrong' % str(config_dict['deconv_method']))
+            if config_dict['merge_method'] is not config.merge_method.ADD:
+                raise ValueError('parameter "method(%s)" wrong...' % str(config_dict['merge_method']))
+            self._deconv(rng)
+            self._head('clf', self.feat_ch, config.total_obj_n, rng)
+            self._head('det', self.feat_ch, 4, rng)
+        self.store.finalize(device)
+
+    # ------------------------------------------------------------------ parameters
+    def _endpoint_channels(self):
+        outs = {'layer_%d' % idx: cout for (idx, _, _, _, _, cout, _, _) in self.backbone.plan}
+        return [outs[n] for n in config.extract_feat_name[self.backbone_name]]
+
+    def _head_bn(self, name, c):
+        self.store.add(name + '/beta', np.zeros(c, np.float32))
+        self.store.add_buffer(name + '/moving_mean', np.zeros(c, np.float32))
+        self.store.add_buffer(name + '/moving_variance', np.ones(c, np.float32))
+
+    def _conv_params(self, name, cout, k, cin, rng, bias=True):
+        self.store.add(name + '/weights', xavier_uniform(rng, (cout, k, k, cin)))
+        if bias:
+            self.store.add(name + '/biases', np.zeros(cout, np.float32))
+
+    def _head(self, scope, in_chs, k, rng):
+        for i, cin in enumerate(in_chs):
+            base = '%s/block_%d' % (scope, i + 1)
+            n = 0
+            for ch in [128, k * self.n_anchor[i]]:
+                for ks in (1, 3):
+                    cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
+                    bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
+                    self._conv_params(cname, ch, ks, cin, rng)
+                    self._head_bn(bname, ch)
+                    cin = ch
+                    n += 1
+
+    def _deconv(self, rng):
+        chs = list(reversed(self.feat_ch))
+        for i in range(len(chs)):
+            base = 'deconv/block_%d' % (i + 1)
+            if i == 0:
+                self._conv_params(base + '/Conv', chs[0], 1, chs[0], rng)
+                self._head_bn(base + '/BatchNorm', chs[0])
+            else:
+                f_c, i_c = chs[i] // 2, chs[i - 1]
+                # tf.get_variable('weight_%d', [2, 2, f_c, i_c], trunc-normal 0.02) (catch_net.py:189)
+                self.store.add(base + '/weight_%d' % i, trunc_normal(rng, (2, 2, f_c, i_c), 0.02))
+                self._conv_params(base + '/Conv', f_c, 1, i_c, rng)
+                self._head_bn(base + '/BatchNorm', 2 * f_c)
+
+    # ------------------------------------------------------------------ forward
+    def _bn(self, x, name, training, act=ops.ROD_ACT_LEAKY):
+        P, B = self.store.params, self.store.buffers
+        return ops.bn_act(x, None, P[name + '/beta'], B[name + '/moving_mean'], B[name + '/moving_variance'],
+                          act, training, HEAD_BN_DECAY, HEAD_BN_EPS)
+
+    def head_out(self, feats, scope, k, training):
+        """__det_out / __clf_out (catch_net.py:276-342)."""
+        P = self.store.params
+        outs = []
+        for i, x in enumerate(feats):
+            base = '%s/block_%d' % (scope, i + 1)
+            n = 0
+            for ch in [128, k * self.n_anchor[i]]:
+                for ks in (1, 3):
+                    cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
+                    bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
+                    x = ops.conv2d(x, P[cname + '/weights'], P[cname + '/biases'], ks)
+                    x = self._bn(x, bname, training)
+                    n += 1
+            B_, fh, fw, _ = x.shape
+            outs.append(x.view(B_, fh, fw, self.n_anchor[i], k))
+        return outs
+
+    def deconv_bone(self, feats, training):
+        """LEARN_HALF deconvolution pyramid (catch_net.py:160-212); returns in reversed order."""
+        P = self.store.params
+        layers = list(reversed(feats))
+        out = []
+        x = layers[0]
+        for i in range(len(layers)):
+            base = 'deconv/block_%d' % (i + 1)
+            if i == 0:
+                x = ops.conv2d(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1)
+                x = self._bn(x, base + '/BatchNorm', training)
+            else:
+                B_, h, w, _ = layers[i].shape
+                f_c = layers[i].shape[3] // 2
+                cat = torch.empty((B_, h, w, 2 * f_c), dtype=x.dtype, device=x.device)
+                up = ops.deconv2x2(x, P[base + '/weight_%d' % i], (h, w))           # conv2d_transpose
+                rs = ops.resize_bilinear(x, (h, w))                                  # resize_images
+                rh = ops.conv2d(rs, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1)
+                cat = ops.channel_concat([up, rh])                                   # tf.concat(-1)
+                x = self._bn(cat, base + '/BatchNorm', training)
+            out.append(x)
+        return out
+
+    def forward(self, inputs, is_training):
+        ep = self.backbone(inputs, is_training)
+        feats = [ep[n] for n in config.extract_feat_name[self.backbone_name]]
+        self.backbone_feats = collections.OrderedDict(('layer_%d' % (i + 1), f) for i, f in enumerate(feats))
+        refine_out = self.head_out(feats, 'refine', 4, is_training)
+        if not self.all_mode:
+            return refine_out
+        deconv = self.deconv_bone(feats, is_training)
+        self.deconv_feats = deconv
+        merged = [ops.add(u, d) for u, d in zip(feats, reversed(deconv))]        # ADD merge
+        self.merge_feats = merged
+        clf_out = self.head_out(merged, 'clf', config.total_obj_n, is_training)
+        det_out = self.head_out(merged, 'det', 4, is_training)
+        return refine_out, det_out, clf_out
+
+
+_NET_CACHE = {}
+
+
+def get_net(backbone_name, config_dict, device='cuda', seed=0):
+    key = (backbone_name, config_dict['train_range'], config_dict['deconv_method'], config_dict['merge_method'],
+           config_dict['process_backbone_method'], str(device), seed)
+    if key not in _NET_CACHE:
+        _NET_CACHE[key] = CatchNet(backbone_name, config_dict, device, seed)
+    return _NET_CACHE[key]
+
+
+class factory(object):
+    """Drop-in for catch_net.factory: runs the network on `inputs` at construction."""
+
+    def __init__(self, inputs, backbone_name, is_training, config_dict, dtype=torch.float32, net=None):
+        assert backbone_name in config.supported_backbone_name
+        self.backbone_name = backbone_name
+        self.is_training = is_training
+        self.train_range = config_dict['train_range']
+        self.net = net if net is not None else get_net(backbone_name, config_dict, inputs.device)
+        x = inputs if inputs.dtype == dtype else ops.cast(inputs, dtype)
+        out = self.net.forward(x, is_training)
+        self.backbone_feats = self.net.backbone_feats
+        if self.net.all_mode:
+            self.refine_out, self.det_out, self.clf_out = out
+            self.deconv_feats = self.net.deconv_feats
+            self.merge_feats = self.net.merge_feats
+        else:
+            self.refine_out = out
+
+    def get_output(self):
+        if self.train_range is config.train_range.ALL:
+            return self.refine_out, self.det_out, self.clf_out
+        elif self.train_range is config.train_range.REFINE:
+            return self.refine_out
+        raise ValueError('Error')

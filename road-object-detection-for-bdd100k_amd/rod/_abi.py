@@ -1,0 +1,172 @@
+"""ctypes binding of librod.so (the C ABI declared in include/rod.h).
+
+The prototypes are read from the header itself, so the header is the single source
+of truth for argument types; every call checks the return code and raises
+RuntimeError with rod_last_error() on failure.  There is no fallback: if the library
+is missing the import of any op fails loudly (the product path never routes through
+a CPU implementation).
+
+Argument conversion for pointer parameters:
+  torch.Tensor  -> data_ptr()   (device tensors for device buffers; CPU tensors are
+                                  accepted only where the header documents a host array)
+  numpy.ndarray -> host pointer (host arrays such as lvl_off / thr)
+  None          -> NULL
+  int           -> raw address
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.environ.get("ROD_LIB", os.path.join(PKG_ROOT, "lib", "librod.so"))
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "rod.h")
+
+ROD_F32 = 0
+ROD_BF16 = 1
+ROD_ACT_NONE = 0
+ROD_ACT_RELU6 = 1
+ROD_ACT_LEAKY = 2
+
+_CTYPE = {
+    "int": ctypes.c_int,
+    "long": ctypes.c_long,
+    "float": ctypes.c_float,
+    "size_t": ctypes.c_size_t,
+    "ptr": ctypes.c_void_p,
+    "cstr": ctypes.c_char_p,
+    "void": None,
+}
+
+_PROTO_RE = re.compile(
+    r"^\s*(const\s+char\s*\*|int|size_t|void)\s+(rod_\w+)\s*\(([^)]*)\)\s*;", re.M | re.S)
+
+
+def parse_header(path: str = HEADER_PATH):
+    """Return {name: (restype, [(argtype, argname), ...])} for every rod_* prototype."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    protos = {}
+    for m in _PROTO_RE.finditer(text):
+        ret, name, args = m.group(1), m.group(2), m.group(3)
+        ret = "cstr" if "char" in ret else ret.strip()
+        argl = []
+        a = " ".join(args.split())
+        if a and a != "void":
+            for piece in a.split(","):
+                piece = piece.strip()
+                if "*" in piece:
+                    argl.append(("ptr", piece.split("*")[-1].strip()))
+                else:
+                    toks = piece.replace("const ", "").split()
+                    argl.append((toks[0], toks[1]))
+        protos[name] = (ret, argl)
+    return protos
+
+
+class _Lib:
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._cdll = None
+        self.protos = None
+
+    def load(self):
+        if self._cdll is not None:
+            return self._cdll
+        with self._lock:
+            if self._cdll is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"librod.so not found at {LIB_PATH}: build it with "
+                        f"`make -C {os.path.join(PKG_ROOT, 'csrc')}` (or __graft_entry__.build())")
+                cdll = ctypes.CDLL(LIB_PATH)
+                protos = parse_header()
+                for name, (ret, args) in protos.items():
+                    fn = getattr(cdll, name)  # AttributeError => header/library mismatch
+                    fn.restype = _CTYPE[ret]
+                    fn.argtypes = [_CTYPE[t] for t, _ in args]
+                self.protos = protos
+                self._cdll = cdll
+        return self._cdll
+
+
+_LIB = _Lib()
+
+
+def lib():
+    return _LIB.load()
+
+
+def _ptr(v):
+    if v is None:
+        return None
+    if isinstance(v, int):
+        return v
+    if isinstance(v, np.ndarray):
+        if not v.flags["C_CONTIGUOUS"]:
+            raise ValueError("host array must be C-contiguous")
+        return v.ctypes.data
+    dp = getattr(v, "data_ptr", None)
+    if dp is not None:
+        return dp()
+    raise TypeError(f"cannot pass {type(v)} as a pointer")
+
+
+class Probe:
+    """Live per-kernel timing for the roofline report (bench.py): when `name` matches,
+    HIP events are recorded on the launching stream around every call and the
+    algorithmic byte / flop count of the call (rod.roofline) is accumulated."""
+
+    def __init__(self):
+        self.name = None
+        self.records = []
+
+    def arm(self, name):
+        self.name = name
+        self.records = []
+
+    def disarm(self):
+        self.name = None
+
+
+PROBE = Probe()
+
+
+def call(name: str, *args):
+    """Call rod_<name>; raise RuntimeError on a non-zero return code."""
+    L = lib()
+    fn = getattr(L, name)
+    ret, argspec = _LIB.protos[name]
+    if len(args) != len(argspec):
+        raise TypeError(f"{name} expects {len(argspec)} args, got {len(args)}")
+    conv = [(_ptr(a) if t == "ptr" else a) for (t, _), a in zip(argspec, args)]
+    if PROBE.name == name:
+        import torch
+        from . import roofline
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        rc = fn(*conv)
+        e1.record(s)
+        PROBE.records.append((e0, e1, roofline.cost(name, args)))
+    else:
+        rc = fn(*conv)
+    if ret == "int" and rc != 0:
+        msg = L.rod_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def query(name: str, *args) -> int:
+    """Call a size_t workspace query."""
+    return int(getattr(lib(), name)(*args))
+
+
+def exported_symbols():
+    return sorted(parse_header().keys())

@@ -1,0 +1,307 @@
+"""Differentiable ops backed by librod (HIP kernels for gfx950).
+
+Every op here launches only librod kernels on the current HIP stream; PyTorch provides
+device memory, streams and the autograd tape.  Parameter gradients are written by the
+kernels straight into the flat gradient buffer of rod.params.ParamStore (the op
+returns None for the parameter), so no PyTorch arithmetic touches gradients either.
+
+Tensor conventions: activations NHWC [N, H, W, C] contiguous in fp32 or bf16; conv
+weights fp32 [Cout, k, k, Cin]; depthwise weights fp32 [3, 3, C]; BN vectors fp32 [C].
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU6  # noqa: F401
+
+_DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
+
+
+def dtcode(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def grad_slot(p):
+    """The flat-buffer gradient view registered for parameter tensor p (or None)."""
+    return getattr(p, "_rod_grad", None)
+
+
+def _mark_written(p):
+    cb = getattr(p, "_rod_on_grad", None)
+    if cb is not None:
+        cb(p)
+
+
+def same_pad(size: int, stride: int, k: int = 3):
+    """TF 'SAME' padding: (out, pad_before) for one spatial dim (conv_blocks.py:40-46)."""
+    out = -(-size // stride)
+    total = max((out - 1) * stride + k - size, 0)
+    return out, total // 2
+
+
+# ----------------------------------------------------------------------------- ingest
+def normalize_image(img_u8: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    """(2/255)*img - 1 (train.py:126) from a uint8 NHWC tensor."""
+    out = torch.empty(img_u8.shape, dtype=dtype, device=img_u8.device)
+    _abi.call("rod_normalize_image", img_u8, out, img_u8.numel(), dtcode(out), stream())
+    return out
+
+
+def cast(x: torch.Tensor, dtype) -> torch.Tensor:
+    if x.dtype == dtype:
+        return x
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    _abi.call("rod_cast", x, dtcode(x), out, dtcode(out), x.numel(), stream())
+    return out
+
+
+def copy2d(src, src_ld_bytes, dst, dst_ld_bytes, rows, cols_bytes, src_off=0, dst_off=0):
+    _abi.call("rod_copy2d", src.data_ptr() + src_off, src_ld_bytes, dst.data_ptr() + dst_off, dst_ld_bytes,
+              rows, cols_bytes, stream())
+
+
+# ----------------------------------------------------------------------------- depthwise
+class _DW3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride):
+        N, H, W, C = x.shape
+        Ho, pt = same_pad(H, stride)
+        Wo, pl = same_pad(W, stride)
+        y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        _abi.call("rod_dw3x3_fwd", x, w, y, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x), stream())
+        ctx.save_for_backward(x, w)
+        ctx.geo = (N, H, W, C, stride, pt, pl, Ho, Wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _abi.call("rod_dw3x3_bwd_data", dy, w, dx, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x), stream())
+        if ctx.needs_input_grad[1]:
+            g = grad_slot(w)
+            ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
+            _abi.call("rod_dw3x3_bwd_filter", x, dy, g, ws, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x), stream())
+            _mark_written(w)
+        return dx, None, None
+
+
+def dw3x3(x, w, stride=1):
+    """Depthwise 3x3, TF-SAME (conv_blocks.py:238-247)."""
+    return _DW3x3.apply(x, w, stride)
+
+
+# ----------------------------------------------------------------------------- dense conv
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, ksize):
+        N, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        assert w.shape == (Cout, ksize, ksize, Cin), (tuple(w.shape), ksize, Cin)
+        wt = torch.empty((Cout, ksize * ksize * Cin), dtype=x.dtype, device=x.device)
+        _abi.call("rod_conv_weight_prep", w, wt, Cout, Cin, ksize, 0, dtcode(x), stream())
+        y = torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
+        _abi.call("rod_conv_fwd", x, wt, b, y, N, H, W, Cin, Cout, ksize, 0, 0, dtcode(x), stream())
+        ctx.save_for_backward(x, w, b)
+        ctx.ksize = ksize
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b = ctx.saved_tensors
+        ks = ctx.ksize
+        N, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt1 = torch.empty((Cin, ks * ks * Cout), dtype=x.dtype, device=x.device)
+            _abi.call("rod_conv_weight_prep", w, wt1, Cout, Cin, ks, 1, dtcode(x), stream())
+            dx = torch.empty_like(x)
+            _abi.call("rod_conv_fwd", dy, wt1, None, dx, N, H, W, Cout, Cin, ks, 0, 0, dtcode(x), stream())
+        need_w = ctx.needs_input_grad[1]
+        need_b = b is not None and ctx.needs_input_grad[2]
+        if need_w or need_b:
+            gw = grad_slot(w) if need_w else None
+            if gw is None:  # bias-only gradient still needs a scratch dW
+                gw = torch.empty(w.shape, dtype=torch.float32, device=x.device)
+            gb = grad_slot(b) if need_b else None
+            ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, H, W, Cin, Cout, ks), x.device)
+            _abi.call("rod_conv_wgrad", x, dy, gw, gb, ws, N, H, W, Cin, Cout, ks, 0, 0, dtcode(x), stream())
+            if need_w:
+                _mark_written(w)
+            if need_b:
+                _mark_written(b)
+        return dx, None, None, None
+
+
+def conv2d(x, w, b=None, ksize=1):
+    """slim.conv2d, stride 1, SAME (1x1 or 3x3), NHWC."""
+    return _Conv.apply(x, w, b, ksize)
+
+
+# ----------------------------------------------------------------------------- batch norm
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, mmean, mvar, act, training, decay, eps):
+        N, H, W, C = x.shape
+        M = N * H * W
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        if training:
+            ws = workspace(_abi.query("rod_bn_stats_workspace", M, C), x.device)
+            _abi.call("rod_bn_stats", x, M, C, 0, eps, decay, mean, rstd, mmean, mvar, ws, dtcode(x), stream())
+        else:
+            _abi.call("rod_bn_eval_stats", mmean, mvar, eps, mean, rstd, C, stream())
+        y = torch.empty_like(x)
+        _abi.call("rod_bn_apply", x, mean, rstd, gamma, beta, residual, y, M, C, 0, 0, 0, act, dtcode(x),
+                  stream())
+        ctx.save_for_backward(x, mean, rstd, gamma, beta)
+        ctx.act = act
+        ctx.training = training
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, gamma, beta = ctx.saved_tensors
+        if not ctx.training:
+            raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
+        N, H, W, C = x.shape
+        M = N * H * W
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        need_g = gamma is not None and ctx.needs_input_grad[1]
+        need_b = beta is not None and ctx.needs_input_grad[2]
+        dg = grad_slot(gamma) if need_g else None
+        db = grad_slot(beta) if need_b else None
+        if need_b and db is None:
+            db = torch.empty(C, dtype=torch.float32, device=x.device)
+        if db is None:
+            db = torch.empty(C, dtype=torch.float32, device=x.device)  # kernel always may write dbeta
+        ws = workspace(_abi.query("rod_bn_bwd_workspace", M, C), x.device)
+        _abi.call("rod_bn_bwd", dy, x, mean, rstd, gamma, beta, dx, dg, db, ws, M, C, 0, 0, 0, ctx.act,
+                  dtcode(x), stream())
+        if need_g:
+            _mark_written(gamma)
+        if need_b:
+            _mark_written(beta)
+        dres = dy if ctx.has_res else None
+        return dx, None, None, dres, None, None, None, None, None, None
+
+
+def bn_act(x, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, residual=None):
+    """slim.batch_norm (fused) + activation (+ residual add after the activation)."""
+    return _BNAct.apply(x, gamma, beta, residual, mmean, mvar, act, training, decay, eps)
+
+
+# ----------------------------------------------------------------------------- levels
+class _LevelsConcat(torch.autograd.Function):
+    """[B, fh, fw, A*k] per level -> [B, sum(fh*fw*A), k] (tf.concat of reshaped levels)."""
+
+    @staticmethod
+    def forward(ctx, k, *levels):
+        B = levels[0].shape[0]
+        sizes = [lv.numel() // B for lv in levels]
+        tot = sum(sizes)
+        out = torch.empty((B, tot // k, k), dtype=levels[0].dtype, device=levels[0].device)
+        es = out.element_size()
+        off = 0
+        for lv, n in zip(levels, sizes):
+            lv = lv.contiguous()
+            copy2d(lv, n * es, out, tot * es, B, n * es, 0, off * es)
+            off += n
+        ctx.shapes = [lv.shape for lv in levels]
+        ctx.sizes = sizes
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        B = g.shape[0]
+        tot = sum(ctx.sizes)
+        es = g.element_size()
+        outs = []
+        off = 0
+        for shp, n in zip(ctx.shapes, ctx.sizes):
+            d = torch.empty(shp, dtype=g.dtype, device=g.device)
+            copy2d(g, tot * es, d, n * es, B, n * es, off * es, 0)
+            outs.append(d)
+            off += n
+        return (None, *outs)
+
+
+def levels_concat(levels, k):
+    return _LevelsConcat.apply(k, *levels)
+
+
+# ----------------------------------------------------------------------------- losses
+class _SmoothL1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target, mask, lvl_off, scale):
+        B, A, _ = pred.shape
+        L = len(lvl_off) - 1
+        loss = torch.empty(L + 1, dtype=torch.float32, device=pred.device)
+        grad = torch.empty_like(pred) if ctx.needs_input_grad[0] else None
+        ws = workspace(_abi.query("rod_smoothl1_workspace", B, A), pred.device)
+        _abi.call("rod_smoothl1_masked", pred, target, mask, np.ascontiguousarray(lvl_off, dtype=np.int32), L,
+                  float(scale), loss, grad, ws, B, A, dtcode(pred), stream())
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        (grad,) = ctx.saved_tensors
+        # the loss vector's consumers take loss[L] (the total) with weight 1
+        return grad, None, None, None, None
+
+
+def smooth_l1_masked(pred, target, mask, lvl_off, scale):
+    """Returns [L+1] fp32: per-level sum(smooth_l1((t - p)*m))/scale and their total."""
+    return _SmoothL1.apply(pred, target, mask, lvl_off, scale)
+
+
+# ----------------------------------------------------------------------------- targets
+def boxes_convert(boxes: torch.Tensor, to_center: bool) -> torch.Tensor:
+    b = boxes.contiguous()
+    out = torch.empty_like(b)
+    _abi.call("rod_boxes_convert", b, out, b.numel() // 4, 1 if to_center else 0, stream())
+    return out
+
+
+def match_anchors(anc_corner, anc_center, lvl_off, thr, gt_center, gt_lbl, gt_n):
+    B, G, _ = gt_center.shape
+    A = anc_corner.shape[0]
+    dev = gt_center.device
+    off = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
+    cbox = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
+    lbl = torch.empty((B, A), dtype=torch.int32, device=dev)
+    pos = torch.empty((B, A), dtype=torch.int32, device=dev)
+    _abi.call("rod_match_anchors", anc_corner, anc_center, np.ascontiguousarray(lvl_off, dtype=np.int32),
+              np.ascontiguousarray(thr, dtype=np.float32), len(lvl_off) - 1, gt_center.contiguous(),
+              gt_lbl.contiguous(), gt_n.contiguous(), off, cbox, lbl, pos, B, A, G, stream())
+    return off, cbox, lbl, pos
+
+
+# ----------------------------------------------------------------------------- optimiser
+def sgd_clip_(param_flat: torch.Tensor, grad_flat: torch.Tensor, lr: float, clip: float = 5.0):
+    _abi.call("rod_sgd_clip", param_flat, grad_flat, param_flat.numel(), float(lr), float(clip), stream())

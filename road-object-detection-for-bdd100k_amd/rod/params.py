@@ -1,0 +1,122 @@
+"""Flat parameter / gradient storage.
+
+All trainable tensors live in one contiguous fp32 buffer (16-byte aligned slices) and
+their gradients in a second buffer of identical layout.  Each parameter is a leaf
+tensor viewing its slice; the rod.ops kernels write its gradient straight into the
+matching grad slice (`p._rod_grad`), so the SGD update is one rod_sgd_clip launch over
+the whole buffer and data-parallel reduction works on contiguous byte ranges.
+
+Names follow the reference's TF/slim variable names (e.g.
+``backbone/MobilenetV2/expanded_conv_3/depthwise/depthwise_weights``) so a checkpoint
+importer maps 1:1; the weight layout differs from TF's [kh, kw, Cin, Cout] and is
+[Cout, kh, kw, Cin] here (depthwise: [3, 3, C] for TF's [3, 3, C, 1]).
+"""
+from __future__ import annotations
+
+import collections
+import math
+
+import numpy as np
+import torch
+
+ALIGN = 4  # fp32 elements (16 bytes)
+
+
+def trunc_normal(rng: np.random.Generator, shape, std: float) -> np.ndarray:
+    """tf.truncated_normal_initializer: N(0, std) redrawn outside +-2 std."""
+    out = rng.standard_normal(size=shape)
+    bad = np.abs(out) > 2.0
+    while bad.any():
+        out[bad] = rng.standard_normal(size=int(bad.sum()))
+        bad = np.abs(out) > 2.0
+    return (out * std).astype(np.float32)
+
+
+def xavier_uniform(rng: np.random.Generator, shape_ohwi) -> np.ndarray:
+    """slim default initializers.xavier_initializer() for a [Cout, kh, kw, Cin] conv."""
+    co, kh, kw, ci = shape_ohwi
+    fan_in, fan_out = kh * kw * ci, kh * kw * co
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    return rng.uniform(-lim, lim, size=shape_ohwi).astype(np.float32)
+
+
+class ParamStore:
+    """Registry of parameters (trainable, fp32) and buffers (BN moving statistics)."""
+
+    def __init__(self):
+        self._specs = collections.OrderedDict()   # name -> (shape, init ndarray)
+        self._buffers = collections.OrderedDict()  # name -> init ndarray
+        self.params = collections.OrderedDict()
+        self.buffers = collections.OrderedDict()
+        self.flat = None
+        self.flat_grad = None
+        self.offsets = {}
+        self.device = None
+
+    # ---- registration (host) ------------------------------------------------------
+    def add(self, name: str, init: np.ndarray):
+        assert name not in self._specs, f"duplicate parameter {name}"
+        self._specs[name] = np.ascontiguousarray(init, dtype=np.float32)
+        return name
+
+    def add_buffer(self, name: str, init: np.ndarray):
+        assert name not in self._buffers, f"duplicate buffer {name}"
+        self._buffers[name] = np.ascontiguousarray(init, dtype=np.float32)
+        return name
+
+    # ---- materialisation (device) ---------------------------------------------------
+    def finalize(self, device):
+        self.device = torch.device(device)
+        off = 0
+        for name, arr in self._specs.items():
+            self.offsets[name] = (off, arr.size)
+            off += -(-arr.size // ALIGN) * ALIGN
+        self.numel = off
+        host = np.zeros(off, dtype=np.float32)
+        for name, arr in self._specs.items():
+            o, n = self.offsets[name]
+            host[o:o + n] = arr.reshape(-1)
+        self.flat = torch.from_numpy(host).to(self.device)
+        self.flat_grad = torch.zeros(off, dtype=torch.float32, device=self.device)
+        for name, arr in self._specs.items():
+            o, n = self.offsets[name]
+            p = self.flat[o:o + n].view(arr.shape).detach().requires_grad_(True)
+            p._rod_grad = self.flat_grad[o:o + n].view(arr.shape)
+            p._rod_name = name
+            self.params[name] = p
+        for name, arr in self._buffers.items():
+            self.buffers[name] = torch.from_numpy(arr.copy()).to(self.device)
+        return self
+
+    def set_trainable(self, predicate):
+        """requires_grad per parameter name (train.py:160-166 trainable-var filtering)."""
+        for name, p in self.params.items():
+            p.requires_grad_(bool(predicate(name)))
+
+    def trainable_count(self):
+        return int(sum(p.numel() for p in self.params.values() if p.requires_grad))
+
+    def zero_grad(self):
+        self.flat_grad.zero_()
+
+    # ---- checkpointing -------------------------------------------------------------
+    def state_dict(self):
+        sd = {n: p.detach().cpu().clone() for n, p in self.params.items()}
+        sd.update({n: b.detach().cpu().clone() for n, b in self.buffers.items()})
+        return sd
+
+    def load_state_dict(self, sd, strict=True, names_regex=None):
+        import re
+        pat = re.compile(names_regex) if names_regex else None
+        missing = []
+        with torch.no_grad():
+            for n, p in list(self.params.items()) + list(self.buffers.items()):
+                if pat is not None and not pat.match(n):
+                    continue
+                if n not in sd:
+                    missing.append(n)
+                    continue
+                p.copy_(sd[n].to(p.device).view(p.shape))
+        if strict and missing:
+            raise KeyError(f"missing entries in checkpoint: {missing[:5]}{'...' if len(missing) > 5 else ''}")
+        return missing

@@ -1,0 +1,54 @@
+"""Algorithmic cost of one librod call (bytes that must cross HBM at minimum, and flops),
+from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
+
+  dw3x3 fwd / bwd_data : es*(in + out) + 9*C*4 bytes, 18*N*Ho*Wo*C flops
+  dw3x3 bwd_filter     : es*(x + dy) + 9*C*4, 18*N*Ho*Wo*C
+  conv fwd (1x1 / 3x3) : es*(M*Cin + M*Cout + Cout*K) (+4*Cout bias), 2*M*K*Cout
+  conv wgrad           : es*(M*Cin + M*Cout) + 4*Cout*K, 2*M*K*Cout
+  bn_stats             : es*M*C;  bn_apply: es*M*C*(2 + residual);  bn_bwd: es*M*C*5
+  match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
+"""
+
+_ES = {0: 4, 1: 2}
+
+MI355X_HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+MI355X_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec, no sparsity)
+MI355X_F32_PEAK_TFLOPS = 157.3    # f32 MFMA / vector
+
+
+def cost(name, a):
+    """(bytes, flops) of the call rod_<name>(*a)."""
+    if name in ("rod_dw3x3_fwd", "rod_dw3x3_bwd_data"):
+        N, H, W, C, s, pt, pl, Ho, Wo, dt = a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12]
+        es = _ES[dt]
+        return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
+    if name == "rod_dw3x3_bwd_filter":
+        N, H, W, C, Ho, Wo, dt = a[4], a[5], a[6], a[7], a[11], a[12], a[13]
+        es = _ES[dt]
+        return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
+    if name == "rod_conv_fwd":
+        N, H, W, Cin, Cout, ks, dt = a[4], a[5], a[6], a[7], a[8], a[9], a[12]
+        es = _ES[dt]
+        M = N * H * W
+        K = ks * ks * Cin
+        return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[2] is not None else 0), 2 * M * K * Cout
+    if name == "rod_conv_wgrad":
+        N, H, W, Cin, Cout, ks, dt = a[5], a[6], a[7], a[8], a[9], a[10], a[13]
+        es = _ES[dt]
+        M = N * H * W
+        K = ks * ks * Cin
+        return es * (M * Cin + M * Cout) + 4 * Cout * K, 2 * M * K * Cout
+    if name == "rod_bn_stats":
+        M, C, dt = a[1], a[2], a[11]
+        return _ES[dt] * M * C, 3 * M * C
+    if name == "rod_bn_apply":
+        M, C, dt = a[7], a[8], a[13]
+        res = a[5] is not None
+        return _ES[dt] * M * C * (3 if res else 2), 5 * M * C
+    if name == "rod_bn_bwd":
+        M, C, dt = a[10], a[11], a[16]
+        return _ES[dt] * M * C * 5, 16 * M * C
+    if name == "rod_match_anchors":
+        B, A, G = a[12], a[13], a[14]
+        return B * A * 56 + A * 32 + B * G * 20, 15 * G * A * B
+    return 0, 0

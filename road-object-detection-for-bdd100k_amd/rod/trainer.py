@@ -1,0 +1,77 @@
+"""One training step of the reference's train.py hot loop (train.py:97-135, 250-327 REFINE;
+140-249 ALL), on librod kernels:
+
+  normalise -> corner->centre -> anchor matching (per image, batched on the GPU) ->
+  network forward -> refine loss (+ det/clf loss in ALL) -> backward -> [DP all-reduce]
+  -> SGD with clip-by-value.
+
+Data-parallel: one process per GPU, the per-image batch sharded across ranks; the
+flat gradient buffer is all-reduced (sum) over RCCL and losses are normalised by the
+GLOBAL batch so the sum equals the single-process gradient (the reference divides by
+bs, net_tools.py:513).  Clipping happens after the reduction (net_tools.py:649).
+BatchNorm statistics are per rank (documented deviation).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import config
+from nets.catch_net import CatchNet, factory
+from rod import ops
+from utils import net_tools
+from utils.common_tools import cornerBboxes_2_centerBboxes
+
+
+class Trainer:
+    def __init__(self, img_size, batch_size, dtype=torch.bfloat16, train_range=config.train_range.REFINE,
+                 learning_rate=1e-3, device='cuda', fix_refine=True, seed=0, world_size=1, reducer=None):
+        self.img_size = tuple(img_size)
+        self.batch_size = batch_size          # per-rank batch
+        self.world_size = world_size
+        self.dtype = dtype
+        self.device = torch.device(device)
+        config.img_size = self.img_size       # init_anchor reads config.img_size (net_tools.py:37-38)
+        self.config_dict = {'train_range': train_range,
+                            'process_backbone_method': config.process_backbone_method.NONE,
+                            'deconv_method': config.deconv_method.LEARN_HALF,
+                            'merge_method': config.merge_method.ADD}
+        self.net = CatchNet('mobilenet_v2', self.config_dict, self.device, seed)
+        layer_n = len(config.extract_feat_name['mobilenet_v2'])
+        self.anchors = net_tools.anchors_all_layer(self.img_size, config.feat_sizes(self.img_size),
+                                                   net_tools.init_anchor(layer_n))
+        self.table = net_tools.anchor_table(self.anchors, self.device)
+        store = self.net.store
+        if train_range is config.train_range.ALL and fix_refine:
+            import re
+            pat = re.compile(r'^((?!(backbone|refine)).)*$')   # train.py:160-163
+            store.set_trainable(lambda n: bool(pat.match(n)))
+        self.opt = net_tools.optimizer(store, batch_size * world_size, learning_rate)
+        self.reducer = reducer
+        self.train_range = train_range
+        self.fix_refine = fix_refine
+
+    def step(self, img_u8, gt_corner, gt_labels, gt_n):
+        x = ops.normalize_image(img_u8, self.dtype)                 # (2/255)x - 1
+        center = cornerBboxes_2_centerBboxes(gt_corner)              # train.py:109
+        tg = net_tools.refine_groundtruth(self.anchors, center, gt_labels, config.refine_method.JACCARD_BIGGER,
+                                          n_boxes=gt_n)
+        out = factory(x, 'mobilenet_v2', True, self.config_dict, self.dtype, net=self.net).get_output()
+        scale = float(self.batch_size * self.world_size)
+        if self.train_range is config.train_range.REFINE:
+            loss = net_tools.refine_loss(out, tg[0], tg[3], targets=tg, scale=scale)
+            losses = (loss,)
+        else:
+            refine_out, det_out, clf_out = out
+            r_loss = net_tools.refine_loss(refine_out, tg[0], tg[3], targets=tg, scale=scale)
+            det_gt, det_mask, det_lbl, iou = net_tools.det_groundtruth(refine_out, tg[0], tg[1], tg[2], tg[3],
+                                                                      self.anchors, targets=tg)
+            d_loss, c_loss = net_tools.det_clf_loss(refine_out, clf_out, det_out, det_gt, det_mask, det_lbl, iou,
+                                                    scale=scale)
+            loss = d_loss + c_loss if self.fix_refine else r_loss + d_loss + c_loss
+            losses = (loss, r_loss, d_loss, c_loss)
+        loss.backward()
+        if self.reducer is not None:
+            self.reducer(self.net.store.flat_grad)
+        self.opt.step()
+        return losses

@@ -1,0 +1,211 @@
+"""Targets, losses, optimiser and post-processing — drop-in for the reference's
+utils/net_tools.py (lines 1-758).  Host-side anchor tables are numpy exactly as in the
+reference; everything per-anchor / per-pixel runs as librod kernels on the GPU.
+
+Batched API: where the reference works on one image inside the TF input pipeline
+(refine_groundtruth), these functions take a batch [B, G, 4] plus the number of valid
+boxes per image, and return per-layer views shaped like the reference's batched
+tensors ([B, fh, fw, A, 4] / [B, fh, fw, A, 1]).
+"""
+from __future__ import annotations
+
+import collections
+import math
+
+import numpy as np
+import torch
+
+import config
+from rod import ops
+
+
+# ================================================================ anchors (host, numpy)
+def init_anchor(n_layers):
+    """Anchor (height, width) in pixels of config.img_size per layer (net_tools.py:21-82)."""
+    boxes = collections.OrderedDict()
+    lo, hi = config.normal_anchor_range
+    step = (hi - lo) / (n_layers - 1)
+    range_min, range_max = lo, lo + step
+    H, W = config.img_size[0], config.img_size[1]
+    r3 = math.sqrt(3)
+    for i in range(n_layers):
+        if i == 0:
+            scales = list(config.special_anchor_range)
+        else:
+            scales = [range_min, (2 * range_min + range_max) / 3, (range_min + 2 * range_max) / 3]
+            range_min, range_max = range_max, range_max + step
+        rows = []
+        for s in scales:
+            rows += [[s * H, s * W], [s * H / r3, s * W * r3], [s * H * r3, s * W / r3]]
+        a = np.array(rows)
+        a[:, 0] = np.minimum(a[:, 0], H)
+        a[:, 1] = np.minimum(a[:, 1], W)
+        boxes['layer_%d' % (i + 1)] = a
+    return boxes
+
+
+def n_anchor_each_layer(backbone_name):
+    assert backbone_name in list(config.extract_feat_name.keys())
+    return [v.shape[0] for v in init_anchor(len(config.extract_feat_name[backbone_name])).values()]
+
+
+def anchors_one_layer(img_shape, feat_shape, anchors_one_layer, dtype=np.float32):
+    """(yc [fh,fw,1], xc [fh,fw,1], h [A], w [A]) normalised (net_tools.py:98-122)."""
+    y, x = np.mgrid[0:feat_shape[0], 0:feat_shape[1]]
+    xc = (x + 0.5) / feat_shape[1]
+    yc = (y + 0.5) / feat_shape[0]
+    h = anchors_one_layer[:, 0] / img_shape[0]
+    w = anchors_one_layer[:, 1] / img_shape[1]
+    return (yc[..., None].astype(dtype), xc[..., None].astype(dtype), h.astype(dtype), w.astype(dtype))
+
+
+def anchors_all_layer(img_shape, feats_shape, anchors_all_layer):
+    return [list(anchors_one_layer(img_shape, feats_shape[k], v)) for k, v in anchors_all_layer.items()]
+
+
+class AnchorTable:
+    """Flattened anchors of all layers in (fh, fw, A) order, on the device.
+
+    corner = (ymin, xmin, ymax, xmax) = (yref - href/2., ...) in float32 and
+    center = ((ymax+ymin)/2., (xmax+xmin)/2., ymax-ymin, xmax-xmin) from those corners,
+    both exactly as numpy computes them in net_tools.py:156-171 / 385-395.
+    """
+
+    def __init__(self, anchors_all, device):
+        corners, centers, off = [], [], [0]
+        self.shapes = []
+        for yref, xref, href, wref in anchors_all:
+            ymin = yref - href / 2.
+            xmin = xref - wref / 2.
+            ymax = yref + href / 2.
+            xmax = xref + wref / 2.
+            ymin, xmin, ymax, xmax = (np.float32(v) for v in (ymin, xmin, ymax, xmax))
+            cy = (ymax + ymin) / 2.
+            cx = (xmax + xmin) / 2.
+            h = ymax - ymin
+            w = xmax - xmin
+            fh, fw, A = ymin.shape
+            self.shapes.append((fh, fw, A))
+            corners.append(np.stack([ymin, xmin, ymax, xmax], -1).reshape(-1, 4))
+            centers.append(np.stack([cy, cx, h, w], -1).reshape(-1, 4))
+            off.append(off[-1] + fh * fw * A)
+        self.corner_np = np.ascontiguousarray(np.concatenate(corners).astype(np.float32))
+        self.center_np = np.ascontiguousarray(np.concatenate(centers).astype(np.float32))
+        self.lvl_off = np.array(off, dtype=np.int32)
+        self.A = int(off[-1])
+        self.corner = torch.from_numpy(self.corner_np).to(device)
+        self.center = torch.from_numpy(self.center_np).to(device)
+
+    def split(self, t: torch.Tensor, k):
+        """[B, A_total, ...] -> list of per-layer views [B, fh, fw, A(, k)]."""
+        outs = []
+        for l, (fh, fw, A) in enumerate(self.shapes):
+            v = t[:, self.lvl_off[l]:self.lvl_off[l + 1]]
+            outs.append(v.view(t.shape[0], fh, fw, A, *([k] if k else [])) if v.is_contiguous()
+                        else v.unflatten(1, (fh, fw, A)))
+        return outs
+
+
+_TABLES = {}
+
+
+def anchor_table(anchors_all, device) -> AnchorTable:
+    key = (id(anchors_all), str(device))
+    if key not in _TABLES:
+        _TABLES[key] = (anchors_all, AnchorTable(anchors_all, device))
+    return _TABLES[key][1]
+
+
+# ================================================================ targets
+def refine_groundtruth(anchors_all_layer, center_bboxes, labels, method, n_boxes=None, scope="refine_encode"):
+    """JACCARD_BIGGER target assignment (net_tools.py:270-428) on the GPU.
+
+    center_bboxes: [B, G, 4] (or [G, 4]) (yc, xc, h, w); labels [B, G]; n_boxes [B]
+    valid boxes per image (default: G).  Returns (gt_list, cbboxes_list, labels_list,
+    pos_mask_list) of per-layer views [B, fh, fw, A, 4|1].
+    """
+    if method == config.refine_method.NEAREST_NEIGHBOR:
+        raise ValueError('NEAREST_NEIGHBOR matching is not on the hot path (DESIGN.md, out of scope)')
+    if method == config.refine_method.JACCARD_TOPK:
+        raise ValueError('Not support now')
+    if method != config.refine_method.JACCARD_BIGGER:
+        raise ValueError('Function parameter "method" wrong')
+    single = center_bboxes.dim() == 2
+    if single:
+        center_bboxes, labels = center_bboxes[None], labels[None]
+    B, G, _ = center_bboxes.shape
+    dev = center_bboxes.device
+    if n_boxes is None:
+        n_boxes = torch.full((B,), G, dtype=torch.int32, device=dev)
+    tab = anchor_table(anchors_all_layer, dev)
+    off, cbox, lbl, pos = ops.match_anchors(tab.corner, tab.center, tab.lvl_off,
+                                            config.refine_pos_jac_val_all_layers[:len(tab.shapes)],
+                                            center_bboxes.float(), labels.to(torch.int32),
+                                            n_boxes.to(torch.int32))
+    res = (tab.split(off, 4), tab.split(cbox, 4), tab.split(lbl[..., None], 1), tab.split(pos[..., None], 1))
+    res = RefineTargets(*res)
+    res.flat = (off, cbox, lbl, pos)
+    res.table = tab
+    return res
+
+
+class RefineTargets(tuple):
+    """(gt_list, cbboxes_list, labels_list, pos_mask_list) + the concatenated buffers."""
+
+    def __new__(cls, *parts):
+        return super().__new__(cls, parts)
+
+
+# ================================================================ losses
+def smooth_l1(x):
+    raise NotImplementedError('smooth_l1 is fused into refine_loss / det_clf_loss kernels')
+
+
+def refine_loss(refine_out, refine_groundtruth, refine_pos_mask, dtype=torch.float32, targets=None, scale=None):
+    """sum_l sum smooth_l1((gt - out) * mask) / bs (net_tools.py:492-516).
+
+    `targets` (the RefineTargets returned by refine_groundtruth) lets the kernel read
+    the concatenated target buffers directly; otherwise the per-layer lists are used.
+    `scale` overrides bs (data-parallel runs divide by the global batch).
+    Returns the scalar loss tensor; the per-layer values (the reference's
+    "layer_%d_each_sample" summaries) are left in refine_loss.last_per_layer.
+    """
+    B = refine_out[0].shape[0]
+    scale = float(B) if scale is None else float(scale)
+    pred = ops.levels_concat(refine_out, 4)
+    if targets is not None:
+        gt_flat, _, _, pos_flat = targets.flat
+        lvl_off = targets.table.lvl_off
+    else:
+        gt_flat = ops.levels_concat([g.contiguous() for g in refine_groundtruth], 4).float()
+        pos_flat = ops.levels_concat([m.contiguous() for m in refine_pos_mask], 1).view(B, -1)
+        sizes = [g[0].numel() // 4 for g in refine_groundtruth]
+        lvl_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    vec = ops.smooth_l1_masked(pred, gt_flat, pos_flat, lvl_off, scale)
+    refine_loss.last_per_layer = vec
+    return vec[len(lvl_off) - 1]
+
+
+# ================================================================ optimiser
+class optimizer(object):
+    """Plain SGD, clip-by-value +-5, undecayed learning rate (net_tools.py:626-654).
+
+    The exponential decay the reference builds is only logged (net_tools.py:638-641,
+    quirk 1 in SURVEY); `decayed_lr(step)` reproduces that logged value.
+    """
+
+    def __init__(self, store, batch_szie, learning_rate=1e-3, fix_learning_rate=True, clip=5.0):
+        self.store = store
+        self.lr = float(learning_rate)
+        self.batch_size = batch_szie
+        self.fix = fix_learning_rate
+        self.clip = clip
+        self.global_step = 0
+
+    def decayed_lr(self, step=None):
+        step = self.global_step if step is None else step
+        return self.lr * 0.97 ** (step // (20000 / self.batch_size))
+
+    def step(self):
+        ops.sgd_clip_(self.store.flat, self.store.flat_grad, self.lr, self.clip)
+        self.global_step += 1

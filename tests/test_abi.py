@@ -1,0 +1,41 @@
+"""The C-ABI library loads and exports every symbol include/rod.h declares (CPU-only:
+no kernel is launched; argument validation paths return before any HIP call)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from rod import _abi
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.lib()
+    protos = _abi.parse_header()
+    assert len(protos) >= 20
+    for name in protos:
+        assert hasattr(lib, name), name
+    nm = ctypes.CDLL(_abi.LIB_PATH)
+    for name in protos:
+        getattr(nm, name)
+
+
+def test_abi_version():
+    assert _abi.lib().rod_abi_version() == 1
+
+
+def test_invalid_arguments_raise_with_message():
+    with pytest.raises(RuntimeError, match='bad shape'):
+        _abi.call('rod_dw3x3_fwd', None, None, None, 0, 8, 8, 8, 1, 1, 1, 8, 8, 0, None)
+    with pytest.raises(RuntimeError, match='ksize'):
+        _abi.call('rod_conv_fwd', None, None, None, None, 1, 4, 4, 8, 8, 5, 0, 0, 0, None)
+    with pytest.raises(RuntimeError, match='dtype'):
+        _abi.call('rod_conv_weight_prep', None, None, 8, 8, 1, 0, 7, None)
+    with pytest.raises(RuntimeError, match='offsets'):
+        _abi.call('rod_match_anchors', None, None, np.array([0, 5, 9], np.int32), np.zeros(2, np.float32), 2,
+                  None, None, None, None, None, None, None, 1, 10, 4, None)
+
+
+def test_workspace_queries_are_host_only():
+    assert _abi.query('rod_bn_stats_workspace', 1000, 64) > 0
+    assert _abi.query('rod_conv_wgrad_workspace', 2, 16, 16, 32, 64, 3) >= 4 * 64 * 9 * 32
+    assert _abi.query('rod_dw3x3_bwd_filter_workspace', 2, 8, 8, 96) >= 4 * 9 * 96

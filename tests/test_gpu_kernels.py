@@ -1,0 +1,233 @@
+"""Kernel parity: librod (HIP, cuda:0) against the CPU oracle on seeded inputs.
+
+Tolerances: fp32 storage 1e-4 relative (north_star) with a small absolute floor for
+values that cancel; bf16 storage is compared against the fp32 oracle at bf16 resolution.
+Integer outputs (positive masks, labels, argmax-selected boxes) are compared bit-exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+import config
+from oracle import anchors as oa
+from oracle import net as onet
+from oracle import targets as ot
+from rod import ops
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: dict(rtol=1e-4, atol=1e-5), torch.bfloat16: dict(rtol=2e-2, atol=2e-2)}
+
+
+def _close(a, b, dtype, scale=1.0, **kw):
+    tol = dict(TOL[dtype])
+    tol['atol'] = tol['atol'] * scale
+    tol.update(kw)
+    torch.testing.assert_close(a.detach().float().cpu(), b.detach().float().cpu(), **tol)
+
+
+def _param(t, dev):
+    p = t.detach().clone().to(dev).requires_grad_(True)
+    p._rod_grad = torch.zeros_like(p)
+    return p
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('C', [24, 6])
+@pytest.mark.parametrize('stride,H,W', [(1, 13, 17), (2, 13, 17), (2, 12, 16), (1, 4, 5)])
+def test_depthwise(dev, dtype, C, stride, H, W):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, H, W, C, generator=g)
+    w = torch.randn(3, 3, C, generator=g) * 0.3
+    xo = x.clone().requires_grad_(True)
+    wo = w.clone().requires_grad_(True)
+    yo = onet.dwconv(xo.permute(0, 3, 1, 2), wo, stride).permute(0, 2, 3, 1)
+    gy = torch.randn(yo.shape, generator=g)
+    (yo * gy).sum().backward()
+
+    xd = x.to(dev, dtype).requires_grad_(True)
+    wd = _param(w, dev)
+    yd = ops.dw3x3(xd, wd, stride)
+    assert yd.shape == yo.shape
+    yd.backward(gy.to(dev, dtype))
+    ref_x = xo.detach() if dtype == torch.float32 else xo.detach().to(torch.bfloat16).float()
+    _close(yd, yo, dtype, scale=3)
+    _close(xd.grad, xo.grad, dtype, scale=3)
+    _close(wd._rod_grad, wo.grad, dtype, scale=10 if dtype == torch.bfloat16 else 3)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('ks,Cin,Cout', [(1, 16, 96), (1, 96, 24), (1, 64, 128), (1, 40, 66), (3, 3, 32),
+                                         (3, 128, 128), (3, 24, 24), (3, 99, 99), (1, 320, 1920)])
+def test_conv(dev, dtype, ks, Cin, Cout):
+    g = torch.Generator().manual_seed(2)
+    N, H, W = 2, 7, 11
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(Cout, ks, ks, Cin, generator=g) / np.sqrt(ks * ks * Cin)
+    b = torch.randn(Cout, generator=g) * 0.1
+    if dtype == torch.bfloat16:  # compare against the oracle on the bf16-rounded operands
+        x = x.to(torch.bfloat16).float()
+        w = w.to(torch.bfloat16).float()
+    xo = x.clone().requires_grad_(True)
+    wo = w.clone().requires_grad_(True)
+    bo = b.clone().requires_grad_(True)
+    yo = onet.conv(xo.permute(0, 3, 1, 2), wo, bo).permute(0, 2, 3, 1)
+    gy = torch.randn(yo.shape, generator=g)
+    if dtype == torch.bfloat16:
+        gy = gy.to(torch.bfloat16).float()
+    (yo * gy).sum().backward()
+
+    xd = x.to(dev, dtype).requires_grad_(True)
+    wd, bd = _param(w, dev), _param(b, dev)
+    yd = ops.conv2d(xd, wd, bd, ks)
+    yd.backward(gy.to(dev, dtype))
+    _close(yd, yo, dtype, scale=5)
+    _close(xd.grad, xo.grad, dtype, scale=5)
+    _close(wd._rod_grad, wo.grad, dtype, scale=20, rtol=1e-4 if dtype == torch.float32 else 2e-2)
+    _close(bd._rod_grad, bo.grad, dtype, scale=20)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('act', [ops.ROD_ACT_NONE, ops.ROD_ACT_RELU6, ops.ROD_ACT_LEAKY])
+@pytest.mark.parametrize('C,gamma,res', [(32, True, False), (24, True, True), (20, False, False), (66, False, False)])
+def test_batchnorm(dev, dtype, act, C, gamma, res):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(3, 9, 10, C, generator=g) * 2 + 3  # non-zero mean exercises the pivot
+    if dtype == torch.bfloat16:
+        x = x.to(torch.bfloat16).float()
+    ga = torch.rand(C, generator=g) + 0.5 if gamma else None
+    be = torch.randn(C, generator=g) * 0.2
+    r = torch.randn(x.shape, generator=g) if res else None
+    if r is not None and dtype == torch.bfloat16:
+        r = r.to(torch.bfloat16).float()
+    mm = torch.randn(C, generator=g) * 0.1
+    mv = torch.rand(C, generator=g) + 0.5
+    decay = 0.997
+
+    xo = x.clone().requires_grad_(True)
+    gao = ga.clone().requires_grad_(True) if gamma else None
+    beo = be.clone().requires_grad_(True)
+    mov = {}
+    yo = onet.batch_norm(xo.permute(0, 3, 1, 2), gao, beo, mm, mv, True, decay, 1e-3, mov, 'bn')
+    yo = {ops.ROD_ACT_NONE: lambda t: t, ops.ROD_ACT_RELU6: onet.relu6, ops.ROD_ACT_LEAKY: onet.leaky}[act](yo)
+    yo = yo.permute(0, 2, 3, 1)
+    if res:
+        yo = yo + r
+    gy = torch.randn(yo.shape, generator=g)
+    if dtype == torch.bfloat16:
+        gy = gy.to(torch.bfloat16).float()
+    (yo * gy).sum().backward()
+
+    xd = x.to(dev, dtype).requires_grad_(True)
+    gad = _param(ga, dev) if gamma else None
+    bed = _param(be, dev)
+    mmd, mvd = mm.clone().to(dev), mv.clone().to(dev)
+    rd = r.to(dev, dtype).requires_grad_(True) if res else None
+    yd = ops.bn_act(xd, gad, bed, mmd, mvd, act, True, decay, 1e-3, rd)
+    yd.backward(gy.to(dev, dtype))
+    _close(yd, yo, dtype, scale=5)
+    _close(mmd, mov['bn/moving_mean'], torch.float32)
+    _close(mvd, mov['bn/moving_variance'], torch.float32)
+    _close(xd.grad, xo.grad, dtype, scale=5)
+    _close(bed._rod_grad, beo.grad, dtype, scale=50, rtol=1e-4 if dtype == torch.float32 else 3e-2)
+    if gamma:
+        _close(gad._rod_grad, gao.grad, dtype, scale=50, rtol=1e-4 if dtype == torch.float32 else 3e-2)
+    if res:
+        _close(rd.grad, gy, dtype)
+
+    # inference: moving statistics
+    with torch.no_grad():
+        ye = ops.bn_act(x.to(dev, dtype), gad, bed, mmd, mvd, act, False, decay)
+        yeo = onet.batch_norm(x.permute(0, 3, 1, 2), ga, be, mmd.cpu(), mvd.cpu(), False, decay)
+        yeo = {ops.ROD_ACT_NONE: lambda t: t, ops.ROD_ACT_RELU6: onet.relu6, ops.ROD_ACT_LEAKY: onet.leaky}[act](
+            yeo).permute(0, 2, 3, 1)
+    _close(ye, yeo, dtype, scale=5)
+
+
+def _anchors(H, W):
+    init = oa.init_anchor(6, (H, W))
+    chain = oa.feat_sizes((H, W), [s for (_, s, _, _, _) in onet.SPEC])
+    return [oa.anchors_one_layer((H, W), chain[t - 1], init[i]) for i, t in enumerate(onet.TAPS)]
+
+
+def _random_gt(rng, B, G, degenerate=False):
+    n = rng.integers(1, G + 1, size=B)
+    n[0] = G
+    cy = rng.uniform(0.05, 0.95, (B, G))
+    cx = rng.uniform(0.05, 0.95, (B, G))
+    h = np.exp(rng.uniform(np.log(0.01), np.log(0.6), (B, G)))
+    w = np.exp(rng.uniform(np.log(0.01), np.log(0.6), (B, G)))
+    corner = np.stack([cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2], -1).clip(0, 1).astype(np.float32)
+    if degenerate:
+        corner[1, 0, 2] = corner[1, 0, 0]  # zero-height box in image 1
+    labels = rng.choice([1, 2, 3, 4, 6, 8, 10], size=(B, G)).astype(np.int32)
+    return corner, labels, n.astype(np.int32)
+
+
+@pytest.mark.parametrize('H,W,degenerate', [(300, 300, False), (418, 418, False), (300, 300, True)])
+def test_match_anchors_bit_exact(dev, H, W, degenerate):
+    from utils import net_tools as nt
+    import utils.common_tools as ct
+    rng = np.random.default_rng(7)
+    B, G = 3, 24
+    corner, labels, n = _random_gt(rng, B, G, degenerate)
+    anchors = _anchors(H, W)
+    center_d = ct.cornerBboxes_2_centerBboxes(torch.from_numpy(corner).to(dev))
+    center_o = ot.corner_to_center(corner)
+    np.testing.assert_array_equal(center_d.cpu().numpy(), center_o)  # box conversion is bit-exact
+    res = nt.refine_groundtruth(anchors, center_d, torch.from_numpy(labels).to(dev), config.refine_method.JACCARD_BIGGER,
+                                n_boxes=torch.from_numpy(n).to(dev))
+    gt_l, cb_l, lb_l, pm_l = res
+    total_pos = 0
+    for b in range(B):
+        og, oc, ol, op = ot.refine_groundtruth(anchors, center_o[b, :n[b]], labels[b, :n[b]],
+                                               config.refine_pos_jac_val_all_layers)
+        for l in range(6):
+            np.testing.assert_array_equal(pm_l[l][b].cpu().numpy(), op[l])
+            np.testing.assert_array_equal(lb_l[l][b].cpu().numpy(), ol[l])
+            np.testing.assert_array_equal(cb_l[l][b].cpu().numpy(), oc[l])
+            np.testing.assert_array_equal(gt_l[l][b].cpu().numpy(), og[l])  # incl. NaN positions
+            total_pos += int(op[l].sum())
+    assert total_pos > 50
+
+
+def test_refine_loss(dev):
+    from utils import net_tools as nt
+    rng = np.random.default_rng(11)
+    H = W = 300
+    B, G = 2, 16
+    corner, labels, n = _random_gt(rng, B, G)
+    anchors = _anchors(H, W)
+    center = torch.from_numpy(ot.corner_to_center(corner)).to(dev)
+    tg = nt.refine_groundtruth(anchors, center, torch.from_numpy(labels).to(dev), config.refine_method.JACCARD_BIGGER,
+                               n_boxes=torch.from_numpy(n).to(dev))
+    g = torch.Generator().manual_seed(5)
+    outs = [torch.randn(B, *a[0].shape[:2], a[2].shape[0], 4, generator=g) for a in anchors]
+    outs_d = [o.to(dev).requires_grad_(True) for o in outs]
+    loss = nt.refine_loss(outs_d, tg[0], tg[3], targets=tg)
+    loss.backward()
+    gts = [t.cpu().numpy() for t in tg[0]]
+    pms = [t.cpu().numpy() for t in tg[3]]
+    per, tot = ot.refine_loss([o.numpy() for o in outs], gts, pms, B)
+    np.testing.assert_allclose(nt.refine_loss.last_per_layer[:6].cpu().numpy(), per, rtol=1e-5)
+    np.testing.assert_allclose(loss.item(), tot, rtol=1e-5)
+    grads = ot.refine_loss_grad([o.numpy() for o in outs], gts, pms, B)
+    for gd, go in zip(outs_d, grads):
+        np.testing.assert_allclose(gd.grad.cpu().numpy(), go, rtol=1e-6, atol=1e-7)
+    # the per-layer list path gives the same loss
+    loss2 = nt.refine_loss([o.detach() for o in outs_d], tg[0], tg[3])
+    assert loss2.item() == loss.item()
+
+
+def test_sgd_clip_and_normalize(dev):
+    g = torch.Generator().manual_seed(9)
+    p = torch.randn(1003, generator=g)
+    gr = torch.randn(1003, generator=g) * 10
+    pd, gd = p.to(dev), gr.to(dev)
+    ops.sgd_clip_(pd, gd, 1e-2, 5.0)
+    ref = (p.numpy() - np.float32(1e-2) * np.clip(gr.numpy(), -5, 5)).astype(np.float32)
+    np.testing.assert_array_equal(pd.cpu().numpy(), ref)
+    img = torch.randint(0, 256, (2, 5, 7, 3), dtype=torch.uint8, generator=g)
+    out = ops.normalize_image(img.to(dev))
+    k = np.float32(2.0 / 255.0)
+    np.testing.assert_array_equal(out.cpu().numpy(), k * img.numpy().astype(np.float32) - np.float32(1.0))

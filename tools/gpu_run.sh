@@ -1,0 +1,32 @@
+#!/bin/bash
+# GPU-box runner: each GPU step under its own timeout; stop at the first fault/abort/timeout
+# (exit 124/134/137/139 or signal), continue past ordinary test failures (exit 1).
+# usage: tools/gpu_run.sh <tag> <step>...   steps: tests smoke bench prof
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+TAG=$1; shift
+fatal() { case $1 in 124|134|137|139|130|143) return 0;; *) [ $1 -gt 128 ] && return 0; return 1;; esac; }
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/${TAG}_steps.log
+  timeout -k 10 $to "$@" > $OUT/${TAG}_${name}.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/${TAG}_steps.log
+  tail -5 $OUT/${TAG}_${name}.log
+  if fatal $rc; then echo "FATAL rc=$rc in $name; stopping"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
+    testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
+    benchfast) run benchfast 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
+echo ALLDONE
