@@ -24,6 +24,40 @@ int check_launch(const char* what) {
   return 0;
 }
 
+// ---------------------------------------------------------------- slab reduction
+__global__ void __launch_bounds__(256) slab_sum_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                       int nslab, long n) {
+  __shared__ double red[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const long i = (long)blockIdx.x * 32 + tx;
+  double s = 0.0;
+  if (i < n)
+    for (int b = ty; b < nslab; b += 8) s += (double)slab[(long)b * n + i];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && i < n) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][tx];
+    out[i] = (float)t;
+  }
+}
+
+void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(cdivl(n, 32)), dim3(256), 0, s, slab, out, nslab, n);
+}
+
+int const_channel_blocks(int CV, long total, int target) {
+  // smallest block count step s with (s*256) % CV == 0
+  int g = CV, b = 256;
+  while (b) { int t = g % b; g = b; b = t; }  // gcd(CV, 256)
+  const int step = CV / g;
+  long want = std::min<long>(target, cdivl(total, 256));
+  long blocks = std::max<long>(1, cdivl(want, step)) * step;
+  return (int)blocks;
+}
+
 // ---------------------------------------------------------------- kernels
 template <typename T>
 __global__ void normalize_image_kernel(const uint8_t* __restrict__ img, T* __restrict__ out, long n) {

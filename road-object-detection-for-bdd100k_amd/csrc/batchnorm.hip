@@ -7,6 +7,11 @@
 // from the data), so E[(x-k)^2] - E[x-k]^2 does not cancel catastrophically; per-block
 // partial sums go to a slab [nblk][2][C] and are combined in f64 by a finalize kernel
 // (deterministic, no atomics).
+//
+// Elementwise passes (apply, backward-apply) are HBM streams: each thread keeps ONE
+// 16-byte channel vector for the whole grid-stride loop (grid*256 is a multiple of the
+// channel-vector count), so the per-channel parameters live in registers and each
+// iteration is one 16-byte load per operand and one 16-byte store.
 #include "rod_common.h"
 
 namespace rod {
@@ -40,12 +45,35 @@ static RedPlan red_plan(long M, int C, bool vec) {
   r.CV = C / r.V;
   r.CVp = std::min(p2(r.CV), 256);
   r.cgroups = cdiv(r.CV, r.CVp);
-  long want = std::max<long>(1, 1024 / r.cgroups);
+  long want = std::max<long>(1, 512 / r.cgroups);
   long lanes = 256 / r.CVp;
   long chunk = std::max<long>(cdivl(M, want), lanes * 16);
   r.chunk = chunk;
   r.nbx = (int)cdivl(M, chunk);
   return r;
+}
+
+template <typename T, bool VEC>
+__device__ __forceinline__ void load_v(const T* p, float (&out)[VEC ? Vec16<T>::N : 1]) {
+  if constexpr (VEC) {
+    Vec16<T> a;
+    a.load(p);
+#pragma unroll
+    for (int v = 0; v < Vec16<T>::N; ++v) out[v] = a.get(v);
+  } else {
+    out[0] = to_f32(p[0]);
+  }
+}
+template <typename T, bool VEC>
+__device__ __forceinline__ void store_v(T* p, const float (&in)[VEC ? Vec16<T>::N : 1]) {
+  if constexpr (VEC) {
+    Vec16<T> a;
+#pragma unroll
+    for (int v = 0; v < Vec16<T>::N; ++v) a.set(v, in[v]);
+    a.store(p);
+  } else {
+    p[0] = from_f32<T>(in[0]);
+  }
 }
 
 // ---------------------------------------------------------------- statistics
@@ -67,29 +95,15 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
 #pragma unroll
   for (int v = 0; v < V; ++v) s1[v] = s2[v] = 0.f;
   if (active) {
-    if constexpr (VEC) {
-      Vec16<T> kv;
-      kv.load(x + c);
-#pragma unroll
-      for (int v = 0; v < V; ++v) k[v] = kv.get(v);
-    } else {
-      k[0] = to_f32(x[c]);
-    }
+    load_v<T, VEC>(x + c, k);
     for (long r = r0 + pln; r < r1; r += lanes) {
-      const T* p = x + r * ldx + c;
-      if constexpr (VEC) {
-        Vec16<T> vv;
-        vv.load(p);
+      float xv[V];
+      load_v<T, VEC>(x + r * ldx + c, xv);
 #pragma unroll
-        for (int v = 0; v < V; ++v) {
-          float d = vv.get(v) - k[v];
-          s1[v] += d;
-          s2[v] = fmaf(d, d, s2[v]);
-        }
-      } else {
-        float d = to_f32(p[0]) - k[0];
-        s1[0] += d;
-        s2[0] = fmaf(d, d, s2[0]);
+      for (int v = 0; v < V; ++v) {
+        const float d = xv[v] - k[v];
+        s1[v] += d;
+        s2[v] = fmaf(d, d, s2[v]);
       }
     }
   }
@@ -118,18 +132,41 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
   }
 }
 
-template <typename T>
-__global__ void bn_stats_finalize_kernel(const T* __restrict__ x, const float* __restrict__ slab, int nblk, long M,
-                                         int C, float eps, float decay, float* __restrict__ mean,
-                                         float* __restrict__ rstd, float* __restrict__ mmean,
-                                         float* __restrict__ mvar) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// sum the two slab rows of 32 channels with 8 lanes each (f64), block = 256 threads
+__device__ __forceinline__ void slab2_sum(const float* __restrict__ slab, int nblk, int C, int c, bool ok, double& a,
+                                          double& b) {
+  __shared__ double red[2][8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s1 += (double)slab[((long)b * 2 + 0) * C + c];
-    s2 += (double)slab[((long)b * 2 + 1) * C + c];
+  if (ok)
+    for (int k = ty; k < nblk; k += 8) {
+      s1 += (double)slab[((long)k * 2 + 0) * C + c];
+      s2 += (double)slab[((long)k * 2 + 1) * C + c];
+    }
+  red[0][ty][tx] = s1;
+  red[1][ty][tx] = s2;
+  __syncthreads();
+  a = b = 0.0;
+  if (ty == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a += red[0][k][tx];
+      b += red[1][k][tx];
+    }
   }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_finalize_kernel(const T* __restrict__ x,
+                                                                const float* __restrict__ slab, int nblk, long M,
+                                                                int C, float eps, float decay,
+                                                                float* __restrict__ mean, float* __restrict__ rstd,
+                                                                float* __restrict__ mmean, float* __restrict__ mvar) {
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool ok = c < C;
+  double s1, s2;
+  slab2_sum(slab, nblk, C, c, ok, s1, s2);
+  if ((threadIdx.x >> 5) != 0 || !ok) return;
   const double k = (double)to_f32(x[c]);
   const double m = s1 / (double)M;
   double var = s2 / (double)M - m * m;
@@ -156,7 +193,7 @@ __global__ void bn_eval_stats_kernel(const float* __restrict__ mm, const float* 
 }
 
 // ---------------------------------------------------------------- apply
-template <typename T, bool VEC>
+template <typename T, bool VEC, bool RES>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd,
                                                        const float* __restrict__ gamma,
@@ -165,44 +202,29 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
                                                        int act) {
   constexpr int V = VEC ? Vec16<T>::N : 1;
   const int CV = C / V;
-  const long total = M * CV;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long r = t / CV;
-    const int c = (int)(t - r * CV) * V;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;  // multiple of CV
+  const int c = (int)(t0 % CV) * V;
+  const long rstep = stride / CV;
+  float mu[V], sc[V], be[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    mu[v] = mean[c + v];
+    sc[v] = gamma ? rstd[c + v] * gamma[c + v] : rstd[c + v];  // rsqrt(var+eps)*scale
+    be[v] = beta ? beta[c + v] : 0.f;
+  }
+  for (long r = t0 / CV; r < M; r += rstep) {
     float xv[V], rv[V];
-    if constexpr (VEC) {
-      Vec16<T> a;
-      a.load(x + r * ldx + c);
-#pragma unroll
-      for (int v = 0; v < V; ++v) xv[v] = a.get(v);
-      if (res) {
-        Vec16<T> b;
-        b.load(res + r * ldr + c);
-#pragma unroll
-        for (int v = 0; v < V; ++v) rv[v] = b.get(v);
-      }
-    } else {
-      xv[0] = to_f32(x[r * ldx + c]);
-      if (res) rv[0] = to_f32(res[r * ldr + c]);
-    }
-    Vec16<T> o;
-    float ov[V];
+    load_v<T, VEC>(x + r * ldx + c, xv);
+    if constexpr (RES) load_v<T, VEC>(res + r * ldr + c, rv);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      const float sc = gamma ? rstd[c + v] * gamma[c + v] : rstd[c + v];  // rsqrt(var+eps)*scale
-      const float b = beta ? beta[c + v] : 0.f;
-      float z = (xv[v] - mean[c + v]) * sc + b;
+      float z = (xv[v] - mu[v]) * sc[v] + be[v];
       z = act_fwd(z, act);
-      if (res) z = z + rv[v];
-      ov[v] = z;
+      if constexpr (RES) z = z + rv[v];
+      xv[v] = z;
     }
-    if constexpr (VEC) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) o.set(v, ov[v]);
-      o.store(y + r * ldy + c);
-    } else {
-      y[r * ldy + c] = from_f32<T>(ov[0]);
-    }
+    store_v<T, VEC>(y + r * ldy + c, xv);
   }
 }
 
@@ -239,19 +261,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
     }
     for (long r = r0 + pln; r < r1; r += lanes) {
       float xv[V], gv[V];
-      if constexpr (VEC) {
-        Vec16<T> a, b;
-        a.load(x + r * ldx + c);
-        b.load(dy + r * lddy + c);
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          xv[v] = a.get(v);
-          gv[v] = b.get(v);
-        }
-      } else {
-        xv[0] = to_f32(x[r * ldx + c]);
-        gv[0] = to_f32(dy[r * lddy + c]);
-      }
+      load_v<T, VEC>(x + r * ldx + c, xv);
+      load_v<T, VEC>(dy + r * lddy + c, gv);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float d = xv[v] - mu[v];
@@ -287,17 +298,16 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ slab, int nblk, long M, int C,
-                                       const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ coef) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sg = 0.0, sgx = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    sg += (double)slab[((long)b * 2 + 0) * C + c];
-    sgx += (double)slab[((long)b * 2 + 1) * C + c];
-  }
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ slab, int nblk, long M, int C,
+                                                              const float* __restrict__ rstd,
+                                                              const float* __restrict__ gamma,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              float* __restrict__ coef) {
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool ok = c < C;
+  double sg, sgx;
+  slab2_sum(slab, nblk, C, c, ok, sg, sgx);
+  if ((threadIdx.x >> 5) != 0 || !ok) return;
   if (dbeta) dbeta[c] = (float)sg;
   if (dgamma) dgamma[c] = (float)sgx;
   coef[c] = gamma ? rstd[c] * gamma[c] : rstd[c];
@@ -315,43 +325,33 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
                                                            long M, int C, int lddy, int ldx, int lddx, int act) {
   constexpr int V = VEC ? Vec16<T>::N : 1;
   const int CV = C / V;
-  const long total = M * CV;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long r = t / CV;
-    const int c = (int)(t - r * CV) * V;
-    float xv[V], gv[V];
-    if constexpr (VEC) {
-      Vec16<T> a, b;
-      a.load(x + r * ldx + c);
-      b.load(dy + r * lddy + c);
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const int c = (int)(t0 % CV) * V;
+  const long rstep = stride / CV;
+  float mu[V], rs[V], sc[V], be[V], a[V], mg[V], mgx[V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        xv[v] = a.get(v);
-        gv[v] = b.get(v);
-      }
-    } else {
-      xv[0] = to_f32(x[r * ldx + c]);
-      gv[0] = to_f32(dy[r * lddy + c]);
-    }
-    float ov[V];
+  for (int v = 0; v < V; ++v) {
+    mu[v] = mean[c + v];
+    rs[v] = rstd[c + v];
+    sc[v] = gamma ? rs[v] * gamma[c + v] : rs[v];
+    be[v] = beta ? beta[c + v] : 0.f;
+    a[v] = coef[c + v];
+    mg[v] = coef[C + c + v];
+    mgx[v] = coef[2 * C + c + v];
+  }
+  for (long r = t0 / CV; r < M; r += rstep) {
+    float xv[V], gv[V];
+    load_v<T, VEC>(x + r * ldx + c, xv);
+    load_v<T, VEC>(dy + r * lddy + c, gv);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      const float rs = rstd[c + v];
-      const float sc = gamma ? rs * gamma[c + v] : rs;
-      const float d = xv[v] - mean[c + v];
-      const float z = d * sc + (beta ? beta[c + v] : 0.f);
+      const float d = xv[v] - mu[v];
+      const float z = d * sc[v] + be[v];
       const float g = gv[v] * act_grad(z, act);
-      const float xh = d * rs;
-      ov[v] = coef[c + v] * (g - coef[C + c + v] - xh * coef[2 * C + c + v]);
+      xv[v] = a[v] * (g - mg[v] - (d * rs[v]) * mgx[v]);
     }
-    if constexpr (VEC) {
-      Vec16<T> o;
-#pragma unroll
-      for (int v = 0; v < V; ++v) o.set(v, ov[v]);
-      o.store(dx + r * lddx + c);
-    } else {
-      dx[r * lddx + c] = from_f32<T>(ov[0]);
-    }
+    store_v<T, VEC>(dx + r * lddx + c, xv);
   }
 }
 
@@ -374,7 +374,63 @@ static int max_nbx(long M, int C) {
   return std::max(a, std::max(b, c));
 }
 
-static int ew_blocks(long vecs) { return (int)std::min<long>(cdivl(vecs, 256), 256L * 16); }
+template <typename T>
+static void apply_launch(bool vec, const void* x, const float* mean, const float* rstd, const float* gamma,
+                         const float* beta, const void* res, void* y, long M, int C, int ldx, int ldr, int ldy,
+                         int act, hipStream_t s) {
+  const int V = vec ? Vec16<T>::N : 1;
+  const int blocks = const_channel_blocks(C / V, M * (C / V));
+#define LA(VE, RE)                                                                                            \
+  hipLaunchKernelGGL((bn_apply_kernel<T, VE, RE>), dim3(blocks), dim3(256), 0, s, (const T*)x, mean, rstd, gamma, \
+                     beta, (const T*)res, (T*)y, M, C, ldx, ldr, ldy, act)
+  if (vec) {
+    if (res) LA(true, true); else LA(true, false);
+  } else {
+    if (res) LA(false, true); else LA(false, false);
+  }
+#undef LA
+}
+
+template <typename T>
+static void stats_launch(bool vec, const void* x, long M, int C, int ldx, float eps, float decay, float* mean,
+                         float* rstd, float* mm, float* mv, float* slab, hipStream_t s) {
+  RedPlan pl = red_plan<T>(M, C, vec);
+  dim3 grid(pl.nbx, pl.cgroups);
+  size_t lds = 2 * 256 * pl.V * sizeof(float);
+  if (vec)
+    hipLaunchKernelGGL((bn_stats_kernel<T, true>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp, pl.chunk,
+                       slab);
+  else
+    hipLaunchKernelGGL((bn_stats_kernel<T, false>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp,
+                       pl.chunk, slab);
+  hipLaunchKernelGGL(bn_stats_finalize_kernel<T>, dim3(cdiv(C, 32)), dim3(256), 0, s, (const T*)x,
+                     (const float*)slab, pl.nbx, M, C, eps, decay, mean, rstd, mm, mv);
+}
+
+template <typename T>
+static void bwd_launch(bool vec, const void* dy, const void* x, const float* mean, const float* rstd,
+                       const float* gamma, const float* beta, void* dx, float* dgamma, float* dbeta, float* slab,
+                       float* coef, long M, int C, int lddy, int ldx, int lddx, int act, hipStream_t s) {
+  RedPlan pl = red_plan<T>(M, C, vec);
+  dim3 grid(pl.nbx, pl.cgroups);
+  size_t lds = 2 * 256 * pl.V * sizeof(float);
+  if (vec)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x, mean,
+                       rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x, mean,
+                       rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 32)), dim3(256), 0, s, slab, pl.nbx, M, C, rstd, gamma,
+                     dgamma, dbeta, coef);
+  const int V = pl.V;
+  const int blocks = const_channel_blocks(C / V, M * (C / V));
+  if (vec)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dy, (const T*)x, mean,
+                       rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false>), dim3(blocks), dim3(256), 0, s, (const T*)dy, (const T*)x,
+                       mean, rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
+}
 
 }  // namespace rod
 
@@ -382,9 +438,7 @@ using namespace rod;
 
 extern "C" {
 
-size_t rod_bn_stats_workspace(long M, int C) {
-  return (size_t)max_nbx(M, C) * 2 * C * sizeof(float);
-}
+size_t rod_bn_stats_workspace(long M, int C) { return (size_t)max_nbx(M, C) * 2 * C * sizeof(float); }
 
 int rod_bn_stats(const void* x, long M, int C, int ldx, float eps, float decay, float* mean, float* rstd,
                  float* moving_mean, float* moving_var, void* workspace, int dtype, void* stream) {
@@ -394,20 +448,8 @@ int rod_bn_stats(const void* x, long M, int C, int ldx, float eps, float decay, 
   ROD_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr), "rod_bn_stats: moving stats mismatch");
   ROD_CHECK_ARG(workspace != nullptr, "rod_bn_stats: workspace is NULL");
   hipStream_t s = ROD_STREAM(stream);
-  ROD_DISPATCH_DTYPE(dtype, {
-    const bool vec = vec_ok<T>(C, {{x, ldx}});
-    RedPlan pl = red_plan<T>(M, C, vec);
-    dim3 grid(pl.nbx, pl.cgroups);
-    size_t lds = 2 * 256 * pl.V * sizeof(float);
-    if (vec)
-      hipLaunchKernelGGL((bn_stats_kernel<T, true>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp,
-                         pl.chunk, (float*)workspace);
-    else
-      hipLaunchKernelGGL((bn_stats_kernel<T, false>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp,
-                         pl.chunk, (float*)workspace);
-    hipLaunchKernelGGL(bn_stats_finalize_kernel<T>, dim3(cdiv(C, 256)), dim3(256), 0, s, (const T*)x,
-                       (const float*)workspace, pl.nbx, M, C, eps, decay, mean, rstd, moving_mean, moving_var);
-  });
+  ROD_DISPATCH_DTYPE(dtype, stats_launch<T>(vec_ok<T>(C, {{x, ldx}}), x, M, C, ldx, eps, decay, mean, rstd,
+                                            moving_mean, moving_var, (float*)workspace, s));
   return check_launch("rod_bn_stats");
 }
 
@@ -429,17 +471,8 @@ int rod_bn_apply(const void* x, const float* mean, const float* rstd, const floa
   if (ldr == 0) ldr = C;
   ROD_CHECK_ARG(ldx >= C && ldy >= C && ldr >= C, "rod_bn_apply: leading dim < C");
   hipStream_t s = ROD_STREAM(stream);
-  ROD_DISPATCH_DTYPE(dtype, {
-    const bool vec = vec_ok<T>(C, {{x, ldx}, {y, ldy}, {residual, ldr}});
-    const int V = vec ? Vec16<T>::N : 1;
-    int blocks = ew_blocks(M * (C / V));
-    if (vec)
-      hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)x, mean, rstd, gamma,
-                         beta, (const T*)residual, (T*)y, M, C, ldx, ldr, ldy, act);
-    else
-      hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(blocks), dim3(256), 0, s, (const T*)x, mean, rstd,
-                         gamma, beta, (const T*)residual, (T*)y, M, C, ldx, ldr, ldy, act);
-  });
+  ROD_DISPATCH_DTYPE(dtype, apply_launch<T>(vec_ok<T>(C, {{x, ldx}, {y, ldy}, {residual, ldr}}), x, mean, rstd,
+                                            gamma, beta, residual, y, M, C, ldx, ldr, ldy, act, s));
   return check_launch("rod_bn_apply");
 }
 
@@ -457,30 +490,10 @@ int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rs
   if (lddx == 0) lddx = C;
   ROD_CHECK_ARG(lddy >= C && ldx >= C && lddx >= C, "rod_bn_bwd: leading dim < C");
   hipStream_t s = ROD_STREAM(stream);
-  ROD_DISPATCH_DTYPE(dtype, {
-    const bool vec = vec_ok<T>(C, {{dy, lddy}, {x, ldx}, {dx, lddx}});
-    RedPlan pl = red_plan<T>(M, C, vec);
-    float* slab = (float*)workspace;
-    float* coef = slab + (size_t)max_nbx(M, C) * 2 * C;  // after the largest slab
-    dim3 grid(pl.nbx, pl.cgroups);
-    size_t lds = 2 * 256 * pl.V * sizeof(float);
-    if (vec)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x, mean,
-                         rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
-    else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x,
-                         mean, rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, slab, pl.nbx, M, C, rstd, gamma,
-                       dgamma, dbeta, coef);
-    const int V = pl.V;
-    int blocks = ew_blocks(M * (C / V));
-    if (vec)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dy, (const T*)x,
-                         mean, rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false>), dim3(blocks), dim3(256), 0, s, (const T*)dy,
-                         (const T*)x, mean, rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
-  });
+  float* slab = (float*)workspace;
+  float* coef = slab + (size_t)max_nbx(M, C) * 2 * C;  // after the largest slab
+  ROD_DISPATCH_DTYPE(dtype, bwd_launch<T>(vec_ok<T>(C, {{dy, lddy}, {x, ldx}, {dx, lddx}}), dy, x, mean, rstd, gamma,
+                                          beta, dx, dgamma, dbeta, slab, coef, M, C, lddy, ldx, lddx, act, s));
   return check_launch("rod_bn_bwd");
 }
 

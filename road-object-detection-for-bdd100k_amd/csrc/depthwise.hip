@@ -319,8 +319,7 @@ static void dw_bwd_filter_launch(const void* x, const void* dy, float* dw, float
   size_t lds = 256 * V * sizeof(float);
   hipLaunchKernelGGL((dw3x3_bwd_filter_kernel<T, S, VK>), grid, dim3(256), lds, s, (const T*)x, (const T*)dy, slab, N,
                      H, W, C, pt, pl, Ho, Wo, pl_.CVp, pl_.chunk);
-  int n = 9 * C;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, slab, dw, pl_.nbx, n);
+  slab_sum(slab, dw, pl_.nbx, 9L * C, s);
 }
 
 }  // namespace rod

@@ -472,13 +472,13 @@ static void wgrad_typed(const void* x, const void* dy, float* dw, float* db, flo
   if (ksize == 1) wgrad_va_vd<T, 1>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
   else wgrad_va_vd<T, 3>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
   const long n = (long)Cout * K;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(cdivl(n, 256)), dim3(256), 0, s, part, dw, p.splits, n);
+  slab_sum(part, dw, p.splits, n, s);
   if (db) {
     long cchunk = std::max<long>(64, cdivl(M, 512));
     int nb = (int)cdivl(M, cchunk);
     hipLaunchKernelGGL(colsum_kernel<T>, dim3(nb, cdiv(Cout, 256)), dim3(256), 0, s, (const T*)dy, M, Cout, lddy,
                        cchunk, part);
-    hipLaunchKernelGGL(split_reduce_kernel, dim3(cdiv(Cout, 256)), dim3(256), 0, s, part, db, nb, (long)Cout);
+    slab_sum(part, db, nb, (long)Cout, s);
   }
 }
 

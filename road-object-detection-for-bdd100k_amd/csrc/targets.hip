@@ -167,12 +167,23 @@ __global__ void __launch_bounds__(256) smoothl1_kernel(const T* __restrict__ pre
 
 __global__ void level_sum_finalize_kernel(const float* __restrict__ slab, int nbx, int L, float scale,
                                           float* __restrict__ out) {
+  // one 256-thread block: strided partial sums per level, fixed-order tree in LDS
+  __shared__ double red[MAXL][256];
+  for (int l = 0; l < L; ++l) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nbx; i += 256) s += (double)slab[(long)l * nbx + i];
+    red[l][threadIdx.x] = s;
+  }
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int l = 0; l < L; ++l) red[l][threadIdx.x] += red[l][threadIdx.x + w];
+    __syncthreads();
+  }
   if (threadIdx.x != 0) return;
   float total = 0.f;  // refine_loss = 0.; refine_loss += layer_loss (net_tools.py:505-515)
   for (int l = 0; l < L; ++l) {
-    double s = 0.0;
-    for (int i = 0; i < nbx; ++i) s += (double)slab[(long)l * nbx + i];
-    out[l] = (float)s / scale;  // reduce_sum(...) / bs
+    out[l] = (float)red[l][0] / scale;  // reduce_sum(...) / bs
     total = total + out[l];
   }
   out[L] = total;
@@ -278,7 +289,7 @@ int rod_smoothl1_masked(const void* pred, const float* target, const int* mask, 
     hipLaunchKernelGGL(smoothl1_kernel<T>, dim3(nbx, L), dim3(256), 0, s, (const T*)pred, target, mask, li, inv,
                        (T*)grad, (float*)workspace, B, A, nbx);
   });
-  hipLaunchKernelGGL(level_sum_finalize_kernel, dim3(1), dim3(64), 0, s, (const float*)workspace, nbx, L, scale,
+  hipLaunchKernelGGL(level_sum_finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nbx, L, scale,
                      loss_lvl);
   return check_launch("rod_smoothl1_masked");
 }

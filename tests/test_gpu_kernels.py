@@ -209,7 +209,7 @@ def test_refine_loss(dev):
     gts = [t.cpu().numpy() for t in tg[0]]
     pms = [t.cpu().numpy() for t in tg[3]]
     per, tot = ot.refine_loss([o.numpy() for o in outs], gts, pms, B)
-    np.testing.assert_allclose(nt.refine_loss.last_per_layer[:6].cpu().numpy(), per, rtol=1e-5)
+    np.testing.assert_allclose(nt.refine_loss.last_per_layer[:6].detach().cpu().numpy(), per, rtol=1e-5)
     np.testing.assert_allclose(loss.item(), tot, rtol=1e-5)
     grads = ot.refine_loss_grad([o.numpy() for o in outs], gts, pms, B)
     for gd, go in zip(outs_d, grads):
