@@ -147,6 +147,61 @@ int rod_boxes_convert(const float* in, float* out, long n_boxes, int to_center, 
 int rod_copy2d(const void* src, long src_ld_bytes, void* dst, long dst_ld_bytes, long rows, long cols_bytes,
                void* stream);
 
+/* ------------------------------------------------ deconvolution pyramid (A6)
+ * Legacy TF1 bilinear resize, align_corners=False: src = dst * in/out, no half-pixel
+ * offset (tf.image.resize_images; catch_net.py:207, tf_image.py:266-278), NHWC. */
+int rod_resize_bilinear(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo,
+                        int dtype, void* stream);
+/* ResizeBilinearGrad: dx [N,H,W,C] from dy [N,Ho,Wo,C] (deterministic gather). */
+int rod_resize_bilinear_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, int Wo,
+                            int dtype, void* stream);
+/* conv2d_transpose(k=2, s=2, SAME) = 1x1 rod_conv_fwd to z [N,h,w,4F] (channel (a*2+b)*F+f,
+ * weight [2,2,F,Cin] read as [4F,Cin]) followed by this scatter into out [N,Ho,Wo,ldo]
+ * (rows/cols >= Ho/Wo cropped; catch_net.py:196).  space_to_depth2 is its adjoint. */
+int rod_depth_to_space2(const void* z, void* out, int N, int h, int w, int F, int Ho, int Wo,
+                        int ldo, int dtype, void* stream);
+int rod_space_to_depth2(const void* dout, void* dz, int N, int h, int w, int F, int Ho, int Wo,
+                        int ldo, int dtype, void* stream);
+/* c = a + b elementwise (ADD merge catch_net.py:269). */
+int rod_add(const void* a, const void* b, void* c, long n, int dtype, void* stream);
+
+/* ------------------------------------------------ decode / ODM targets / classification loss
+ * decode_locations_one_layer (net_tools.py:182-234) of off_a (+ off_b, NULL = none) against
+ * the anchor centres, levels concatenated: out fp32 [B,A,4] centre boxes, or corners when
+ * to_corner (centerBboxes_2_cornerBboxes, predict.py:133). */
+int rod_decode(const float* anc_center, const void* off_a, const void* off_b, float* out, int B,
+               int A, int to_corner, int dtype, void* stream);
+/* det_groundtruth (net_tools.py:431-475): IoU of the refined anchor with its matched box,
+ * det_pos = (iou >= thr[level]) & refine_pos, det_gt = (refine_gt - refine_out)*det_pos,
+ * det_lbl = label*det_pos; iou [B,A] fp32 is also returned for the IoU factor.
+ * lvl_off[L+1], thr[L] (det_pos_jac_val_all_layers) are host arrays. */
+int rod_det_targets(const float* anc_center, const void* refine_out, const float* refine_gt,
+                    const float* cbox, const int* label, const int* refine_pos, const int* lvl_off,
+                    const float* thr, int L, float* det_gt, int* det_pos, int* det_lbl, float* iou,
+                    int B, int A, int dtype, void* stream);
+/* probs[r, k] = softmax(logits[r, :]) over K <= 16 classes, fp32 out (slim.softmax). */
+int rod_softmax(const void* logits, float* probs, long rows, int K, int dtype, void* stream);
+/* Classification half of det_clf_loss with global hard-negative mining (net_tools.py:551-615),
+ * all on the device: nvalues, k = min(int(3*n_pos)+B, n_neg), exact radix select of the
+ * k-th smallest nvalue, strict '<' negative mask, per-(image,level) IoU factor, CE losses.
+ * logits [B*A, K] (dtype), det_lbl/det_pos int [B*A], iou fp32 [B*A], lvl_off host [L+1].
+ * out fp32 [8] (device): pos_loss, neg_loss, clf_loss, max_hard_pred, n_pos, k,
+ * n_neg_selected, 0.  grad (nullable, dtype [B*A, K]) = d clf_loss / d logits. */
+size_t rod_softmax_ce_hnm_workspace(int B, int A, int L);
+int rod_softmax_ce_hnm(const void* logits, const int* det_lbl, const int* det_pos, const float* iou,
+                       const int* lvl_off, int L, float bs, float* out, void* grad, void* workspace,
+                       int B, int A, int K, int dtype, void* stream);
+
+/* ------------------------------------------------ post-processing (A15)
+ * detected_bboxes (net_tools.py:739-758) for every image and class 1..K-1: select
+ * (p >= select_threshold), top_k sort (score desc, ties by index), greedy NMS (IoU >
+ * nms_threshold, tf.image.non_max_suppression semantics), zero-pad to keep_top_k.
+ * probs fp32 [B,A,K]; boxes fp32 corner [B,A,4];
+ * out_scores [B,K-1,keep_top_k], out_boxes [B,K-1,keep_top_k,4]; top_k, keep_top_k <= 1024. */
+int rod_select_topk_nms(const float* probs, const float* boxes, int B, int A, int K,
+                        float select_threshold, int top_k, int keep_top_k, float nms_threshold,
+                        float* out_scores, float* out_boxes, void* stream);
+
 /* ------------------------------------------------ optimiser (A14)
  * Plain SGD with clip by value (net_tools.py:645-651):
  *   p -= lr * clamp(g, -clip, clip)   over one flat fp32 buffer. */

@@ -305,3 +305,187 @@ def match_anchors(anc_corner, anc_center, lvl_off, thr, gt_center, gt_lbl, gt_n)
 # ----------------------------------------------------------------------------- optimiser
 def sgd_clip_(param_flat: torch.Tensor, grad_flat: torch.Tensor, lr: float, clip: float = 5.0):
     _abi.call("rod_sgd_clip", param_flat, grad_flat, param_flat.numel(), float(lr), float(clip), stream())
+
+
+# ----------------------------------------------------------------------------- deconv pyramid
+class _Resize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ho, wo):
+        N, H, W, C = x.shape
+        y = torch.empty((N, ho, wo, C), dtype=x.dtype, device=x.device)
+        _abi.call("rod_resize_bilinear", x.contiguous(), y, N, H, W, C, ho, wo, dtcode(x), stream())
+        ctx.geo = (N, H, W, C, ho, wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C, ho, wo = ctx.geo
+        dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+        _abi.call("rod_resize_bilinear_bwd", dy.contiguous(), dx, N, H, W, C, ho, wo, dtcode(dy), stream())
+        return dx, None, None
+
+
+def resize_bilinear(x, size):
+    """tf.image.resize_images(BILINEAR, align_corners=False), TF1 legacy scaling."""
+    return _Resize.apply(x, int(size[0]), int(size[1]))
+
+
+class _Deconv2x2(torch.autograd.Function):
+    """conv2d_transpose(stride 2, SAME, 2x2 kernel [2, 2, F, Cin]) (catch_net.py:189-197)."""
+
+    @staticmethod
+    def forward(ctx, x, w, ho, wo):
+        N, h, wd, Cin = x.shape
+        F = w.shape[2]
+        assert w.shape == (2, 2, F, Cin)
+        x = x.contiguous()
+        wt = torch.empty((4 * F, Cin), dtype=x.dtype, device=x.device)
+        _abi.call("rod_conv_weight_prep", w, wt, 4 * F, Cin, 1, 0, dtcode(x), stream())
+        z = torch.empty((N, h, wd, 4 * F), dtype=x.dtype, device=x.device)
+        _abi.call("rod_conv_fwd", x, wt, None, z, N, h, wd, Cin, 4 * F, 1, 0, 0, dtcode(x), stream())
+        y = torch.empty((N, ho, wo, F), dtype=x.dtype, device=x.device)
+        _abi.call("rod_depth_to_space2", z, y, N, h, wd, F, ho, wo, 0, dtcode(x), stream())
+        ctx.save_for_backward(x, w)
+        ctx.geo = (N, h, wd, Cin, F, ho, wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        N, h, wd, Cin, F, ho, wo = ctx.geo
+        dz = torch.empty((N, h, wd, 4 * F), dtype=dy.dtype, device=dy.device)
+        _abi.call("rod_space_to_depth2", dy.contiguous(), dz, N, h, wd, F, ho, wo, 0, dtcode(dy), stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt1 = torch.empty((Cin, 4 * F), dtype=dy.dtype, device=dy.device)
+            _abi.call("rod_conv_weight_prep", w, wt1, 4 * F, Cin, 1, 1, dtcode(dy), stream())
+            dx = torch.empty_like(x)
+            _abi.call("rod_conv_fwd", dz, wt1, None, dx, N, h, wd, 4 * F, Cin, 1, 0, 0, dtcode(dy), stream())
+        if ctx.needs_input_grad[1]:
+            ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, h, wd, Cin, 4 * F, 1), x.device)
+            _abi.call("rod_conv_wgrad", x, dz, grad_slot(w), None, ws, N, h, wd, Cin, 4 * F, 1, 0, 0, dtcode(x),
+                      stream())
+            _mark_written(w)
+        return dx, None, None, None
+
+
+def deconv2x2(x, w, size):
+    return _Deconv2x2.apply(x, w, int(size[0]), int(size[1]))
+
+
+class _ChannelConcat(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        N, H, W = xs[0].shape[:3]
+        cs = [x.shape[3] for x in xs]
+        Ct = sum(cs)
+        out = torch.empty((N, H, W, Ct), dtype=xs[0].dtype, device=xs[0].device)
+        es = out.element_size()
+        off = 0
+        for x, c in zip(xs, cs):
+            copy2d(x.contiguous(), c * es, out, Ct * es, N * H * W, c * es, 0, off * es)
+            off += c
+        ctx.cs = cs
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        N, H, W, Ct = g.shape
+        es = g.element_size()
+        outs, off = [], 0
+        for c in ctx.cs:
+            d = torch.empty((N, H, W, c), dtype=g.dtype, device=g.device)
+            copy2d(g, Ct * es, d, c * es, N * H * W, c * es, off * es, 0)
+            outs.append(d)
+            off += c
+        return tuple(outs)
+
+
+def channel_concat(xs):
+    """tf.concat(xs, axis=-1) on NHWC tensors."""
+    return _ChannelConcat.apply(*xs)
+
+
+class _Add(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        assert a.shape == b.shape and a.dtype == b.dtype
+        c = torch.empty_like(a)
+        _abi.call("rod_add", a, b, c, a.numel(), dtcode(a), stream())
+        return c
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add(a, b):
+    return _Add.apply(a, b)
+
+
+# ----------------------------------------------------------------------------- ODM / inference
+def decode(anc_center, off_a, off_b=None, to_corner=False):
+    """[B, A, 4] offsets (+ second offsets) -> fp32 boxes (centre or corner form)."""
+    B, A = off_a.shape[0], off_a.shape[1]
+    out = torch.empty((B, A, 4), dtype=torch.float32, device=off_a.device)
+    _abi.call("rod_decode", anc_center, off_a.contiguous(), None if off_b is None else off_b.contiguous(), out, B, A,
+              1 if to_corner else 0, dtcode(off_a), stream())
+    return out
+
+
+def det_targets(anc_center, refine_out, refine_gt, cbox, label, refine_pos, lvl_off, thr):
+    B, A = refine_out.shape[0], refine_out.shape[1]
+    dev = refine_out.device
+    det_gt = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
+    det_pos = torch.empty((B, A), dtype=torch.int32, device=dev)
+    det_lbl = torch.empty((B, A), dtype=torch.int32, device=dev)
+    iou = torch.empty((B, A), dtype=torch.float32, device=dev)
+    _abi.call("rod_det_targets", anc_center, refine_out.contiguous(), refine_gt, cbox, label, refine_pos,
+              np.ascontiguousarray(lvl_off, dtype=np.int32), np.ascontiguousarray(thr, dtype=np.float32),
+              len(lvl_off) - 1, det_gt, det_pos, det_lbl, iou, B, A, dtcode(refine_out), stream())
+    return det_gt, det_pos, det_lbl, iou
+
+
+def softmax(logits, K):
+    rows = logits.numel() // K
+    out = torch.empty(logits.shape, dtype=torch.float32, device=logits.device)
+    _abi.call("rod_softmax", logits.contiguous(), out, rows, K, dtcode(logits), stream())
+    return out
+
+
+class _SoftmaxCEHNM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, det_lbl, det_pos, iou, lvl_off, bs):
+        B, A, K = logits.shape
+        L = len(lvl_off) - 1
+        out = torch.empty(8, dtype=torch.float32, device=logits.device)
+        grad = torch.empty_like(logits) if ctx.needs_input_grad[0] else None
+        ws = workspace(_abi.query("rod_softmax_ce_hnm_workspace", B, A, L), logits.device)
+        _abi.call("rod_softmax_ce_hnm", logits.contiguous(), det_lbl, det_pos, iou,
+                  np.ascontiguousarray(lvl_off, dtype=np.int32), L, float(bs), out, grad, ws, B, A, K,
+                  dtcode(logits), stream())
+        ctx.save_for_backward(grad)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        # consumers take out[2] (clf_loss) with weight 1 (net_tools.det_clf_loss)
+        return grad, None, None, None, None, None
+
+
+def softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, bs):
+    """[8]: pos_loss, neg_loss, clf_loss, max_hard_pred, n_pos, k, n_neg_selected, 0."""
+    return _SoftmaxCEHNM.apply(logits, det_lbl, det_pos, iou, lvl_off, bs)
+
+
+def select_topk_nms(probs, boxes, select_threshold, top_k, keep_top_k, nms_threshold):
+    B, A, K = probs.shape
+    dev = probs.device
+    scores = torch.empty((B, K - 1, keep_top_k), dtype=torch.float32, device=dev)
+    bxs = torch.empty((B, K - 1, keep_top_k, 4), dtype=torch.float32, device=dev)
+    _abi.call("rod_select_topk_nms", probs.contiguous(), boxes.contiguous(), B, A, K, float(select_threshold),
+              int(top_k), int(keep_top_k), float(nms_threshold), scores, bxs, stream())
+    return scores, bxs

@@ -42,6 +42,10 @@ class Trainer:
                                                    net_tools.init_anchor(layer_n))
         self.table = net_tools.anchor_table(self.anchors, self.device)
         store = self.net.store
+        if train_range is config.train_range.ALL and not fix_refine:
+            raise NotImplementedError(
+                'ALL with fix_refine=False needs the gradient through the ODM IoU factor into refine_out '
+                '(net_tools.py:590-599); not built yet (DESIGN.md, "next")')
         if train_range is config.train_range.ALL and fix_refine:
             import re
             pat = re.compile(r'^((?!(backbone|refine)).)*$')   # train.py:160-163
@@ -64,9 +68,8 @@ class Trainer:
         else:
             refine_out, det_out, clf_out = out
             r_loss = net_tools.refine_loss(refine_out, tg[0], tg[3], targets=tg, scale=scale)
-            det_gt, det_mask, det_lbl, iou = net_tools.det_groundtruth(refine_out, tg[0], tg[1], tg[2], tg[3],
-                                                                      self.anchors, targets=tg)
-            d_loss, c_loss = net_tools.det_clf_loss(refine_out, clf_out, det_out, det_gt, det_mask, det_lbl, iou,
+            dgt = net_tools.det_groundtruth(refine_out, tg[0], tg[1], tg[2], tg[3], self.anchors, targets=tg)
+            d_loss, c_loss = net_tools.det_clf_loss(refine_out, clf_out, det_out, dgt, dgt[1], dgt[2], dgt[3],
                                                     scale=scale)
             loss = d_loss + c_loss if self.fix_refine else r_loss + d_loss + c_loss
             losses = (loss, r_loss, d_loss, c_loss)

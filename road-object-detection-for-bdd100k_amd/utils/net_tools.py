@@ -209,3 +209,103 @@ class optimizer(object):
     def step(self):
         ops.sgd_clip_(self.store.flat, self.store.flat_grad, self.lr, self.clip)
         self.global_step += 1
+
+
+# ================================================================ ODM targets and loss
+def _flat_levels(tensors, k, table):
+    """Per-layer tensors [B, fh, fw, A(, k)] -> concatenated [B, A_total(, k)] (no copy when
+    they are already views of one buffer laid out that way)."""
+    return ops.levels_concat([t.contiguous() for t in tensors], k)
+
+
+def det_groundtruth(refine_out, offset_gt, cbboxes, refine_labels, refine_pos_mask, anchors, scope="det_encode",
+                    targets=None):
+    """ODM targets (net_tools.py:431-475).  Returns (det_gt, det_pos_mask, det_labels, iou)
+    as per-layer views [B, fh, fw, A, 4|1] / iou [B, fh, fw, A]; the concatenated buffers
+    are attached as `.flat` for the fused loss kernels."""
+    tab = targets.table if targets is not None else anchor_table(anchors, refine_out[0].device)
+    ro = ops.levels_concat(refine_out, 4)
+    if targets is not None:
+        rgt, cbox, lbl, rpos = targets.flat
+    else:
+        B = refine_out[0].shape[0]
+        rgt = _flat_levels(offset_gt, 4, tab).float()
+        cbox = _flat_levels(cbboxes, 4, tab).float()
+        lbl = _flat_levels(refine_labels, 1, tab).view(B, -1)
+        rpos = _flat_levels(refine_pos_mask, 1, tab).view(B, -1)
+    det_gt, det_pos, det_lbl, iou = ops.det_targets(tab.center, ro.detach(), rgt, cbox, lbl, rpos, tab.lvl_off,
+                                                    config.det_pos_jac_val_all_layers[:len(tab.shapes)])
+    res = RefineTargets(tab.split(det_gt, 4), tab.split(det_pos[..., None], 1), tab.split(det_lbl[..., None], 1),
+                        tab.split(iou, 0))
+    res.flat = (det_gt, det_pos, det_lbl, iou)
+    res.table = tab
+    return res
+
+
+def det_clf_loss(refine_out, clf_out, det_out, det_groundtruth, det_pos_mask, det_labels, iou_all_layers,
+                 dtype=torch.float32, scale=None, targets=None):
+    """(det_loss, clf_loss) (net_tools.py:519-623): masked smooth-L1 on the ODM offsets and
+    softmax cross-entropy with global hard-negative mining and the IoU focal factor.
+
+    `det_groundtruth` may be the object returned by det_groundtruth() (fast path).  The
+    summaries the reference logs (pos/neg/clf loss, max hard prediction, positives) are
+    left in det_clf_loss.last_stats ([8] device tensor, see rod_softmax_ce_hnm)."""
+    B = clf_out[0].shape[0]
+    scale = float(B) if scale is None else float(scale)
+    tg = det_groundtruth if isinstance(det_groundtruth, RefineTargets) and hasattr(det_groundtruth, 'flat') \
+        else targets
+    if tg is None:
+        raise ValueError('det_clf_loss needs the det_groundtruth() result (per-layer lists are views of it)')
+    det_gt, det_pos, det_lbl, iou = tg.flat
+    lvl_off = tg.table.lvl_off
+    pred = ops.levels_concat(det_out, 4)
+    dvec = ops.smooth_l1_masked(pred, det_gt, det_pos, lvl_off, scale)
+    det_loss_one = dvec[len(lvl_off) - 1]
+    logits = ops.levels_concat(clf_out, config.total_obj_n)
+    cvec = ops.softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, scale)
+    det_clf_loss.last_stats = cvec
+    det_clf_loss.last_det_per_layer = dvec
+    return det_loss_one, cvec[2]
+
+
+# ================================================================ decode / post-processing
+def decode_locations_one_layer(anchors_one_layer, offset_bboxes):
+    """Centre boxes from [B, fh, fw, A, 4] offsets (net_tools.py:182-234)."""
+    tab = AnchorTable([anchors_one_layer], offset_bboxes.device)
+    B = offset_bboxes.shape[0]
+    out = ops.decode(tab.center, offset_bboxes.reshape(B, -1, 4))
+    return out.view(offset_bboxes.shape)
+
+
+def decode_all_layers(anchors_all, refine_out, det_out=None, to_corner=True):
+    """predict.py:130-134 / evaluate.py:139-143 for all layers at once: corner boxes of
+    decode(anchor, refine_out + det_out), concatenated [B, A_total, 4] fp32."""
+    tab = anchor_table(anchors_all, refine_out[0].device)
+    a = ops.levels_concat(refine_out, 4)
+    b = ops.levels_concat(det_out, 4) if det_out is not None else None
+    return ops.decode(tab.center, a, b, to_corner=to_corner)
+
+
+def class_probabilities(clf_out):
+    """slim.softmax over every layer's logits, concatenated [B, A_total, K] fp32."""
+    logits = ops.levels_concat(clf_out, config.total_obj_n)
+    return ops.softmax(logits, config.total_obj_n)
+
+
+def detected_bboxes(predictions, localisations, select_threshold=None, nms_threshold=0.5, clipping_bbox=None,
+                    top_k=800, keep_top_k=200):
+    """Per-class select -> top_k -> NMS -> pad (net_tools.py:739-758) in one kernel.
+
+    predictions: [B, A_total, K] probabilities (or the per-layer list of them);
+    localisations: [B, A_total, 4] corner boxes (or the per-layer list).
+    Returns dicts {c: scores [B, keep_top_k]}, {c: boxes [B, keep_top_k, 4]} for c = 1..K-1."""
+    if isinstance(predictions, (list, tuple)):
+        predictions = ops.levels_concat([p.float() for p in predictions], config.total_obj_n)
+    if isinstance(localisations, (list, tuple)):
+        localisations = ops.levels_concat([l.float() for l in localisations], 4)
+    thr = 0.0 if select_threshold is None else select_threshold
+    scores, boxes = ops.select_topk_nms(predictions, localisations, thr, top_k, keep_top_k, nms_threshold)
+    if clipping_bbox is not None:
+        raise NotImplementedError('clipping_bbox is never used by the reference CLIs (predict.py:136)')
+    K = predictions.shape[-1]
+    return ({c: scores[:, c - 1] for c in range(1, K)}, {c: boxes[:, c - 1] for c in range(1, K)})
