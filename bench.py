@@ -43,6 +43,8 @@ def parse():
     ap.add_argument('--probe', default='rod_conv_fwd', help='kernel reported in "roofline"')
     ap.add_argument('--cpu-baseline', dest='cpu_baseline', action='store_true', default=True)
     ap.add_argument('--no-cpu-baseline', dest='cpu_baseline', action='store_false')
+    ap.add_argument('--inference', dest='inference', action='store_true', default=True)
+    ap.add_argument('--no-inference', dest='inference', action='store_false')
     return ap.parse_args()
 
 
@@ -88,6 +90,27 @@ def cpu_baseline(H, W):
                       f'{dt:.1f} s'}
 
 
+def inference_fps(args, dev, dtype, batch=32, steps=5, warmup=2):
+    """BASELINE configs[3]: predict.py inference (ALL network, eval BN, decode, per-class
+    top-k + NMS) at the bench resolution, batch 32, 1 GPU, synthetic batch in HBM."""
+    import predict
+    from rod.data import synthetic_batch
+    pr = predict.Predictor((args.height, args.width), dev, dtype)
+    img = synthetic_batch(batch, args.height, args.width, dev, seed=77)[0]
+    for _ in range(warmup):
+        pr(img)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        scores, _ = pr(img)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {'metric': 'inference FPS (predict.py path: forward + decode + per-class NMS)',
+            'value': round(batch * steps / dt, 2), 'unit': 'images/s', 'batch': batch, 'steps': steps,
+            'ms_per_batch': round(dt / steps * 1e3, 3), 'dtype': args.dtype,
+            'mAP@0.5': None, 'mAP_note': 'no BDD100K data or trained checkpoint on the box (synthetic inputs)'}
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -106,8 +129,8 @@ def main():
     tr_range = config.train_range.REFINE if args.train_range == 'REFINE' else config.train_range.ALL
     reducer = None
     if world > 1:
-        def reducer(flat_grad):
-            torch.distributed.all_reduce(flat_grad)  # RCCL ring/tree over xGMI, one 22 MB buffer
+        from rod.ddp import GradReducer
+        reducer = GradReducer(world)  # bucketed RCCL all-reduce, launched during backward
     tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
                  world_size=world, reducer=reducer)
     batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED + rank)
@@ -171,6 +194,8 @@ def main():
             'loss': round(loss_val, 5),
             'roofline': rl,
         }
+        if args.inference and world == 1:
+            out['inference'] = inference_fps(args, dev, dtype)
         if args.cpu_baseline and world == 1:
             out['cpu_baseline'] = cpu_baseline(args.height, args.width)
         print(json.dumps(out), flush=True)

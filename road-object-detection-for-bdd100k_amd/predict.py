@@ -1,0 +1,116 @@
+"""Inference CLI — drop-in for the reference's predict.py (flags 27-53, flow 61-200).
+
+ALL-mode network in inference mode -> softmax(clf_out) -> decode(refine_out + det_out)
+-> corner boxes -> detected_bboxes(select 0.1, nms 0.4, top_k 400, keep 200)
+(predict.py:127-137).  The reference shows each image in cv2 windows; visualisation is
+out of scope here, so detections are printed / written as JSON.
+--batch_size > 1 reports throughput (BASELINE config: predict b=32 at 1280x720).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+
+import config  # noqa: E402
+from utils.common_tools import logger  # noqa: E402
+
+
+def str2bool(v):
+    return str(v).lower() in ('1', 'true', 't', 'yes', 'y')
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument('--backbone_name', default='mobilenet_v2')
+    ap.add_argument('--num_readers', type=int, default=4)
+    ap.add_argument('--num_preprocessing_threads', type=int, default=4)
+    ap.add_argument('--checkpoint_all', default='checkpoint/mobilenet_v2.model')
+    ap.add_argument('--vis_height', type=int, default=720)
+    ap.add_argument('--vis_width', type=int, default=1080)
+    ap.add_argument('--vis_groundtruth', type=str2bool, default=True)
+    # additions
+    ap.add_argument('--batch_size', type=int, default=1)
+    ap.add_argument('--num_batches', type=int, default=1)
+    ap.add_argument('--select_threshold', type=float, default=0.1)
+    ap.add_argument('--nms_threshold', type=float, default=0.4)
+    ap.add_argument('--top_k', type=int, default=400)
+    ap.add_argument('--keep_top_k', type=int, default=200)
+    ap.add_argument('--img_height', type=int, default=config.img_size[0])
+    ap.add_argument('--img_width', type=int, default=config.img_size[1])
+    ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
+    ap.add_argument('--dataset_dir', default='./dataset/bdd100k_TfRecord/')
+    ap.add_argument('--output', default=None, help='write detections of the last batch as JSON')
+    return ap.parse_args(argv)
+
+
+class Predictor(object):
+    """Forward + decode + per-class NMS; reused by bench (inference FPS)."""
+
+    def __init__(self, img_size, device, dtype=torch.float32, checkpoint=None, select_threshold=0.1,
+                 nms_threshold=0.4, top_k=400, keep_top_k=200, seed=0):
+        from nets.catch_net import CatchNet
+        from utils import net_tools
+        config.img_size = tuple(img_size)
+        self.config_dict = {'process_backbone_method': config.process_backbone_method.NONE,
+                            'deconv_method': config.deconv_method.LEARN_HALF,
+                            'merge_method': config.merge_method.ADD, 'train_range': config.train_range.ALL}
+        self.net = CatchNet('mobilenet_v2', self.config_dict, device, seed)
+        if checkpoint is not None:
+            sd = torch.load(checkpoint, map_location='cpu', weights_only=True)
+            self.net.store.load_state_dict(sd['variables'])
+        self.anchors = net_tools.anchors_all_layer(config.img_size, config.feat_sizes(config.img_size),
+                                                   net_tools.init_anchor(6))
+        self.dtype = dtype
+        self.kw = dict(select_threshold=select_threshold, nms_threshold=nms_threshold, top_k=top_k,
+                       keep_top_k=keep_top_k)
+
+    @torch.no_grad()
+    def __call__(self, img_u8):
+        from nets.catch_net import factory
+        from rod import ops
+        from utils import net_tools
+        x = ops.normalize_image(img_u8, self.dtype)
+        refine_out, det_out, clf_out = factory(x, 'mobilenet_v2', False, self.config_dict, self.dtype,
+                                               net=self.net).get_output()
+        probs = net_tools.class_probabilities(clf_out)                                     # predict.py:127-128
+        boxes = net_tools.decode_all_layers(self.anchors, refine_out, det_out, to_corner=True)  # 130-134
+        return net_tools.detected_bboxes(probs, boxes, **self.kw)                          # 136-137
+
+
+def main(argv=None):
+    F = parse(argv)
+    logger.info('Asserting parameters')
+    assert F.backbone_name in config.supported_backbone_name
+    from rod.dataio import make_source
+    dev = torch.device('cuda', 0)
+    dtype = torch.bfloat16 if F.dtype == 'bf16' else torch.float32
+    ckpt = F.checkpoint_all if F.checkpoint_all and os.path.exists(F.checkpoint_all) else None
+    if ckpt is None:
+        logger.warning('checkpoint %r not found: predicting with randomly initialised weights', F.checkpoint_all)
+    pred = Predictor((F.img_height, F.img_width), dev, dtype, ckpt, F.select_threshold, F.nms_threshold, F.top_k,
+                     F.keep_top_k)
+    logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
+    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev)
+    t0 = time.time()
+    for _ in range(F.num_batches):
+        img, _, _, _ = next(source)
+        scores, bboxes = pred(img)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    n_det = {c: int((s > 0).sum().item()) for c, s in scores.items()}
+    logger.info('detections per class (batch of %d): %s' % (F.batch_size, n_det))
+    logger.info('%.2f images/s' % (F.batch_size * F.num_batches / dt))
+    if F.output:
+        out = {str(c): {'scores': scores[c].cpu().tolist(), 'bboxes': bboxes[c].cpu().tolist()} for c in scores}
+        with open(F.output, 'w') as f:
+            json.dump(out, f)
+    return scores, bboxes
+
+
+if __name__ == '__main__':
+    main()

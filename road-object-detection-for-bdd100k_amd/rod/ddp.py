@@ -1,0 +1,80 @@
+"""Data-parallel gradient reduction over RCCL (torch.distributed 'nccl' = RCCL on ROCm).
+
+The flat gradient buffer of rod.params.ParamStore is cut into contiguous buckets of
+~`bucket_mb` MB aligned to parameter boundaries.  Every rod.ops kernel that writes a
+parameter gradient calls the parameter's `_rod_on_grad` hook; when the last trainable
+parameter of a bucket has been written, that bucket's all-reduce (sum) is issued
+immediately with async_op=True.  RCCL runs it on its own stream, ordered after the
+kernels already enqueued on the compute stream, so the reduction of the head / late
+backbone buckets overlaps the early-backbone (depthwise) backward that is still running.
+`__call__` (after backward) issues any bucket not yet launched and makes the compute
+stream wait for all of them before the SGD update — clipping happens after the sum
+(net_tools.py:649).  Works with any torch.distributed backend (gloo in CPU tests).
+
+xGMI note: 8 GPUs are fully connected point-to-point; a 22 MB (REFINE) / 35 MB (ALL) fp32
+gradient in ~4 MB buckets gives RCCL messages large enough to run its multi-channel rings
+at link bandwidth while leaving room to overlap.
+"""
+import torch
+import torch.distributed as dist
+
+
+class GradReducer(object):
+    def __init__(self, world_size, bucket_mb=4.0, group=None):
+        self.world = world_size
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.group = group
+        self.store = None
+        self.buckets = []
+
+    def attach(self, store):
+        """Build buckets over the trainable parameters (in reverse registration order,
+        i.e. roughly the order backward produces their gradients)."""
+        self.store = store
+        trainable = [(n, p) for n, p in store.params.items() if p.requires_grad]
+        spans = sorted(((store.offsets[n][0], store.offsets[n][1], p) for n, p in trainable), key=lambda t: -t[0])
+        self.buckets = []
+        cur = None
+        for off, n, p in spans:
+            if cur is None or (cur['hi'] - off) * 4 > self.bucket_bytes:
+                cur = {'lo': off, 'hi': off + n, 'params': [], 'pending': 0, 'work': None}
+                self.buckets.append(cur)
+            cur['lo'] = min(cur['lo'], off)
+            cur['params'].append(p)
+            p._rod_bucket = cur
+            p._rod_on_grad = self._on_grad
+        self.reset()
+        return self
+
+    def reset(self):
+        for b in self.buckets:
+            b['pending'] = len(b['params'])
+            b['work'] = None
+            for p in b['params']:
+                p._rod_seen = False
+
+    def _launch(self, b):
+        if b['work'] is None:
+            view = self.store.flat_grad[b['lo']:b['hi']]
+            b['work'] = dist.all_reduce(view, group=self.group, async_op=True)
+
+    def _on_grad(self, p):
+        b = getattr(p, '_rod_bucket', None)
+        if b is None or p._rod_seen:
+            return
+        p._rod_seen = True
+        b['pending'] -= 1
+        if b['pending'] == 0:
+            self._launch(b)
+
+    def __call__(self, flat_grad):
+        if self.store is None:
+            raise RuntimeError('GradReducer.attach(store) was not called')
+        for b in self.buckets:
+            self._launch(b)
+        for b in self.buckets:
+            b['work'].wait()
+        self.reset()
+
+    def launched(self):
+        return sum(1 for b in self.buckets if b['work'] is not None)

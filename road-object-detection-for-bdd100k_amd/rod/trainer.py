@@ -52,6 +52,8 @@ class Trainer:
             store.set_trainable(lambda n: bool(pat.match(n)))
         self.opt = net_tools.optimizer(store, batch_size * world_size, learning_rate)
         self.reducer = reducer
+        if reducer is not None and hasattr(reducer, 'attach'):
+            reducer.attach(store)  # buckets over the trainable parameters (rod.ddp)
         self.train_range = train_range
         self.fix_refine = fix_refine
 

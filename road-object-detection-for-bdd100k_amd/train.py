@@ -1,0 +1,166 @@
+"""Training CLI — drop-in for the reference's train.py (flags train.py:26-77, loop 84-334).
+
+    python train.py [--batch_size=20] [--learning_rate=1e-3] [--train_range=REFINE|ALL] ...
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 train.py ...
+
+Same flag names and defaults as the reference, plus: --train_range (the reference
+hard-codes REFINE at train.py:130), --img_height/--img_width (config.img_size), --dtype
+(fp32 like the reference's DTYPE, or bf16), --dataset_dir, --seed.  Data parallel when
+launched with several ranks (RCCL all-reduce of the flat gradient, global-batch loss
+normalisation; --batch_size is then per GPU).  Checkpoints are torch files holding the
+slim-named variables and global_step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+
+import config  # noqa: E402
+from utils.common_tools import logger  # noqa: E402
+
+
+def str2bool(v):
+    if isinstance(v, bool):
+        return v
+    return str(v).lower() in ('1', 'true', 't', 'yes', 'y')
+
+
+def none_or_str(v):
+    return None if v in (None, '', 'None', 'none') else v
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument('--backbone_name', default='mobilenet_v2')
+    ap.add_argument('--learning_rate', type=float, default=1e-3)
+    ap.add_argument('--batch_size', type=int, default=20)
+    ap.add_argument('--num_readers', type=int, default=4)
+    ap.add_argument('--num_preprocessing_threads', type=int, default=4)
+    ap.add_argument('--checkpoint_all', type=none_or_str, default=None)
+    ap.add_argument('--checkpoint_refine', type=none_or_str, default='checkpoint/mbn_none53x35/refine/mobilenet_v2.model')
+    ap.add_argument('--train_dir', default='checkpoint/')
+    ap.add_argument('--summary_dir', default='summary/')
+    ap.add_argument('--max_number_of_steps', type=int, default=None)
+    ap.add_argument('--log_every_n_steps', type=int, default=20)
+    ap.add_argument('--summary_every_n_steps', type=int, default=20)
+    ap.add_argument('--save_every_n_steps', type=int, default=2000)
+    ap.add_argument('--fix_refine', type=str2bool, default=True)
+    # additions
+    ap.add_argument('--train_range', default='REFINE', choices=['REFINE', 'ALL'])
+    ap.add_argument('--img_height', type=int, default=config.img_size[0])
+    ap.add_argument('--img_width', type=int, default=config.img_size[1])
+    ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
+    ap.add_argument('--dataset_dir', default='./dataset/bdd100k_TfRecord/')
+    ap.add_argument('--seed', type=int, default=0)
+    return ap.parse_args(argv)
+
+
+def load_ckpt(store, path, names_regex=None):
+    sd = torch.load(path, map_location='cpu', weights_only=True)
+    store.load_state_dict(sd['variables'], strict=names_regex is None, names_regex=names_regex)
+    return int(sd.get('global_step', 0))
+
+
+def save_ckpt(store, path, step):
+    os.makedirs(os.path.dirname(path) or '.', exist_ok=True)
+    torch.save({'variables': store.state_dict(), 'global_step': step}, path)
+
+
+def main(argv=None):
+    F = parse(argv)
+    logger.info('Asserting parameters')
+    assert F.batch_size > 0
+    assert F.learning_rate >= 0.
+    assert F.log_every_n_steps is None or F.log_every_n_steps > 0
+    assert F.summary_every_n_steps is None or F.summary_every_n_steps > 0
+    assert F.save_every_n_steps is None or F.save_every_n_steps > 0
+    assert F.backbone_name in config.supported_backbone_name
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    from rod.dataio import make_source
+    from rod.ddp import GradReducer
+    from rod.trainer import Trainer
+
+    config.img_size = (F.img_height, F.img_width)
+    tr_range = getattr(config.train_range, F.train_range)
+    dtype = torch.bfloat16 if F.dtype == 'bf16' else torch.float32
+    logger.info('Building model, using backbone---%s' % F.backbone_name)
+    trainer = Trainer(config.img_size, F.batch_size, dtype=dtype, train_range=tr_range, learning_rate=F.learning_rate,
+                      device=dev, fix_refine=F.fix_refine, seed=F.seed, world_size=world,
+                      reducer=GradReducer(world) if world > 1 else None)
+    store = trainer.net.store
+    logger.info('Total trainable parameters:%s' % str(store.trainable_count()))
+    step0 = 0
+    if tr_range is config.train_range.ALL:
+        if F.checkpoint_all is not None:
+            step0 = load_ckpt(store, F.checkpoint_all)
+            logger.info('Load checkpoint for all net success...')
+        if F.checkpoint_refine is not None:
+            load_ckpt(store, F.checkpoint_refine, names_regex=r'backbone.+|refine.+')
+            logger.info('Load checkpoint for refine net success...')
+    else:
+        if F.checkpoint_refine is not None:
+            step0 = load_ckpt(store, F.checkpoint_refine)
+            logger.info('Load checkpoint success...')
+        else:
+            logger.info('TF variables init success...')
+    trainer.opt.global_step = step0
+    logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
+    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, seed=1000 * rank + F.seed)
+
+    os.makedirs(F.summary_dir, exist_ok=True)
+    summ = open(os.path.join(F.summary_dir, 'train_rank%d.jsonl' % rank), 'a') if rank == 0 else None
+    avg = [0., 0., 0.]
+    avg_t = 0.
+    while True:
+        start = time.time()
+        losses = trainer.step(*next(source))
+        vals = [float(l.item()) for l in losses]  # the reference's sess.run returns host values too
+        t = round(time.time() - start, 3)
+        current_step = trainer.opt.global_step - 1
+        if F.log_every_n_steps is not None:
+            s = current_step % F.log_every_n_steps
+            if tr_range is config.train_range.ALL:
+                tot, _, dl, cl = vals
+                avg = [(avg[0] * s + tot) / (s + 1.), (avg[1] * s + dl) / (s + 1.), (avg[2] * s + cl) / (s + 1.)]
+            else:
+                avg[0] = (avg[0] * s + vals[0]) / (s + 1.)
+            avg_t = (avg_t * s + t) / (s + 1.)
+            if current_step % F.log_every_n_steps == F.log_every_n_steps - 1 and rank == 0:
+                if tr_range is config.train_range.ALL:
+                    logger.info('Step%s total_loss:%s det_loss:%s clf_loss:%s time_each_step:%s' %
+                                (str(current_step + 1), str(avg[0]), str(avg[1]), str(avg[2]), str(avg_t)))
+                else:
+                    logger.info('Step_%s refine_loss:%s time:%s' % (str(current_step + 1), str(avg[0]), str(avg_t)))
+                avg = [0., 0., 0.]
+                avg_t = 0.
+        if summ is not None and F.summary_every_n_steps is not None and \
+                current_step % F.summary_every_n_steps == F.summary_every_n_steps - 1:
+            rec = {'step': current_step, 'loss': vals, 'lr': trainer.opt.decayed_lr(current_step)}
+            summ.write(json.dumps(rec) + '\n')
+            summ.flush()
+        if F.save_every_n_steps is not None and current_step % F.save_every_n_steps == F.save_every_n_steps - 1 \
+                and rank == 0:
+            logger.info('Saving model...')
+            save_ckpt(store, os.path.join(F.train_dir, F.backbone_name + '.model'), current_step + 1)
+            logger.info('Save model sucess...')
+        if F.max_number_of_steps is not None and current_step >= F.max_number_of_steps:
+            logger.info('Exit training...')
+            break
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()
