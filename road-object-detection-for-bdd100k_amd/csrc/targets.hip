@@ -211,23 +211,16 @@ __global__ void boxes_convert_kernel(const float* __restrict__ in, float* __rest
 }
 
 // dst[r, c] = src[r, c] for a rows x cols block with independent row strides (bytes)
+template <int WB>
 __global__ void copy2d_kernel(const char* __restrict__ src, long sld, char* __restrict__ dst, long dld, long rows,
-                              long cols_bytes) {
-  const long r = blockIdx.y;
-  if (r >= rows) return;
-  const char* s = src + r * sld;
-  char* d = dst + r * dld;
-  if ((((uintptr_t)s | (uintptr_t)d | (uintptr_t)cols_bytes) & 15) == 0) {
-    for (long c = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 16; c < cols_bytes;
-         c += (long)gridDim.x * blockDim.x * 16)
-      *(f32x4*)(d + c) = *(const f32x4*)(s + c);
-  } else if ((((uintptr_t)s | (uintptr_t)d | (uintptr_t)cols_bytes) & 3) == 0) {
-    for (long c = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; c < cols_bytes;
-         c += (long)gridDim.x * blockDim.x * 4)
-      *(float*)(d + c) = *(const float*)(s + c);
-  } else {
-    for (long c = (long)blockIdx.x * blockDim.x + threadIdx.x; c < cols_bytes; c += (long)gridDim.x * blockDim.x)
-      d[c] = s[c];
+                              long chunks) {
+  // flattened (row, chunk) grid-stride: efficient for many short rows (channel concat)
+  const long total = rows * chunks;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / chunks, c = (i - r * chunks) * WB;
+    if constexpr (WB == 16) *(f32x4*)(dst + r * dld + c) = *(const f32x4*)(src + r * sld + c);
+    else if constexpr (WB == 4) *(float*)(dst + r * dld + c) = *(const float*)(src + r * sld + c);
+    else dst[r * dld + c] = src[r * sld + c];
   }
 }
 
@@ -305,11 +298,23 @@ int rod_boxes_convert(const float* in, float* out, long n_boxes, int to_center, 
 
 int rod_copy2d(const void* src, long src_ld_bytes, void* dst, long dst_ld_bytes, long rows, long cols_bytes,
                void* stream) {
-  ROD_CHECK_ARG(rows >= 0 && cols_bytes >= 0 && rows <= 65535, "rod_copy2d: bad extent");
+  ROD_CHECK_ARG(rows >= 0 && cols_bytes >= 0, "rod_copy2d: bad extent");
   if (rows == 0 || cols_bytes == 0) return 0;
-  int gx = (int)std::min<long>(cdivl(cols_bytes, 256 * 16), 1024);
-  hipLaunchKernelGGL(copy2d_kernel, dim3(gx, rows), dim3(256), 0, ROD_STREAM(stream), (const char*)src,
-                     src_ld_bytes, (char*)dst, dst_ld_bytes, rows, cols_bytes);
+  const uintptr_t al = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)src_ld_bytes | (uintptr_t)dst_ld_bytes |
+                       (uintptr_t)cols_bytes;
+  hipStream_t s = ROD_STREAM(stream);
+  const int wb = (al & 15) == 0 ? 16 : ((al & 3) == 0 ? 4 : 1);
+  const long chunks = cols_bytes / wb;
+  const int grid = (int)std::min<long>(cdivl(rows * chunks, 256), 8192);
+  if (wb == 16)
+    hipLaunchKernelGGL(copy2d_kernel<16>, dim3(grid), dim3(256), 0, s, (const char*)src, src_ld_bytes, (char*)dst,
+                       dst_ld_bytes, rows, chunks);
+  else if (wb == 4)
+    hipLaunchKernelGGL(copy2d_kernel<4>, dim3(grid), dim3(256), 0, s, (const char*)src, src_ld_bytes, (char*)dst,
+                       dst_ld_bytes, rows, chunks);
+  else
+    hipLaunchKernelGGL(copy2d_kernel<1>, dim3(grid), dim3(256), 0, s, (const char*)src, src_ld_bytes, (char*)dst,
+                       dst_ld_bytes, rows, chunks);
   return check_launch("rod_copy2d");
 }
 

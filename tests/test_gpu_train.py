@@ -77,6 +77,9 @@ def test_refine_step_matches_oracle(dev, dtype):
     p0 = tr.net.store.flat.detach().clone()
     P32, mov32, ref32, loss32 = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.float32)
     P64, mov64, ref64, loss64 = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.float64)
+    if dtype == torch.bfloat16:
+        # baseline: the same oracle step evaluated with every tensor in bf16 (PyTorch CPU)
+        Pb, movb, refb, _ = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.bfloat16)
 
     from nets.catch_net import factory
     import utils.net_tools as nt
@@ -88,9 +91,6 @@ def test_refine_step_matches_oracle(dev, dtype):
     loss = nt.refine_loss(out, tg[0], tg[3], targets=tg)
     loss.backward()
     report = []
-    if dtype == torch.bfloat16:
-        # baseline: the same oracle step evaluated with every tensor in bf16 (PyTorch CPU)
-        Pb, _, refb, _ = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.bfloat16)
     for l, (a, o32, o64) in enumerate(zip(out, ref32, ref64)):
         e_h, e_o = _nerr(a, o64), _nerr(o32, o64)
         report.append((l, e_h, e_o))
@@ -109,8 +109,8 @@ def test_refine_step_matches_oracle(dev, dtype):
         e_o = _nerr(mov32[k], v)
         if dtype == torch.float32:
             assert _nerr(got, v) <= max(1e-4, 4 * e_o), k
-        elif e_o < 1e-2:
-            assert _cos(got, v) >= 0.98, k
+        elif e_o < 1e-2 and _cos(movb[k].float(), v) >= 0.95:
+            assert _cos(got, v) >= min(0.98, _cos(movb[k].float(), v) - 0.02), k
     bad = []
     for name, p in tr.net.store.params.items():
         g64, g32, gd = P64[name].grad, P32[name].grad, p._rod_grad
@@ -171,7 +171,7 @@ def test_all_mode_step_matches_oracle(dev):
     ref = op.det_clf_loss(do, r_gt, r_pos, co, r_lbl, r_iou, tab.lvl_off, B)
     assert abs(d_loss.item() - ref['det_loss']) <= 1e-5 * abs(ref['det_loss'])
     assert abs(c_loss.item() - ref['clf_loss']) <= 1e-5 * abs(ref['clf_loss'])
-    st = nt.det_clf_loss.last_stats.cpu().numpy()
+    st = nt.det_clf_loss.last_stats.detach().cpu().numpy()
     assert st[3] == np.float32(ref['max_hard_pred']) and int(st[6]) == ref['n_neg_selected']
     # same upstream gradients into both oracle graphs; fp64 graph is the truth
     gd = torch.from_numpy(ref['g_det'])
