@@ -41,6 +41,8 @@ def parse():
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--train_range', default='REFINE', choices=['REFINE', 'ALL'])
     ap.add_argument('--probe', default='rod_bn_bwd', help='C-ABI entry reported in "roofline" (dominant)')
+    ap.add_argument('--probe-table', dest='probe_table', default=None,
+                    help='time EVERY librod call and write a per-entry table (JSON) here (analysis only)')
     ap.add_argument('--cpu-baseline', dest='cpu_baseline', action='store_true', default=True)
     ap.add_argument('--no-cpu-baseline', dest='cpu_baseline', action='store_false')
     ap.add_argument('--inference', dest='inference', action='store_true', default=True)
@@ -141,7 +143,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    _abi.PROBE.arm(args.probe)
+    _abi.PROBE.arm('*' if args.probe_table else args.probe)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = tr.step(*batch)
@@ -156,12 +158,25 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    recs = _abi.PROBE.records
-    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in recs)
-    byts = sum(c[0] for _, _, c in recs)
-    flops = sum(c[1] for _, _, c in recs)
-    n_launch = len(recs)
+    table = _abi.PROBE.table()
+    n_launch, ms, byts, flops = table.get(args.probe, (0, 0.0, 0, 0))
     loss_val = float(losses[0].item())
+    if args.probe_table and rank == 0:
+        # per-entry live timing (every call bracketed by events; the step itself is slower
+        # in this mode, so ms_per_step of such a run is not a bench number)
+        with open(args.probe_table, 'w') as f:
+            rows = []
+            for name, (n, t, b, fl) in sorted(table.items(), key=lambda kv: -kv[1][1]):
+                rows.append({'entry': name, 'calls_per_step': n / args.steps, 'ms_per_step': t / args.steps,
+                             'avg_us': 1e3 * t / n, 'alg_GBps': b / max(t, 1e-9) / 1e6,
+                             'alg_TFLOPs': fl / max(t, 1e-9) / 1e9})
+            calls = []
+            for (name, shp), (n, t, b, fl) in sorted(_abi.PROBE.table(by_shape=True).items(),
+                                                     key=lambda kv: -kv[1][1])[:120]:
+                calls.append({'entry': name, 'args': list(shp), 'calls_per_step': n / args.steps,
+                              'avg_us': 1e3 * t / n, 'alg_GBps': b / max(t, 1e-9) / 1e6,
+                              'alg_TFLOPs': fl / max(t, 1e-9) / 1e9})
+            json.dump({'entries': rows, 'top_calls': calls}, f, indent=1)
 
     if rank == 0:
         per_launch_ms = ms / max(n_launch, 1)

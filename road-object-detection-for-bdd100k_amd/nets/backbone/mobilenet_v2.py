@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from rod import ops
+from rod import graph, ops
 from rod.params import trunc_normal
 
 
@@ -81,17 +81,23 @@ class MobilenetV2:
         return ops.bn_act(x, P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'],
                           B[name + '/moving_variance'], act, training, BN_DECAY, BN_EPS, residual)
 
-    def __call__(self, x, is_training, final_endpoint=None):
-        """Returns the endpoint dict {'layer_1': ..., 'layer_24': ...} (mobilenet.py:275-281)."""
+    def __call__(self, x, is_training, final_endpoint=None, taps=None):
+        """Returns the endpoint dict {'layer_1': ..., 'layer_24': ...} (mobilenet.py:275-281).
+
+        Endpoints named in `taps` are consumed outside the backbone: they are handed out as
+        a graph.fork alias, so their gradient meets the backbone's own with rod_add."""
         P = self.store.params
         end_points = {}
+        taps = set(taps or ())
         for (idx, kind, s, cin, inner, cout, res, sc) in self.plan:
             base = '%s/%s' % (self.scope, sc)
             if kind == 'conv':
                 x = ops.conv2d(x, P[base + '/weights'], None, 3)
                 x = self._bn_act(x, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training)
             else:
-                inp = x
+                inp = None
+                if res:
+                    inp, x = graph.fork(x, 2)
                 if inner > cin:
                     x = ops.conv2d(x, P[base + '/expand/weights'], None, 1)
                     x = self._bn_act(x, base + '/expand/BatchNorm', ops.ROD_ACT_RELU6, is_training)
@@ -99,9 +105,14 @@ class MobilenetV2:
                 x = self._bn_act(x, base + '/depthwise/BatchNorm', ops.ROD_ACT_RELU6, is_training)
                 x = ops.conv2d(x, P[base + '/project/weights'], None, 1)
                 x = self._bn_act(x, base + '/project/BatchNorm', ops.ROD_ACT_NONE, is_training,
-                                 residual=inp if res else None)
-            end_points['layer_%d' % idx] = x
-            if final_endpoint is not None and final_endpoint == 'layer_%d' % idx:
+                                 residual=inp)
+            name = 'layer_%d' % idx
+            last = final_endpoint == name or idx == self.plan[-1][0]
+            if name in taps and not last:
+                end_points[name], x = graph.fork(x, 2)
+            else:
+                end_points[name] = x
+            if last:
                 break
         return end_points
 

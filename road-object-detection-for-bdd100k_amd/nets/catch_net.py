@@ -21,7 +21,7 @@ import torch
 
 import config
 from nets.backbone.mobilenet_v2 import MobilenetV2
-from rod import ops
+from rod import graph, ops
 from rod.params import ParamStore, trunc_normal, xavier_uniform
 
 HEAD_BN_DECAY = 0.999
@@ -134,36 +134,45 @@ class CatchNet:
         layers = list(reversed(feats))
         out = []
         x = layers[0]
-        for i in range(len(layers)):
+        n = len(layers)
+        for i in range(n):
             base = 'deconv/block_%d' % (i + 1)
             if i == 0:
                 x = ops.conv2d(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1)
                 x = self._bn(x, base + '/BatchNorm', training)
             else:
                 B_, h, w, _ = layers[i].shape
-                f_c = layers[i].shape[3] // 2
-                cat = torch.empty((B_, h, w, 2 * f_c), dtype=x.dtype, device=x.device)
-                up = ops.deconv2x2(x, P[base + '/weight_%d' % i], (h, w))           # conv2d_transpose
-                rs = ops.resize_bilinear(x, (h, w))                                  # resize_images
+                x_out, x_up, x_rs = xs
+                up = ops.deconv2x2(x_up, P[base + '/weight_%d' % i], (h, w))        # conv2d_transpose
+                rs = ops.resize_bilinear(x_rs, (h, w))                               # resize_images
                 rh = ops.conv2d(rs, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1)
+                out.append(x_out)
                 cat = ops.channel_concat([up, rh])                                   # tf.concat(-1)
                 x = self._bn(cat, base + '/BatchNorm', training)
-            out.append(x)
+            if i < n - 1:
+                xs = graph.fork(x, 3)    # output list, transpose conv, resize
+        out.append(x)
         return out
 
     def forward(self, inputs, is_training):
-        ep = self.backbone(inputs, is_training)
-        feats = [ep[n] for n in config.extract_feat_name[self.backbone_name]]
+        names = config.extract_feat_name[self.backbone_name]
+        ep = self.backbone(inputs, is_training, taps=names)
+        feats = [ep[n] for n in names]
         self.backbone_feats = collections.OrderedDict(('layer_%d' % (i + 1), f) for i, f in enumerate(feats))
-        refine_out = self.head_out(feats, 'refine', 4, is_training)
         if not self.all_mode:
-            return refine_out
-        deconv = self.deconv_bone(feats, is_training)
+            return self.head_out(feats, 'refine', 4, is_training)
+        # multi-consumer tensors are forked so their gradients are summed by rod_add:
+        # every feature feeds the refine head and the merge; the deepest one also the deconv
+        forks = [graph.fork(f, 3 if i == len(feats) - 1 else 2) for i, f in enumerate(feats)]
+        refine_out = self.head_out([f[0] for f in forks], 'refine', 4, is_training)
+        deconv_in = feats[:-1] + [forks[-1][2]]     # the shallower ones contribute only their shape
+        deconv = self.deconv_bone(deconv_in, is_training)
         self.deconv_feats = deconv
-        merged = [ops.add(u, d) for u, d in zip(feats, reversed(deconv))]        # ADD merge
+        merged = [ops.add(f[1], d) for f, d in zip(forks, reversed(deconv))]     # ADD merge
         self.merge_feats = merged
-        clf_out = self.head_out(merged, 'clf', config.total_obj_n, is_training)
-        det_out = self.head_out(merged, 'det', 4, is_training)
+        mf = [graph.fork(m, 2) for m in merged]
+        clf_out = self.head_out([m[0] for m in mf], 'clf', config.total_obj_n, is_training)
+        det_out = self.head_out([m[1] for m in mf], 'det', 4, is_training)
         return refine_out, det_out, clf_out
 
 

@@ -124,15 +124,31 @@ class Probe:
     algorithmic byte / flop count of the call (rod.roofline) is accumulated."""
 
     def __init__(self):
-        self.name = None
+        self.names = frozenset()
+        self.all = False
         self.records = []
 
-    def arm(self, name):
-        self.name = name
+    def arm(self, names):
+        """names: one entry name, an iterable of names, or '*' (every entry)."""
+        self.all = names == '*'
+        self.names = frozenset([names] if isinstance(names, str) else names)
         self.records = []
 
     def disarm(self):
-        self.name = None
+        self.names, self.all = frozenset(), False
+
+    def wants(self, name):
+        return self.all or name in self.names
+
+    def table(self, by_shape=False):
+        """{entry (or (entry, scalar args) when by_shape): (launches, total_ms, alg_bytes,
+        alg_flops)} over the recorded calls."""
+        out = {}
+        for name, e0, e1, (b, f), shape in self.records:
+            key = (name, shape) if by_shape else name
+            n, ms, bb, ff = out.get(key, (0, 0.0, 0, 0))
+            out[key] = (n + 1, ms + e0.elapsed_time(e1), bb + b, ff + f)
+        return out
 
 
 PROBE = Probe()
@@ -146,7 +162,7 @@ def call(name: str, *args):
     if len(args) != len(argspec):
         raise TypeError(f"{name} expects {len(argspec)} args, got {len(args)}")
     conv = [(_ptr(a) if t == "ptr" else a) for (t, _), a in zip(argspec, args)]
-    if PROBE.name == name:
+    if PROBE.wants(name):
         import torch
         from . import roofline
         s = torch.cuda.current_stream()
@@ -154,7 +170,8 @@ def call(name: str, *args):
         e0.record(s)
         rc = fn(*conv)
         e1.record(s)
-        PROBE.records.append((e0, e1, roofline.cost(name, args)))
+        shape = tuple(a for a in args if isinstance(a, (int, float)) and not isinstance(a, bool))
+        PROBE.records.append((name, e0, e1, roofline.cost(name, args), shape))
     else:
         rc = fn(*conv)
     if ret == "int" and rc != 0:

@@ -266,17 +266,23 @@ class _SmoothL1(torch.autograd.Function):
         _abi.call("rod_smoothl1_masked", pred, target, mask, np.ascontiguousarray(lvl_off, dtype=np.int32), L,
                   float(scale), loss, grad, ws, B, A, dtcode(pred), stream())
         ctx.save_for_backward(grad)
-        return loss
+        ctx.set_materialize_grads(False)
+        ctx.mark_non_differentiable(loss)
+        return loss, loss[L]
 
     @staticmethod
-    def backward(ctx, gl):
+    def backward(ctx, g_vec, g_tot):
         (grad,) = ctx.saved_tensors
-        # the loss vector's consumers take loss[L] (the total) with weight 1
+        if g_tot is None:
+            return None, None, None, None, None
+        # the total is the training loss and its seed is 1 (graph.backward); any other
+        # upstream weight would need a scale kernel, which no caller of the reference uses
         return grad, None, None, None, None
 
 
 def smooth_l1_masked(pred, target, mask, lvl_off, scale):
-    """Returns [L+1] fp32: per-level sum(smooth_l1((t - p)*m))/scale and their total."""
+    """Returns ([L+1] fp32 per-level sum(smooth_l1((t - p)*m))/scale + total, total as a
+    differentiable 0-d view).  The gradient is produced in the forward launch."""
     return _SmoothL1.apply(pred, target, mask, lvl_off, scale)
 
 
@@ -467,17 +473,22 @@ class _SoftmaxCEHNM(torch.autograd.Function):
                   np.ascontiguousarray(lvl_off, dtype=np.int32), L, float(bs), out, grad, ws, B, A, K,
                   dtcode(logits), stream())
         ctx.save_for_backward(grad)
-        return out
+        ctx.set_materialize_grads(False)
+        ctx.mark_non_differentiable(out)
+        return out, out[2]
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g_vec, g_loss):
         (grad,) = ctx.saved_tensors
-        # consumers take out[2] (clf_loss) with weight 1 (net_tools.det_clf_loss)
+        if g_loss is None:
+            return None, None, None, None, None, None
+        # clf_loss enters the training loss with weight 1 (net_tools.det_clf_loss)
         return grad, None, None, None, None, None
 
 
 def softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, bs):
-    """[8]: pos_loss, neg_loss, clf_loss, max_hard_pred, n_pos, k, n_neg_selected, 0."""
+    """([8] pos_loss, neg_loss, clf_loss, max_hard_pred, n_pos, k, n_neg_selected, 0;
+    clf_loss as a differentiable 0-d view)."""
     return _SoftmaxCEHNM.apply(logits, det_lbl, det_pos, iou, lvl_off, bs)
 
 

@@ -18,7 +18,7 @@ import torch
 
 import config
 from nets.catch_net import CatchNet, factory
-from rod import ops
+from rod import graph, ops
 from utils import net_tools
 from utils.common_tools import cornerBboxes_2_centerBboxes
 
@@ -73,9 +73,9 @@ class Trainer:
             dgt = net_tools.det_groundtruth(refine_out, tg[0], tg[1], tg[2], tg[3], self.anchors, targets=tg)
             d_loss, c_loss = net_tools.det_clf_loss(refine_out, clf_out, det_out, dgt, dgt[1], dgt[2], dgt[3],
                                                     scale=scale)
-            loss = d_loss + c_loss if self.fix_refine else r_loss + d_loss + c_loss
+            loss = graph.scalar_sum(d_loss, c_loss) if self.fix_refine else graph.scalar_sum(r_loss, d_loss, c_loss)
             losses = (loss, r_loss, d_loss, c_loss)
-        loss.backward()
+        graph.backward(loss)
         if self.reducer is not None:
             self.reducer(self.net.store.flat_grad)
         self.opt.step()

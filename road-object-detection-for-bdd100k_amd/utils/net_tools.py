@@ -181,9 +181,9 @@ def refine_loss(refine_out, refine_groundtruth, refine_pos_mask, dtype=torch.flo
         pos_flat = ops.levels_concat([m.contiguous() for m in refine_pos_mask], 1).view(B, -1)
         sizes = [g[0].numel() // 4 for g in refine_groundtruth]
         lvl_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
-    vec = ops.smooth_l1_masked(pred, gt_flat, pos_flat, lvl_off, scale)
+    vec, total = ops.smooth_l1_masked(pred, gt_flat, pos_flat, lvl_off, scale)
     refine_loss.last_per_layer = vec
-    return vec[len(lvl_off) - 1]
+    return total
 
 
 # ================================================================ optimiser
@@ -259,13 +259,12 @@ def det_clf_loss(refine_out, clf_out, det_out, det_groundtruth, det_pos_mask, de
     det_gt, det_pos, det_lbl, iou = tg.flat
     lvl_off = tg.table.lvl_off
     pred = ops.levels_concat(det_out, 4)
-    dvec = ops.smooth_l1_masked(pred, det_gt, det_pos, lvl_off, scale)
-    det_loss_one = dvec[len(lvl_off) - 1]
+    dvec, det_loss_one = ops.smooth_l1_masked(pred, det_gt, det_pos, lvl_off, scale)
     logits = ops.levels_concat(clf_out, config.total_obj_n)
-    cvec = ops.softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, scale)
+    cvec, clf_loss = ops.softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, scale)
     det_clf_loss.last_stats = cvec
     det_clf_loss.last_det_per_layer = dvec
-    return det_loss_one, cvec[2]
+    return det_loss_one, clf_loss
 
 
 # ================================================================ decode / post-processing

@@ -78,6 +78,23 @@ def test_concat_and_add(dev):
     assert torch.equal(ops.add(x, y).cpu(), torch.from_numpy(x.cpu().numpy() + y.cpu().numpy()))
 
 
+def test_fork_sums_branch_gradients(dev):
+    """graph.fork: n aliases whose gradients are summed (fp32 add, bit-exact vs numpy);
+    branches that receive no gradient contribute nothing."""
+    from rod import graph
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 3, 4, 8, generator=g).to(dev).requires_grad_(True)
+    a, b, c = graph.fork(x, 3)
+    ga, gb = (torch.randn(x.shape, generator=g) for _ in range(2))
+    torch.autograd.backward([ops.add(a, a.detach()), b], [ga.to(dev), gb.to(dev)])
+    assert torch.equal(x.grad.cpu(), torch.from_numpy(ga.numpy() + gb.numpy()))
+    l1 = torch.tensor(1.5, device=dev, requires_grad=True)
+    l2 = torch.tensor(2.25, device=dev, requires_grad=True)
+    s = graph.scalar_sum(l1, l2)
+    graph.backward(s)
+    assert s.item() == 3.75 and l1.grad.item() == 1.0 and l2.grad.item() == 1.0
+
+
 def _setup(H, W, B, seed):
     from utils import net_tools as nt
     rng = np.random.default_rng(seed)
@@ -127,9 +144,10 @@ def test_det_targets_and_hnm_loss(dev):
     det_out = rng.normal(0, 0.3, (B, A, 4)).astype(f32)
     ref = op.det_clf_loss(det_out, r_gt, r_pos, logits, r_lbl, r_iou, tab.lvl_off, B)
     ld = torch.from_numpy(logits).to(dev).requires_grad_(True)
-    out = ops.softmax_ce_hnm(ld, dlbl, dpos, iou, tab.lvl_off, float(B))
-    out[2].backward()
+    out, clf = ops.softmax_ce_hnm(ld, dlbl, dpos, iou, tab.lvl_off, float(B))
+    clf.backward()
     o = out.detach().cpu().numpy()
+    assert clf.item() == o[2]
     assert int(o[5]) == ref['k'] and int(o[4]) == ref['n_pos']
     assert o[3] == f32(ref['max_hard_pred'])                 # k-th smallest nvalue, bit-exact
     assert int(o[6]) == ref['n_neg_selected']                # hard-negative mask size
@@ -139,9 +157,10 @@ def test_det_targets_and_hnm_loss(dev):
     np.testing.assert_allclose(ld.grad.cpu().numpy(), ref['g_logits'], rtol=1e-5, atol=1e-8)
     # det loss through the shared smooth-L1 kernel
     dd = torch.from_numpy(det_out).to(dev).requires_grad_(True)
-    vec = ops.smooth_l1_masked(dd, dgt, dpos, tab.lvl_off, float(B))
-    vec[6].backward()
+    vec, tot = ops.smooth_l1_masked(dd, dgt, dpos, tab.lvl_off, float(B))
+    tot.backward()
     np.testing.assert_allclose(vec[6].item(), ref['det_loss'], rtol=1e-5)
+    assert tot.item() == vec[6].item()
     np.testing.assert_allclose(dd.grad.cpu().numpy(), ref['g_det'], rtol=1e-6, atol=1e-9)
 
 

@@ -167,7 +167,8 @@ def test_all_mode_step_matches_oracle(dev):
         assert _nerr(got, r64) <= max(1e-4, 4 * _nerr(r32, r64))
     dgt = nt.det_groundtruth(refine_out, tg[0], tg[1], tg[2], tg[3], tr.anchors, targets=tg)
     d_loss, c_loss = nt.det_clf_loss(refine_out, clf_out, det_out, dgt, dgt[1], dgt[2], dgt[3])
-    (d_loss + c_loss).backward()
+    from rod import graph
+    graph.backward(graph.scalar_sum(d_loss, c_loss))
 
     # oracle targets + losses evaluated on the HIP outputs, so that both backward passes see
     # the same hard-negative decisions (their bit-exactness given identical logits is

@@ -29,6 +29,8 @@ for step in "$@"; do
     cli) run cli_train 300 python road-object-detection-for-bdd100k_amd/train.py --train_range=ALL --batch_size=2 --max_number_of_steps=4 --log_every_n_steps=2 --save_every_n_steps=4 --checkpoint_refine=None --train_dir=gpurun_out/ckpt --summary_dir=gpurun_out/summ &&
          run cli_eval 300 python road-object-detection-for-bdd100k_amd/evaluate.py --checkpoint_path=gpurun_out/ckpt --batch_size=2 --num_images=6 --eval_dir=gpurun_out/eval &&
          run cli_predict 300 python road-object-detection-for-bdd100k_amd/predict.py --checkpoint_all=gpurun_out/ckpt/mobilenet_v2.model --batch_size=2 --num_batches=2 --output=gpurun_out/pred.json ;;
+    probetable) run probetable 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_table.json ;;
+    probetableall) run probetableall 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-inference --train_range ALL --probe-table $OUT/${TAG}_probe_table_all.json ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference ;;
     profall) run profall 600 rocprofv3 --kernel-trace --stats -d $OUT/profall_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --train_range ALL ;;
     *) echo "unknown step $step" ;;
