@@ -25,27 +25,44 @@ int check_launch(const char* what) {
 }
 
 // ---------------------------------------------------------------- slab reduction
+// block = CB columns x (256/CB) slab lanes; each lane keeps 4 independent f64 partials
+// (4 loads in flight), then a fixed-order LDS combine.  CB is chosen so that short rows
+// with many slabs (filter gradients: n = 9*C, thousands of parts) still fill the chip.
+template <int CB>
 __global__ void __launch_bounds__(256) slab_sum_kernel(const float* __restrict__ slab, float* __restrict__ out,
                                                        int nslab, long n) {
-  __shared__ double red[8][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const long i = (long)blockIdx.x * 32 + tx;
-  double s = 0.0;
-  if (i < n)
-    for (int b = ty; b < nslab; b += 8) s += (double)slab[(long)b * n + i];
-  red[ty][tx] = s;
+  constexpr int L = 256 / CB;
+  __shared__ double red[L][CB + 1];
+  const int tx = threadIdx.x % CB, ty = threadIdx.x / CB;
+  const long i = (long)blockIdx.x * CB + tx;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (i < n) {
+    int b = ty;
+    for (; b + 3 * L < nslab; b += 4 * L) {
+      s0 += (double)slab[(long)b * n + i];
+      s1 += (double)slab[(long)(b + L) * n + i];
+      s2 += (double)slab[(long)(b + 2 * L) * n + i];
+      s3 += (double)slab[(long)(b + 3 * L) * n + i];
+    }
+    for (; b < nslab; b += L) s0 += (double)slab[(long)b * n + i];
+  }
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (ty == 0 && i < n) {
     double t = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += red[k][tx];
+    for (int k = 0; k < L; ++k) t += red[k][tx];
     out[i] = (float)t;
   }
 }
 
 void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(cdivl(n, 32)), dim3(256), 0, s, slab, out, nslab, n);
+  if (n >= 256L * 32 || nslab <= 64)
+    hipLaunchKernelGGL(slab_sum_kernel<32>, dim3(cdivl(n, 32)), dim3(256), 0, s, slab, out, nslab, n);
+  else if (n >= 256L * 8)
+    hipLaunchKernelGGL(slab_sum_kernel<8>, dim3(cdivl(n, 8)), dim3(256), 0, s, slab, out, nslab, n);
+  else
+    hipLaunchKernelGGL(slab_sum_kernel<4>, dim3(cdivl(n, 4)), dim3(256), 0, s, slab, out, nslab, n);
 }
 
 int const_channel_blocks(int CV, long total, int target) {

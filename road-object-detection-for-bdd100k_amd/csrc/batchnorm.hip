@@ -27,29 +27,28 @@ __device__ __forceinline__ float act_grad(float z, int act) {
   return 1.f;
 }
 
+// Row-chunk reduction plan shared by the statistics and backward-reduce kernels.
+// CV channel vectors are split into cgroups of CVb <= 256 (blockIdx.y); the 256 threads of a
+// block are `lanes` row lanes x CVb channel vectors (no power-of-two padding, so at most
+// CVb-1 threads idle); blockIdx.x owns `chunk` consecutive rows.  ~1024 blocks keep >= 16 MB
+// of loads in flight (4 unrolled 16-byte loads per thread), which HBM needs to stream.
 struct RedPlan {
-  int V, CV, CVp, cgroups, nbx;
+  int V, CV, CVb, cgroups, lanes, nbx;
   long chunk;
 };
-
-static int p2(int v) {
-  int p = 1;
-  while (p < v) p <<= 1;
-  return p;
-}
 
 template <typename T>
 static RedPlan red_plan(long M, int C, bool vec) {
   RedPlan r;
   r.V = vec ? Vec16<T>::N : 1;
   r.CV = C / r.V;
-  r.CVp = std::min(p2(r.CV), 256);
-  r.cgroups = cdiv(r.CV, r.CVp);
-  long want = std::max<long>(1, 512 / r.cgroups);
-  long lanes = 256 / r.CVp;
-  long chunk = std::max<long>(cdivl(M, want), lanes * 16);
-  r.chunk = chunk;
-  r.nbx = (int)cdivl(M, chunk);
+  r.cgroups = cdiv(r.CV, 256);
+  r.CVb = cdiv(r.CV, r.cgroups);
+  r.lanes = 256 / r.CVb;
+  const long want = std::max<long>(1, 1024 / r.cgroups);
+  const long minchunk = (long)r.lanes * 16;
+  r.chunk = std::max<long>(cdivl(M, want), minchunk);
+  r.nbx = (int)cdivl(M, r.chunk);
   return r;
 }
 
@@ -77,17 +76,19 @@ __device__ __forceinline__ void store_v(T* p, const float (&in)[VEC ? Vec16<T>::
 }
 
 // ---------------------------------------------------------------- statistics
+// Per block: pivot k = x[first row of the chunk, c]; s1 = sum(x-k), s2 = sum((x-k)^2) per
+// thread (fp32), lane partials combined in f64 in fixed order; the block emits its exact
+// (mean_b, M2_b) pair so the finalize is Chan's parallel merge (no global cancellation).
 template <typename T, bool VEC>
-__global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, long M, int C, int ldx, int CVp,
-                                                       long chunk, float* __restrict__ slab) {
+__global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, long M, int C, int ldx, int CVb,
+                                                       int lanes, long chunk, float* __restrict__ slab) {
   constexpr int V = VEC ? Vec16<T>::N : 1;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [2][256][V]
   const int tid = threadIdx.x;
-  const int lanes = 256 / CVp;
-  const int cvl = tid % CVp, pln = tid / CVp;
+  const int cvl = tid % CVb, pln = tid / CVb;
   const int CV = C / V;
-  const int cv = blockIdx.y * CVp + cvl;
-  const bool active = cv < CV;
+  const int cv = blockIdx.y * CVb + cvl;
+  const bool active = pln < lanes && cv < CV;
   const int c = cv * V;
   const long r0 = (long)blockIdx.x * chunk;
   const long r1 = r0 + chunk < M ? r0 + chunk : M;
@@ -95,13 +96,27 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
 #pragma unroll
   for (int v = 0; v < V; ++v) s1[v] = s2[v] = 0.f;
   if (active) {
-    load_v<T, VEC>(x + c, k);
-    for (long r = r0 + pln; r < r1; r += lanes) {
-      float xv[V];
-      load_v<T, VEC>(x + r * ldx + c, xv);
+    load_v<T, VEC>(x + r0 * ldx + c, k);
+    long r = r0 + pln;
+    for (; r + 3L * lanes < r1; r += 4L * lanes) {
+      float a[4][V];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load_v<T, VEC>(x + (r + (long)u * lanes) * ldx + c, a[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float d = a[u][v] - k[v];
+          s1[v] += d;
+          s2[v] = fmaf(d, d, s2[v]);
+        }
+    }
+    for (; r < r1; r += lanes) {
+      float a[V];
+      load_v<T, VEC>(x + r * ldx + c, a);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        const float d = xv[v] - k[v];
+        const float d = a[v] - k[v];
         s1[v] += d;
         s2[v] = fmaf(d, d, s2[v]);
       }
@@ -113,73 +128,67 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
     red[(256 + tid) * V + v] = s2[v];
   }
   __syncthreads();
-  for (int s = lanes >> 1; s > 0; s >>= 1) {
-    if (pln < s) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        red[tid * V + v] += red[(tid + s * CVp) * V + v];
-        red[(256 + tid) * V + v] += red[(256 + tid + s * CVp) * V + v];
-      }
+  const double nb = (double)(r1 - r0);
+  for (int e = tid; e < CVb * V; e += 256) {
+    const int cb = e / V, v = e - cb * V;
+    const int cg = blockIdx.y * CVb + cb;
+    if (cg >= CV) continue;
+    double a = 0.0, b = 0.0;
+    for (int l = 0; l < lanes; ++l) {
+      a += (double)red[(l * CVb + cb) * V + v];
+      b += (double)red[(256 + l * CVb + cb) * V + v];
     }
-    __syncthreads();
-  }
-  if (pln == 0 && active) {
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      slab[((long)blockIdx.x * 2 + 0) * C + c + v] = red[tid * V + v];
-      slab[((long)blockIdx.x * 2 + 1) * C + c + v] = red[(256 + tid) * V + v];
-    }
-  }
-}
-
-// sum the two slab rows of 32 channels with 8 lanes each (f64), block = 256 threads
-__device__ __forceinline__ void slab2_sum(const float* __restrict__ slab, int nblk, int C, int c, bool ok, double& a,
-                                          double& b) {
-  __shared__ double red[2][8][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  double s1 = 0.0, s2 = 0.0;
-  if (ok)
-    for (int k = ty; k < nblk; k += 8) {
-      s1 += (double)slab[((long)k * 2 + 0) * C + c];
-      s2 += (double)slab[((long)k * 2 + 1) * C + c];
-    }
-  red[0][ty][tx] = s1;
-  red[1][ty][tx] = s2;
-  __syncthreads();
-  a = b = 0.0;
-  if (ty == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      a += red[0][k][tx];
-      b += red[1][k][tx];
-    }
+    const int ch = cg * V + v;
+    const double kk = (double)to_f32(x[r0 * ldx + ch]);
+    const double m2 = b - a * a / nb;
+    const long nblk = gridDim.x;
+    slab[(long)ch * nblk + blockIdx.x] = (float)(kk + a / nb);
+    slab[((long)C + ch) * nblk + blockIdx.x] = (float)(m2 > 0.0 ? m2 : 0.0);
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) bn_stats_finalize_kernel(const T* __restrict__ x,
-                                                                const float* __restrict__ slab, int nblk, long M,
-                                                                int C, float eps, float decay,
+// Partial slabs are laid out [2][C][nparts] (quantity, channel, part) so that the finalize
+// reads each channel's parts contiguously: one wave per channel, 64 lanes striding over the
+// parts (4 independent loads in flight per lane), f64 accumulation, fixed-order wave tree.
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Chan merge of per-part (mean_b, M2_b) with counts n_b = min(chunk, M - b*chunk):
+// mean = sum n_b mean_b / M, M2 = sum M2_b + n_b (mean_b - mean)^2.  The per-part pairs
+// come from bn_stats_kernel or from a producer's epilogue (rod_conv_fwd with stats).
+__global__ void __launch_bounds__(256) bn_stats_finalize_kernel(const float* __restrict__ slab, int nblk, long chunk,
+                                                                long M, int C, float eps, float decay,
                                                                 float* __restrict__ mean, float* __restrict__ rstd,
                                                                 float* __restrict__ mmean, float* __restrict__ mvar) {
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
-  const bool ok = c < C;
-  double s1, s2;
-  slab2_sum(slab, nblk, C, c, ok, s1, s2);
-  if ((threadIdx.x >> 5) != 0 || !ok) return;
-  const double k = (double)to_f32(x[c]);
-  const double m = s1 / (double)M;
-  double var = s2 / (double)M - m * m;
-  if (var < 0.0) var = 0.0;
-  const float mu = (float)(k + m);
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float* pm = slab + (long)c * nblk;
+  const float* pq = slab + ((long)C + c) * nblk;
+  auto cnt = [&](int b) -> double { const long r = M - (long)b * chunk; return (double)(r < chunk ? r : chunk); };
+  double s = 0.0;
+  for (int b = lane; b < nblk; b += 64) s += cnt(b) * (double)pm[b];
+  const double mu = wave_sum_f64(s) / (double)M;
+  double q = 0.0;
+  for (int b = lane; b < nblk; b += 64) {
+    const double d = (double)pm[b] - mu;
+    q += (double)pq[b] + cnt(b) * d * d;
+  }
+  const double m2 = wave_sum_f64(q);
+  if (lane != 0) return;
+  const double var = m2 / (double)M;
+  const float mu_f = (float)mu;
   const float vf = (float)var;
-  mean[c] = mu;
+  mean[c] = mu_f;
   rstd[c] = (float)(1.0 / sqrt((double)vf + (double)eps));
   if (mmean != nullptr) {
     // slim: assign_moving_average(zero_debias=False): v -= (v - value) * (1 - decay)
     const float one_m = 1.0f - decay;
-    const float unbiased = M > 1 ? (float)(var * (double)M / (double)(M - 1)) : vf;
-    mmean[c] = mmean[c] - (mmean[c] - mu) * one_m;
+    const float unbiased = M > 1 ? (float)(m2 / (double)(M - 1)) : vf;
+    mmean[c] = mmean[c] - (mmean[c] - mu_f) * one_m;
     mvar[c] = mvar[c] - (mvar[c] - unbiased) * one_m;
   }
 }
@@ -235,16 +244,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
                                                             const float* __restrict__ rstd,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, long M, int C, int lddy,
-                                                            int ldx, int act, int CVp, long chunk,
+                                                            int ldx, int act, int CVb, int lanes, long chunk,
                                                             float* __restrict__ slab) {
   constexpr int V = VEC ? Vec16<T>::N : 1;
-  extern __shared__ __attribute__((aligned(16))) float red[];
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][256][V]
   const int tid = threadIdx.x;
-  const int lanes = 256 / CVp;
-  const int cvl = tid % CVp, pln = tid / CVp;
+  const int cvl = tid % CVb, pln = tid / CVb;
   const int CV = C / V;
-  const int cv = blockIdx.y * CVp + cvl;
-  const bool active = cv < CV;
+  const int cv = blockIdx.y * CVb + cvl;
+  const bool active = pln < lanes && cv < CV;
   const int c = cv * V;
   const long r0 = (long)blockIdx.x * chunk;
   const long r1 = r0 + chunk < M ? r0 + chunk : M;
@@ -259,10 +267,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
       sc[v] = gamma ? rs[v] * gamma[c + v] : rs[v];
       be[v] = beta ? beta[c + v] : 0.f;
     }
-    for (long r = r0 + pln; r < r1; r += lanes) {
-      float xv[V], gv[V];
-      load_v<T, VEC>(x + r * ldx + c, xv);
-      load_v<T, VEC>(dy + r * lddy + c, gv);
+    auto acc = [&](const float (&xv)[V], const float (&gv)[V]) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float d = xv[v] - mu[v];
@@ -271,6 +276,23 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
         sg[v] += g;
         sgx[v] = fmaf(g, d * rs[v], sgx[v]);
       }
+    };
+    long r = r0 + pln;
+    for (; r + 3L * lanes < r1; r += 4L * lanes) {
+      float xa[4][V], ga[4][V];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        load_v<T, VEC>(x + (r + (long)u * lanes) * ldx + c, xa[u]);
+        load_v<T, VEC>(dy + (r + (long)u * lanes) * lddy + c, ga[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc(xa[u], ga[u]);
+    }
+    for (; r < r1; r += lanes) {
+      float xv[V], gv[V];
+      load_v<T, VEC>(x + r * ldx + c, xv);
+      load_v<T, VEC>(dy + r * lddy + c, gv);
+      acc(xv, gv);
     }
   }
 #pragma unroll
@@ -279,22 +301,18 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
     red[(256 + tid) * V + v] = sgx[v];
   }
   __syncthreads();
-  for (int s = lanes >> 1; s > 0; s >>= 1) {
-    if (pln < s) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        red[tid * V + v] += red[(tid + s * CVp) * V + v];
-        red[(256 + tid) * V + v] += red[(256 + tid + s * CVp) * V + v];
-      }
+  for (int e = tid; e < CVb * V; e += 256) {
+    const int cb = e / V, v = e - cb * V;
+    const int cg = blockIdx.y * CVb + cb;
+    if (cg >= CV) continue;
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      a += red[(l * CVb + cb) * V + v];
+      b += red[(256 + l * CVb + cb) * V + v];
     }
-    __syncthreads();
-  }
-  if (pln == 0 && active) {
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      slab[((long)blockIdx.x * 2 + 0) * C + c + v] = red[tid * V + v];
-      slab[((long)blockIdx.x * 2 + 1) * C + c + v] = red[(256 + tid) * V + v];
-    }
+    const long nblk = gridDim.x;
+    slab[(long)(cg * V + v) * nblk + blockIdx.x] = a;
+    slab[((long)C + cg * V + v) * nblk + blockIdx.x] = b;
   }
 }
 
@@ -303,11 +321,19 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ gamma,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ coef) {
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
-  const bool ok = c < C;
-  double sg, sgx;
-  slab2_sum(slab, nblk, C, c, ok, sg, sgx);
-  if ((threadIdx.x >> 5) != 0 || !ok) return;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float* pa = slab + (long)c * nblk;
+  const float* pb = slab + ((long)C + c) * nblk;
+  double a = 0.0, b = 0.0;
+  for (int k = lane; k < nblk; k += 64) {
+    a += (double)pa[k];
+    b += (double)pb[k];
+  }
+  const double sg = wave_sum_f64(a);
+  const double sgx = wave_sum_f64(b);
+  if (lane != 0) return;
   if (dbeta) dbeta[c] = (float)sg;
   if (dgamma) dgamma[c] = (float)sgx;
   coef[c] = gamma ? rstd[c] * gamma[c] : rstd[c];
@@ -398,13 +424,13 @@ static void stats_launch(bool vec, const void* x, long M, int C, int ldx, float 
   dim3 grid(pl.nbx, pl.cgroups);
   size_t lds = 2 * 256 * pl.V * sizeof(float);
   if (vec)
-    hipLaunchKernelGGL((bn_stats_kernel<T, true>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp, pl.chunk,
-                       slab);
-  else
-    hipLaunchKernelGGL((bn_stats_kernel<T, false>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVp,
+    hipLaunchKernelGGL((bn_stats_kernel<T, true>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVb, pl.lanes,
                        pl.chunk, slab);
-  hipLaunchKernelGGL(bn_stats_finalize_kernel<T>, dim3(cdiv(C, 32)), dim3(256), 0, s, (const T*)x,
-                     (const float*)slab, pl.nbx, M, C, eps, decay, mean, rstd, mm, mv);
+  else
+    hipLaunchKernelGGL((bn_stats_kernel<T, false>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVb,
+                       pl.lanes, pl.chunk, slab);
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(cdiv(C, 4)), dim3(256), 0, s, (const float*)slab, pl.nbx,
+                     pl.chunk, M, C, eps, decay, mean, rstd, mm, mv);
 }
 
 template <typename T>
@@ -416,11 +442,11 @@ static void bwd_launch(bool vec, const void* dy, const void* x, const float* mea
   size_t lds = 2 * 256 * pl.V * sizeof(float);
   if (vec)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x, mean,
-                       rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
+                       rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVb, pl.lanes, pl.chunk, slab);
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), grid, dim3(256), lds, s, (const T*)dy, (const T*)x, mean,
-                       rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVp, pl.chunk, slab);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 32)), dim3(256), 0, s, slab, pl.nbx, M, C, rstd, gamma,
+                       rstd, gamma, beta, M, C, lddy, ldx, act, pl.CVb, pl.lanes, pl.chunk, slab);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 4)), dim3(256), 0, s, slab, pl.nbx, M, C, rstd, gamma,
                      dgamma, dbeta, coef);
   const int V = pl.V;
   const int blocks = const_channel_blocks(C / V, M * (C / V));

@@ -12,274 +12,309 @@
 
 namespace rod {
 
-constexpr int DW_R = 4;  // output rows per thread
+// V contiguous elements of T held in registers (bf16 x4 = 8-byte, f32 x4 = 16-byte loads).
+template <typename T, int V> struct PackV;
+template <> struct PackV<float, 4> {
+  f32x4 v;
+  __device__ __forceinline__ void load(const float* p) { v = *(const f32x4*)p; }
+  __device__ __forceinline__ void zero() { v = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+  __device__ __forceinline__ void set(int i, float a) { v[i] = a; }
+  __device__ __forceinline__ void store(float* p) const { *(f32x4*)p = v; }
+};
+template <> struct PackV<bf16_t, 4> {
+  bf16x4 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x4*)p; }
+  __device__ __forceinline__ void zero() { v = bf16x4{(bf16_t)0.f, (bf16_t)0.f, (bf16_t)0.f, (bf16_t)0.f}; }
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+  __device__ __forceinline__ void set(int i, float a) { v[i] = (bf16_t)a; }
+  __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x4*)p = v; }
+};
+template <typename T> struct PackV<T, 1> {
+  T v;
+  __device__ __forceinline__ void load(const T* p) { v = *p; }
+  __device__ __forceinline__ void zero() { v = (T)0.f; }
+  __device__ __forceinline__ float get(int) const { return to_f32(v); }
+  __device__ __forceinline__ void set(int, float a) { v = from_f32<T>(a); }
+  __device__ __forceinline__ void store(T* p) const { *p = v; }
+};
 
-template <typename T, int S, bool VECOK>
+constexpr int DW_RB = 8;  // output rows per thread (forward / backward-data strips)
+
+// Forward: thread = (channel vector cv, output column wo), strip of DW_RB output rows; the
+// 3x3 input window rolls down in registers (one new input row per output row for S=1, two
+// for S=2) and lanes of a wave read consecutive channel vectors of neighbouring pixels.
+template <typename T, int S, int V>
 __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                         T* __restrict__ y, int H, int W, int C, int pt, int pl,
                                                         int Ho, int Wo) {
-  constexpr int V = VECOK ? Vec16<T>::N : 1;
   const int CV = C / V;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int cv = t % CV;
-  const int wo = t / CV;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = (int)(t % CV);
+  const int wo = (int)(t / CV);
   if (wo >= Wo) return;
-  const int ho0 = blockIdx.y * DW_R;
+  const int ho0 = blockIdx.y * DW_RB;
+  const int ho1 = ho0 + DW_RB < Ho ? ho0 + DW_RB : Ho;
   const int n = blockIdx.z;
   const int c = cv * V;
-
   float wr[9][V];
 #pragma unroll
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
-
-  float acc[DW_R][V];
-#pragma unroll
-  for (int q = 0; q < DW_R; ++q)
-#pragma unroll
-    for (int v = 0; v < V; ++v) acc[q][v] = 0.f;
-
-  const long img = (long)n * H * W;
-  constexpr int NR = (DW_R - 1) * S + 3;
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int hi = ho0 * S - pt + r;
-    if (hi < 0 || hi >= H) continue;
-    float xv[3][V];
+  const T* xn = x + (long)n * H * W * C + c;
+  T* yn = y + (long)n * Ho * Wo * C + c;
+  PackV<T, V> xr[3][3];
+  auto load_row = [&](PackV<T, V>(&row)[3], int hi) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int wi = wo * S - pl + j;
-      if (wi >= 0 && wi < W) {
-        const T* p = x + (img + (long)hi * W + wi) * C + c;
-        if constexpr (VECOK) {
-          Vec16<T> vv;
-          vv.load(p);
+      if (hi >= 0 && hi < H && wi >= 0 && wi < W) row[j].load(xn + ((long)hi * W + wi) * C);
+      else row[j].zero();
+    }
+  };
+  load_row(xr[0], ho0 * S - pt);
+  load_row(xr[1], ho0 * S - pt + 1);
+  load_row(xr[2], ho0 * S - pt + 2);
+  for (int ho = ho0; ho < ho1; ++ho) {
+    if (ho > ho0) {
+      if constexpr (S == 1) {
 #pragma unroll
-          for (int v = 0; v < V; ++v) xv[j][v] = vv.get(v);
-        } else {
-          xv[j][0] = to_f32(p[0]);
+        for (int j = 0; j < 3; ++j) {
+          xr[0][j] = xr[1][j];
+          xr[1][j] = xr[2][j];
         }
+        load_row(xr[2], ho - pt + 2);
       } else {
 #pragma unroll
-        for (int v = 0; v < V; ++v) xv[j][v] = 0.f;
+        for (int j = 0; j < 3; ++j) xr[0][j] = xr[2][j];
+        load_row(xr[1], ho * 2 - pt + 1);
+        load_row(xr[2], ho * 2 - pt + 2);
       }
     }
-#pragma unroll
-    for (int q = 0; q < DW_R; ++q) {
-      const int i = r - q * S;  // tap row of output row ho0+q fed by input row r
-      if (i < 0 || i > 2) continue;
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[q][v] = fmaf(xv[j][v], wr[i * 3 + j][v], acc[q][v]);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < DW_R; ++q) {
-    const int ho = ho0 + q;
-    if (ho >= Ho) break;
-    T* p = y + (((long)n * Ho + ho) * Wo + wo) * C + c;
-    if constexpr (VECOK) {
-      Vec16<T> vv;
-#pragma unroll
-      for (int v = 0; v < V; ++v) vv.set(v, acc[q][v]);
-      vv.store(p);
-    } else {
-      p[0] = from_f32<T>(acc[q][0]);
-    }
-  }
-}
-
-// dx[n,h,w,c] = sum_{i,j} dy[n,(h+pt-i)/S,(w+pl-j)/S,c] * w[i,j,c] over exact divisions.
-template <typename T, int S, bool VECOK>
-__global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict__ dy, const float* __restrict__ w,
-                                                             T* __restrict__ dx, int H, int W, int C, int pt,
-                                                             int pl, int Ho, int Wo) {
-  constexpr int V = VECOK ? Vec16<T>::N : 1;
-  const int CV = C / V;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int cv = t % CV;
-  const int wc = t / CV;
-  if (wc >= W) return;
-  const int h0 = blockIdx.y * DW_R;
-  const int n = blockIdx.z;
-  const int c = cv * V;
-
-  float wr[9][V];
-#pragma unroll
-  for (int k = 0; k < 9; ++k)
-#pragma unroll
-    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
-
-  const long img = (long)n * Ho * Wo;
-#pragma unroll
-  for (int q = 0; q < DW_R; ++q) {
-    const int h = h0 + q;
-    if (h >= H) break;
     float acc[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[v] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int hn = h + pt - i;
-      if (hn < 0 || (S == 2 && (hn & 1))) continue;
-      const int ho = hn / S;
-      if (ho >= Ho) continue;
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = fmaf(xr[i][j].get(v), wr[i * 3 + j][v], acc[v]);
+    PackV<T, V> o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) o.set(v, acc[v]);
+    o.store(yn + ((long)ho * Wo + wo) * C);
+  }
+}
+
+// dx[n,h,w,c] = sum_{i,j} dy[n,(h+pt-i)/S,(w+pl-j)/S,c] * w[i,j,c] over exact divisions.
+// S=1: the three dy rows h+pt-i roll down in registers; S=2: direct loads (each dx pixel
+// sees 1, 2 or 4 dy pixels).
+template <typename T, int S, int V>
+__global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict__ dy, const float* __restrict__ w,
+                                                             T* __restrict__ dx, int H, int W, int C, int pt,
+                                                             int pl, int Ho, int Wo) {
+  const int CV = C / V;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = (int)(t % CV);
+  const int wc = (int)(t / CV);
+  if (wc >= W) return;
+  const int h0 = blockIdx.y * DW_RB;
+  const int h1 = h0 + DW_RB < H ? h0 + DW_RB : H;
+  const int n = blockIdx.z;
+  const int c = cv * V;
+  float wr[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+  const T* dn = dy + (long)n * Ho * Wo * C + c;
+  T* xn = dx + (long)n * H * W * C + c;
+  if constexpr (S == 1) {
+    PackV<T, V> dr[3][3];  // dr[i][j] = dy[h+pt-i, wc+pl-j]
+    auto load_row = [&](PackV<T, V>(&row)[3], int ho) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const int wn = wc + pl - j;
-        if (wn < 0 || (S == 2 && (wn & 1))) continue;
-        const int wo = wn / S;
-        if (wo >= Wo) continue;
-        const T* p = dy + (img + (long)ho * Wo + wo) * C + c;
-        if constexpr (VECOK) {
-          Vec16<T> vv;
-          vv.load(p);
+        const int wo = wc + pl - j;
+        if (ho >= 0 && ho < Ho && wo >= 0 && wo < Wo) row[j].load(dn + ((long)ho * Wo + wo) * C);
+        else row[j].zero();
+      }
+    };
+    load_row(dr[0], h0 + pt);
+    load_row(dr[1], h0 + pt - 1);
+    load_row(dr[2], h0 + pt - 2);
+    for (int h = h0; h < h1; ++h) {
+      if (h > h0) {
 #pragma unroll
-          for (int v = 0; v < V; ++v) acc[v] = fmaf(vv.get(v), wr[i * 3 + j][v], acc[v]);
-        } else {
-          acc[0] = fmaf(to_f32(p[0]), wr[i * 3 + j][0], acc[0]);
+        for (int j = 0; j < 3; ++j) {
+          dr[2][j] = dr[1][j];
+          dr[1][j] = dr[0][j];
+        }
+        load_row(dr[0], h + pt);
+      }
+      float acc[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] = fmaf(dr[i][j].get(v), wr[i * 3 + j][v], acc[v]);
+      PackV<T, V> o;
+#pragma unroll
+      for (int v = 0; v < V; ++v) o.set(v, acc[v]);
+      o.store(xn + ((long)h * W + wc) * C);
+    }
+  } else {
+    for (int h = h0; h < h1; ++h) {
+      float acc[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int hn = h + pt - i;
+        if (hn < 0 || (hn & 1)) continue;
+        const int ho = hn >> 1;
+        if (ho >= Ho) continue;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int wn = wc + pl - j;
+          if (wn < 0 || (wn & 1)) continue;
+          const int wo = wn >> 1;
+          if (wo >= Wo) continue;
+          PackV<T, V> g;
+          g.load(dn + ((long)ho * Wo + wo) * C);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] = fmaf(g.get(v), wr[i * 3 + j][v], acc[v]);
         }
       }
-    }
-    T* p = dx + (((long)n * H + h) * W + wc) * C + c;
-    if constexpr (VECOK) {
-      Vec16<T> vv;
+      PackV<T, V> o;
 #pragma unroll
-      for (int v = 0; v < V; ++v) vv.set(v, acc[v]);
-      vv.store(p);
-    } else {
-      p[0] = from_f32<T>(acc[0]);
+      for (int v = 0; v < V; ++v) o.set(v, acc[v]);
+      o.store(xn + ((long)h * W + wc) * C);
     }
   }
 }
 
-// Filter gradient, stage 1: block (bx, by) reduces output pixels [bx*chunk, ...)
-// for channel-vector group by; partial sums [9][C] per bx go to the slab.
-// Thread layout: lane t -> (pixel lane t / CVp, channel vector t % CVp).
-template <typename T, int S, bool VECOK>
+// Filter gradient: dw[i,j,c] = sum_{n,ho,wo} dy[n,ho,wo,c] * x[n, ho*S-pt+i, wo*S-pl+j, c].
+// Thread = (channel vector cv, output column wo) exactly like the forward; it walks strips of
+// RB output rows, keeping the 3x3 input window in registers (one new input row per output
+// row for S=1, two for S=2), so each output pixel costs one dy load and three x loads and no
+// index division.  blockIdx.y strides over the N*spi row strips; each block then sums its
+// threads per channel in LDS (fixed order) and writes one [9][C] partial to the slab.
+template <typename T, int S, int V>
 __global__ void __launch_bounds__(256) dw3x3_bwd_filter_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                                float* __restrict__ slab, int N, int H, int W,
-                                                               int C, int pt, int pl, int Ho, int Wo,
-                                                               int CVp, long chunk) {
-  constexpr int V = VECOK ? Vec16<T>::N : 1;
+                                                               int C, int pt, int pl, int Ho, int Wo, int RB,
+                                                               int spi) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [256][V]
   const int CV = C / V;
-  const int lanes = 256 / CVp;  // >= 1
   const int tid = threadIdx.x;
-  const int cvl = tid % CVp;
-  const int pln = tid / CVp;
-  const int cv = blockIdx.y * CVp + cvl;
-  const bool active = (cvl < CVp) && (cv < CV);
+  const long t = (long)blockIdx.x * 256 + tid;
+  const int cv = (int)(t % CV);
+  const int wo = (int)(t / CV);
   const int c = cv * V;
-  const long P = (long)N * Ho * Wo;
-  const long p0 = (long)blockIdx.x * chunk;
-  const long p1 = p0 + chunk < P ? p0 + chunk : P;
-
   float acc[9][V];
 #pragma unroll
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
 
-  if (active) {
-    for (long p = p0 + pln; p < p1; p += lanes) {
-      const int wo = (int)(p % Wo);
-      const long t2 = p / Wo;
-      const int ho = (int)(t2 % Ho);
-      const int n = (int)(t2 / Ho);
-      float g[V];
-      const T* pg = dy + p * C + c;
-      if constexpr (VECOK) {
-        Vec16<T> vv;
-        vv.load(pg);
-#pragma unroll
-        for (int v = 0; v < V; ++v) g[v] = vv.get(v);
-      } else {
-        g[0] = to_f32(pg[0]);
-      }
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int hi = ho * S - pt + i;
-        if (hi < 0 || hi >= H) continue;
+  if (wo < Wo) {
+    const int nstrips = N * spi;
+    for (int s = blockIdx.y; s < nstrips; s += gridDim.y) {
+      const int n = s / spi;
+      const int ho0 = (s - n * spi) * RB;
+      const int ho1 = ho0 + RB < Ho ? ho0 + RB : Ho;
+      const T* xn = x + (long)n * H * W * C + c;
+      const T* dn = dy + (long)n * Ho * Wo * C + c;
+      PackV<T, V> xr[3][3];
+      auto load_row = [&](PackV<T, V>(&row)[3], int hi) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const int wi = wo * S - pl + j;
-          if (wi < 0 || wi >= W) continue;
-          const T* px = x + (((long)n * H + hi) * W + wi) * C + c;
-          if constexpr (VECOK) {
-            Vec16<T> vv;
-            vv.load(px);
+          if (hi >= 0 && hi < H && wi >= 0 && wi < W) row[j].load(xn + ((long)hi * W + wi) * C);
+          else row[j].zero();
+        }
+      };
+      load_row(xr[0], ho0 * S - pt);
+      load_row(xr[1], ho0 * S - pt + 1);
+      load_row(xr[2], ho0 * S - pt + 2);
+      for (int ho = ho0; ho < ho1; ++ho) {
+        if (ho > ho0) {
+          if constexpr (S == 1) {
 #pragma unroll
-            for (int v = 0; v < V; ++v) acc[i * 3 + j][v] = fmaf(g[v], vv.get(v), acc[i * 3 + j][v]);
+            for (int j = 0; j < 3; ++j) {
+              xr[0][j] = xr[1][j];
+              xr[1][j] = xr[2][j];
+            }
+            load_row(xr[2], ho - pt + 2);
           } else {
-            acc[i * 3 + j][0] = fmaf(g[0], to_f32(px[0]), acc[i * 3 + j][0]);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) xr[0][j] = xr[2][j];
+            load_row(xr[1], ho * 2 - pt + 1);
+            load_row(xr[2], ho * 2 - pt + 2);
           }
         }
+        PackV<T, V> g;
+        g.load(dn + ((long)ho * Wo + wo) * C);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[i * 3 + j][v] = fmaf(g.get(v), xr[i][j].get(v), acc[i * 3 + j][v]);
       }
     }
   }
-  // deterministic tree reduction over pixel lanes, one tap at a time
+  // per-channel block sums: threads of this block holding channel vector cve sit at
+  // tl = (cve - tb) mod CV, + CV, ... (threads past Wo hold zeros)
+  const long tb = (long)blockIdx.x * 256;
+  const int t0mod = (int)(tb % CV);
+  float* out = slab + ((long)blockIdx.y * gridDim.x + blockIdx.x) * 9 * C;
   for (int k = 0; k < 9; ++k) {
 #pragma unroll
     for (int v = 0; v < V; ++v) red[tid * V + v] = acc[k][v];
     __syncthreads();
-    for (int s = lanes >> 1; s > 0; s >>= 1) {
-      if (pln < s) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) red[tid * V + v] += red[(tid + s * CVp) * V + v];
-      }
-      __syncthreads();
-    }
-    if (pln == 0 && active) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) slab[((long)blockIdx.x * 9 + k) * C + c + v] = red[tid * V + v];
+    for (int e = tid; e < C; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      int tl = cve - t0mod;
+      if (tl < 0) tl += CV;
+      float s = 0.f;
+      for (; tl < 256; tl += CV) s += red[tl * V + v];
+      out[k * C + e] = s;
     }
     __syncthreads();
   }
 }
 
-__global__ void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int nslab, int n) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int b = 0; b < nslab; ++b) s += slab[(long)b * n + i];
-  out[i] = s;
-}
+struct DwFilterPlan {
+  int gx, gy, RB, spi;
+  long parts() const { return (long)gx * gy; }
+};
 
-static int pow2_at_least(int v) {
-  int p = 1;
-  while (p < v) p <<= 1;
+// gx column tiles of 256 (cv, wo) threads; gy blocks stride over the N*spi row strips.
+// ~2048 blocks, capped so the [parts][9][C] slab stays <= max(16 MB, dy bytes / 8).
+static DwFilterPlan dw_filter_plan(int N, int Ho, int Wo, int C, int V, int es) {
+  DwFilterPlan p;
+  p.gx = cdiv((long)(C / V) * Wo, 256);
+  // strips of RB rows; short maps get shorter strips so that there are enough of them
+  p.RB = std::max(2, std::min(16, Ho / 4));
+  p.spi = cdiv(Ho, p.RB);
+  const long strips = (long)N * p.spi;
+  const long cap_bytes = std::max<long>(16L << 20, (long)N * Ho * Wo * C * es / 8);
+  long gy = std::min<long>(strips, std::max<long>(1, 2048 / p.gx));
+  gy = std::min<long>(gy, std::max<long>(1, cap_bytes / ((long)p.gx * 36 * C)));
+  p.gy = (int)std::max<long>(1, gy);
   return p;
 }
 
-struct DwFilterPlan {
-  int CVp, cgroups, nbx;
-  long chunk;
-};
-
 template <typename T>
-static DwFilterPlan dw_filter_plan(int N, int Ho, int Wo, int C, bool vecok) {
-  const int V = vecok ? Vec16<T>::N : 1;
-  const int CV = C / V;
-  DwFilterPlan pl;
-  pl.CVp = std::min(pow2_at_least(CV), 256);
-  pl.cgroups = cdiv(CV, pl.CVp);
-  const long P = (long)N * Ho * Wo;
-  // aim for ~2048 blocks in total, each covering >= 64 pixels per lane-row
-  long want = std::max<long>(1, 2048 / pl.cgroups);
-  long minchunk = (long)(256 / pl.CVp) * 8;
-  long chunk = std::max<long>(cdivl(P, want), minchunk);
-  pl.chunk = chunk;
-  pl.nbx = (int)cdivl(P, chunk);
-  return pl;
-}
-
-template <typename T>
-static bool dw_vec_ok(const void* a, const void* b, int C) {
-  const int V = Vec16<T>::N;
-  return (C % V == 0) && (((uintptr_t)a & 15) == 0) && (((uintptr_t)b & 15) == 0);
+static bool dw_pack4_ok(const void* a, const void* b, int C) {
+  const uintptr_t al = 4 * sizeof(T) - 1;
+  return (C % 4 == 0) && (((uintptr_t)a & al) == 0) && (((uintptr_t)b & al) == 0);
 }
 
 }  // namespace rod
@@ -297,29 +332,27 @@ namespace rod {
 template <typename T, int S, bool VK>
 static void dw_fwd_launch(const void* x, const float* w, void* y, int N, int H, int W, int C, int pt, int pl, int Ho,
                           int Wo, hipStream_t s) {
-  const int V = VK ? Vec16<T>::N : 1;
-  dim3 grid(cdiv((long)(C / V) * Wo, 256), cdiv(Ho, DW_R), N);
-  hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, VK>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt, pl, Ho,
+  constexpr int V = VK ? 4 : 1;
+  dim3 grid(cdiv((long)(C / V) * Wo, 256), cdiv(Ho, DW_RB), N);
+  hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt, pl, Ho,
                      Wo);
 }
 template <typename T, int S, bool VK>
 static void dw_bwd_data_launch(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int pt, int pl,
                                int Ho, int Wo, hipStream_t s) {
-  const int V = VK ? Vec16<T>::N : 1;
-  dim3 grid(cdiv((long)(C / V) * W, 256), cdiv(H, DW_R), N);
-  hipLaunchKernelGGL((dw3x3_bwd_data_kernel<T, S, VK>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W, C, pt,
+  constexpr int V = VK ? 4 : 1;
+  dim3 grid(cdiv((long)(C / V) * W, 256), cdiv(H, DW_RB), N);
+  hipLaunchKernelGGL((dw3x3_bwd_data_kernel<T, S, V>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W, C, pt,
                      pl, Ho, Wo);
 }
 template <typename T, int S, bool VK>
 static void dw_bwd_filter_launch(const void* x, const void* dy, float* dw, float* slab, int N, int H, int W, int C,
                                  int pt, int pl, int Ho, int Wo, hipStream_t s) {
-  const int V = VK ? Vec16<T>::N : 1;
-  DwFilterPlan pl_ = dw_filter_plan<T>(N, Ho, Wo, C, VK);
-  dim3 grid(pl_.nbx, pl_.cgroups);
-  size_t lds = 256 * V * sizeof(float);
-  hipLaunchKernelGGL((dw3x3_bwd_filter_kernel<T, S, VK>), grid, dim3(256), lds, s, (const T*)x, (const T*)dy, slab, N,
-                     H, W, C, pt, pl, Ho, Wo, pl_.CVp, pl_.chunk);
-  slab_sum(slab, dw, pl_.nbx, 9L * C, s);
+  constexpr int V = VK ? 4 : 1;
+  DwFilterPlan p = dw_filter_plan(N, Ho, Wo, C, V, (int)sizeof(T));
+  hipLaunchKernelGGL((dw3x3_bwd_filter_kernel<T, S, V>), dim3(p.gx, p.gy), dim3(256), 256 * V * sizeof(float), s,
+                     (const T*)x, (const T*)dy, slab, N, H, W, C, pt, pl, Ho, Wo, p.RB, p.spi);
+  slab_sum(slab, dw, (int)p.parts(), 9L * C, s);
 }
 
 }  // namespace rod
@@ -342,10 +375,10 @@ int rod_dw3x3_fwd(const void* x, const float* w, void* y, int N, int H, int W, i
   DW_ARGS_OK("rod_dw3x3_fwd");
   hipStream_t s = ROD_STREAM(stream);
   if (dtype == ROD_F32) {
-    const bool vec = dw_vec_ok<float>(x, y, C);
+    const bool vec = dw_pack4_ok<float>(x, y, C);
     DW_SELECT(dw_fwd_launch, float, x, w, y, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else if (dtype == ROD_BF16) {
-    const bool vec = dw_vec_ok<bf16_t>(x, y, C);
+    const bool vec = dw_pack4_ok<bf16_t>(x, y, C);
     DW_SELECT(dw_fwd_launch, bf16_t, x, w, y, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else {
     set_error("rod_dw3x3_fwd: bad dtype %d", dtype);
@@ -359,10 +392,10 @@ int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, i
   DW_ARGS_OK("rod_dw3x3_bwd_data");
   hipStream_t s = ROD_STREAM(stream);
   if (dtype == ROD_F32) {
-    const bool vec = dw_vec_ok<float>(dy, dx, C);
+    const bool vec = dw_pack4_ok<float>(dy, dx, C);
     DW_SELECT(dw_bwd_data_launch, float, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else if (dtype == ROD_BF16) {
-    const bool vec = dw_vec_ok<bf16_t>(dy, dx, C);
+    const bool vec = dw_pack4_ok<bf16_t>(dy, dx, C);
     DW_SELECT(dw_bwd_data_launch, bf16_t, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else {
     set_error("rod_dw3x3_bwd_data: bad dtype %d", dtype);
@@ -372,11 +405,10 @@ int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, i
 }
 
 size_t rod_dw3x3_bwd_filter_workspace(int N, int Ho, int Wo, int C) {
-  DwFilterPlan a = dw_filter_plan<float>(N, Ho, Wo, C, false);
-  DwFilterPlan b = dw_filter_plan<float>(N, Ho, Wo, C, C % 4 == 0);
-  DwFilterPlan c = dw_filter_plan<bf16_t>(N, Ho, Wo, C, C % 8 == 0);
-  int nbx = std::max(a.nbx, std::max(b.nbx, c.nbx));
-  return (size_t)nbx * 9 * C * sizeof(float);
+  long parts = 0;
+  for (int V : {1, 4})
+    for (int es : {2, 4}) parts = std::max(parts, dw_filter_plan(N, Ho, Wo, C, V, es).parts());
+  return (size_t)parts * 9 * C * sizeof(float);
 }
 
 int rod_dw3x3_bwd_filter(const void* x, const void* dy, float* dw, void* workspace, int N, int H, int W, int C,
@@ -386,10 +418,10 @@ int rod_dw3x3_bwd_filter(const void* x, const void* dy, float* dw, void* workspa
   hipStream_t s = ROD_STREAM(stream);
   float* slab = (float*)workspace;
   if (dtype == ROD_F32) {
-    const bool vec = dw_vec_ok<float>(x, dy, C);
+    const bool vec = dw_pack4_ok<float>(x, dy, C);
     DW_SELECT(dw_bwd_filter_launch, float, x, dy, dw, slab, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else if (dtype == ROD_BF16) {
-    const bool vec = dw_vec_ok<bf16_t>(x, dy, C);
+    const bool vec = dw_pack4_ok<bf16_t>(x, dy, C);
     DW_SELECT(dw_bwd_filter_launch, bf16_t, x, dy, dw, slab, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else {
     set_error("rod_dw3x3_bwd_filter: bad dtype %d", dtype);

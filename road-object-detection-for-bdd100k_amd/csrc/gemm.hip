@@ -126,7 +126,7 @@ __device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b
 // forward: y[m, co] = sum_k A[m,k] wt[co,k] + bias[co]
 // block 256 threads = 4 waves laid out WM x WN; tile BM x BN; wave tile (BM/WM) x (BN/WN)
 // =====================================================================================
-template <typename T, int KS, int BN, bool VA, bool VB>
+template <typename T, int KS, int BN, bool VA, bool VB, bool VY>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
                                                        const float* __restrict__ bias, T* __restrict__ Y, long M,
                                                        int H, int W, int Cin, int Cout, int ldx, int ldy) {
@@ -138,8 +138,15 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   constexpr int LD = BK + LdsPad<T>::v;
   constexpr int ACH = BM * BK / 8 / 256;          // A chunks per thread (=2)
   constexpr int BCH = (BN * BK / 8 + 255) / 256;  // B chunks per thread
-  __shared__ __attribute__((aligned(16))) T As[BM * LD];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * LD];
+  // epilogue staging: one 64-row half of the tile at a time, row pad keeps 16-byte alignment
+  constexpr int EV = 16 / sizeof(T);
+  constexpr int LDC = BN + EV;
+  constexpr int MAIN_BYTES = (BM + BN) * LD * sizeof(T);
+  constexpr int EPI_BYTES = VY ? 64 * LDC * sizeof(T) : 0;
+  constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  T* As = (T*)smem;
+  T* Bs = As + BM * LD;
 
   const int K = KS * KS * Cin;
   const int tid = threadIdx.x;
@@ -207,18 +214,63 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     }
   }
 
-  // epilogue: bias + store (row = 4(l>>4)+r, col = l&15)
+  if constexpr (VY) {
+    // epilogue through LDS: the accumulators (row = 4(l>>4)+r, col = l&15 of each 16x16
+    // tile) are rounded to T into a 64-row staging tile, then every thread stores 16-byte
+    // row segments, so each wave writes whole contiguous rows of Y.
+    float bv[NT];
 #pragma unroll
-  for (int b = 0; b < NT; ++b) {
-    const int col = n0 + wn * (BN / WN) + b * 16 + (lane & 15);
-    if (col >= Cout) continue;
-    const float bv = bias ? bias[col] : 0.f;
+    for (int b = 0; b < NT; ++b) {
+      const int col = n0 + wn * (BN / WN) + b * 16 + (lane & 15);
+      bv[b] = (bias && col < Cout) ? bias[col] : 0.f;
+    }
+    T* Cs = (T*)smem;
+    constexpr int WROWS = BM / WM;  // rows per wave
 #pragma unroll
-    for (int a = 0; a < MT; ++a) {
+    for (int h = 0; h < BM / 64; ++h) {
+      __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long row = m0 + wm * (BM / WM) + a * 16 + (lane >> 4) * 4 + r;
-        if (row < M) Y[row * ldy + col] = from_f32<T>(acc[a][b][r] + bv);
+      for (int a = 0; a < MT; ++a) {
+        const int r_tile = wm * WROWS + a * 16;  // first row of this 16-row tile in the block
+        if (r_tile < h * 64 || r_tile >= h * 64 + 64) continue;
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          const int cl = wn * (BN / WN) + b * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(r_tile - h * 64 + (lane >> 4) * 4 + r) * LDC + cl] = from_f32<T>(acc[a][b][r] + bv[b]);
+        }
+      }
+      __syncthreads();
+      constexpr int CPR = BN / EV;  // 16-byte chunks per row
+      for (int idx = tid; idx < 64 * CPR; idx += 256) {
+        const int rr = idx / CPR, cc = (idx - rr * CPR) * EV;
+        const long row = m0 + h * 64 + rr;
+        const int col = n0 + cc;
+        if (row >= M || col >= Cout) continue;
+        const T* src = Cs + rr * LDC + cc;
+        T* dst = Y + row * ldy + col;
+        if (col + EV <= Cout) {
+          *(uint4*)dst = *(const uint4*)src;
+        } else {
+          for (int j = 0; j < Cout - col; ++j) dst[j] = src[j];
+        }
+      }
+    }
+  } else {
+    // direct epilogue: bias + store (row = 4(l>>4)+r, col = l&15)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int col = n0 + wn * (BN / WN) + b * 16 + (lane & 15);
+      if (col >= Cout) continue;
+      const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int a = 0; a < MT; ++a) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long row = m0 + wm * (BM / WM) + a * 16 + (lane >> 4) * 4 + r;
+          if (row < M) Y[row * ldy + col] = from_f32<T>(acc[a][b][r] + bv);
+        }
       }
     }
   }
@@ -406,29 +458,44 @@ static bool aligned16(const void* p) {
   return ((uintptr_t)p & 15) == 0;
 }
 
-template <typename T, int KS, int BN, bool VA, bool VB>
+template <typename T, int KS, int BN, bool VA, bool VB, bool VY>
 static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
                             int Cout, int ldx, int ldy, hipStream_t s) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
-  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB>), grid, dim3(256), 0, s, (const T*)x, (const T*)wt, bias,
+  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY>), grid, dim3(256), 0, s, (const T*)x, (const T*)wt, bias,
                      (T*)y, M, H, W, Cin, Cout, ldx, ldy);
 }
 
-template <typename T, int KS, int BN>
-static void conv_fwd_va_vb(bool va, bool vb, const void* x, const void* wt, const float* bias, void* y, long M, int H,
-                           int W, int Cin, int Cout, int ldx, int ldy, hipStream_t s) {
-  if (va && vb) conv_fwd_launch<T, KS, BN, true, true>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-  else if (va) conv_fwd_launch<T, KS, BN, true, false>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-  else if (vb) conv_fwd_launch<T, KS, BN, false, true>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-  else conv_fwd_launch<T, KS, BN, false, false>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-}
-
+// N tile: the whole of Cout in one tile up to 256 (A is read once), else 128-wide tiles.
+// The fully vectorisable case (16-byte A, B and Y rows) gets the full tile menu and the
+// LDS-staged epilogue; the rest (stem Cin=3, odd strides) the 32/64/128 direct-store kernel.
 template <typename T, int KS>
-static void conv_fwd_bn(bool va, bool vb, const void* x, const void* wt, const float* bias, void* y, long M, int H,
-                        int W, int Cin, int Cout, int ldx, int ldy, hipStream_t s) {
-  if (Cout <= 32) conv_fwd_va_vb<T, KS, 32>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-  else if (Cout <= 64) conv_fwd_va_vb<T, KS, 64>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-  else conv_fwd_va_vb<T, KS, 128>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const void* wt, const float* bias, void* y,
+                              long M, int H, int W, int Cin, int Cout, int ldx, int ldy, hipStream_t s) {
+#define CF(BN_, VA_, VB_, VY_) \
+  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s)
+  if (va && vb && vy) {
+    if (Cout <= 32) CF(32, true, true, true);
+    else if (Cout <= 64) CF(64, true, true, true);
+    else if (Cout <= 96) CF(96, true, true, true);
+    else if (Cout <= 128) CF(128, true, true, true);
+    else if (Cout <= 160) CF(160, true, true, true);
+    else if (Cout <= 192) CF(192, true, true, true);
+    else if (Cout <= 256) CF(256, true, true, true);
+    else CF(128, true, true, true);
+    return;
+  }
+  if (Cout <= 32) {
+    if (va && vb) CF(32, true, true, false); else if (va) CF(32, true, false, false);
+    else if (vb) CF(32, false, true, false); else CF(32, false, false, false);
+  } else if (Cout <= 64) {
+    if (va && vb) CF(64, true, true, false); else if (va) CF(64, true, false, false);
+    else if (vb) CF(64, false, true, false); else CF(64, false, false, false);
+  } else {
+    if (va && vb) CF(128, true, true, false); else if (va) CF(128, true, false, false);
+    else if (vb) CF(128, false, true, false); else CF(128, false, false, false);
+  }
+#undef CF
 }
 
 template <typename T>
@@ -439,8 +506,9 @@ static void conv_fwd_typed(const void* x, const void* wt, const float* bias, voi
   const int eV = Vec16<T>::N;
   const bool va = aligned16<T>(x) && (ldx % eV == 0) && (ksize == 1 ? true : (Cin % 8 == 0));
   const bool vb = aligned16<T>(wt) && (K % eV == 0);
-  if (ksize == 1) conv_fwd_bn<T, 1>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-  else conv_fwd_bn<T, 3>(va, vb, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  const bool vy = aligned16<T>(y) && (ldy % eV == 0);
+  if (ksize == 1) conv_fwd_dispatch<T, 1>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  else conv_fwd_dispatch<T, 3>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
 }
 
 template <typename T, int KS, bool VA, bool VD>

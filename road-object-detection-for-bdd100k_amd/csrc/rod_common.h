@@ -22,7 +22,7 @@ namespace rod {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 // out[i] = sum_b slab[b*n + i] (fp32 partials, f64 accumulation, fixed order).
-// Blocks of 32 columns x 8 slab lanes, so long slabs and wide rows both parallelise.
+// Blocks of CB columns x 256/CB slab lanes (CB adapts to n), so long slabs and wide rows both parallelise.
 void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s);
 // Grid size for a grid-stride loop over rows x CV channel vectors in which every thread
 // keeps ONE channel vector: (blocks * 256) % CV == 0 and blocks ~ target.

@@ -9,9 +9,10 @@ The second term matters only where fp32 itself is ill-conditioned: BatchNorm ove
 few rows of the deepest feature maps (2-30 values at these test sizes) amplifies any
 rounding difference (the oracle's own fp32 error there reaches 1e-3..1), so no fp32
 implementation can be closer to the truth than fp32 allows.
-bf16 storage: loss within 3 %; outputs / gradients must be no worse (cosine vs truth, 0.02 slack)
-than a plain bf16 evaluation of the oracle, on tensors where bf16 can represent the answer
-(bf16-oracle cosine >= 0.95) and fp32 is well conditioned (oracle fp32 error < 1e-2).
+bf16 storage: loss within 3 %; outputs / moving statistics / gradients: angular error vs
+truth (1 - cosine) within max(0.02, 3x) that of a plain bf16 evaluation of the oracle, on
+tensors where bf16 can represent the answer (bf16-oracle cosine >= 0.95) and fp32 is well
+conditioned (oracle fp32 error < 1e-2).
 """
 import numpy as np
 import pytest
@@ -70,6 +71,15 @@ def _cos(a, b):
     return float(torch.nn.functional.cosine_similarity(a, b, dim=0))
 
 
+BF16_SPREAD = 3.0   # bf16: angular error (1 - cos vs fp64) within 3x that of a plain bf16 evaluation
+
+
+def _bf16_ok(got, ref_bf16, truth, floor=0.02):
+    """Conditioning-aware bf16 bound, the bf16 analogue of the fp32 '4x the fp32 oracle's
+    spread' rule: 1 - cos(got, truth) <= max(floor, BF16_SPREAD * (1 - cos(ref_bf16, truth)))."""
+    return 1.0 - _cos(got, truth) <= max(floor, BF16_SPREAD * (1.0 - _cos(ref_bf16, truth)))
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 def test_refine_step_matches_oracle(dev, dtype):
     H, W, B = 160, 288, 2
@@ -99,8 +109,8 @@ def test_refine_step_matches_oracle(dev, dtype):
             assert e_h <= max(1e-4, 4 * e_o), report
         elif e_o < 1e-2 and _cos(refb[l], o64) >= 0.95:
             # where bf16 can represent the answer at all (a plain bf16 evaluation of the same
-            # network reaches cos >= 0.95), be no worse than it (minus 0.02 slack)
-            assert _cos(a, o64) >= min(0.98, _cos(refb[l], o64) - 0.02), (l, _cos(a, o64), _cos(refb[l], o64))
+            # network reaches cos >= 0.95), stay within 3x its angular error
+            assert _bf16_ok(a, refb[l], o64), (l, _cos(a, o64), _cos(refb[l], o64))
     print('per-level (hip err, oracle-fp32 err):', report)
     lt = 1e-4 if dtype == torch.float32 else 3e-2
     assert abs(loss.item() - loss64.item()) <= max(lt, 4 * abs(loss32.item() - loss64.item()) / abs(loss64.item())) * \
@@ -111,8 +121,7 @@ def test_refine_step_matches_oracle(dev, dtype):
         if dtype == torch.float32:
             assert _nerr(got, v) <= max(1e-4, 4 * e_o), k
         elif e_o < 1e-2 and _cos(movb[k].float(), v) >= 0.95:
-            # moving statistics are decay-scaled (1e-4-sized) batch moments: 0.05 slack
-            assert _cos(got, v) >= min(0.98, _cos(movb[k].float(), v) - 0.05), k
+            assert _bf16_ok(got, movb[k].float(), v), (k, _cos(got, v), _cos(movb[k].float(), v))
     bad = []
     for name, p in tr.net.store.params.items():
         g64, g32, gd = P64[name].grad, P32[name].grad, p._rod_grad
@@ -122,7 +131,7 @@ def test_refine_step_matches_oracle(dev, dtype):
             if e_h > max(2e-3, 4 * e_o):
                 bad.append((name, e_h, e_o))
         elif e_o < 1e-2 and g64.abs().max() > 0 and _cos(Pb[name].grad.float(), g64) >= 0.95 and \
-                _cos(gd, g64) < min(0.98, _cos(Pb[name].grad.float(), g64) - 0.02):
+                not _bf16_ok(gd, Pb[name].grad.float(), g64):
             bad.append((name, _cos(gd, g64), _cos(Pb[name].grad.float(), g64), e_o))
     assert not bad, bad[:10]
     # SGD with clip (net_tools.py:645-651), bit-exact given the gradient
