@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 1
+#define ROD_ABI_VERSION 2
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -51,8 +51,12 @@ int rod_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, v
  * slim.separable_conv2d(num_outputs=None, depth_multiplier=1), padding SAME
  * (conv_blocks.py:238-247): y[n,ho,wo,c] = sum_ij x[n,ho*s+i-pt,wo*s+j-pl,c]*w[i,j,c].
  * w is fp32 [3][3][C] (TF depthwise_weights [3,3,C,1]). */
-int rod_dw3x3_fwd(const void* x, const float* w, void* y, int N, int H, int W, int C,
-                  int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
+/* stat_parts (nullable): BatchNorm partial statistics of y ([3][C][nparts], see
+ * rod_bn_finalize) with nparts = rod_dw3x3_fwd_stat_parts(), reduced in the epilogue from
+ * the rounded outputs (the depthwise BatchNorm, conv_blocks.py:247 + mobilenet.py:417). */
+int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C);
+int rod_dw3x3_fwd(const void* x, const float* w, void* y, float* stat_parts, int N, int H, int W,
+                  int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
 /* dx = d y / d x  (DepthwiseConv2dNativeBackpropInput) */
 int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, int W, int C,
                        int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
@@ -75,6 +79,14 @@ size_t rod_bn_stats_workspace(long M, int C);
 int rod_bn_stats(const void* x, long M, int C, int ldx, float eps, float decay,
                  float* mean, float* rstd, float* moving_mean, float* moving_var,
                  void* workspace, int dtype, void* stream);
+/* The same statistics (and moving-average update) from partial statistics written by a
+ * producer's epilogue: parts [3][C][nparts] = (count, mean, M2) per part; parts with
+ * count 0 are ignored; M = total count.  Chan's merge in f64, fixed order (two levels when
+ * nparts > 2048: workspace = rod_bn_finalize_workspace() bytes, else may be NULL). */
+size_t rod_bn_finalize_workspace(int nparts, int C);
+int rod_bn_finalize(const float* parts, int nparts, long M, int C, float eps, float decay,
+                    float* mean, float* rstd, float* moving_mean, float* moving_var,
+                    void* workspace, void* stream);
 /* inference: mean = moving_mean, rstd = 1/sqrt(moving_var + eps). */
 int rod_bn_eval_stats(const float* moving_mean, const float* moving_var, float eps,
                       float* mean, float* rstd, int C, void* stream);
@@ -100,9 +112,19 @@ int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rs
  *            (stem mobilenet_v2.py:58; heads catch_net.py:303, 336)
  * wt: [Cout][ksize*ksize*Cin] in the activation dtype; bias fp32 or NULL.
  * ldx / ldy: row strides of x / y in elements (0 => Cin / Cout), so a conv can
- * read or write a channel slice of a concatenated buffer (catch_net.py:211). */
-int rod_conv_fwd(const void* x, const void* wt, const float* bias, void* y, int N, int H,
-                 int W, int Cin, int Cout, int ksize, int ldx, int ldy, int dtype, void* stream);
+ * read or write a channel slice of a concatenated buffer (catch_net.py:211).
+ * workspace: rod_conv_fwd_workspace() bytes; non-zero when the output has too few
+ * 128-row tiles to fill the chip and K is deep (head convs on the small pyramid levels):
+ * K is then split over workgroups into fp32 partial slabs summed in fixed order.  NULL
+ * is accepted and disables the split.
+ * stat_parts (nullable): BatchNorm partial statistics of y for rod_bn_finalize, as
+ * [3][Cout][ceil(M/128)] (count, mean, M2) per 128-row tile, computed in the epilogue from
+ * the rounded outputs (the BatchNorm that follows every conv, mobilenet.py:417,
+ * catch_net.py:302) so no separate statistics pass re-reads y. */
+size_t rod_conv_fwd_workspace(int N, int H, int W, int Cin, int Cout, int ksize);
+int rod_conv_fwd(const void* x, const void* wt, const float* bias, void* y, void* workspace,
+                 float* stat_parts, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
+                 int ldy, int dtype, void* stream);
 /* Weight layouts derived from the fp32 master weight w[Cout][ksize][ksize][Cin]:
  *   mode 0: forward operand      wt[co][i][j][ci]           (cast to dtype)
  *   mode 1: backward-data operand wt[ci][2-i][2-j][co]       (transposed, flipped)

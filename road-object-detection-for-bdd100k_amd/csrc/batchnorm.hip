@@ -92,6 +92,13 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
   const int c = cv * V;
   const long r0 = (long)blockIdx.x * chunk;
   const long r1 = r0 + chunk < M ? r0 + chunk : M;
+  if (r0 >= M) {  // a part past the end (grid sized to a producer's part count): count 0
+    for (int e = tid; e < CVb * V; e += 256) {
+      const int cg = blockIdx.y * CVb + e / V;
+      if (cg < CV) store_stat_part(slab, C, blockIdx.x, cg * V + e % V, 0.f, 0.f, 0.f);
+    }
+    return;
+  }
   float s1[V], s2[V], k[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) s1[v] = s2[v] = 0.f;
@@ -141,9 +148,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
     const int ch = cg * V + v;
     const double kk = (double)to_f32(x[r0 * ldx + ch]);
     const double m2 = b - a * a / nb;
-    const long nblk = gridDim.x;
-    slab[(long)ch * nblk + blockIdx.x] = (float)(kk + a / nb);
-    slab[((long)C + ch) * nblk + blockIdx.x] = (float)(m2 > 0.0 ? m2 : 0.0);
+    store_stat_part(slab, C, blockIdx.x, ch, (float)nb, (float)(kk + a / nb), (float)(m2 > 0.0 ? m2 : 0.0));
   }
 }
 
@@ -156,40 +161,111 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-// Chan merge of per-part (mean_b, M2_b) with counts n_b = min(chunk, M - b*chunk):
-// mean = sum n_b mean_b / M, M2 = sum M2_b + n_b (mean_b - mean)^2.  The per-part pairs
-// come from bn_stats_kernel or from a producer's epilogue (rod_conv_fwd with stats).
-__global__ void __launch_bounds__(256) bn_stats_finalize_kernel(const float* __restrict__ slab, int nblk, long chunk,
-                                                                long M, int C, float eps, float decay,
-                                                                float* __restrict__ mean, float* __restrict__ rstd,
-                                                                float* __restrict__ mmean, float* __restrict__ mvar) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= C) return;
-  const float* pm = slab + (long)c * nblk;
-  const float* pq = slab + ((long)C + c) * nblk;
-  auto cnt = [&](int b) -> double { const long r = M - (long)b * chunk; return (double)(r < chunk ? r : chunk); };
-  double s = 0.0;
-  for (int b = lane; b < nblk; b += 64) s += cnt(b) * (double)pm[b];
-  const double mu = wave_sum_f64(s) / (double)M;
-  double q = 0.0;
-  for (int b = lane; b < nblk; b += 64) {
-    const double d = (double)pm[b] - mu;
-    q += (double)pq[b] + cnt(b) * d * d;
+// Merge of part-major partial statistics, one level: block (s, g) merges parts
+// [s*slice, (s+1)*slice) of channels [g*CB, (g+1)*CB) — PL = 256/CB part lanes per channel,
+// <= 32 serial f64 Chan merges per thread on coalesced rows, then a fixed-order LDS tree
+// over the lanes — into part s of `out`.  When a single part remains (gridDim.x == 1) the
+// same block finishes: mean, rstd and the moving-average update.
+__device__ __forceinline__ void chan_merge_d(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
+  if (nb == 0.0) return;
+  if (n == 0.0) {
+    n = nb;
+    mean = meanb;
+    m2 = m2b;
+    return;
   }
-  const double m2 = wave_sum_f64(q);
-  if (lane != 0) return;
-  const double var = m2 / (double)M;
-  const float mu_f = (float)mu;
-  const float vf = (float)var;
-  mean[c] = mu_f;
-  rstd[c] = (float)(1.0 / sqrt((double)vf + (double)eps));
-  if (mmean != nullptr) {
-    // slim: assign_moving_average(zero_debias=False): v -= (v - value) * (1 - decay)
-    const float one_m = 1.0f - decay;
-    const float unbiased = M > 1 ? (float)(m2 / (double)(M - 1)) : vf;
-    mmean[c] = mmean[c] - (mmean[c] - mu_f) * one_m;
-    mvar[c] = mvar[c] - (mvar[c] - unbiased) * one_m;
+  const double nt = n + nb;
+  const double d = meanb - mean;
+  mean += d * (nb / nt);
+  m2 += m2b + d * d * (n * nb / nt);
+  n = nt;
+}
+
+struct MergePlan {
+  int CB, PL, slice;
+};
+static MergePlan merge_plan(int C) {
+  MergePlan p;
+  p.CB = C < 256 ? C : 256;
+  p.PL = 256 / p.CB;
+  p.slice = 32 * p.PL;
+  return p;
+}
+
+__global__ void __launch_bounds__(256) bn_parts_merge_kernel(const float* __restrict__ parts, int nparts, int C, int CB,
+                                                             int slice, float* __restrict__ out, long M, float eps,
+                                                             float decay, float* __restrict__ mean,
+                                                             float* __restrict__ rstd, float* __restrict__ mmean,
+                                                             float* __restrict__ mvar) {
+  __shared__ double sn[256], sm[256], sq[256];
+  const int tid = threadIdx.x;
+  const int PL = 256 / CB;
+  const int cl = tid % CB, pl = tid / CB;
+  const int c = blockIdx.y * CB + cl;
+  const bool ok = pl < PL && c < C;
+  double n = 0.0, mu = 0.0, m2 = 0.0;
+  if (ok) {
+    // all (<= 32) parts of this thread are loaded before the first merge: one latency round
+    const int b0 = blockIdx.x * slice + pl;
+    const int b1 = blockIdx.x * slice + slice < nparts ? blockIdx.x * slice + slice : nparts;
+    float vn[32], vm[32], vq[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int bb = b0 + u * PL;
+      const bool in = bb < b1;
+      const float* p = parts + (long)(in ? bb : 0) * 3 * C + c;
+      vn[u] = in ? p[0] : 0.f;
+      vm[u] = in ? p[C] : 0.f;
+      vq[u] = in ? p[2 * C] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) chan_merge_d(n, mu, m2, (double)vn[u], (double)vm[u], (double)vq[u]);
+  }
+  sn[tid] = n;
+  sm[tid] = mu;
+  sq[tid] = m2;
+  __syncthreads();
+  if (ok && pl == 0) {
+    for (int l = 1; l < PL; ++l) chan_merge_d(n, mu, m2, sn[l * CB + cl], sm[l * CB + cl], sq[l * CB + cl]);
+    if (gridDim.x > 1) {
+      store_stat_part(out, C, blockIdx.x, c, (float)n, (float)mu, (float)m2);
+      return;
+    }
+    const double var = m2 / (double)M;
+    const float mu_f = (float)mu;
+    const float vf = (float)var;
+    mean[c] = mu_f;
+    rstd[c] = (float)(1.0 / sqrt((double)vf + (double)eps));
+    if (mmean != nullptr) {
+      // slim: assign_moving_average(zero_debias=False): v -= (v - value) * (1 - decay)
+      const float one_m = 1.0f - decay;
+      const float unbiased = M > 1 ? (float)(m2 / (double)(M - 1)) : vf;
+      mmean[c] = mmean[c] - (mmean[c] - mu_f) * one_m;
+      mvar[c] = mvar[c] - (mvar[c] - unbiased) * one_m;
+    }
+  }
+}
+
+// merge levels until one part remains; ws holds two ping-pong part buffers
+static size_t finalize_ws_bytes(int nparts, int C) {
+  const MergePlan p = merge_plan(C);
+  const int s1 = cdiv(nparts, p.slice);
+  return s1 > 1 ? 2 * (size_t)s1 * 3 * C * sizeof(float) : 0;
+}
+static void finalize_launch(const float* parts, int nparts, long M, int C, float eps, float decay, float* mean,
+                            float* rstd, float* mm, float* mv, float* ws, hipStream_t s) {
+  const MergePlan p = merge_plan(C);
+  const int s1 = cdiv(nparts, p.slice);
+  float* buf[2] = {ws, ws ? ws + (size_t)s1 * 3 * C : nullptr};
+  int k = 0;
+  while (true) {
+    const int S = cdiv(nparts, p.slice);
+    hipLaunchKernelGGL(bn_parts_merge_kernel, dim3(S, cdiv(C, p.CB)), dim3(256), 0, s, parts, nparts, C, p.CB, p.slice,
+                       S > 1 ? buf[k] : nullptr, M, eps, decay, mean, rstd, mm, mv);
+    if (S == 1) break;
+    parts = buf[k];
+    nparts = S;
+    k ^= 1;
   }
 }
 
@@ -429,8 +505,29 @@ static void stats_launch(bool vec, const void* x, long M, int C, int ldx, float 
   else
     hipLaunchKernelGGL((bn_stats_kernel<T, false>), grid, dim3(256), lds, s, (const T*)x, M, C, ldx, pl.CVb,
                        pl.lanes, pl.chunk, slab);
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(cdiv(C, 4)), dim3(256), 0, s, (const float*)slab, pl.nbx,
-                     pl.chunk, M, C, eps, decay, mean, rstd, mm, mv);
+  finalize_launch(slab, pl.nbx, M, C, eps, decay, mean, rstd, mm, mv, slab + (size_t)pl.nbx * 3 * C, s);
+}
+
+// Partial statistics of y[M, C] (row stride ld) as exactly `nparts` parts of
+// ceil(M / nparts) rows: the fallback for producers that cannot fuse the statistics.
+template <typename T>
+static void stat_parts_typed(const void* y, long M, int C, int ld, float* parts, int nparts, hipStream_t s) {
+  const bool vec = vec_ok<T>(C, {{y, ld}});
+  RedPlan pl = red_plan<T>(M, C, vec);
+  pl.chunk = cdivl(M, nparts);
+  dim3 grid(nparts, pl.cgroups);
+  size_t lds = 2 * 256 * pl.V * sizeof(float);
+  if (vec)
+    hipLaunchKernelGGL((bn_stats_kernel<T, true>), grid, dim3(256), lds, s, (const T*)y, M, C, ld, pl.CVb, pl.lanes,
+                       pl.chunk, parts);
+  else
+    hipLaunchKernelGGL((bn_stats_kernel<T, false>), grid, dim3(256), lds, s, (const T*)y, M, C, ld, pl.CVb,
+                       pl.lanes, pl.chunk, parts);
+}
+
+void stat_parts(int dtype, const void* y, long M, int C, int ld, float* parts, int nparts, hipStream_t s) {
+  if (dtype == ROD_F32) stat_parts_typed<float>(y, M, C, ld, parts, nparts, s);
+  else stat_parts_typed<bf16_t>(y, M, C, ld, parts, nparts, s);
 }
 
 template <typename T>
@@ -464,7 +561,22 @@ using namespace rod;
 
 extern "C" {
 
-size_t rod_bn_stats_workspace(long M, int C) { return (size_t)max_nbx(M, C) * 2 * C * sizeof(float); }
+size_t rod_bn_stats_workspace(long M, int C) {
+  const int nbx = max_nbx(M, C);
+  return (size_t)nbx * 3 * C * sizeof(float) + finalize_ws_bytes(nbx, C);
+}
+
+size_t rod_bn_finalize_workspace(int nparts, int C) { return finalize_ws_bytes(nparts, C); }
+
+int rod_bn_finalize(const float* parts, int nparts, long M, int C, float eps, float decay, float* mean, float* rstd,
+                    float* moving_mean, float* moving_var, void* workspace, void* stream) {
+  ROD_CHECK_ARG(parts != nullptr && nparts > 0 && M > 0 && C > 0, "rod_bn_finalize: bad arguments");
+  ROD_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr), "rod_bn_finalize: moving stats mismatch");
+  ROD_CHECK_ARG(workspace != nullptr || finalize_ws_bytes(nparts, C) == 0, "rod_bn_finalize: workspace is NULL");
+  finalize_launch(parts, nparts, M, C, eps, decay, mean, rstd, moving_mean, moving_var, (float*)workspace,
+                  ROD_STREAM(stream));
+  return check_launch("rod_bn_finalize");
+}
 
 int rod_bn_stats(const void* x, long M, int C, int ldx, float eps, float decay, float* mean, float* rstd,
                  float* moving_mean, float* moving_var, void* workspace, int dtype, void* stream) {

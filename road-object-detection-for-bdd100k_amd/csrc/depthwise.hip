@@ -44,67 +44,125 @@ constexpr int DW_RB = 8;  // output rows per thread (forward / backward-data str
 // Forward: thread = (channel vector cv, output column wo), strip of DW_RB output rows; the
 // 3x3 input window rolls down in registers (one new input row per output row for S=1, two
 // for S=2) and lanes of a wave read consecutive channel vectors of neighbouring pixels.
-template <typename T, int S, int V>
+template <typename T, int S, int V, bool STATS>
 __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                         T* __restrict__ y, int H, int W, int C, int pt, int pl,
-                                                        int Ho, int Wo) {
+                                                        int Ho, int Wo, float* __restrict__ parts) {
   const int CV = C / V;
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cv = (int)(t % CV);
   const int wo = (int)(t / CV);
-  if (wo >= Wo) return;
+  const bool active = wo < Wo;
   const int ho0 = blockIdx.y * DW_RB;
   const int ho1 = ho0 + DW_RB < Ho ? ho0 + DW_RB : Ho;
   const int n = blockIdx.z;
   const int c = cv * V;
-  float wr[9][V];
+  // STATS: this thread's rounded outputs, for its (n, mean, M2) per channel
+  float keep[STATS ? DW_RB : 1][V];
+  if (active) {
+    float wr[9][V];
 #pragma unroll
-  for (int k = 0; k < 9; ++k)
+    for (int k = 0; k < 9; ++k)
 #pragma unroll
-    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
-  const T* xn = x + (long)n * H * W * C + c;
-  T* yn = y + (long)n * Ho * Wo * C + c;
-  PackV<T, V> xr[3][3];
-  auto load_row = [&](PackV<T, V>(&row)[3], int hi) {
+      for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+    const T* xn = x + (long)n * H * W * C + c;
+    T* yn = y + (long)n * Ho * Wo * C + c;
+    PackV<T, V> xr[3][3];
+    auto load_row = [&](PackV<T, V>(&row)[3], int hi) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int wi = wo * S - pl + j;
-      if (hi >= 0 && hi < H && wi >= 0 && wi < W) row[j].load(xn + ((long)hi * W + wi) * C);
-      else row[j].zero();
-    }
-  };
-  load_row(xr[0], ho0 * S - pt);
-  load_row(xr[1], ho0 * S - pt + 1);
-  load_row(xr[2], ho0 * S - pt + 2);
-  for (int ho = ho0; ho < ho1; ++ho) {
-    if (ho > ho0) {
-      if constexpr (S == 1) {
+      for (int j = 0; j < 3; ++j) {
+        const int wi = wo * S - pl + j;
+        if (hi >= 0 && hi < H && wi >= 0 && wi < W) row[j].load(xn + ((long)hi * W + wi) * C);
+        else row[j].zero();
+      }
+    };
+    // window rows ho*S-pt+{0,1,2}; the row(s) the NEXT output row adds are prefetched into
+    // nx before this row's FMAs, so one row of arithmetic covers the load latency
+    PackV<T, V> nx[S][3];
+    auto prefetch = [&](int ho) {
+#pragma unroll
+      for (int q = 0; q < S; ++q) load_row(nx[q], ho * S - pt + 3 - S + q);
+    };
+    load_row(xr[0], ho0 * S - pt);
+    load_row(xr[1], ho0 * S - pt + 1);
+    load_row(xr[2], ho0 * S - pt + 2);
+    if (ho0 + 1 < ho1) prefetch(ho0 + 1);
+#pragma unroll
+    for (int q = 0; q < DW_RB; ++q) {
+      const int ho = ho0 + q;
+      if (ho >= ho1) break;
+      float acc[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] = fmaf(xr[i][j].get(v), wr[i * 3 + j][v], acc[v]);
+      PackV<T, V> o;
+#pragma unroll
+      for (int v = 0; v < V; ++v) o.set(v, acc[v]);
+      o.store(yn + ((long)ho * Wo + wo) * C);
+      if constexpr (STATS) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) keep[q][v] = o.get(v);
+      }
+      if (ho + 1 < ho1) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          xr[0][j] = xr[1][j];
-          xr[1][j] = xr[2][j];
+          if constexpr (S == 1) {
+            xr[0][j] = xr[1][j];
+            xr[1][j] = xr[2][j];
+            xr[2][j] = nx[0][j];
+          } else {
+            xr[0][j] = xr[2][j];
+            xr[1][j] = nx[0][j];
+            xr[2][j] = nx[1][j];
+          }
         }
-        load_row(xr[2], ho - pt + 2);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) xr[0][j] = xr[2][j];
-        load_row(xr[1], ho * 2 - pt + 1);
-        load_row(xr[2], ho * 2 - pt + 2);
+        if (ho + 2 < ho1) prefetch(ho + 2);
       }
     }
-    float acc[V];
+  }
+  if constexpr (STATS) {
+    // per thread: exact two-pass (mean, M2) of its <= DW_RB rows; per block: Chan merge of
+    // the threads holding each channel vector, in thread order, into part
+    // (z*gy + y)*gx + x of the [3][C][nparts] slab
+    __shared__ float sn[256], sm[256 * V], sq[256 * V];
+    const int tid = threadIdx.x;
+    const int nr = active ? ho1 - ho0 : 0;
 #pragma unroll
-    for (int v = 0; v < V; ++v) acc[v] = 0.f;
+    for (int v = 0; v < V; ++v) {
+      float sum = 0.f;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+      for (int q = 0; q < DW_RB; ++q)
+        if (q < nr) sum += keep[q][v];
+      const float mu = nr > 0 ? sum / (float)nr : 0.f;
+      float m2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = fmaf(xr[i][j].get(v), wr[i * 3 + j][v], acc[v]);
-    PackV<T, V> o;
-#pragma unroll
-    for (int v = 0; v < V; ++v) o.set(v, acc[v]);
-    o.store(yn + ((long)ho * Wo + wo) * C);
+      for (int q = 0; q < DW_RB; ++q)
+        if (q < nr) {
+          const float d = keep[q][v] - mu;
+          m2 = fmaf(d, d, m2);
+        }
+      sm[tid * V + v] = mu;
+      sq[tid * V + v] = m2;
+    }
+    sn[tid] = (float)nr;
+    __syncthreads();
+    const long tb = (long)blockIdx.x * 256;
+    const int t0mod = (int)(tb % CV);
+    const long nparts = (long)gridDim.x * gridDim.y * gridDim.z;
+    const long part = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    for (int e = tid; e < C; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      int tl = cve - t0mod;
+      if (tl < 0) tl += CV;
+      float pn = 0.f, pm = 0.f, pq = 0.f;
+      for (; tl < 256; tl += CV) chan_merge(pn, pm, pq, sn[tl], sm[tl * V + v], sq[tl * V + v]);
+      store_stat_part(parts, C, part, e, pn, pm, pq);
+    }
   }
 }
 
@@ -141,18 +199,12 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
         else row[j].zero();
       }
     };
+    PackV<T, V> nx[3];
     load_row(dr[0], h0 + pt);
     load_row(dr[1], h0 + pt - 1);
     load_row(dr[2], h0 + pt - 2);
+    if (h0 + 1 < h1) load_row(nx, h0 + 1 + pt);
     for (int h = h0; h < h1; ++h) {
-      if (h > h0) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          dr[2][j] = dr[1][j];
-          dr[1][j] = dr[0][j];
-        }
-        load_row(dr[0], h + pt);
-      }
       float acc[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[v] = 0.f;
@@ -166,6 +218,15 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
       o.store(xn + ((long)h * W + wc) * C);
+      if (h + 1 < h1) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          dr[2][j] = dr[1][j];
+          dr[1][j] = dr[0][j];
+          dr[0][j] = nx[j];
+        }
+        if (h + 2 < h1) load_row(nx, h + 2 + pt);
+      }
     }
   } else {
     for (int h = h0; h < h1; ++h) {
@@ -194,6 +255,80 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
       o.store(xn + ((long)h * W + wc) * C);
+    }
+  }
+}
+
+// Stride-2 backward data, phase-split: with u = h + pt and v = w + pl, dx row u=2a takes dy
+// rows a (tap 0) and a-1 (tap 2), row u=2a+1 takes dy row a (tap 1); columns likewise.  A
+// thread owns the 2x2 dx block u in {2a, 2a+1}, v in {2b, 2b+1} for a strip of a; it needs
+// dy[a-1..a][b-1..b], of which row a-1 is carried from the previous step, so each step
+// loads two dy pixels (one shared with the left neighbour via L1) and stores four.
+constexpr int DW_S2_RP = 4;  // row pairs per thread
+template <typename T, int V>
+__global__ void __launch_bounds__(256) dw3x3_bwd_data_s2_kernel(const T* __restrict__ dy, const float* __restrict__ w,
+                                                                T* __restrict__ dx, int H, int W, int C, int pt,
+                                                                int pl, int Ho, int Wo, int Bc) {
+  const int CV = C / V;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = (int)(t % CV);
+  const int b = (int)(t / CV);
+  if (b >= Bc) return;
+  const int a0 = blockIdx.y * DW_S2_RP;
+  const int amax = (H - 1 + pt) >> 1;  // last a with a dx row
+  const int a1 = a0 + DW_S2_RP - 1 < amax ? a0 + DW_S2_RP - 1 : amax;
+  const int n = blockIdx.z;
+  const int c = cv * V;
+  float wr[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+  const T* dn = dy + (long)n * Ho * Wo * C + c;
+  T* xn = dx + (long)n * H * W * C + c;
+  auto load2 = [&](PackV<T, V>(&p)[2], int a) {  // p[0] = dy[a][b-1], p[1] = dy[a][b]
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int bb = b - 1 + q;
+      if (a >= 0 && a < Ho && bb >= 0 && bb < Wo) p[q].load(dn + ((long)a * Wo + bb) * C);
+      else p[q].zero();
+    }
+  };
+  const int w0 = 2 * b - pl, w1 = 2 * b + 1 - pl;  // dx columns of this thread
+  PackV<T, V> prev[2], cur[2], nxt[2];
+  load2(prev, a0 - 1);
+  load2(cur, a0);
+  if (a0 + 1 <= a1) load2(nxt, a0 + 1);
+  for (int a = a0; a <= a1; ++a) {
+    float o00[V], o01[V], o10[V], o11[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float c1 = cur[1].get(v), c0 = cur[0].get(v), p1 = prev[1].get(v), p0 = prev[0].get(v);
+      // (u=2a, v=2b) taps (0,0),(0,2),(2,0),(2,2); (2a,2b+1) taps (0,1),(2,1);
+      // (2a+1,2b) taps (1,0),(1,2); (2a+1,2b+1) tap (1,1)
+      o00[v] = fmaf(p0, wr[8][v], fmaf(p1, wr[6][v], fmaf(c0, wr[2][v], c1 * wr[0][v])));
+      o01[v] = fmaf(p1, wr[7][v], c1 * wr[1][v]);
+      o10[v] = fmaf(c0, wr[5][v], c1 * wr[3][v]);
+      o11[v] = c1 * wr[4][v];
+    }
+    auto put = [&](int h, int ww, const float (&o)[V]) {
+      if (h < 0 || h >= H || ww < 0 || ww >= W) return;
+      PackV<T, V> pk;
+#pragma unroll
+      for (int v = 0; v < V; ++v) pk.set(v, o[v]);
+      pk.store(xn + ((long)h * W + ww) * C);
+    };
+    put(2 * a - pt, w0, o00);
+    put(2 * a - pt, w1, o01);
+    put(2 * a + 1 - pt, w0, o10);
+    put(2 * a + 1 - pt, w1, o11);
+    if (a + 1 <= a1) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        prev[q] = cur[q];
+        cur[q] = nxt[q];
+      }
+      if (a + 2 <= a1) load2(nxt, a + 2);
     }
   }
 }
@@ -239,33 +374,40 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_filter_kernel(const T* __restri
           else row[j].zero();
         }
       };
+      PackV<T, V> nx[S][3], g, ng;
+      auto prefetch = [&](int ho) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) load_row(nx[q], ho * S - pt + 3 - S + q);
+        ng.load(dn + ((long)ho * Wo + wo) * C);
+      };
       load_row(xr[0], ho0 * S - pt);
       load_row(xr[1], ho0 * S - pt + 1);
       load_row(xr[2], ho0 * S - pt + 2);
+      g.load(dn + ((long)ho0 * Wo + wo) * C);
+      if (ho0 + 1 < ho1) prefetch(ho0 + 1);
       for (int ho = ho0; ho < ho1; ++ho) {
-        if (ho > ho0) {
-          if constexpr (S == 1) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              xr[0][j] = xr[1][j];
-              xr[1][j] = xr[2][j];
-            }
-            load_row(xr[2], ho - pt + 2);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) xr[0][j] = xr[2][j];
-            load_row(xr[1], ho * 2 - pt + 1);
-            load_row(xr[2], ho * 2 - pt + 2);
-          }
-        }
-        PackV<T, V> g;
-        g.load(dn + ((long)ho * Wo + wo) * C);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < 3; ++j)
 #pragma unroll
             for (int v = 0; v < V; ++v) acc[i * 3 + j][v] = fmaf(g.get(v), xr[i][j].get(v), acc[i * 3 + j][v]);
+        if (ho + 1 < ho1) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            if constexpr (S == 1) {
+              xr[0][j] = xr[1][j];
+              xr[1][j] = xr[2][j];
+              xr[2][j] = nx[0][j];
+            } else {
+              xr[0][j] = xr[2][j];
+              xr[1][j] = nx[0][j];
+              xr[2][j] = nx[1][j];
+            }
+          }
+          g = ng;
+          if (ho + 2 < ho1) prefetch(ho + 2);
+        }
       }
     }
   }
@@ -329,18 +471,35 @@ using namespace rod;
 
 namespace rod {
 
+static dim3 dw_fwd_grid(int N, int Ho, int Wo, int C, int V) {
+  return dim3(cdiv((long)(C / V) * Wo, 256), cdiv(Ho, DW_RB), N);
+}
+
 template <typename T, int S, bool VK>
-static void dw_fwd_launch(const void* x, const float* w, void* y, int N, int H, int W, int C, int pt, int pl, int Ho,
-                          int Wo, hipStream_t s) {
+static void dw_fwd_launch(const void* x, const float* w, void* y, float* parts, int N, int H, int W, int C, int pt,
+                          int pl, int Ho, int Wo, hipStream_t s) {
   constexpr int V = VK ? 4 : 1;
-  dim3 grid(cdiv((long)(C / V) * Wo, 256), cdiv(Ho, DW_RB), N);
-  hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt, pl, Ho,
-                     Wo);
+  const dim3 grid = dw_fwd_grid(N, Ho, Wo, C, V);
+  if (parts)
+    hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V, true>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt,
+                       pl, Ho, Wo, parts);
+  else
+    hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V, false>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt,
+                       pl, Ho, Wo, nullptr);
 }
 template <typename T, int S, bool VK>
 static void dw_bwd_data_launch(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int pt, int pl,
                                int Ho, int Wo, hipStream_t s) {
   constexpr int V = VK ? 4 : 1;
+  static const bool no_s2 = getenv("ROD_DEBUG_NOS2") != nullptr;  // debug bisection
+  if (S == 2 && pt <= 1 && pl <= 1 && !no_s2) {
+    const int Bc = (W - 1 + pl) / 2 + 1;
+    const int Ar = (H - 1 + pt) / 2 + 1;
+    dim3 g2(cdiv((long)(C / V) * Bc, 256), cdiv(Ar, DW_S2_RP), N);
+    hipLaunchKernelGGL((dw3x3_bwd_data_s2_kernel<T, V>), g2, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W, C, pt,
+                       pl, Ho, Wo, Bc);
+    return;
+  }
   dim3 grid(cdiv((long)(C / V) * W, 256), cdiv(H, DW_RB), N);
   hipLaunchKernelGGL((dw3x3_bwd_data_kernel<T, S, V>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W, C, pt,
                      pl, Ho, Wo);
@@ -370,16 +529,28 @@ using namespace rod;
 
 extern "C" {
 
-int rod_dw3x3_fwd(const void* x, const float* w, void* y, int N, int H, int W, int C, int stride, int pad_t,
-                  int pad_l, int Ho, int Wo, int dtype, void* stream) {
+int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C) {
+  const dim3 g = dw_fwd_grid(N, Ho, Wo, C, C % 4 == 0 ? 4 : 1);
+  return (int)(g.x * g.y * g.z);
+}
+
+int rod_dw3x3_fwd(const void* x, const float* w, void* y, float* stat_parts, int N, int H, int W, int C, int stride,
+                  int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream) {
   DW_ARGS_OK("rod_dw3x3_fwd");
   hipStream_t s = ROD_STREAM(stream);
   if (dtype == ROD_F32) {
     const bool vec = dw_pack4_ok<float>(x, y, C);
-    DW_SELECT(dw_fwd_launch, float, x, w, y, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    // parts are laid out for the pack-4 grid; a misaligned pack-4 shape gets the separate pass
+    float* fused = (vec || C % 4 != 0) ? stat_parts : nullptr;
+    DW_SELECT(dw_fwd_launch, float, x, w, y, fused, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    if (stat_parts && !fused)
+      ::rod::stat_parts(ROD_F32, y, (long)N * Ho * Wo, C, C, stat_parts, rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C), s);
   } else if (dtype == ROD_BF16) {
     const bool vec = dw_pack4_ok<bf16_t>(x, y, C);
-    DW_SELECT(dw_fwd_launch, bf16_t, x, w, y, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    float* fused = (vec || C % 4 != 0) ? stat_parts : nullptr;
+    DW_SELECT(dw_fwd_launch, bf16_t, x, w, y, fused, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    if (stat_parts && !fused)
+      ::rod::stat_parts(ROD_BF16, y, (long)N * Ho * Wo, C, C, stat_parts, rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C), s);
   } else {
     set_error("rod_dw3x3_fwd: bad dtype %d", dtype);
     return ROD_EINVAL;

@@ -54,7 +54,7 @@ template <> struct Chunk8<float> {
 };
 
 // ---- A-row source: one output pixel of the conv (fixed for the whole K loop) --------
-template <typename T, int KS>
+template <typename T, int KS, int CIN = 0>  // CIN > 0: Cin known at compile time (stem: 3)
 struct RowSrc {
   const T* base;  // KS==1: &x[m*ldx]; KS==3: &x[pixel (n,0,0)]
   int y, x;       // KS==3 only
@@ -93,12 +93,13 @@ struct RowSrc {
         else
           c.zero();
       } else {
+        const int cin = CIN > 0 ? CIN : Cin;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int kk = k + j;
           T v = (T)0.f;
           if (kk < K) {
-            const int tap = kk / Cin, ci = kk - tap * Cin;
+            const int tap = kk / cin, ci = kk - tap * cin;
             const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
             if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = base[((long)yy * W + xx) * ldx + ci];
           }
@@ -126,10 +127,11 @@ __device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b
 // forward: y[m, co] = sum_k A[m,k] wt[co,k] + bias[co]
 // block 256 threads = 4 waves laid out WM x WN; tile BM x BN; wave tile (BM/WM) x (BN/WN)
 // =====================================================================================
-template <typename T, int KS, int BN, bool VA, bool VB, bool VY>
+template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool SPLIT = false, bool STATS = false>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
                                                        const float* __restrict__ bias, T* __restrict__ Y, long M,
-                                                       int H, int W, int Cin, int Cout, int ldx, int ldy) {
+                                                       int H, int W, int Cin, int Cout, int ldx, int ldy,
+                                                       float* __restrict__ part = nullptr, int kper = 0) {
   constexpr int BM = 128;
   constexpr int WN = BN >= 64 ? 2 : 1;
   constexpr int WM = 4 / WN;
@@ -190,8 +192,11 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.f;
 
-  load_tiles(0);
-  for (int k0 = 0; k0 < K; k0 += BK) {
+  // split-K: this workgroup reduces k in [kb, ke) only
+  const int kb = SPLIT ? blockIdx.z * kper : 0;
+  const int ke = SPLIT ? (kb + kper < K ? kb + kper : K) : K;
+  load_tiles(kb);
+  for (int k0 = kb; k0 < ke; k0 += BK) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < ACH; ++i) ra[i].store_lds(As + ((tid >> 2) + i * 64) * LD + kc);
@@ -201,7 +206,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
       if (cid < BN * BK / 8) rb[i].store_lds(Bs + (cid >> 2) * LD + kc);
     }
     __syncthreads();
-    if (k0 + BK < K) load_tiles(k0 + BK);  // next tile in flight under the MFMAs
+    if (k0 + BK < ke) load_tiles(k0 + BK);  // next tile in flight under the MFMAs
     const int fr = lane & 15, fk = (lane >> 4) * 8;
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
@@ -214,7 +219,22 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     }
   }
 
-  if constexpr (VY) {
+  if constexpr (SPLIT) {
+    // fp32 partial tile -> part[split][m][co]; bias and rounding happen in the combine
+    float* out = part + (long)blockIdx.z * M * Cout;
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int col = n0 + wn * (BN / WN) + b * 16 + (lane & 15);
+      if (col >= Cout) continue;
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long row = m0 + wm * (BM / WM) + a * 16 + (lane >> 4) * 4 + r;
+          if (row < M) out[row * Cout + col] = acc[a][b][r];
+        }
+    }
+  } else if constexpr (VY) {
     // epilogue through LDS: the accumulators (row = 4(l>>4)+r, col = l&15 of each 16x16
     // tile) are rounded to T into a 64-row staging tile, then every thread stores 16-byte
     // row segments, so each wave writes whole contiguous rows of Y.
@@ -226,6 +246,12 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     }
     T* Cs = (T*)smem;
     constexpr int WROWS = BM / WM;  // rows per wave
+    // BatchNorm partial statistics of this 128-row tile (STATS): TPC threads per column
+    // walk the staged (already rounded) rows of each half; (n, mean, M2) Chan-merged
+    constexpr int TPC = 256 / BN > 0 ? 256 / BN : 1;
+    const int scol = tid % BN, spart = tid / BN;
+    const bool sact = STATS && spart < TPC && n0 + scol < Cout;
+    float st_n = 0.f, st_mean = 0.f, st_m2 = 0.f;
 #pragma unroll
     for (int h = 0; h < BM / 64; ++h) {
       __syncthreads();
@@ -242,6 +268,26 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         }
       }
       __syncthreads();
+      if constexpr (STATS) {
+        const long left = M - (m0 + h * 64);
+        const int nrows = left < 64 ? (int)left : 64;
+        if (sact && nrows > 0) {
+          float sum = 0.f, cnt = 0.f;
+          for (int r = spart; r < nrows; r += TPC) {
+            sum += to_f32(Cs[r * LDC + scol]);
+            cnt += 1.f;
+          }
+          if (cnt > 0.f) {
+            const float mu = sum / cnt;
+            float q = 0.f;
+            for (int r = spart; r < nrows; r += TPC) {
+              const float d = to_f32(Cs[r * LDC + scol]) - mu;
+              q = fmaf(d, d, q);
+            }
+            chan_merge(st_n, st_mean, st_m2, cnt, mu, q);
+          }
+        }
+      }
       constexpr int CPR = BN / EV;  // 16-byte chunks per row
       for (int idx = tid; idx < 64 * CPR; idx += 256) {
         const int rr = idx / CPR, cc = (idx - rr * CPR) * EV;
@@ -255,6 +301,18 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         } else {
           for (int j = 0; j < Cout - col; ++j) dst[j] = src[j];
         }
+      }
+    }
+    if constexpr (STATS) {
+      __shared__ float sred[3][256];
+      sred[0][tid] = st_n;
+      sred[1][tid] = st_mean;
+      sred[2][tid] = st_m2;
+      __syncthreads();
+      if (sact && spart == 0) {
+        for (int q = 1; q < TPC; ++q)
+          chan_merge(st_n, st_mean, st_m2, sred[0][q * BN + scol], sred[1][q * BN + scol], sred[2][q * BN + scol]);
+        store_stat_part(part, Cout, blockIdx.x, n0 + scol, st_n, st_mean, st_m2);
       }
     }
   } else {
@@ -276,6 +334,103 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   }
 }
 
+// split-K combine: y[m, co] = round(sum_s part[s][m][co] + bias[co]), fixed split order
+template <typename T>
+__global__ void splitk_combine_kernel(const float* __restrict__ part, const float* __restrict__ bias,
+                                      T* __restrict__ Y, long M, int Cout, int ldy, int splits) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = M * Cout;
+  if (i >= n) return;
+  const long m = i / Cout;
+  const int co = (int)(i - m * Cout);
+  float acc = 0.f;
+  for (int z = 0; z < splits; ++z) acc += part[(long)z * n + i];
+  if (bias) acc += bias[co];
+  Y[m * ldy + co] = from_f32<T>(acc);
+}
+
+struct SplitPlan {
+  int splits, kper;
+};
+// split K when the output has fewer than 128 tiles of 128 rows x 128 columns and K is
+// at least 8 k-steps deep: ~256 workgroups, each >= 2 k-steps
+static SplitPlan split_plan(long M, int Cout, int K) {
+  SplitPlan p{1, K};
+  const long tiles = cdivl(M, 128) * cdivl(Cout, 128);
+  const int ksteps = cdiv(K, BK);
+  if (tiles >= 128 || ksteps < 8) return p;
+  int splits = (int)std::min<long>(ksteps / 2, cdivl(256, tiles));
+  if (splits < 2) return p;
+  const int per = cdiv(ksteps, splits);
+  p.kper = per * BK;
+  p.splits = cdiv(ksteps, per);
+  return p;
+}
+
+// =====================================================================================
+// stem: 3x3 / stride 1 / TF-SAME conv with Cin = 3 (the normalised image, mobilenet_v2.py
+// Conv layer) — a direct VALU convolution.  A block makes TW = 4096/CO consecutive pixels
+// of one image row: the 3 x (TW+2) x 3 input patch and the [27][CO] weights are staged in
+// LDS, each thread makes one pixel x 16 channels (27 taps, fp32 FMAs) and stores them as
+// two 16-byte vectors, so a wave writes whole contiguous output rows.
+// =====================================================================================
+template <typename T, int CO>
+__global__ void __launch_bounds__(256) stem_conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
+                                                            const float* __restrict__ bias, T* __restrict__ Y, int H,
+                                                            int W, int ldx, int ldy) {
+  constexpr int G = CO / 16;         // 16-channel groups per pixel
+  constexpr int TW = 256 / G;        // pixels per block
+  __shared__ float patch[3][TW + 2][3];
+  __shared__ __attribute__((aligned(16))) float ws[27][CO];
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * TW;
+  const int yy = blockIdx.y;
+  const int n = blockIdx.z;
+  for (int e = tid; e < 3 * (TW + 2) * 3; e += 256) {
+    const int ci = e % 3, t = e / 3;
+    const int cx = t % (TW + 2), r = t / (TW + 2);
+    const int iy = yy + r - 1, ix = x0 + cx - 1;
+    float v = 0.f;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = to_f32(X[(((long)n * H + iy) * W + ix) * ldx + ci]);
+    patch[r][cx][ci] = v;
+  }
+  for (int e = tid; e < 27 * CO; e += 256) {
+    const int co = e / 27, k = e - co * 27;  // Wt is [CO][27] (k = (i*3 + j)*3 + ci)
+    ws[k][co] = to_f32(Wt[e]);
+  }
+  __syncthreads();
+  const int p = tid / G, cg = (tid % G) * 16;
+  const int xo = x0 + p;
+  if (xo >= W) return;
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = bias ? bias[cg + j] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) {
+        const float a = patch[r][p + c][ci];
+        const f32x4* wv = (const f32x4*)&ws[(r * 3 + c) * 3 + ci][cg];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 w4 = wv[q];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[q * 4 + u] = fmaf(a, w4[u], acc[q * 4 + u]);
+        }
+      }
+  T* dst = Y + (((long)n * H + yy) * W + xo) * ldy + cg;
+  constexpr int EV = Vec16<T>::N;
+#pragma unroll
+  for (int q = 0; q < 16 / EV; ++q) {
+    Vec16<T> o;
+#pragma unroll
+    for (int u = 0; u < EV; ++u) o.set(u, acc[q * EV + u]);
+    o.store(dst + q * EV);
+  }
+}
+
 // =====================================================================================
 // weight gradient: part[s][co][k] = sum_{m in split s} dy[m, co] * A[m, k]
 // tile 64 (co) x 64 (k); rows staged m-major in LDS and read transposed
@@ -291,7 +446,7 @@ __device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
   return __builtin_bit_cast(bf16x4, r);
 }
 
-template <typename T, int KS, bool VA, bool VD>
+template <typename T, int KS, bool VA, bool VD, int CIN = 0>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X, const T* __restrict__ DY,
                                                          float* __restrict__ part, long M, int H, int W, int Cin,
                                                          int Cout, int ldx, int lddy, long chunk, int ktiles) {
@@ -329,7 +484,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
 #pragma unroll
       for (int j = 0; j < 8; ++j) rd.set(j, (co0 + lc + j < Cout) ? DY[row * lddy + co0 + lc + j] : (T)0.f);
     }
-    RowSrc<T, KS> rs;
+    RowSrc<T, KS, CIN> rs;
     rs.init(X, row < me ? row : M, M, H, W, ldx);
     rs.template load<VA>(rx, k0 + lc, K, Cin, H, W, ldx);
   };
@@ -460,10 +615,17 @@ static bool aligned16(const void* p) {
 
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY>
 static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
-                            int Cout, int ldx, int ldy, hipStream_t s) {
+                            int Cout, int ldx, int ldy, float* stats, hipStream_t s) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
+  if constexpr (VY) {
+    if (stats) {
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, true>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, stats, 0);
+      return;
+    }
+  }
   hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY>), grid, dim3(256), 0, s, (const T*)x, (const T*)wt, bias,
-                     (T*)y, M, H, W, Cin, Cout, ldx, ldy);
+                     (T*)y, M, H, W, Cin, Cout, ldx, ldy, nullptr, 0);
 }
 
 // N tile: the whole of Cout in one tile up to 256 (A is read once), else 128-wide tiles.
@@ -471,9 +633,9 @@ static void conv_fwd_launch(const void* x, const void* wt, const float* bias, vo
 // LDS-staged epilogue; the rest (stem Cin=3, odd strides) the 32/64/128 direct-store kernel.
 template <typename T, int KS>
 static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const void* wt, const float* bias, void* y,
-                              long M, int H, int W, int Cin, int Cout, int ldx, int ldy, hipStream_t s) {
+                              long M, int H, int W, int Cin, int Cout, int ldx, int ldy, float* stats, hipStream_t s) {
 #define CF(BN_, VA_, VB_, VY_) \
-  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s)
+  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, s)
   if (va && vb && vy) {
     if (Cout <= 32) CF(32, true, true, true);
     else if (Cout <= 64) CF(64, true, true, true);
@@ -498,17 +660,52 @@ static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const vo
 #undef CF
 }
 
+template <typename T, int KS>
+static void conv_fwd_split(const SplitPlan& p, const void* x, const void* wt, float* part, long M, int H, int W,
+                           int Cin, int Cout, int ldx, hipStream_t s) {
+  dim3 grid(cdivl(M, 128), cdiv(Cout, 128), p.splits);
+  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, 128, true, true, false, true>), grid, dim3(256), 0, s, (const T*)x,
+                     (const T*)wt, nullptr, nullptr, M, H, W, Cin, Cout, ldx, 0, part, p.kper);
+}
+
 template <typename T>
-static void conv_fwd_typed(const void* x, const void* wt, const float* bias, void* y, int N, int H, int W, int Cin,
-                           int Cout, int ksize, int ldx, int ldy, hipStream_t s) {
+static void conv_fwd_typed(const void* x, const void* wt, const float* bias, void* y, void* ws, float* stats, int N,
+                           int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy, hipStream_t s) {
   const long M = (long)N * H * W;
   const int K = ksize * ksize * Cin;
   const int eV = Vec16<T>::N;
   const bool va = aligned16<T>(x) && (ldx % eV == 0) && (ksize == 1 ? true : (Cin % 8 == 0));
   const bool vb = aligned16<T>(wt) && (K % eV == 0);
   const bool vy = aligned16<T>(y) && (ldy % eV == 0);
-  if (ksize == 1) conv_fwd_dispatch<T, 1>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
-  else conv_fwd_dispatch<T, 3>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, s);
+  const SplitPlan sp = split_plan(M, Cout, K);
+  const int nparts = (int)cdivl(M, 128);
+  const int dt = sizeof(T) == 4 ? ROD_F32 : ROD_BF16;
+  if (ws != nullptr && sp.splits > 1 && va && vb) {
+    float* part = (float*)ws;
+    if (ksize == 1) conv_fwd_split<T, 1>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, s);
+    else conv_fwd_split<T, 3>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, s);
+    hipLaunchKernelGGL(splitk_combine_kernel<T>, dim3(cdivl(M * Cout, 256)), dim3(256), 0, s, (const float*)part,
+                       bias, (T*)y, M, Cout, ldy, sp.splits);
+    if (stats) stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
+    return;
+  }
+  if (stats && !(va && vb && vy)) {  // no fused epilogue on this path: separate statistics pass
+    conv_fwd_typed<T>(x, wt, bias, y, ws, nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy, s);
+    stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
+    return;
+  }
+  static const bool no_stem = getenv("ROD_DEBUG_NOSTEM") != nullptr;  // debug bisection
+  if (ksize == 3 && Cin == 3 && (Cout == 32 || Cout == 64) && vy && !no_stem) {
+    if (Cout == 32)
+      hipLaunchKernelGGL((stem_conv_fwd_kernel<T, 32>), dim3(cdiv(W, 128), H, N), dim3(256), 0, s, (const T*)x,
+                         (const T*)wt, bias, (T*)y, H, W, ldx, ldy);
+    else
+      hipLaunchKernelGGL((stem_conv_fwd_kernel<T, 64>), dim3(cdiv(W, 64), H, N), dim3(256), 0, s, (const T*)x,
+                         (const T*)wt, bias, (T*)y, H, W, ldx, ldy);
+    return;
+  }
+  if (ksize == 1) conv_fwd_dispatch<T, 1>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, s);
+  else conv_fwd_dispatch<T, 3>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, s);
 }
 
 template <typename T, int KS, bool VA, bool VD>
@@ -537,8 +734,15 @@ static void wgrad_typed(const void* x, const void* dy, float* dw, float* db, flo
   const int eV = Vec16<T>::N;
   const bool va = aligned16<T>(x) && (ldx % eV == 0) && (ksize == 1 ? true : (Cin % 8 == 0));
   const bool vd = aligned16<T>(dy) && (lddy % eV == 0);
-  if (ksize == 1) wgrad_va_vd<T, 1>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
-  else wgrad_va_vd<T, 3>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  if (ksize == 3 && Cin == 3 && vd) {
+    dim3 grid(p.ctiles * p.ktiles, p.splits);
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, 3, false, true, 3>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy,
+                       part, M, H, W, Cin, Cout, ldx, lddy, p.chunk, p.ktiles);
+  } else if (ksize == 1) {
+    wgrad_va_vd<T, 1>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  } else {
+    wgrad_va_vd<T, 3>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+  }
   const long n = (long)Cout * K;
   slab_sum(part, dw, p.splits, n, s);
   if (db) {
@@ -556,15 +760,21 @@ using namespace rod;
 
 extern "C" {
 
-int rod_conv_fwd(const void* x, const void* wt, const float* bias, void* y, int N, int H, int W, int Cin, int Cout,
-                 int ksize, int ldx, int ldy, int dtype, void* stream) {
+size_t rod_conv_fwd_workspace(int N, int H, int W, int Cin, int Cout, int ksize) {
+  const long M = (long)N * H * W;
+  const SplitPlan p = split_plan(M, Cout, ksize * ksize * Cin);
+  return p.splits > 1 ? (size_t)p.splits * M * Cout * sizeof(float) : 0;
+}
+
+int rod_conv_fwd(const void* x, const void* wt, const float* bias, void* y, void* workspace, float* stat_parts, int N,
+                 int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy, int dtype, void* stream) {
   ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "rod_conv_fwd: bad shape");
   ROD_CHECK_ARG(ksize == 1 || ksize == 3, "rod_conv_fwd: ksize must be 1 or 3");
   if (ldx == 0) ldx = Cin;
   if (ldy == 0) ldy = Cout;
   ROD_CHECK_ARG(ldx >= Cin && ldy >= Cout, "rod_conv_fwd: leading dim too small");
-  ROD_DISPATCH_DTYPE(dtype, conv_fwd_typed<T>(x, wt, bias, y, N, H, W, Cin, Cout, ksize, ldx, ldy,
-                                              ROD_STREAM(stream)));
+  ROD_DISPATCH_DTYPE(dtype, conv_fwd_typed<T>(x, wt, bias, y, workspace, stat_parts, N, H, W, Cin, Cout, ksize, ldx,
+                                              ldy, ROD_STREAM(stream)));
   return check_launch("rod_conv_fwd");
 }
 

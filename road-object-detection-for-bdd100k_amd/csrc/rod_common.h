@@ -66,6 +66,36 @@ __device__ __forceinline__ float warp_sum(float v) {
   return v;
 }
 
+// BatchNorm partial statistics: slab [nparts][3][C] of (count, mean, M2) per part and
+// channel, part-major so that a producer block writes its 3*C values contiguously (parts
+// with count 0 are ignored by the merge).  Written by bn_stats_kernel and by the epilogues
+// of the producers that fuse it (rod_conv_fwd, rod_dw3x3_fwd).
+__device__ __forceinline__ void store_stat_part(float* slab, int C, long part, int c, float n, float mean, float m2) {
+  float* p = slab + part * 3 * C + c;
+  p[0] = n;
+  p[C] = mean;
+  p[2 * C] = m2;
+}
+
+// fp32 Chan merge of (n, mean, M2) accumulators
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  if (nb == 0.f) return;
+  if (n == 0.f) {
+    n = nb;
+    mean = meanb;
+    m2 = m2b;
+    return;
+  }
+  const float nt = n + nb;
+  const float d = meanb - mean;
+  mean = fmaf(d, nb / nt, mean);
+  m2 = m2 + m2b + d * d * (n * nb / nt);
+  n = nt;
+}
+
+// Fallback: parts of y[M, C] computed by a separate pass (batchnorm.hip).
+void stat_parts(int dtype, const void* y, long M, int C, int ld, float* parts, int nparts, hipStream_t s);
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 inline long cdivl(long a, long b) { return (a + b - 1) / b; }
 

@@ -76,10 +76,17 @@ class MobilenetV2:
         self.store.add_buffer(name + '/moving_mean', np.zeros(c, np.float32))
         self.store.add_buffer(name + '/moving_variance', np.ones(c, np.float32))
 
-    def _bn_act(self, x, name, act, training, residual=None):
+    def _bn_act(self, x, name, act, training, residual=None, parts=None):
         P, B = self.store.params, self.store.buffers
         return ops.bn_act(x, P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'],
-                          B[name + '/moving_variance'], act, training, BN_DECAY, BN_EPS, residual)
+                          B[name + '/moving_variance'], act, training, BN_DECAY, BN_EPS, residual, parts)
+
+    @staticmethod
+    def _conv(x, w, ks, training):
+        """conv whose epilogue also reduces the following BatchNorm's statistics (training)."""
+        if training:
+            return ops.conv2d(x, w, None, ks, want_stats=True)
+        return ops.conv2d(x, w, None, ks), None
 
     def __call__(self, x, is_training, final_endpoint=None, taps=None):
         """Returns the endpoint dict {'layer_1': ..., 'layer_24': ...} (mobilenet.py:275-281).
@@ -92,20 +99,23 @@ class MobilenetV2:
         for (idx, kind, s, cin, inner, cout, res, sc) in self.plan:
             base = '%s/%s' % (self.scope, sc)
             if kind == 'conv':
-                x = ops.conv2d(x, P[base + '/weights'], None, 3)
-                x = self._bn_act(x, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training)
+                x, st = self._conv(x, P[base + '/weights'], 3, is_training)
+                x = self._bn_act(x, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st)
             else:
                 inp = None
                 if res:
                     inp, x = graph.fork(x, 2)
                 if inner > cin:
-                    x = ops.conv2d(x, P[base + '/expand/weights'], None, 1)
-                    x = self._bn_act(x, base + '/expand/BatchNorm', ops.ROD_ACT_RELU6, is_training)
-                x = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s)
-                x = self._bn_act(x, base + '/depthwise/BatchNorm', ops.ROD_ACT_RELU6, is_training)
-                x = ops.conv2d(x, P[base + '/project/weights'], None, 1)
+                    x, st = self._conv(x, P[base + '/expand/weights'], 1, is_training)
+                    x = self._bn_act(x, base + '/expand/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st)
+                if is_training:
+                    x, st = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s, want_stats=True)
+                else:
+                    x, st = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s), None
+                x = self._bn_act(x, base + '/depthwise/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st)
+                x, st = self._conv(x, P[base + '/project/weights'], 1, is_training)
                 x = self._bn_act(x, base + '/project/BatchNorm', ops.ROD_ACT_NONE, is_training,
-                                 residual=inp)
+                                 residual=inp, parts=st)
             name = 'layer_%d' % idx
             last = final_endpoint == name or idx == self.plan[-1][0]
             if name in taps and not last:

@@ -105,10 +105,17 @@ class CatchNet:
                 self._head_bn(base + '/BatchNorm', 2 * f_c)
 
     # ------------------------------------------------------------------ forward
-    def _bn(self, x, name, training, act=ops.ROD_ACT_LEAKY):
+    def _bn(self, x, name, training, act=ops.ROD_ACT_LEAKY, parts=None):
         P, B = self.store.params, self.store.buffers
         return ops.bn_act(x, None, P[name + '/beta'], B[name + '/moving_mean'], B[name + '/moving_variance'],
-                          act, training, HEAD_BN_DECAY, HEAD_BN_EPS)
+                          act, training, HEAD_BN_DECAY, HEAD_BN_EPS, parts=parts)
+
+    @staticmethod
+    def _conv(x, w, b, ks, training):
+        """conv(+bias) whose epilogue also reduces the following BatchNorm's statistics."""
+        if training:
+            return ops.conv2d(x, w, b, ks, want_stats=True)
+        return ops.conv2d(x, w, b, ks), None
 
     def head_out(self, feats, scope, k, training):
         """__det_out / __clf_out (catch_net.py:276-342)."""
@@ -121,8 +128,8 @@ class CatchNet:
                 for ks in (1, 3):
                     cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
                     bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
-                    x = ops.conv2d(x, P[cname + '/weights'], P[cname + '/biases'], ks)
-                    x = self._bn(x, bname, training)
+                    x, st = self._conv(x, P[cname + '/weights'], P[cname + '/biases'], ks, training)
+                    x = self._bn(x, bname, training, parts=st)
                     n += 1
             B_, fh, fw, _ = x.shape
             outs.append(x.view(B_, fh, fw, self.n_anchor[i], k))
@@ -138,8 +145,8 @@ class CatchNet:
         for i in range(n):
             base = 'deconv/block_%d' % (i + 1)
             if i == 0:
-                x = ops.conv2d(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1)
-                x = self._bn(x, base + '/BatchNorm', training)
+                x, st = self._conv(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1, training)
+                x = self._bn(x, base + '/BatchNorm', training, parts=st)
             else:
                 B_, h, w, _ = layers[i].shape
                 x_out, x_up, x_rs = xs

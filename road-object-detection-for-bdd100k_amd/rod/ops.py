@@ -11,6 +11,7 @@ weights fp32 [Cout, k, k, Cin]; depthwise weights fp32 [3, 3, C]; BN vectors fp3
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -19,6 +20,8 @@ from . import _abi
 from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU6  # noqa: F401
 
 _DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
+# debug bisection switches (comma list): splitk, epistats, convstats, dwstats
+_DISABLE = set(os.environ.get("ROD_DISABLE", "").split(","))
 
 
 def dtcode(t: torch.Tensor) -> int:
@@ -78,18 +81,26 @@ def copy2d(src, src_ld_bytes, dst, dst_ld_bytes, rows, cols_bytes, src_off=0, ds
 # ----------------------------------------------------------------------------- depthwise
 class _DW3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride):
+    def forward(ctx, x, w, stride, want_stats=False):
         N, H, W, C = x.shape
         Ho, pt = same_pad(H, stride)
         Wo, pl = same_pad(W, stride)
         y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
-        _abi.call("rod_dw3x3_fwd", x, w, y, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x), stream())
+        parts = None
+        if want_stats:  # BatchNorm partial statistics from the epilogue
+            nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C)
+            parts = torch.empty((3, C, nparts), dtype=torch.float32, device=x.device)
+        _abi.call("rod_dw3x3_fwd", x, w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x), stream())
         ctx.save_for_backward(x, w)
         ctx.geo = (N, H, W, C, stride, pt, pl, Ho, Wo)
+        if want_stats:
+            ctx.mark_non_differentiable(parts)
+            ctx.set_materialize_grads(False)
+            return y, parts
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *_):
         x, w = ctx.saved_tensors
         N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
         dy = dy.contiguous()
@@ -102,31 +113,48 @@ class _DW3x3(torch.autograd.Function):
             ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
             _abi.call("rod_dw3x3_bwd_filter", x, dy, g, ws, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x), stream())
             _mark_written(w)
-        return dx, None, None
+        return dx, None, None, None
 
 
-def dw3x3(x, w, stride=1):
-    """Depthwise 3x3, TF-SAME (conv_blocks.py:238-247)."""
-    return _DW3x3.apply(x, w, stride)
+def dw3x3(x, w, stride=1, want_stats=False):
+    """Depthwise 3x3, TF-SAME (conv_blocks.py:238-247).  want_stats: also return the
+    BatchNorm partial statistics of the output (for bn_act(..., parts=))."""
+    if want_stats and "dwstats" in _DISABLE:
+        return _DW3x3.apply(x, w, stride, False), None
+    return _DW3x3.apply(x, w, stride, want_stats)
 
 
 # ----------------------------------------------------------------------------- dense conv
+def conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, stat_parts=None):
+    """rod_conv_fwd with its split-K workspace (allocated only when the plan splits)."""
+    nb = 0 if "splitk" in _DISABLE else _abi.query("rod_conv_fwd_workspace", N, H, W, Cin, Cout, ksize)
+    ws = workspace(nb, x.device) if nb else None
+    _abi.call("rod_conv_fwd", x, wt, b, y, ws, stat_parts, N, H, W, Cin, Cout, ksize, 0, 0, dtcode(x), stream())
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, ksize):
+    def forward(ctx, x, w, b, ksize, want_stats=False):
         N, H, W, Cin = x.shape
         Cout = w.shape[0]
         assert w.shape == (Cout, ksize, ksize, Cin), (tuple(w.shape), ksize, Cin)
         wt = torch.empty((Cout, ksize * ksize * Cin), dtype=x.dtype, device=x.device)
         _abi.call("rod_conv_weight_prep", w, wt, Cout, Cin, ksize, 0, dtcode(x), stream())
         y = torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
-        _abi.call("rod_conv_fwd", x, wt, b, y, N, H, W, Cin, Cout, ksize, 0, 0, dtcode(x), stream())
+        parts = None
+        if want_stats:  # BatchNorm partial statistics from the epilogue ([3][Cout][ceil(M/128)])
+            parts = torch.empty((3, Cout, -(-(N * H * W) // 128)), dtype=torch.float32, device=x.device)
+        conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, parts)
         ctx.save_for_backward(x, w, b)
         ctx.ksize = ksize
+        if want_stats:
+            ctx.mark_non_differentiable(parts)
+            ctx.set_materialize_grads(False)
+            return y, parts
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *_):
         x, w, b = ctx.saved_tensors
         ks = ctx.ksize
         N, H, W, Cin = x.shape
@@ -137,7 +165,7 @@ class _Conv(torch.autograd.Function):
             wt1 = torch.empty((Cin, ks * ks * Cout), dtype=x.dtype, device=x.device)
             _abi.call("rod_conv_weight_prep", w, wt1, Cout, Cin, ks, 1, dtcode(x), stream())
             dx = torch.empty_like(x)
-            _abi.call("rod_conv_fwd", dy, wt1, None, dx, N, H, W, Cout, Cin, ks, 0, 0, dtcode(x), stream())
+            conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks)
         need_w = ctx.needs_input_grad[1]
         need_b = b is not None and ctx.needs_input_grad[2]
         if need_w or need_b:
@@ -151,23 +179,33 @@ class _Conv(torch.autograd.Function):
                 _mark_written(w)
             if need_b:
                 _mark_written(b)
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
-def conv2d(x, w, b=None, ksize=1):
-    """slim.conv2d, stride 1, SAME (1x1 or 3x3), NHWC."""
-    return _Conv.apply(x, w, b, ksize)
+def conv2d(x, w, b=None, ksize=1, want_stats=False):
+    """slim.conv2d, stride 1, SAME (1x1 or 3x3), NHWC.  want_stats: also return the
+    BatchNorm partial statistics of the output (for bn_act(..., parts=))."""
+    if want_stats and "convstats" in _DISABLE:
+        return _Conv.apply(x, w, b, ksize, False), None
+    return _Conv.apply(x, w, b, ksize, want_stats)
 
 
 # ----------------------------------------------------------------------------- batch norm
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, mmean, mvar, act, training, decay, eps):
+    def forward(ctx, x, gamma, beta, residual, mmean, mvar, act, training, decay, eps, parts):
         N, H, W, C = x.shape
         M = N * H * W
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         rstd = torch.empty(C, dtype=torch.float32, device=x.device)
-        if training:
+        if "epistats" in _DISABLE:
+            parts = None
+        if training and parts is not None:  # statistics already reduced by the producer's epilogue
+            nb = _abi.query("rod_bn_finalize_workspace", parts.shape[2], C)
+            ws = workspace(nb, x.device) if nb else None
+            _abi.call("rod_bn_finalize", parts, parts.shape[2], M, C, eps, decay, mean, rstd, mmean, mvar, ws,
+                      stream())
+        elif training:
             ws = workspace(_abi.query("rod_bn_stats_workspace", M, C), x.device)
             _abi.call("rod_bn_stats", x, M, C, 0, eps, decay, mean, rstd, mmean, mvar, ws, dtcode(x), stream())
         else:
@@ -206,12 +244,13 @@ class _BNAct(torch.autograd.Function):
         if need_b:
             _mark_written(beta)
         dres = dy if ctx.has_res else None
-        return dx, None, None, dres, None, None, None, None, None, None
+        return dx, None, None, dres, None, None, None, None, None, None, None
 
 
-def bn_act(x, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, residual=None):
-    """slim.batch_norm (fused) + activation (+ residual add after the activation)."""
-    return _BNAct.apply(x, gamma, beta, residual, mmean, mvar, act, training, decay, eps)
+def bn_act(x, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, residual=None, parts=None):
+    """slim.batch_norm (fused) + activation (+ residual add after the activation).
+    parts: partial statistics of x from its producer (conv2d(..., want_stats=True))."""
+    return _BNAct.apply(x, gamma, beta, residual, mmean, mvar, act, training, decay, eps, parts)
 
 
 # ----------------------------------------------------------------------------- levels
@@ -348,7 +387,7 @@ class _Deconv2x2(torch.autograd.Function):
         wt = torch.empty((4 * F, Cin), dtype=x.dtype, device=x.device)
         _abi.call("rod_conv_weight_prep", w, wt, 4 * F, Cin, 1, 0, dtcode(x), stream())
         z = torch.empty((N, h, wd, 4 * F), dtype=x.dtype, device=x.device)
-        _abi.call("rod_conv_fwd", x, wt, None, z, N, h, wd, Cin, 4 * F, 1, 0, 0, dtcode(x), stream())
+        conv_fwd_raw(x, wt, None, z, N, h, wd, Cin, 4 * F, 1)
         y = torch.empty((N, ho, wo, F), dtype=x.dtype, device=x.device)
         _abi.call("rod_depth_to_space2", z, y, N, h, wd, F, ho, wo, 0, dtcode(x), stream())
         ctx.save_for_backward(x, w)
@@ -366,7 +405,7 @@ class _Deconv2x2(torch.autograd.Function):
             wt1 = torch.empty((Cin, 4 * F), dtype=dy.dtype, device=dy.device)
             _abi.call("rod_conv_weight_prep", w, wt1, 4 * F, Cin, 1, 1, dtcode(dy), stream())
             dx = torch.empty_like(x)
-            _abi.call("rod_conv_fwd", dz, wt1, None, dx, N, h, wd, 4 * F, Cin, 1, 0, 0, dtcode(dy), stream())
+            conv_fwd_raw(dz, wt1, None, dx, N, h, wd, 4 * F, Cin, 1)
         if ctx.needs_input_grad[1]:
             ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, h, wd, Cin, 4 * F, 1), x.device)
             _abi.call("rod_conv_wgrad", x, dz, grad_slot(w), None, ws, N, h, wd, Cin, 4 * F, 1, 0, 0, dtcode(x),

@@ -21,7 +21,8 @@ MI355X_F32_PEAK_TFLOPS = 157.3    # f32 MFMA / vector
 def cost(name, a):
     """(bytes, flops) of the call rod_<name>(*a)."""
     if name in ("rod_dw3x3_fwd", "rod_dw3x3_bwd_data"):
-        N, H, W, C, s, pt, pl, Ho, Wo, dt = a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12]
+        o = 1 if name == "rod_dw3x3_fwd" else 0   # rod_dw3x3_fwd has the stat_parts pointer
+        N, H, W, C, Ho, Wo, dt = a[3 + o], a[4 + o], a[5 + o], a[6 + o], a[10 + o], a[11 + o], a[12 + o]
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
     if name == "rod_dw3x3_bwd_filter":
@@ -29,13 +30,13 @@ def cost(name, a):
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
     if name == "rod_conv_fwd":
-        N, H, W, Cin, Cout, ks, dt = a[4], a[5], a[6], a[7], a[8], a[9], a[12]
+        N, H, W, Cin, Cout, ks, dt = a[6], a[7], a[8], a[9], a[10], a[11], a[14]
         es = _ES[dt]
         M = N * H * W
         K = ks * ks * Cin
         return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[2] is not None else 0), 2 * M * K * Cout
     if name == "rod_conv_wgrad":
-        N, H, W, Cin, Cout, ks, dt = a[5], a[6], a[7], a[8], a[9], a[10], a[13]
+        N, H, W, Cin, Cout, ks, dt = a[6], a[7], a[8], a[9], a[10], a[11], a[14]
         es = _ES[dt]
         M = N * H * W
         K = ks * ks * Cin

@@ -33,16 +33,21 @@ def _param(t, dev):
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize('C', [24, 6])
-@pytest.mark.parametrize('stride,H,W', [(1, 13, 17), (2, 13, 17), (2, 12, 16), (1, 4, 5)])
+@pytest.mark.parametrize('C,stride,H,W', [(c, s, h, w) for c in (24, 6)
+                                          for (s, h, w) in [(1, 13, 17), (2, 13, 17), (2, 12, 16), (1, 4, 5)]] +
+                         [(144, 2, 45, 80), (144, 1, 45, 80), (96, 2, 90, 161), (960, 1, 23, 40), (32, 1, 90, 160)])
 def test_depthwise(dev, dtype, C, stride, H, W):
     g = torch.Generator().manual_seed(1)
     x = torch.randn(2, H, W, C, generator=g)
     w = torch.randn(3, 3, C, generator=g) * 0.3
+    if dtype == torch.bfloat16:  # the oracle sees the bf16-rounded activations (dw weights stay fp32)
+        x = x.to(torch.bfloat16).float()
     xo = x.clone().requires_grad_(True)
     wo = w.clone().requires_grad_(True)
     yo = onet.dwconv(xo.permute(0, 3, 1, 2), wo, stride).permute(0, 2, 3, 1)
     gy = torch.randn(yo.shape, generator=g)
+    if dtype == torch.bfloat16:
+        gy = gy.to(torch.bfloat16).float()
     (yo * gy).sum().backward()
 
     xd = x.to(dev, dtype).requires_grad_(True)
@@ -50,18 +55,25 @@ def test_depthwise(dev, dtype, C, stride, H, W):
     yd = ops.dw3x3(xd, wd, stride)
     assert yd.shape == yo.shape
     yd.backward(gy.to(dev, dtype))
-    ref_x = xo.detach() if dtype == torch.float32 else xo.detach().to(torch.bfloat16).float()
     _close(yd, yo, dtype, scale=3)
     _close(xd.grad, xo.grad, dtype, scale=3)
-    _close(wd._rod_grad, wo.grad, dtype, scale=10 if dtype == torch.bfloat16 else 3)
+    npix = x.shape[0] * yo.shape[1] * yo.shape[2]   # filter gradient = sum over npix products
+    _close(wd._rod_grad, wo.grad, dtype, scale=max(10 if dtype == torch.bfloat16 else 3, np.sqrt(npix) / 8))
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize('ks,Cin,Cout', [(1, 16, 96), (1, 96, 24), (1, 64, 128), (1, 40, 66), (3, 3, 32),
-                                         (3, 128, 128), (3, 24, 24), (3, 99, 99), (1, 320, 1920)])
-def test_conv(dev, dtype, ks, Cin, Cout):
+@pytest.mark.parametrize('ks,Cin,Cout,NHW', [(1, 16, 96, None), (1, 96, 24, None), (1, 64, 128, None), (1, 40, 66, None),
+                                             (3, 3, 32, None), (3, 128, 128, None), (3, 24, 24, None), (3, 99, 99, None),
+                                             (1, 320, 1920, None), (1, 24, 144, (2, 45, 80)), (1, 32, 192, (2, 23, 40)),
+                                             (1, 96, 160, (2, 23, 40)), (1, 64, 256, (1, 30, 41)),
+                                             (3, 36, 36, (2, 3, 5)), (1, 1920, 320, (2, 3, 5)),
+                                             (3, 128, 128, (2, 3, 5)), (3, 128, 128, (2, 5, 9)),
+                                             (1, 256, 128, (2, 3, 5)), (1, 128, 36, (2, 3, 5)),
+                                             (3, 36, 36, (2, 2, 3)), (3, 128, 128, (2, 2, 3)), (1, 256, 128, (2, 2, 3)),
+                                             (1, 128, 36, (2, 2, 3)), (3, 36, 36, (2, 1, 2))])
+def test_conv(dev, dtype, ks, Cin, Cout, NHW):
     g = torch.Generator().manual_seed(2)
-    N, H, W = 2, 7, 11
+    N, H, W = NHW or (2, 7, 11)
     x = torch.randn(N, H, W, Cin, generator=g)
     w = torch.randn(Cout, ks, ks, Cin, generator=g) / np.sqrt(ks * ks * Cin)
     b = torch.randn(Cout, generator=g) * 0.1
@@ -142,6 +154,95 @@ def test_batchnorm(dev, dtype, act, C, gamma, res):
         yeo = {ops.ROD_ACT_NONE: lambda t: t, ops.ROD_ACT_RELU6: onet.relu6, ops.ROD_ACT_LEAKY: onet.leaky}[act](
             yeo).permute(0, 2, 3, 1)
     _close(ye, yeo, dtype, scale=5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('ks,Cin,Cout,NHW', [(1, 16, 96, (2, 45, 80)), (3, 128, 128, (2, 3, 5)), (3, 36, 36, (2, 10, 18)),
+                                             (1, 64, 256, (1, 30, 41)), (3, 3, 32, (1, 20, 30)),
+                                             (1, 320, 1920, (2, 3, 5)), (1, 24, 144, (2, 23, 40))])
+def test_conv_epilogue_bn_stats(dev, dtype, ks, Cin, Cout, NHW):
+    """BatchNorm statistics reduced in the conv epilogue (rod_conv_fwd stat_parts ->
+    rod_bn_finalize) against the separate statistics pass (rod_bn_stats) on the same conv
+    output: normalised outputs and moving statistics agree to fp32 rounding."""
+    g = torch.Generator().manual_seed(4)
+    N, H, W = NHW
+    x = (torch.randn(N, H, W, Cin, generator=g) + 0.5).to(dev, dtype)
+    w = (torch.randn(Cout, ks, ks, Cin, generator=g) / np.sqrt(ks * ks * Cin)).to(dev)
+    b = (torch.randn(Cout, generator=g) * 0.3).to(dev)
+    be = torch.zeros(Cout, device=dev)
+    y1, parts = ops.conv2d(x, w, b, ks, want_stats=True)
+    y2 = ops.conv2d(x, w, b, ks)
+    assert torch.equal(y1, y2)
+    mm1, mv1 = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    mm2, mv2 = mm1.clone(), mv1.clone()
+    z1 = ops.bn_act(y1, None, be, mm1, mv1, ops.ROD_ACT_NONE, True, 0.9, 1e-3, parts=parts)
+    z2 = ops.bn_act(y2, None, be, mm2, mv2, ops.ROD_ACT_NONE, True, 0.9, 1e-3)
+    torch.testing.assert_close(mm1, mm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mv1, mv2, rtol=1e-5, atol=1e-6)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(z1.float(), z2.float(), **tol)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('C,stride,H,W', [(144, 1, 45, 80), (96, 2, 90, 161), (6, 1, 13, 17), (960, 1, 3, 5),
+                                          (32, 1, 33, 70)])
+def test_dw_epilogue_bn_stats(dev, dtype, C, stride, H, W):
+    """Depthwise forward with the BatchNorm statistics reduced in its epilogue agrees with
+    the separate statistics pass on the same output."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(2, H, W, C, generator=g) + 0.3).to(dev, dtype)
+    w = (torch.randn(3, 3, C, generator=g) * 0.3).to(dev)
+    y1, parts = ops.dw3x3(x, w, stride, want_stats=True)
+    y2 = ops.dw3x3(x, w, stride)
+    assert torch.equal(y1, y2)
+    be = torch.zeros(C, device=dev)
+    mm1, mv1 = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    mm2, mv2 = mm1.clone(), mv1.clone()
+    z1 = ops.bn_act(y1, None, be, mm1, mv1, ops.ROD_ACT_NONE, True, 0.9, 1e-3, parts=parts)
+    z2 = ops.bn_act(y2, None, be, mm2, mv2, ops.ROD_ACT_NONE, True, 0.9, 1e-3)
+    torch.testing.assert_close(mm1, mm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mv1, mv2, rtol=1e-5, atol=1e-6)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(z1.float(), z2.float(), **tol)
+
+
+def test_head_chain_small_level(dev):
+    """One refine head (catch_net.py:276-342) on a 2x3 map, B=2 (M = 12 rows): conv1x1 ->
+    BN -> leaky -> conv3x3 -> BN -> leaky -> conv1x1 -> BN -> leaky -> conv3x3 -> BN -> leaky,
+    with the epilogue statistics, against the oracle chain in fp32 (forward and every grad)."""
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(2, 2, 3, 256, generator=g)
+    chans = [(256, 128, 1), (128, 128, 3), (128, 36, 1), (36, 36, 3)]
+    Ws = [torch.randn(co, k, k, ci, generator=g) / np.sqrt(k * k * ci) for ci, co, k in chans]
+    Bs = [torch.randn(co, generator=g) * 0.1 for _, co, _ in chans]
+    Be = [torch.randn(co, generator=g) * 0.1 for _, co, _ in chans]
+    # oracle
+    Wo = [w.clone().requires_grad_(True) for w in Ws]
+    Bo = [b.clone().requires_grad_(True) for b in Bs]
+    Beo = [b.clone().requires_grad_(True) for b in Be]
+    h = x.permute(0, 3, 1, 2)
+    for i in range(4):
+        h = onet.conv(h, Wo[i], Bo[i])
+        h = onet.leaky(onet.batch_norm(h, None, Beo[i], torch.zeros(h.shape[1]), torch.ones(h.shape[1]), True,
+                                       0.999, 1e-3, {}, 'b%d' % i))
+    gy = torch.randn(h.shape, generator=g)
+    (h * gy).sum().backward()
+    # librod
+    Wd = [_param(w, dev) for w in Ws]
+    Bd = [_param(b, dev) for b in Bs]
+    Bed = [_param(b, dev) for b in Be]
+    hd = x.to(dev).requires_grad_(True)
+    t = hd
+    for i, (ci, co, k) in enumerate(chans):
+        t, st = ops.conv2d(t, Wd[i], Bd[i], k, want_stats=True)
+        t = ops.bn_act(t, None, Bed[i], torch.zeros(co, device=dev), torch.ones(co, device=dev), ops.ROD_ACT_LEAKY,
+                       True, 0.999, 1e-3, parts=st)
+    t.backward(gy.permute(0, 2, 3, 1).contiguous().to(dev))
+    _close(t, h.permute(0, 2, 3, 1), torch.float32, scale=10)
+    for i in range(4):
+        _close(Bed[i]._rod_grad, Beo[i].grad, torch.float32, scale=10, rtol=1e-4)
+        _close(Wd[i]._rod_grad, Wo[i].grad, torch.float32, scale=10, rtol=1e-4)
+        _close(Bd[i]._rod_grad, Bo[i].grad, torch.float32, scale=10, rtol=1e-4)
 
 
 def _anchors(H, W):

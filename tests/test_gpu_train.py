@@ -4,7 +4,11 @@ network outputs, moving statistics, loss, every parameter gradient and the SGD u
 Tolerance design (normwise error e(a, b) = max|a-b| / max|b|, measured against the
 oracle evaluated in float64 = "truth"):
   fp32 outputs:  e(hip, truth) <= max(1e-4, 4 * e(oracle_fp32, truth))   per level
-  fp32 grads:    e(hip, truth) <= max(2e-3, 4 * e(oracle_fp32, truth))   per tensor
+  fp32 grads:    e(hip, truth) <= max(2e-3, 4 * e(oracle_fp32, truth), 4 * s) per tensor,
+                 s = e(truth under 1e-6 relative input noise, truth): activation kinks near
+                 zero on the few-row levels make single gradient entries jump under ANY
+                 fp32 evaluation order (measured: swapping only the stem conv's summation
+                 order moves refine/block_5 grads by 5-20 %)
 The second term matters only where fp32 itself is ill-conditioned: BatchNorm over the
 few rows of the deepest feature maps (2-30 values at these test sizes) amplifies any
 rounding difference (the oracle's own fp32 error there reaches 1e-3..1), so no fp32
@@ -35,10 +39,13 @@ def _nerr(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-def _oracle_step(tr, img, corner, labels, n, H, W, B, dt):
+def _oracle_step(tr, img, corner, labels, n, H, W, B, dt, perturb=0.0, seed=0):
     P = {k: v.detach().cpu().clone().to(dt).requires_grad_(v.requires_grad) for k, v in tr.net.store.params.items()}
     Bf = {k: v.detach().cpu().clone().to(dt) for k, v in tr.net.store.buffers.items()}
     x = torch.from_numpy(np.float32(2.0 / 255.0) * img.cpu().numpy().astype(np.float32) - np.float32(1.0)).to(dt)
+    if perturb:  # fp32-sized relative noise on the input (sensitivity probe of the fp64 truth)
+        g = torch.Generator().manual_seed(seed)
+        x = x * (1 + perturb * torch.randn(x.shape, generator=g, dtype=dt))
     mov = {}
     refine = onet.forward(x, P, Bf, True, moving=mov)
     init = oa.init_anchor(6, (H, W))
@@ -88,6 +95,12 @@ def test_refine_step_matches_oracle(dev, dtype):
     p0 = tr.net.store.flat.detach().clone()
     P32, mov32, ref32, loss32 = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.float32)
     P64, mov64, ref64, loss64 = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.float64)
+    if dtype == torch.float32:
+        # sensitivity of the fp64 truth itself to fp32-level noise (2 draws of 1e-6 relative
+        # input noise): activation kinks (relu6 / leaky) near zero on the few-row pyramid
+        # levels make some gradients legitimately jump under any fp32 evaluation order
+        Pp = [_oracle_step(tr, img, corner, labels, n, H, W, B, torch.float64, perturb=1e-6, seed=s_)[0]
+              for s_ in (11, 12)]
     if dtype == torch.bfloat16:
         # baseline: the same oracle step evaluated with every tensor in bf16 (PyTorch CPU)
         Pb, movb, refb, _ = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.bfloat16)
@@ -128,12 +141,15 @@ def test_refine_step_matches_oracle(dev, dtype):
         e_o = _nerr(g32, g64)
         if dtype == torch.float32:
             e_h = _nerr(gd, g64)
-            if e_h > max(2e-3, 4 * e_o):
-                bad.append((name, e_h, e_o))
+            e_s = max(_nerr(pp[name].grad, g64) for pp in Pp)
+            if e_h > max(2e-3, 4 * e_o, 4 * e_s):
+                bad.append((name, e_h, e_o, e_s))
         elif e_o < 1e-2 and g64.abs().max() > 0 and _cos(Pb[name].grad.float(), g64) >= 0.95 and \
                 not _bf16_ok(gd, Pb[name].grad.float(), g64):
             bad.append((name, _cos(gd, g64), _cos(Pb[name].grad.float(), g64), e_o))
-    assert not bad, bad[:10]
+    for b_ in bad:
+        print('BAD', b_)
+    assert not bad, [b_[0] for b_ in bad]
     # SGD with clip (net_tools.py:645-651), bit-exact given the gradient
     flat_g = tr.net.store.flat_grad.detach().clone()
     tr.opt.step()
