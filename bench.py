@@ -43,6 +43,8 @@ def parse():
     ap.add_argument('--probe', default='rod_bn_bwd', help='C-ABI entry reported in "roofline" (dominant)')
     ap.add_argument('--probe-table', dest='probe_table', default=None,
                     help='time EVERY librod call and write a per-entry table (JSON) here (analysis only)')
+    ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'),
+                    help='per-entry HBM bytes per launch from rocprofv3 PMC passes (tools/pmc_traffic.py)')
     ap.add_argument('--cpu-baseline', dest='cpu_baseline', action='store_true', default=True)
     ap.add_argument('--no-cpu-baseline', dest='cpu_baseline', action='store_false')
     ap.add_argument('--inference', dest='inference', action='store_true', default=True)
@@ -192,7 +194,15 @@ def main():
         else:
             rl = {'bound': 'mfma', 'achieved': round(achieved_tf, 2), 'peak': peak_tf, 'unit': 'TFLOP/s',
                   'frac': round(achieved_tf / peak_tf, 4)}
-        rl.update({'traffic': None, 'kernel': args.probe, 'launches_per_step': n_launch // max(args.steps, 1),
+        traffic, tsrc = None, None
+        if args.traffic and os.path.exists(args.traffic):
+            tj = json.load(open(args.traffic))
+            te = tj.get('entries', {}).get(args.probe)
+            if te is not None and tj.get('config') == [args.train_range, args.batch, args.height, args.width, args.dtype]:
+                traffic = round(te['bytes_per_launch'])
+                tsrc = os.path.relpath(args.traffic, ROOT)
+        rl.update({'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, PMC)', 'traffic_source': tsrc,
+                   'alg_bytes_per_launch': byts // max(n_launch, 1), 'kernel': args.probe, 'launches_per_step': n_launch // max(args.steps, 1),
                    'avg_launch_us': round(per_launch_ms * 1e3, 2), 'alg_bytes_per_step': byts // max(args.steps, 1),
                    'alg_flops_per_step': flops // max(args.steps, 1)})
         imgs = args.batch * world * args.steps

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 2
+#define ROD_ABI_VERSION 3
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -37,6 +37,20 @@ enum { ROD_F32 = 0, ROD_BF16 = 1 };
  *   RELU6 = tf.nn.relu6 (mobilenet_v2.py:47)
  *   LEAKY = tf.nn.leaky_relu, alpha 0.2 (catch_net.py:302) */
 enum { ROD_ACT_NONE = 0, ROD_ACT_RELU6 = 1, ROD_ACT_LEAKY = 2 };
+
+/* BatchNorm-apply prologue (ABI 3).  rod_conv_fwd, rod_conv_wgrad, rod_dw3x3_fwd and
+ * rod_dw3x3_bwd_filter take, right after their input x, the five arguments
+ *     const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+ *     const float* pro_beta, int pro_act
+ * With pro_mean == NULL x is used as is.  Otherwise x is the PRE-BatchNorm tensor y of the
+ * layer below and the kernel reads, wherever the reference reads that layer's BatchNorm +
+ * activation output (slim.batch_norm then relu6 / leaky_relu, mobilenet.py:417-420,
+ * catch_net.py:302), z = act(y*scale + offset) (one fma; scale = rstd*gamma, offset =
+ * beta - mean*scale, TF's fused batch-norm form) rounded to the storage
+ * dtype — bit for bit the tensor rod_bn_apply would have written — formed in registers as
+ * y is loaded (padding taps stay 0).  gamma / beta may be NULL (1 / 0), as in rod_bn_apply.
+ * The normalised activation therefore never crosses HBM in forward or in the weight
+ * gradients; channel count <= 2048 for the GEMM prologues. */
 
 int rod_abi_version(void);
 const char* rod_last_error(void);
@@ -51,21 +65,23 @@ int rod_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, v
  * slim.separable_conv2d(num_outputs=None, depth_multiplier=1), padding SAME
  * (conv_blocks.py:238-247): y[n,ho,wo,c] = sum_ij x[n,ho*s+i-pt,wo*s+j-pl,c]*w[i,j,c].
  * w is fp32 [3][3][C] (TF depthwise_weights [3,3,C,1]). */
-/* stat_parts (nullable): BatchNorm partial statistics of y ([3][C][nparts], see
+/* stat_parts (nullable): BatchNorm partial statistics of y ([nparts][3][C], see
  * rod_bn_finalize) with nparts = rod_dw3x3_fwd_stat_parts(), reduced in the epilogue from
  * the rounded outputs (the depthwise BatchNorm, conv_blocks.py:247 + mobilenet.py:417). */
 int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C);
-int rod_dw3x3_fwd(const void* x, const float* w, void* y, float* stat_parts, int N, int H, int W,
-                  int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
+int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                  const float* pro_beta, int pro_act, const float* w, void* y, float* stat_parts, int N, int H,
+                  int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
 /* dx = d y / d x  (DepthwiseConv2dNativeBackpropInput) */
 int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, int W, int C,
                        int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
 /* dw[3][3][C] (fp32, overwritten) (DepthwiseConv2dNativeBackpropFilter).
  * workspace: rod_dw3x3_bwd_filter_workspace() bytes. */
 size_t rod_dw3x3_bwd_filter_workspace(int N, int Ho, int Wo, int C);
-int rod_dw3x3_bwd_filter(const void* x, const void* dy, float* dw, void* workspace,
-                         int N, int H, int W, int C, int stride, int pad_t, int pad_l,
-                         int Ho, int Wo, int dtype, void* stream);
+int rod_dw3x3_bwd_filter(const void* x, const float* pro_mean, const float* pro_rstd,
+                         const float* pro_gamma, const float* pro_beta, int pro_act, const void* dy,
+                         float* dw, void* workspace, int N, int H, int W, int C, int stride, int pad_t,
+                         int pad_l, int Ho, int Wo, int dtype, void* stream);
 
 /* ------------------------------------------------ BatchNorm (A4)
  * slim.batch_norm, fused, NHWC (mobilenet.py:417-420; catch_net.py:302).
@@ -80,7 +96,7 @@ int rod_bn_stats(const void* x, long M, int C, int ldx, float eps, float decay,
                  float* mean, float* rstd, float* moving_mean, float* moving_var,
                  void* workspace, int dtype, void* stream);
 /* The same statistics (and moving-average update) from partial statistics written by a
- * producer's epilogue: parts [3][C][nparts] = (count, mean, M2) per part; parts with
+ * producer's epilogue: parts [nparts][3][C] = (count, mean, M2) per part; parts with
  * count 0 are ignored; M = total count.  Chan's merge in f64, fixed order (two levels when
  * nparts > 2048: workspace = rod_bn_finalize_workspace() bytes, else may be NULL). */
 size_t rod_bn_finalize_workspace(int nparts, int C);
@@ -90,7 +106,8 @@ int rod_bn_finalize(const float* parts, int nparts, long M, int C, float eps, fl
 /* inference: mean = moving_mean, rstd = 1/sqrt(moving_var + eps). */
 int rod_bn_eval_stats(const float* moving_mean, const float* moving_var, float eps,
                       float* mean, float* rstd, int C, void* stream);
-/* y = act((x - mean)*rstd*gamma + beta) + residual   (gamma NULL => 1,
+/* y = act(x*scale + offset) + residual, scale = rstd*gamma, offset = beta - mean*scale
+ * (one fma, TF's fused batch-norm form; gamma NULL => 1,
  * beta NULL => 0, residual NULL => none; residual added after act, as
  * expanded_conv's `net += input_tensor`, conv_blocks.py:311). */
 int rod_bn_apply(const void* x, const float* mean, const float* rstd, const float* gamma,
@@ -118,13 +135,14 @@ int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rs
  * K is then split over workgroups into fp32 partial slabs summed in fixed order.  NULL
  * is accepted and disables the split.
  * stat_parts (nullable): BatchNorm partial statistics of y for rod_bn_finalize, as
- * [3][Cout][ceil(M/128)] (count, mean, M2) per 128-row tile, computed in the epilogue from
+ * [ceil(M/128)][3][Cout] (count, mean, M2) per 128-row tile, computed in the epilogue from
  * the rounded outputs (the BatchNorm that follows every conv, mobilenet.py:417,
  * catch_net.py:302) so no separate statistics pass re-reads y. */
 size_t rod_conv_fwd_workspace(int N, int H, int W, int Cin, int Cout, int ksize);
-int rod_conv_fwd(const void* x, const void* wt, const float* bias, void* y, void* workspace,
-                 float* stat_parts, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
-                 int ldy, int dtype, void* stream);
+int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                 const float* pro_beta, int pro_act, const void* wt, const float* bias, void* y,
+                 void* workspace, float* stat_parts, int N, int H, int W, int Cin, int Cout, int ksize,
+                 int ldx, int ldy, int dtype, void* stream);
 /* Weight layouts derived from the fp32 master weight w[Cout][ksize][ksize][Cin]:
  *   mode 0: forward operand      wt[co][i][j][ci]           (cast to dtype)
  *   mode 1: backward-data operand wt[ci][2-i][2-j][co]       (transposed, flipped)
@@ -134,9 +152,10 @@ int rod_conv_weight_prep(const float* w, void* wt, int Cout, int Cin, int ksize,
 /* dw[co][k] = sum_m dy[m, co] * A[m, k]  (Conv2DBackpropFilter), fp32 out,
  * db[co] = sum_m dy[m, co] when db != NULL.  workspace: see query. */
 size_t rod_conv_wgrad_workspace(int N, int H, int W, int Cin, int Cout, int ksize);
-int rod_conv_wgrad(const void* x, const void* dy, float* dw, float* db, void* workspace,
-                   int N, int H, int W, int Cin, int Cout, int ksize, int ldx, int lddy,
-                   int dtype, void* stream);
+int rod_conv_wgrad(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                   const float* pro_beta, int pro_act, const void* dy, float* dw, float* db,
+                   void* workspace, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
+                   int lddy, int dtype, void* stream);
 
 /* ------------------------------------------------ targets and losses
  * Anchor matching, JACCARD_BIGGER (utils/net_tools.py:270-428, branch 382-421).

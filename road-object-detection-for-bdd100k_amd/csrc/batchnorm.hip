@@ -16,17 +16,6 @@
 
 namespace rod {
 
-__device__ __forceinline__ float act_fwd(float z, int act) {
-  if (act == ROD_ACT_RELU6) return fminf(fmaxf(z, 0.f), 6.f);   // tf.nn.relu6
-  if (act == ROD_ACT_LEAKY) return z > 0.f ? z : z * 0.2f;       // tf.nn.leaky_relu(alpha=0.2)
-  return z;
-}
-__device__ __forceinline__ float act_grad(float z, int act) {
-  if (act == ROD_ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;  // Relu6Grad
-  if (act == ROD_ACT_LEAKY) return z > 0.f ? 1.f : 0.2f;               // LeakyReluGrad
-  return 1.f;
-}
-
 // Row-chunk reduction plan shared by the statistics and backward-reduce kernels.
 // CV channel vectors are split into cgroups of CVb <= 256 (blockIdx.y); the 256 threads of a
 // block are `lanes` row lanes x CVb channel vectors (no power-of-two padding, so at most
@@ -291,21 +280,16 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
   const long stride = (long)gridDim.x * blockDim.x;  // multiple of CV
   const int c = (int)(t0 % CV) * V;
   const long rstep = stride / CV;
-  float mu[V], sc[V], be[V];
+  float sc[V], sh[V];
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    mu[v] = mean[c + v];
-    sc[v] = gamma ? rstd[c + v] * gamma[c + v] : rstd[c + v];  // rsqrt(var+eps)*scale
-    be[v] = beta ? beta[c + v] : 0.f;
-  }
+  for (int v = 0; v < V; ++v) bn_affine(mean, rstd, gamma, beta, c + v, sc[v], sh[v]);
   for (long r = t0 / CV; r < M; r += rstep) {
     float xv[V], rv[V];
     load_v<T, VEC>(x + r * ldx + c, xv);
     if constexpr (RES) load_v<T, VEC>(res + r * ldr + c, rv);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      float z = (xv[v] - mu[v]) * sc[v] + be[v];
-      z = act_fwd(z, act);
+      float z = act_fwd(fmaf(xv[v], sc[v], sh[v]), act);
       if constexpr (RES) z = z + rv[v];
       xv[v] = z;
     }
@@ -332,7 +316,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
   const int c = cv * V;
   const long r0 = (long)blockIdx.x * chunk;
   const long r1 = r0 + chunk < M ? r0 + chunk : M;
-  float sg[V], sgx[V], mu[V], rs[V], sc[V], be[V];
+  float sg[V], sgx[V], mu[V], rs[V], sc[V], sh[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) sg[v] = sgx[v] = 0.f;
   if (active) {
@@ -340,14 +324,13 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
     for (int v = 0; v < V; ++v) {
       mu[v] = mean[c + v];
       rs[v] = rstd[c + v];
-      sc[v] = gamma ? rs[v] * gamma[c + v] : rs[v];
-      be[v] = beta ? beta[c + v] : 0.f;
+      bn_affine(mean, rstd, gamma, beta, c + v, sc[v], sh[v]);
     }
     auto acc = [&](const float (&xv)[V], const float (&gv)[V]) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float d = xv[v] - mu[v];
-        const float z = d * sc[v] + be[v];
+        const float z = fmaf(xv[v], sc[v], sh[v]);
         const float g = gv[v] * act_grad(z, act);
         sg[v] += g;
         sgx[v] = fmaf(g, d * rs[v], sgx[v]);
@@ -431,13 +414,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   const long stride = (long)gridDim.x * blockDim.x;
   const int c = (int)(t0 % CV) * V;
   const long rstep = stride / CV;
-  float mu[V], rs[V], sc[V], be[V], a[V], mg[V], mgx[V];
+  float mu[V], rs[V], sc[V], sh[V], a[V], mg[V], mgx[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     mu[v] = mean[c + v];
     rs[v] = rstd[c + v];
-    sc[v] = gamma ? rs[v] * gamma[c + v] : rs[v];
-    be[v] = beta ? beta[c + v] : 0.f;
+    bn_affine(mean, rstd, gamma, beta, c + v, sc[v], sh[v]);
     a[v] = coef[c + v];
     mg[v] = coef[C + c + v];
     mgx[v] = coef[2 * C + c + v];
@@ -449,7 +431,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float d = xv[v] - mu[v];
-      const float z = d * sc[v] + be[v];
+      const float z = fmaf(xv[v], sc[v], sh[v]);
       const float g = gv[v] * act_grad(z, act);
       xv[v] = a[v] * (g - mg[v] - (d * rs[v]) * mgx[v]);
     }

@@ -30,6 +30,17 @@ template <> struct PackV<bf16_t, 4> {
   __device__ __forceinline__ void set(int i, float a) { v[i] = (bf16_t)a; }
   __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x4*)p = v; }
 };
+template <> struct PackV<bf16_t, 8> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x8*)p; }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (bf16_t)0.f;
+  }
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+  __device__ __forceinline__ void set(int i, float a) { v[i] = (bf16_t)a; }
+  __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x8*)p = v; }
+};
 template <typename T> struct PackV<T, 1> {
   T v;
   __device__ __forceinline__ void load(const T* p) { v = *p; }
@@ -42,12 +53,43 @@ template <typename T> struct PackV<T, 1> {
 constexpr int DW_RB = 8;  // output rows per thread (forward / backward-data strips)
 
 // Forward: thread = (channel vector cv, output column wo), strip of DW_RB output rows; the
-// 3x3 input window rolls down in registers (one new input row per output row for S=1, two
-// for S=2) and lanes of a wave read consecutive channel vectors of neighbouring pixels.
-template <typename T, int S, int V, bool STATS>
+// 3x3 input window rolls down in fp32 registers (one new input row per output row for S=1,
+// two for S=2) and lanes of a wave read consecutive channel vectors of neighbouring pixels.
+// The row(s) the NEXT output row adds are prefetched raw before this row's FMAs and only
+// converted when they enter the window, so one row of arithmetic covers the load latency.
+// PACT: BatchNorm-apply prologue on the input (rod_common.h): -1 none, ROD_ACT_RELU6 the
+// fixed ReLU6 form, 3 any activation (runtime); padding stays 0.
+template <typename T, int V, int PACT>
+struct DwIn {
+  float sc[PACT >= 0 ? V : 1], sh[PACT >= 0 ? V : 1];
+  int act;
+  __device__ __forceinline__ void init(const BnPro& p, int c) {
+    if constexpr (PACT >= 0) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) bn_pro_affine(p, c + v, sc[v], sh[v]);
+      act = p.act;
+    }
+  }
+  // raw pack -> fp32 window entry (the activation the reference convolves, rounded to T)
+  __device__ __forceinline__ void cvt(const PackV<T, V>& p, bool ok, float (&o)[V]) const {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float a = p.get(v);
+      if constexpr (PACT >= 0) {
+        float z = fmaf(a, sc[v], sh[v]);
+        z = PACT == ROD_ACT_RELU6 ? act_t<ROD_ACT_RELU6>(z) : act_fwd(z, act);
+        a = ok ? to_f32(from_f32<T>(z)) : 0.f;
+      }
+      o[v] = a;
+    }
+  }
+};
+
+template <typename T, int S, int V, bool STATS, int PACT = -1>
 __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                         T* __restrict__ y, int H, int W, int C, int pt, int pl,
-                                                        int Ho, int Wo, float* __restrict__ parts) {
+                                                        int Ho, int Wo, float* __restrict__ parts,
+                                                        BnPro pro = BnPro{}) {
   const int CV = C / V;
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cv = (int)(t % CV);
@@ -57,35 +99,45 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x,
   const int ho1 = ho0 + DW_RB < Ho ? ho0 + DW_RB : Ho;
   const int n = blockIdx.z;
   const int c = cv * V;
-  // STATS: this thread's rounded outputs, for its (n, mean, M2) per channel
-  float keep[STATS ? DW_RB : 1][V];
+  // STATS: shifted sums of this thread's rounded outputs (pivot = its first output), for
+  // its (n, mean, M2) per channel
+  float piv[V], s1[V], s2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) piv[v] = s1[v] = s2[v] = 0.f;
   if (active) {
     float wr[9][V];
 #pragma unroll
     for (int k = 0; k < 9; ++k)
 #pragma unroll
       for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+    DwIn<T, V, PACT> in;
+    in.init(pro, c);
     const T* xn = x + (long)n * H * W * C + c;
     T* yn = y + (long)n * Ho * Wo * C + c;
-    PackV<T, V> xr[3][3];
-    auto load_row = [&](PackV<T, V>(&row)[3], int hi) {
+    float xr[3][3][V];
+    PackV<T, V> nx[S][3];
+    bool nok[S][3];
+    auto load_row = [&](PackV<T, V>(&row)[3], bool (&ok)[3], int hi) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int wi = wo * S - pl + j;
-        if (hi >= 0 && hi < H && wi >= 0 && wi < W) row[j].load(xn + ((long)hi * W + wi) * C);
+        ok[j] = hi >= 0 && hi < H && wi >= 0 && wi < W;
+        if (ok[j]) row[j].load(xn + ((long)hi * W + wi) * C);
         else row[j].zero();
       }
     };
-    // window rows ho*S-pt+{0,1,2}; the row(s) the NEXT output row adds are prefetched into
-    // nx before this row's FMAs, so one row of arithmetic covers the load latency
-    PackV<T, V> nx[S][3];
     auto prefetch = [&](int ho) {
 #pragma unroll
-      for (int q = 0; q < S; ++q) load_row(nx[q], ho * S - pt + 3 - S + q);
+      for (int q = 0; q < S; ++q) load_row(nx[q], nok[q], ho * S - pt + 3 - S + q);
     };
-    load_row(xr[0], ho0 * S - pt);
-    load_row(xr[1], ho0 * S - pt + 1);
-    load_row(xr[2], ho0 * S - pt + 2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      PackV<T, V> r0[3];
+      bool k0[3];
+      load_row(r0, k0, ho0 * S - pt + i);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) in.cvt(r0[j], k0[j], xr[i][j]);
+    }
     if (ho0 + 1 < ho1) prefetch(ho0 + 1);
 #pragma unroll
     for (int q = 0; q < DW_RB; ++q) {
@@ -99,26 +151,36 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x,
 #pragma unroll
         for (int j = 0; j < 3; ++j)
 #pragma unroll
-          for (int v = 0; v < V; ++v) acc[v] = fmaf(xr[i][j].get(v), wr[i * 3 + j][v], acc[v]);
+          for (int v = 0; v < V; ++v) acc[v] = fmaf(xr[i][j][v], wr[i * 3 + j][v], acc[v]);
       PackV<T, V> o;
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
       o.store(yn + ((long)ho * Wo + wo) * C);
       if constexpr (STATS) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) keep[q][v] = o.get(v);
+        for (int v = 0; v < V; ++v) {
+          const float ov = o.get(v);
+          if (q == 0) piv[v] = ov;
+          const float d = ov - piv[v];
+          s1[v] += d;
+          s2[v] = fmaf(d, d, s2[v]);
+        }
       }
       if (ho + 1 < ho1) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           if constexpr (S == 1) {
-            xr[0][j] = xr[1][j];
-            xr[1][j] = xr[2][j];
-            xr[2][j] = nx[0][j];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+              xr[0][j][v] = xr[1][j][v];
+              xr[1][j][v] = xr[2][j][v];
+            }
+            in.cvt(nx[0][j], nok[0][j], xr[2][j]);
           } else {
-            xr[0][j] = xr[2][j];
-            xr[1][j] = nx[0][j];
-            xr[2][j] = nx[1][j];
+#pragma unroll
+            for (int v = 0; v < V; ++v) xr[0][j][v] = xr[2][j][v];
+            in.cvt(nx[0][j], nok[0][j], xr[1][j]);
+            in.cvt(nx[1][j], nok[1][j], xr[2][j]);
           }
         }
         if (ho + 2 < ho1) prefetch(ho + 2);
@@ -126,34 +188,23 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x,
     }
   }
   if constexpr (STATS) {
-    // per thread: exact two-pass (mean, M2) of its <= DW_RB rows; per block: Chan merge of
-    // the threads holding each channel vector, in thread order, into part
-    // (z*gy + y)*gx + x of the [3][C][nparts] slab
+    // per thread: (mean, M2) of its <= DW_RB rows from the pivot-shifted sums; per block:
+    // Chan merge of the threads holding each channel vector, in thread order, into part
+    // (z*gy + y)*gx + x of the [nparts][3][C] slab
     __shared__ float sn[256], sm[256 * V], sq[256 * V];
     const int tid = threadIdx.x;
     const int nr = active ? ho1 - ho0 : 0;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      float sum = 0.f;
-#pragma unroll
-      for (int q = 0; q < DW_RB; ++q)
-        if (q < nr) sum += keep[q][v];
-      const float mu = nr > 0 ? sum / (float)nr : 0.f;
-      float m2 = 0.f;
-#pragma unroll
-      for (int q = 0; q < DW_RB; ++q)
-        if (q < nr) {
-          const float d = keep[q][v] - mu;
-          m2 = fmaf(d, d, m2);
-        }
-      sm[tid * V + v] = mu;
-      sq[tid * V + v] = m2;
+      const float inv = nr > 0 ? 1.f / (float)nr : 0.f;
+      const float dm = s1[v] * inv;
+      sm[tid * V + v] = piv[v] + dm;
+      sq[tid * V + v] = nr > 0 ? fmaxf(s2[v] - s1[v] * dm, 0.f) : 0.f;
     }
     sn[tid] = (float)nr;
     __syncthreads();
     const long tb = (long)blockIdx.x * 256;
     const int t0mod = (int)(tb % CV);
-    const long nparts = (long)gridDim.x * gridDim.y * gridDim.z;
     const long part = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     for (int e = tid; e < C; e += 256) {
       const int cve = e / V, v = e - cve * V;
@@ -339,11 +390,11 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_s2_kernel(const T* __restr
 // row for S=1, two for S=2), so each output pixel costs one dy load and three x loads and no
 // index division.  blockIdx.y strides over the N*spi row strips; each block then sums its
 // threads per channel in LDS (fixed order) and writes one [9][C] partial to the slab.
-template <typename T, int S, int V>
+template <typename T, int S, int V, int PACT = -1>
 __global__ void __launch_bounds__(256) dw3x3_bwd_filter_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                                float* __restrict__ slab, int N, int H, int W,
                                                                int C, int pt, int pl, int Ho, int Wo, int RB,
-                                                               int spi) {
+                                                               int spi, BnPro pro = BnPro{}) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [256][V]
   const int CV = C / V;
   const int tid = threadIdx.x;
@@ -358,6 +409,8 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_filter_kernel(const T* __restri
     for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
 
   if (wo < Wo) {
+    DwIn<T, V, PACT> in;  // the forward's input (BatchNorm prologue when PACT >= 0)
+    in.init(pro, c);
     const int nstrips = N * spi;
     for (int s = blockIdx.y; s < nstrips; s += gridDim.y) {
       const int n = s / spi;
@@ -365,44 +418,58 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_filter_kernel(const T* __restri
       const int ho1 = ho0 + RB < Ho ? ho0 + RB : Ho;
       const T* xn = x + (long)n * H * W * C + c;
       const T* dn = dy + (long)n * Ho * Wo * C + c;
-      PackV<T, V> xr[3][3];
-      auto load_row = [&](PackV<T, V>(&row)[3], int hi) {
+      float xr[3][3][V];
+      auto load_row = [&](PackV<T, V>(&row)[3], bool (&ok)[3], int hi) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const int wi = wo * S - pl + j;
-          if (hi >= 0 && hi < H && wi >= 0 && wi < W) row[j].load(xn + ((long)hi * W + wi) * C);
+          ok[j] = hi >= 0 && hi < H && wi >= 0 && wi < W;
+          if (ok[j]) row[j].load(xn + ((long)hi * W + wi) * C);
           else row[j].zero();
         }
       };
       PackV<T, V> nx[S][3], g, ng;
+      bool nok[S][3];
       auto prefetch = [&](int ho) {
 #pragma unroll
-        for (int q = 0; q < S; ++q) load_row(nx[q], ho * S - pt + 3 - S + q);
+        for (int q = 0; q < S; ++q) load_row(nx[q], nok[q], ho * S - pt + 3 - S + q);
         ng.load(dn + ((long)ho * Wo + wo) * C);
       };
-      load_row(xr[0], ho0 * S - pt);
-      load_row(xr[1], ho0 * S - pt + 1);
-      load_row(xr[2], ho0 * S - pt + 2);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        PackV<T, V> r0[3];
+        bool k0[3];
+        load_row(r0, k0, ho0 * S - pt + i);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) in.cvt(r0[j], k0[j], xr[i][j]);
+      }
       g.load(dn + ((long)ho0 * Wo + wo) * C);
       if (ho0 + 1 < ho1) prefetch(ho0 + 1);
       for (int ho = ho0; ho < ho1; ++ho) {
+        float gv[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) gv[v] = g.get(v);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < 3; ++j)
 #pragma unroll
-            for (int v = 0; v < V; ++v) acc[i * 3 + j][v] = fmaf(g.get(v), xr[i][j].get(v), acc[i * 3 + j][v]);
+            for (int v = 0; v < V; ++v) acc[i * 3 + j][v] = fmaf(gv[v], xr[i][j][v], acc[i * 3 + j][v]);
         if (ho + 1 < ho1) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             if constexpr (S == 1) {
-              xr[0][j] = xr[1][j];
-              xr[1][j] = xr[2][j];
-              xr[2][j] = nx[0][j];
+#pragma unroll
+              for (int v = 0; v < V; ++v) {
+                xr[0][j][v] = xr[1][j][v];
+                xr[1][j][v] = xr[2][j][v];
+              }
+              in.cvt(nx[0][j], nok[0][j], xr[2][j]);
             } else {
-              xr[0][j] = xr[2][j];
-              xr[1][j] = nx[0][j];
-              xr[2][j] = nx[1][j];
+#pragma unroll
+              for (int v = 0; v < V; ++v) xr[0][j][v] = xr[2][j][v];
+              in.cvt(nx[0][j], nok[0][j], xr[1][j]);
+              in.cvt(nx[1][j], nok[1][j], xr[2][j]);
             }
           }
           g = ng;
@@ -453,11 +520,6 @@ static DwFilterPlan dw_filter_plan(int N, int Ho, int Wo, int C, int V, int es) 
   return p;
 }
 
-template <typename T>
-static bool dw_pack4_ok(const void* a, const void* b, int C) {
-  const uintptr_t al = 4 * sizeof(T) - 1;
-  return (C % 4 == 0) && (((uintptr_t)a & al) == 0) && (((uintptr_t)b & al) == 0);
-}
 
 }  // namespace rod
 
@@ -475,22 +537,39 @@ static dim3 dw_fwd_grid(int N, int Ho, int Wo, int C, int V) {
   return dim3(cdiv((long)(C / V) * Wo, 256), cdiv(Ho, DW_RB), N);
 }
 
-template <typename T, int S, bool VK>
-static void dw_fwd_launch(const void* x, const float* w, void* y, float* parts, int N, int H, int W, int C, int pt,
-                          int pl, int Ho, int Wo, hipStream_t s) {
-  constexpr int V = VK ? 4 : 1;
-  const dim3 grid = dw_fwd_grid(N, Ho, Wo, C, V);
-  if (parts)
-    hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V, true>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt,
-                       pl, Ho, Wo, parts);
-  else
-    hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V, false>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt,
-                       pl, Ho, Wo, nullptr);
+// channel pack per thread: 16-byte (bf16 x8 / f32 x4) when C and the pointers allow it,
+// bf16 x4 (8-byte) when only C % 4 == 0, else scalar
+// `cap`: the forward and the filter gradient keep an fp32 3x3 window per channel, so they
+// use 4-channel packs; the data gradient 16-byte packs (ROD_DW_PACK overrides, A/B only)
+template <typename T>
+static int dw_pack(const void* a, const void* b, int C, int cap) {
+  auto al = [&](uintptr_t n) { return (((uintptr_t)a | (uintptr_t)b) & (n - 1)) == 0; };
+  static const int force = getenv("ROD_DW_PACK") ? atoi(getenv("ROD_DW_PACK")) : 0;
+  if (force) cap = force;
+  if (sizeof(T) == 2 && C % 8 == 0 && al(16) && cap >= 8) return 8;
+  if (C % 4 == 0 && al(4 * sizeof(T))) return 4;
+  return 1;
 }
-template <typename T, int S, bool VK>
+
+template <typename T, int S, int V>
+static void dw_fwd_launch(const void* x, const BnPro* pro, const float* w, void* y, float* parts, int N, int H, int W,
+                          int C, int pt, int pl, int Ho, int Wo, hipStream_t s) {
+  const dim3 grid = dw_fwd_grid(N, Ho, Wo, C, V);
+  const BnPro pv = pro ? *pro : BnPro{};
+#define DWF(ST, PA)                                                                                              \
+  hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V, ST, PA>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt, \
+                     pl, Ho, Wo, parts, pv)
+  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
+  if (parts) {
+    if (pa == ROD_ACT_RELU6) DWF(true, ROD_ACT_RELU6); else if (pa == 3) DWF(true, 3); else DWF(true, -1);
+  } else {
+    if (pa == ROD_ACT_RELU6) DWF(false, ROD_ACT_RELU6); else if (pa == 3) DWF(false, 3); else DWF(false, -1);
+  }
+#undef DWF
+}
+template <typename T, int S, int V>
 static void dw_bwd_data_launch(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int pt, int pl,
                                int Ho, int Wo, hipStream_t s) {
-  constexpr int V = VK ? 4 : 1;
   static const bool no_s2 = getenv("ROD_DEBUG_NOS2") != nullptr;  // debug bisection
   if (S == 2 && pt <= 1 && pl <= 1 && !no_s2) {
     const int Bc = (W - 1 + pl) / 2 + 1;
@@ -504,13 +583,17 @@ static void dw_bwd_data_launch(const void* dy, const float* w, void* dx, int N, 
   hipLaunchKernelGGL((dw3x3_bwd_data_kernel<T, S, V>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W, C, pt,
                      pl, Ho, Wo);
 }
-template <typename T, int S, bool VK>
-static void dw_bwd_filter_launch(const void* x, const void* dy, float* dw, float* slab, int N, int H, int W, int C,
-                                 int pt, int pl, int Ho, int Wo, hipStream_t s) {
-  constexpr int V = VK ? 4 : 1;
+template <typename T, int S, int V>
+static void dw_bwd_filter_launch(const void* x, const BnPro* pro, const void* dy, float* dw, float* slab, int N, int H,
+                                 int W, int C, int pt, int pl, int Ho, int Wo, hipStream_t s) {
   DwFilterPlan p = dw_filter_plan(N, Ho, Wo, C, V, (int)sizeof(T));
-  hipLaunchKernelGGL((dw3x3_bwd_filter_kernel<T, S, V>), dim3(p.gx, p.gy), dim3(256), 256 * V * sizeof(float), s,
-                     (const T*)x, (const T*)dy, slab, N, H, W, C, pt, pl, Ho, Wo, p.RB, p.spi);
+  const BnPro pv = pro ? *pro : BnPro{};
+#define DWW(PA)                                                                                                   \
+  hipLaunchKernelGGL((dw3x3_bwd_filter_kernel<T, S, V, PA>), dim3(p.gx, p.gy), dim3(256), 256 * V * sizeof(float), \
+                     s, (const T*)x, (const T*)dy, slab, N, H, W, C, pt, pl, Ho, Wo, p.RB, p.spi, pv)
+  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
+  if (pa == ROD_ACT_RELU6) DWW(ROD_ACT_RELU6); else if (pa == 3) DWW(3); else DWW(-1);
+#undef DWW
   slab_sum(slab, dw, (int)p.parts(), 9L * C, s);
 }
 
@@ -518,40 +601,55 @@ static void dw_bwd_filter_launch(const void* x, const void* dy, float* dw, float
 
 using namespace rod;
 
-#define DW_SELECT(FN, T_, ...)                                         \
-  do {                                                                 \
-    if (stride == 1) {                                                 \
-      if (vec) FN<T_, 1, true>(__VA_ARGS__); else FN<T_, 1, false>(__VA_ARGS__); \
-    } else {                                                           \
-      if (vec) FN<T_, 2, true>(__VA_ARGS__); else FN<T_, 2, false>(__VA_ARGS__); \
-    }                                                                  \
+// dispatch on stride and channel pack; defines the launch for T_ (pack from the pointers)
+#define DW_SELECT(FN, T_, PK, ...)                                            \
+  do {                                                                        \
+    if (stride == 1) {                                                        \
+      if ((PK) == 8) FN<T_, 1, (sizeof(T_) == 2 ? 8 : 4)>(__VA_ARGS__);      \
+      else if ((PK) == 4) FN<T_, 1, 4>(__VA_ARGS__);                          \
+      else FN<T_, 1, 1>(__VA_ARGS__);                                         \
+    } else {                                                                  \
+      if ((PK) == 8) FN<T_, 2, (sizeof(T_) == 2 ? 8 : 4)>(__VA_ARGS__);      \
+      else if ((PK) == 4) FN<T_, 2, 4>(__VA_ARGS__);                          \
+      else FN<T_, 2, 1>(__VA_ARGS__);                                         \
+    }                                                                         \
   } while (0)
 
 extern "C" {
 
 int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C) {
-  const dim3 g = dw_fwd_grid(N, Ho, Wo, C, C % 4 == 0 ? 4 : 1);
-  return (int)(g.x * g.y * g.z);
+  // the pack the bf16 / f32 launch will use for aligned pointers (the caller allocates the
+  // slab for this; a smaller pack falls back to the separate statistics pass)
+  const int V = C % 8 == 0 ? 8 : (C % 4 == 0 ? 4 : 1);
+  const dim3 g = dw_fwd_grid(N, Ho, Wo, C, V);
+  const dim3 g4 = dw_fwd_grid(N, Ho, Wo, C, C % 4 == 0 ? 4 : 1);
+  return (int)std::max(g.x * g.y * g.z, g4.x * g4.y * g4.z);
 }
 
-int rod_dw3x3_fwd(const void* x, const float* w, void* y, float* stat_parts, int N, int H, int W, int C, int stride,
-                  int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream) {
+int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                  const float* pro_beta, int pro_act, const float* w, void* y, float* stat_parts, int N, int H, int W,
+                  int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream) {
   DW_ARGS_OK("rod_dw3x3_fwd");
+  ROD_CHECK_ARG(!pro_mean || pro_rstd, "rod_dw3x3_fwd: BatchNorm prologue needs mean and rstd");
   hipStream_t s = ROD_STREAM(stream);
-  if (dtype == ROD_F32) {
-    const bool vec = dw_pack4_ok<float>(x, y, C);
-    // parts are laid out for the pack-4 grid; a misaligned pack-4 shape gets the separate pass
-    float* fused = (vec || C % 4 != 0) ? stat_parts : nullptr;
-    DW_SELECT(dw_fwd_launch, float, x, w, y, fused, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
-    if (stat_parts && !fused)
-      ::rod::stat_parts(ROD_F32, y, (long)N * Ho * Wo, C, C, stat_parts, rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C), s);
-  } else if (dtype == ROD_BF16) {
-    const bool vec = dw_pack4_ok<bf16_t>(x, y, C);
-    float* fused = (vec || C % 4 != 0) ? stat_parts : nullptr;
-    DW_SELECT(dw_fwd_launch, bf16_t, x, w, y, fused, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
-    if (stat_parts && !fused)
-      ::rod::stat_parts(ROD_BF16, y, (long)N * Ho * Wo, C, C, stat_parts, rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C), s);
-  } else {
+  const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  const BnPro* pp = pro_mean ? &pro : nullptr;
+  const int nparts = rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C);
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    const int pk = dw_pack<T>(x, y, C, 4);
+    const int V = pk == 8 ? (sizeof(T) == 2 ? 8 : 4) : pk;
+    const dim3 g = dw_fwd_grid(N, Ho, Wo, C, V);
+    // the fused statistics write g.x*g.y*g.z parts; pad the rest of the slab with empty parts
+    float* fused = stat_parts;
+    DW_SELECT(dw_fwd_launch, T, pk, x, pp, w, y, fused, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    const long used = (long)g.x * g.y * g.z;
+    if (stat_parts && used < nparts)
+      (void)hipMemsetAsync(stat_parts + used * 3 * C, 0, (size_t)(nparts - used) * 3 * C * sizeof(float), s);
+  };
+  if (dtype == ROD_F32) run(float{});
+  else if (dtype == ROD_BF16) run(bf16_t{});
+  else {
     set_error("rod_dw3x3_fwd: bad dtype %d", dtype);
     return ROD_EINVAL;
   }
@@ -563,11 +661,11 @@ int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, i
   DW_ARGS_OK("rod_dw3x3_bwd_data");
   hipStream_t s = ROD_STREAM(stream);
   if (dtype == ROD_F32) {
-    const bool vec = dw_pack4_ok<float>(dy, dx, C);
-    DW_SELECT(dw_bwd_data_launch, float, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    const int pk = dw_pack<float>(dy, dx, C, 8);
+    DW_SELECT(dw_bwd_data_launch, float, pk, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else if (dtype == ROD_BF16) {
-    const bool vec = dw_pack4_ok<bf16_t>(dy, dx, C);
-    DW_SELECT(dw_bwd_data_launch, bf16_t, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    const int pk = dw_pack<bf16_t>(dy, dx, C, 8);
+    DW_SELECT(dw_bwd_data_launch, bf16_t, pk, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else {
     set_error("rod_dw3x3_bwd_data: bad dtype %d", dtype);
     return ROD_EINVAL;
@@ -577,23 +675,29 @@ int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, i
 
 size_t rod_dw3x3_bwd_filter_workspace(int N, int Ho, int Wo, int C) {
   long parts = 0;
-  for (int V : {1, 4})
+  for (int V : {1, 4, 8}) {
+    if (C % V) continue;
     for (int es : {2, 4}) parts = std::max(parts, dw_filter_plan(N, Ho, Wo, C, V, es).parts());
+  }
   return (size_t)parts * 9 * C * sizeof(float);
 }
 
-int rod_dw3x3_bwd_filter(const void* x, const void* dy, float* dw, void* workspace, int N, int H, int W, int C,
-                         int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream) {
+int rod_dw3x3_bwd_filter(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                         const float* pro_beta, int pro_act, const void* dy, float* dw, void* workspace, int N, int H,
+                         int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream) {
   DW_ARGS_OK("rod_dw3x3_bwd_filter");
   ROD_CHECK_ARG(workspace != nullptr, "rod_dw3x3_bwd_filter: workspace is NULL");
+  ROD_CHECK_ARG(!pro_mean || pro_rstd, "rod_dw3x3_bwd_filter: BatchNorm prologue needs mean and rstd");
   hipStream_t s = ROD_STREAM(stream);
   float* slab = (float*)workspace;
+  const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  const BnPro* pp = pro_mean ? &pro : nullptr;
   if (dtype == ROD_F32) {
-    const bool vec = dw_pack4_ok<float>(x, dy, C);
-    DW_SELECT(dw_bwd_filter_launch, float, x, dy, dw, slab, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    const int pk = dw_pack<float>(x, dy, C, 4);
+    DW_SELECT(dw_bwd_filter_launch, float, pk, x, pp, dy, dw, slab, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else if (dtype == ROD_BF16) {
-    const bool vec = dw_pack4_ok<bf16_t>(x, dy, C);
-    DW_SELECT(dw_bwd_filter_launch, bf16_t, x, dy, dw, slab, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    const int pk = dw_pack<bf16_t>(x, dy, C, 4);
+    DW_SELECT(dw_bwd_filter_launch, bf16_t, pk, x, pp, dy, dw, slab, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else {
     set_error("rod_dw3x3_bwd_filter: bad dtype %d", dtype);
     return ROD_EINVAL;

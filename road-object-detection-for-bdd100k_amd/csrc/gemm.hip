@@ -24,25 +24,52 @@ template <> struct LdsPad<float> { static constexpr int v = 4; };    // 144-byte
 
 // ---- 8-element chunk of T held in registers ------------------------------------
 template <typename T> struct Chunk8;
+// `ok`: the chunk holds raw loaded data that still needs the BatchNorm prologue (set by
+// load_vec, cleared by zero()); the prologue runs when the chunk is stored to LDS, so the
+// register prefetch of the next k step is not waited on at issue time.
 template <> struct Chunk8<bf16_t> {
   bf16x8 v;
+  bool ok;
   __device__ __forceinline__ void zero() {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (bf16_t)0.f;
+    ok = false;
   }
-  __device__ __forceinline__ void load_vec(const bf16_t* p) { v = *(const bf16x8*)p; }
+  __device__ __forceinline__ void load_vec(const bf16_t* p) {
+    v = *(const bf16x8*)p;
+    ok = true;
+  }
   __device__ __forceinline__ void set(int j, bf16_t x) { v[j] = x; }
   __device__ __forceinline__ void store_lds(bf16_t* p) const { *(bf16x8*)p = v; }
+  // BatchNorm-apply prologue on channels c..c+7 (c % 8 == 0; LDS table of (scale, offset))
+  template <int ACT>
+  __device__ __forceinline__ void pro_t(const float* pt, int c) {
+    const f32x4* q = (const f32x4*)(pt + 2 * c);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const f32x4 t = q[h];
+      v[2 * h] = (bf16_t)act_t<ACT>(fmaf((float)v[2 * h], t[0], t[1]));
+      v[2 * h + 1] = (bf16_t)act_t<ACT>(fmaf((float)v[2 * h + 1], t[2], t[3]));
+    }
+  }
+  __device__ __forceinline__ void pro(const float* pt, int c, int act) {
+    if (act == ROD_ACT_RELU6) pro_t<ROD_ACT_RELU6>(pt, c);
+    else if (act == ROD_ACT_LEAKY) pro_t<ROD_ACT_LEAKY>(pt, c);
+    else pro_t<ROD_ACT_NONE>(pt, c);
+  }
 };
 template <> struct Chunk8<float> {
   f32x4 a, b;
+  bool ok;
   __device__ __forceinline__ void zero() {
 #pragma unroll
     for (int j = 0; j < 4; ++j) a[j] = b[j] = 0.f;
+    ok = false;
   }
   __device__ __forceinline__ void load_vec(const float* p) {
     a = *(const f32x4*)p;
     b = *(const f32x4*)(p + 4);
+    ok = true;
   }
   __device__ __forceinline__ void set(int j, float x) {
     if (j < 4) a[j] = x; else b[j - 4] = x;
@@ -50,6 +77,23 @@ template <> struct Chunk8<float> {
   __device__ __forceinline__ void store_lds(float* p) const {
     *(f32x4*)p = a;
     *(f32x4*)(p + 4) = b;
+  }
+  template <int ACT>
+  __device__ __forceinline__ void pro_t(const float* pt, int c) {
+    const f32x4* q = (const f32x4*)(pt + 2 * c);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 t = q[h], u = q[h + 2];
+      a[2 * h] = act_t<ACT>(fmaf(a[2 * h], t[0], t[1]));
+      a[2 * h + 1] = act_t<ACT>(fmaf(a[2 * h + 1], t[2], t[3]));
+      b[2 * h] = act_t<ACT>(fmaf(b[2 * h], u[0], u[1]));
+      b[2 * h + 1] = act_t<ACT>(fmaf(b[2 * h + 1], u[2], u[3]));
+    }
+  }
+  __device__ __forceinline__ void pro(const float* pt, int c, int act) {
+    if (act == ROD_ACT_RELU6) pro_t<ROD_ACT_RELU6>(pt, c);
+    else if (act == ROD_ACT_LEAKY) pro_t<ROD_ACT_LEAKY>(pt, c);
+    else pro_t<ROD_ACT_NONE>(pt, c);
   }
 };
 
@@ -73,25 +117,33 @@ struct RowSrc {
       base = X + n * (long)H * W * ldx;
     }
   }
-  // load A[m, k..k+7]; K = KS*KS*Cin
-  template <bool VEC>
-  __device__ __forceinline__ void load(Chunk8<T>& c, int k, int K, int Cin, int H, int W, int ldx) const {
+  // load A[m, k..k+7]; K = KS*KS*Cin.  PRO: x holds the pre-BatchNorm tensor and every
+  // in-bounds element goes through the BatchNorm-apply prologue (table pt = [Cin][2] of
+  // (scale, offset) in LDS); padding taps and k >= K stay 0.
+  template <bool VEC, bool PRO = false>
+  __device__ __forceinline__ void load(Chunk8<T>& c, int k, int K, int Cin, int H, int W, int ldx,
+                                       const float* pt = nullptr, int act = 0) const {
     if (!valid || k >= K) { c.zero(); return; }
     if constexpr (KS == 1) {
       if (VEC && k + 8 <= K) {
-        c.load_vec(base + k);
+        c.load_vec(base + k);  // prologue deferred to pro_pending()
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) c.set(j, (k + j < K) ? base[k + j] : (T)0.f);
+        for (int j = 0; j < 8; ++j) {
+          T v = (k + j < K) ? base[k + j] : (T)0.f;
+          if constexpr (PRO) {
+            if (k + j < K) v = from_f32<T>(act_fwd(fmaf(to_f32(v), pt[2 * (k + j)], pt[2 * (k + j) + 1]), act));
+          }
+          c.set(j, v);
+        }
+        c.ok = false;
       }
     } else {
       if (VEC) {  // Cin % 8 == 0 : the chunk lies inside one tap
         const int tap = k / Cin, ci = k - tap * Cin;
         const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
-        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-          c.load_vec(base + ((long)yy * W + xx) * ldx + ci);
-        else
-          c.zero();
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) c.load_vec(base + ((long)yy * W + xx) * ldx + ci);
+        else c.zero();  // prologue deferred to pro_pending()
       } else {
         const int cin = CIN > 0 ? CIN : Cin;
 #pragma unroll
@@ -101,14 +153,30 @@ struct RowSrc {
           if (kk < K) {
             const int tap = kk / cin, ci = kk - tap * cin;
             const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
-            if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = base[((long)yy * W + xx) * ldx + ci];
+            if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+              v = base[((long)yy * W + xx) * ldx + ci];
+              if constexpr (PRO) v = from_f32<T>(act_fwd(fmaf(to_f32(v), pt[2 * ci], pt[2 * ci + 1]), act));
+            }
           }
           c.set(j, v);
         }
+        c.ok = false;
       }
     }
   }
+  // the deferred prologue of a chunk loaded for k (vector paths), just before it is stored
+  template <bool PRO>
+  __device__ __forceinline__ void pro_pending(Chunk8<T>& c, int k, int Cin, const float* pt, int act) const {
+    if constexpr (PRO) {
+      if (c.ok) c.pro(pt, KS == 1 ? k : k % Cin, act);
+    }
+  }
 };
+
+// Stage the prologue table [Cin][2] = (scale, offset) into LDS (caller syncs).
+__device__ __forceinline__ void stage_pro(float* pt, const BnPro& p, int Cin) {
+  for (int c = threadIdx.x; c < Cin; c += blockDim.x) bn_pro_affine(p, c, pt[2 * c], pt[2 * c + 1]);
+}
 
 // ---- MFMA over one 32-deep k step for one 16x16 tile ---------------------------------
 __device__ __forceinline__ void mma32(f32x4& acc, const bf16_t* a, const bf16_t* b) {
@@ -127,11 +195,13 @@ __device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b
 // forward: y[m, co] = sum_k A[m,k] wt[co,k] + bias[co]
 // block 256 threads = 4 waves laid out WM x WN; tile BM x BN; wave tile (BM/WM) x (BN/WN)
 // =====================================================================================
-template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool SPLIT = false, bool STATS = false>
+template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool SPLIT = false, bool STATS = false,
+          bool PRO = false>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
                                                        const float* __restrict__ bias, T* __restrict__ Y, long M,
                                                        int H, int W, int Cin, int Cout, int ldx, int ldy,
-                                                       float* __restrict__ part = nullptr, int kper = 0) {
+                                                       float* __restrict__ part = nullptr, int kper = 0,
+                                                       BnPro pro = BnPro{}) {
   constexpr int BM = 128;
   constexpr int WN = BN >= 64 ? 2 : 1;
   constexpr int WM = 4 / WN;
@@ -161,11 +231,17 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   RowSrc<T, KS> rows[ACH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) rows[i].init(X, m0 + (tid >> 2) + i * 64, M, H, W, ldx);
+  extern __shared__ float pro_lds[];  // PRO: [Cin][2] prologue table (dynamic LDS)
+  if constexpr (PRO) {
+    stage_pro(pro_lds, pro, Cin);
+    __syncthreads();
+  }
 
   Chunk8<T> ra[ACH], rb[BCH];
   auto load_tiles = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) rows[i].template load<VA>(ra[i], k0 + kc, K, Cin, H, W, ldx);
+    for (int i = 0; i < ACH; ++i)
+      rows[i].template load<VA, PRO>(ra[i], k0 + kc, K, Cin, H, W, ldx, pro_lds, pro.act);
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int cid = tid + i * 256;
@@ -199,7 +275,10 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   for (int k0 = kb; k0 < ke; k0 += BK) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) ra[i].store_lds(As + ((tid >> 2) + i * 64) * LD + kc);
+    for (int i = 0; i < ACH; ++i) {
+      rows[i].template pro_pending<PRO>(ra[i], k0 + kc, Cin, pro_lds, pro.act);
+      ra[i].store_lds(As + ((tid >> 2) + i * 64) * LD + kc);
+    }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int cid = tid + i * 256;
@@ -446,12 +525,18 @@ __device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
   return __builtin_bit_cast(bf16x4, r);
 }
 
-template <typename T, int KS, bool VA, bool VD, int CIN = 0>
+template <typename T, int KS, bool VA, bool VD, int CIN = 0, bool PRO = false>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X, const T* __restrict__ DY,
                                                          float* __restrict__ part, long M, int H, int W, int Cin,
-                                                         int Cout, int ldx, int lddy, long chunk, int ktiles) {
+                                                         int Cout, int ldx, int lddy, long chunk, int ktiles,
+                                                         BnPro pro = BnPro{}) {
   __shared__ __attribute__((aligned(16))) T Ds[BK * WG_LD];  // [m][co]
   __shared__ __attribute__((aligned(16))) T Xs[BK * WG_LD];  // [m][k]
+  extern __shared__ float pro_lds[];  // PRO: [Cin][2] prologue table (dynamic LDS)
+  if constexpr (PRO) {
+    stage_pro(pro_lds, pro, Cin);
+    __syncthreads();
+  }
   const int K = KS * KS * Cin;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves of 32x32
@@ -486,13 +571,17 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
     }
     RowSrc<T, KS, CIN> rs;
     rs.init(X, row < me ? row : M, M, H, W, ldx);
-    rs.template load<VA>(rx, k0 + lc, K, Cin, H, W, ldx);
+    rs.template load<VA, PRO>(rx, k0 + lc, K, Cin, H, W, ldx, pro_lds, pro.act);
   };
 
   if (mb < me) load_step(mb);
   for (long m = mb; m < me; m += BK) {
     __syncthreads();
     rd.store_lds(Ds + lr * WG_LD + lc);
+    if constexpr (PRO) {
+      RowSrc<T, KS, CIN> rp;  // (pro_pending only needs KS)
+      rp.template pro_pending<PRO>(rx, k0 + lc, Cin, pro_lds, pro.act);
+    }
     rx.store_lds(Xs + lr * WG_LD + lc);
     __syncthreads();
     if (m + BK < me) load_step(m + BK);
@@ -613,29 +702,34 @@ static bool aligned16(const void* p) {
   return ((uintptr_t)p & 15) == 0;
 }
 
-template <typename T, int KS, int BN, bool VA, bool VB, bool VY>
+// `pro` (nullable): BatchNorm-apply prologue on the A operand; its table takes 8*Cin bytes of
+// dynamic LDS.
+template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool PRO>
 static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
-                            int Cout, int ldx, int ldy, float* stats, hipStream_t s) {
+                            int Cout, int ldx, int ldy, float* stats, const BnPro& pro, hipStream_t s) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
+  const size_t lds = PRO ? 8 * (size_t)Cin : 0;
   if constexpr (VY) {
     if (stats) {
-      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, true>), grid, dim3(256), 0, s, (const T*)x,
-                         (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, stats, 0);
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, true, PRO>), grid, dim3(256), lds, s,
+                         (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, stats, 0, pro);
       return;
     }
   }
-  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY>), grid, dim3(256), 0, s, (const T*)x, (const T*)wt, bias,
-                     (T*)y, M, H, W, Cin, Cout, ldx, ldy, nullptr, 0);
+  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO>), grid, dim3(256), lds, s,
+                     (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, nullptr, 0, pro);
 }
 
 // N tile: the whole of Cout in one tile up to 256 (A is read once), else 128-wide tiles.
 // The fully vectorisable case (16-byte A, B and Y rows) gets the full tile menu and the
-// LDS-staged epilogue; the rest (stem Cin=3, odd strides) the 32/64/128 direct-store kernel.
-template <typename T, int KS>
+// LDS-staged epilogue; the rest (stem Cin=3, odd strides) the 32/64/128 direct-store kernel
+// (with a prologue: the 128-wide one only).
+template <typename T, int KS, bool PRO>
 static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const void* wt, const float* bias, void* y,
-                              long M, int H, int W, int Cin, int Cout, int ldx, int ldy, float* stats, hipStream_t s) {
+                              long M, int H, int W, int Cin, int Cout, int ldx, int ldy, float* stats,
+                              const BnPro& pro, hipStream_t s) {
 #define CF(BN_, VA_, VB_, VY_) \
-  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, s)
+  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, s)
   if (va && vb && vy) {
     if (Cout <= 32) CF(32, true, true, true);
     else if (Cout <= 64) CF(64, true, true, true);
@@ -647,30 +741,32 @@ static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const vo
     else CF(128, true, true, true);
     return;
   }
-  if (Cout <= 32) {
-    if (va && vb) CF(32, true, true, false); else if (va) CF(32, true, false, false);
-    else if (vb) CF(32, false, true, false); else CF(32, false, false, false);
-  } else if (Cout <= 64) {
-    if (va && vb) CF(64, true, true, false); else if (va) CF(64, true, false, false);
-    else if (vb) CF(64, false, true, false); else CF(64, false, false, false);
-  } else {
+  if (PRO || Cout > 64) {
     if (va && vb) CF(128, true, true, false); else if (va) CF(128, true, false, false);
     else if (vb) CF(128, false, true, false); else CF(128, false, false, false);
+  } else if (Cout <= 32) {
+    if (va && vb) CF(32, true, true, false); else if (va) CF(32, true, false, false);
+    else if (vb) CF(32, false, true, false); else CF(32, false, false, false);
+  } else {
+    if (va && vb) CF(64, true, true, false); else if (va) CF(64, true, false, false);
+    else if (vb) CF(64, false, true, false); else CF(64, false, false, false);
   }
 #undef CF
 }
 
-template <typename T, int KS>
+template <typename T, int KS, bool PRO>
 static void conv_fwd_split(const SplitPlan& p, const void* x, const void* wt, float* part, long M, int H, int W,
-                           int Cin, int Cout, int ldx, hipStream_t s) {
+                           int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, 128), p.splits);
-  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, 128, true, true, false, true>), grid, dim3(256), 0, s, (const T*)x,
-                     (const T*)wt, nullptr, nullptr, M, H, W, Cin, Cout, ldx, 0, part, p.kper);
+  const size_t lds = PRO ? 8 * (size_t)Cin : 0;
+  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, 128, true, true, false, true, false, PRO>), grid, dim3(256), lds, s,
+                     (const T*)x, (const T*)wt, nullptr, nullptr, M, H, W, Cin, Cout, ldx, 0, part, p.kper, pro);
 }
 
 template <typename T>
-static void conv_fwd_typed(const void* x, const void* wt, const float* bias, void* y, void* ws, float* stats, int N,
-                           int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy, hipStream_t s) {
+static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, const float* bias, void* y, void* ws,
+                           float* stats, int N, int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy,
+                           hipStream_t s) {
   const long M = (long)N * H * W;
   const int K = ksize * ksize * Cin;
   const int eV = Vec16<T>::N;
@@ -680,22 +776,28 @@ static void conv_fwd_typed(const void* x, const void* wt, const float* bias, voi
   const SplitPlan sp = split_plan(M, Cout, K);
   const int nparts = (int)cdivl(M, 128);
   const int dt = sizeof(T) == 4 ? ROD_F32 : ROD_BF16;
+  const BnPro pv = pro ? *pro : BnPro{};
   if (ws != nullptr && sp.splits > 1 && va && vb) {
     float* part = (float*)ws;
-    if (ksize == 1) conv_fwd_split<T, 1>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, s);
-    else conv_fwd_split<T, 3>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, s);
+    if (ksize == 1) {
+      if (pro) conv_fwd_split<T, 1, true>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+      else conv_fwd_split<T, 1, false>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+    } else {
+      if (pro) conv_fwd_split<T, 3, true>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+      else conv_fwd_split<T, 3, false>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+    }
     hipLaunchKernelGGL(splitk_combine_kernel<T>, dim3(cdivl(M * Cout, 256)), dim3(256), 0, s, (const float*)part,
                        bias, (T*)y, M, Cout, ldy, sp.splits);
     if (stats) stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
     return;
   }
   if (stats && !(va && vb && vy)) {  // no fused epilogue on this path: separate statistics pass
-    conv_fwd_typed<T>(x, wt, bias, y, ws, nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy, s);
+    conv_fwd_typed<T>(x, pro, wt, bias, y, ws, nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy, s);
     stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
     return;
   }
   static const bool no_stem = getenv("ROD_DEBUG_NOSTEM") != nullptr;  // debug bisection
-  if (ksize == 3 && Cin == 3 && (Cout == 32 || Cout == 64) && vy && !no_stem) {
+  if (!pro && ksize == 3 && Cin == 3 && (Cout == 32 || Cout == 64) && vy && !no_stem) {
     if (Cout == 32)
       hipLaunchKernelGGL((stem_conv_fwd_kernel<T, 32>), dim3(cdiv(W, 128), H, N), dim3(256), 0, s, (const T*)x,
                          (const T*)wt, bias, (T*)y, H, W, ldx, ldy);
@@ -704,44 +806,53 @@ static void conv_fwd_typed(const void* x, const void* wt, const float* bias, voi
                          (const T*)wt, bias, (T*)y, H, W, ldx, ldy);
     return;
   }
-  if (ksize == 1) conv_fwd_dispatch<T, 1>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, s);
-  else conv_fwd_dispatch<T, 3>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, s);
+  if (ksize == 1) {
+    if (pro) conv_fwd_dispatch<T, 1, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
+    else conv_fwd_dispatch<T, 1, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
+  } else {
+    if (pro) conv_fwd_dispatch<T, 3, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
+    else conv_fwd_dispatch<T, 3, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
+  }
 }
 
-template <typename T, int KS, bool VA, bool VD>
+template <typename T, int KS, bool VA, bool VD, bool PRO>
 static void wgrad_launch(const WgradPlan& p, const void* x, const void* dy, float* part, long M, int H, int W,
-                         int Cin, int Cout, int ldx, int lddy, hipStream_t s) {
+                         int Cin, int Cout, int ldx, int lddy, const BnPro& pro, hipStream_t s) {
   dim3 grid(p.ctiles * p.ktiles, p.splits);
-  hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, VA, VD>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, part, M,
-                     H, W, Cin, Cout, ldx, lddy, p.chunk, p.ktiles);
+  const size_t lds = PRO ? 8 * (size_t)Cin : 0;
+  hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, VA, VD, 0, PRO>), grid, dim3(256), lds, s, (const T*)x, (const T*)dy,
+                     part, M, H, W, Cin, Cout, ldx, lddy, p.chunk, p.ktiles, pro);
 }
 
-template <typename T, int KS>
+template <typename T, int KS, bool PRO>
 static void wgrad_va_vd(bool va, bool vd, const WgradPlan& p, const void* x, const void* dy, float* part, long M,
-                        int H, int W, int Cin, int Cout, int ldx, int lddy, hipStream_t s) {
-  if (va && vd) wgrad_launch<T, KS, true, true>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
-  else if (va) wgrad_launch<T, KS, true, false>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
-  else if (vd) wgrad_launch<T, KS, false, true>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
-  else wgrad_launch<T, KS, false, false>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+                        int H, int W, int Cin, int Cout, int ldx, int lddy, const BnPro& pro, hipStream_t s) {
+  if (va && vd) wgrad_launch<T, KS, true, true, PRO>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pro, s);
+  else if (va) wgrad_launch<T, KS, true, false, PRO>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pro, s);
+  else if (vd) wgrad_launch<T, KS, false, true, PRO>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pro, s);
+  else wgrad_launch<T, KS, false, false, PRO>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pro, s);
 }
 
 template <typename T>
-static void wgrad_typed(const void* x, const void* dy, float* dw, float* db, float* part, int N, int H, int W, int Cin,
-                        int Cout, int ksize, int ldx, int lddy, hipStream_t s) {
+static void wgrad_typed(const void* x, const BnPro* pro, const void* dy, float* dw, float* db, float* part, int N,
+                        int H, int W, int Cin, int Cout, int ksize, int ldx, int lddy, hipStream_t s) {
   const long M = (long)N * H * W;
   const long K = (long)ksize * ksize * Cin;
   WgradPlan p = wgrad_plan(M, Cin, Cout, ksize);
   const int eV = Vec16<T>::N;
   const bool va = aligned16<T>(x) && (ldx % eV == 0) && (ksize == 1 ? true : (Cin % 8 == 0));
   const bool vd = aligned16<T>(dy) && (lddy % eV == 0);
-  if (ksize == 3 && Cin == 3 && vd) {
+  const BnPro pv = pro ? *pro : BnPro{};
+  if (!pro && ksize == 3 && Cin == 3 && vd) {
     dim3 grid(p.ctiles * p.ktiles, p.splits);
     hipLaunchKernelGGL((conv_wgrad_kernel<T, 3, false, true, 3>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy,
-                       part, M, H, W, Cin, Cout, ldx, lddy, p.chunk, p.ktiles);
+                       part, M, H, W, Cin, Cout, ldx, lddy, p.chunk, p.ktiles, pv);
   } else if (ksize == 1) {
-    wgrad_va_vd<T, 1>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+    if (pro) wgrad_va_vd<T, 1, true>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pv, s);
+    else wgrad_va_vd<T, 1, false>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pv, s);
   } else {
-    wgrad_va_vd<T, 3>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, s);
+    if (pro) wgrad_va_vd<T, 3, true>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pv, s);
+    else wgrad_va_vd<T, 3, false>(va, vd, p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pv, s);
   }
   const long n = (long)Cout * K;
   slab_sum(part, dw, p.splits, n, s);
@@ -766,15 +877,19 @@ size_t rod_conv_fwd_workspace(int N, int H, int W, int Cin, int Cout, int ksize)
   return p.splits > 1 ? (size_t)p.splits * M * Cout * sizeof(float) : 0;
 }
 
-int rod_conv_fwd(const void* x, const void* wt, const float* bias, void* y, void* workspace, float* stat_parts, int N,
-                 int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy, int dtype, void* stream) {
+int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                 const float* pro_beta, int pro_act, const void* wt, const float* bias, void* y, void* workspace,
+                 float* stat_parts, int N, int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy, int dtype,
+                 void* stream) {
   ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "rod_conv_fwd: bad shape");
   ROD_CHECK_ARG(ksize == 1 || ksize == 3, "rod_conv_fwd: ksize must be 1 or 3");
   if (ldx == 0) ldx = Cin;
   if (ldy == 0) ldy = Cout;
   ROD_CHECK_ARG(ldx >= Cin && ldy >= Cout, "rod_conv_fwd: leading dim too small");
-  ROD_DISPATCH_DTYPE(dtype, conv_fwd_typed<T>(x, wt, bias, y, workspace, stat_parts, N, H, W, Cin, Cout, ksize, ldx,
-                                              ldy, ROD_STREAM(stream)));
+  ROD_CHECK_ARG(!pro_mean || (pro_rstd && Cin <= PRO_MAXC), "rod_conv_fwd: bad BatchNorm prologue (Cin %d)", Cin);
+  const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  ROD_DISPATCH_DTYPE(dtype, conv_fwd_typed<T>(x, pro_mean ? &pro : nullptr, wt, bias, y, workspace, stat_parts, N, H,
+                                              W, Cin, Cout, ksize, ldx, ldy, ROD_STREAM(stream)));
   return check_launch("rod_conv_fwd");
 }
 
@@ -798,16 +913,19 @@ size_t rod_conv_wgrad_workspace(int N, int H, int W, int Cin, int Cout, int ksiz
   return std::max(part, cs);
 }
 
-int rod_conv_wgrad(const void* x, const void* dy, float* dw, float* db, void* workspace, int N, int H, int W,
-                   int Cin, int Cout, int ksize, int ldx, int lddy, int dtype, void* stream) {
+int rod_conv_wgrad(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                   const float* pro_beta, int pro_act, const void* dy, float* dw, float* db, void* workspace, int N,
+                   int H, int W, int Cin, int Cout, int ksize, int ldx, int lddy, int dtype, void* stream) {
   ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "rod_conv_wgrad: bad shape");
   ROD_CHECK_ARG(ksize == 1 || ksize == 3, "rod_conv_wgrad: ksize must be 1 or 3");
   ROD_CHECK_ARG(workspace != nullptr, "rod_conv_wgrad: workspace is NULL");
   if (ldx == 0) ldx = Cin;
   if (lddy == 0) lddy = Cout;
   ROD_CHECK_ARG(ldx >= Cin && lddy >= Cout, "rod_conv_wgrad: leading dim too small");
-  ROD_DISPATCH_DTYPE(dtype, wgrad_typed<T>(x, dy, dw, db, (float*)workspace, N, H, W, Cin, Cout, ksize, ldx, lddy,
-                                           ROD_STREAM(stream)));
+  ROD_CHECK_ARG(!pro_mean || (pro_rstd && Cin <= PRO_MAXC), "rod_conv_wgrad: bad BatchNorm prologue (Cin %d)", Cin);
+  const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  ROD_DISPATCH_DTYPE(dtype, wgrad_typed<T>(x, pro_mean ? &pro : nullptr, dy, dw, db, (float*)workspace, N, H, W, Cin,
+                                           Cout, ksize, ldx, lddy, ROD_STREAM(stream)));
   return check_launch("rod_conv_wgrad");
 }
 

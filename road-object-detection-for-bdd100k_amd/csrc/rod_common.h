@@ -93,6 +93,52 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   n = nt;
 }
 
+// ---- activations (after BatchNorm) ---------------------------------------------
+// relu6 = clamp (v_med3_f32), leaky = max(z, 0.2 z) (== z > 0 ? z : 0.2 z bit for bit)
+template <int ACT>
+__device__ __forceinline__ float act_t(float z) {
+  if constexpr (ACT == ROD_ACT_RELU6) return __builtin_amdgcn_fmed3f(z, 0.f, 6.f);  // tf.nn.relu6
+  else if constexpr (ACT == ROD_ACT_LEAKY) return fmaxf(z, z * 0.2f);                // leaky_relu(0.2)
+  else return z;
+}
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  if (act == ROD_ACT_RELU6) return act_t<ROD_ACT_RELU6>(z);
+  if (act == ROD_ACT_LEAKY) return act_t<ROD_ACT_LEAKY>(z);
+  return z;
+}
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == ROD_ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;  // Relu6Grad
+  if (act == ROD_ACT_LEAKY) return z > 0.f ? 1.f : 0.2f;               // LeakyReluGrad
+  return 1.f;
+}
+
+// ---- BatchNorm affine -------------------------------------------------------------
+// z = x*scale + offset (one FMA), scale = rstd*gamma, offset = beta - mean*scale — the form of
+// TF's fused batch-norm kernel; every librod kernel that forms z (rod_bn_apply, the backward's
+// activation mask, the consumer prologues) uses exactly this, so they agree bit for bit.
+__device__ __forceinline__ void bn_affine(const float* mean, const float* rstd, const float* gamma,
+                                          const float* beta, int c, float& sc, float& sh) {
+  sc = gamma ? rstd[c] * gamma[c] : rstd[c];
+  sh = (beta ? beta[c] : 0.f) - mean[c] * sc;
+}
+
+// ---- BatchNorm-apply prologue -----------------------------------------------------
+// A consumer kernel that reads the PRE-BatchNorm tensor y instead of the BatchNorm output:
+// z = act(fma(y, scale, offset)), rounded to the storage type — exactly the value
+// rod_bn_apply would have written — is formed in registers as each element is consumed, so
+// the normalised activation never crosses HBM.  Padding taps stay 0.
+struct BnPro {
+  const float* mean;
+  const float* rstd;
+  const float* gamma;  // NULL => 1
+  const float* beta;   // NULL => 0
+  int act;
+};
+constexpr int PRO_MAXC = 2048;  // channel limit of the LDS-staged prologue tables
+__device__ __forceinline__ void bn_pro_affine(const BnPro& p, int c, float& sc, float& sh) {
+  bn_affine(p.mean, p.rstd, p.gamma, p.beta, c, sc, sh);
+}
+
 // Fallback: parts of y[M, C] computed by a separate pass (batchnorm.hip).
 void stat_parts(int dtype, const void* y, long M, int C, int ld, float* parts, int nparts, hipStream_t s);
 

@@ -76,10 +76,13 @@ class MobilenetV2:
         self.store.add_buffer(name + '/moving_mean', np.zeros(c, np.float32))
         self.store.add_buffer(name + '/moving_variance', np.ones(c, np.float32))
 
-    def _bn_act(self, x, name, act, training, residual=None, parts=None):
+    def _bn_act(self, x, name, act, training, residual=None, parts=None, pending=False):
+        """BatchNorm + activation (+ residual).  pending: leave it to the single consumer's
+        load prologue (ops.Pending) instead of writing it out."""
         P, B = self.store.params, self.store.buffers
-        return ops.bn_act(x, P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'],
-                          B[name + '/moving_variance'], act, training, BN_DECAY, BN_EPS, residual, parts)
+        p = ops.bn_pending(x, P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'],
+                           B[name + '/moving_variance'], act, training, BN_DECAY, BN_EPS, parts)
+        return p if pending and residual is None else ops.materialize(p, residual)
 
     @staticmethod
     def _conv(x, w, ks, training):
@@ -96,27 +99,35 @@ class MobilenetV2:
         P = self.store.params
         end_points = {}
         taps = set(taps or ())
+        # The stem, expand and depthwise BatchNorms each feed exactly one consumer (the next
+        # depthwise or project conv), so they stay Pending and are applied in that consumer's
+        # load prologue; the project BatchNorm (+ residual) is written out as the endpoint.
+        fuse = 'bnpro' not in ops._DISABLE
         for (idx, kind, s, cin, inner, cout, res, sc) in self.plan:
             base = '%s/%s' % (self.scope, sc)
+            name = 'layer_%d' % idx
+            tapped = name in taps or final_endpoint == name
             if kind == 'conv':
                 x, st = self._conv(x, P[base + '/weights'], 3, is_training)
-                x = self._bn_act(x, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st)
+                x = self._bn_act(x, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st,
+                                 pending=fuse and not tapped)
             else:
                 inp = None
                 if res:
                     inp, x = graph.fork(x, 2)
                 if inner > cin:
                     x, st = self._conv(x, P[base + '/expand/weights'], 1, is_training)
-                    x = self._bn_act(x, base + '/expand/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st)
+                    x = self._bn_act(x, base + '/expand/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st,
+                                     pending=fuse)
                 if is_training:
                     x, st = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s, want_stats=True)
                 else:
                     x, st = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s), None
-                x = self._bn_act(x, base + '/depthwise/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st)
+                x = self._bn_act(x, base + '/depthwise/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st,
+                                 pending=fuse)
                 x, st = self._conv(x, P[base + '/project/weights'], 1, is_training)
                 x = self._bn_act(x, base + '/project/BatchNorm', ops.ROD_ACT_NONE, is_training,
                                  residual=inp, parts=st)
-            name = 'layer_%d' % idx
             last = final_endpoint == name or idx == self.plan[-1][0]
             if name in taps and not last:
                 end_points[name], x = graph.fork(x, 2)

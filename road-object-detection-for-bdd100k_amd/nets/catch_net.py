@@ -105,10 +105,12 @@ class CatchNet:
                 self._head_bn(base + '/BatchNorm', 2 * f_c)
 
     # ------------------------------------------------------------------ forward
-    def _bn(self, x, name, training, act=ops.ROD_ACT_LEAKY, parts=None):
+    def _bn(self, x, name, training, act=ops.ROD_ACT_LEAKY, parts=None, pending=False):
+        """BatchNorm (beta only) + leaky; pending: applied in the next conv's load prologue."""
         P, B = self.store.params, self.store.buffers
-        return ops.bn_act(x, None, P[name + '/beta'], B[name + '/moving_mean'], B[name + '/moving_variance'],
-                          act, training, HEAD_BN_DECAY, HEAD_BN_EPS, parts=parts)
+        p = ops.bn_pending(x, None, P[name + '/beta'], B[name + '/moving_mean'], B[name + '/moving_variance'],
+                           act, training, HEAD_BN_DECAY, HEAD_BN_EPS, parts)
+        return p if pending and 'bnpro' not in ops._DISABLE else ops.materialize(p)
 
     @staticmethod
     def _conv(x, w, b, ks, training):
@@ -129,7 +131,8 @@ class CatchNet:
                     cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
                     bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
                     x, st = self._conv(x, P[cname + '/weights'], P[cname + '/biases'], ks, training)
-                    x = self._bn(x, bname, training, parts=st)
+                    # the first three BatchNorms feed only the next conv of the head
+                    x = self._bn(x, bname, training, parts=st, pending=n < 3)
                     n += 1
             B_, fh, fw, _ = x.shape
             outs.append(x.view(B_, fh, fw, self.n_anchor[i], k))

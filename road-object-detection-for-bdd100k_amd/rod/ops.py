@@ -78,10 +78,65 @@ def copy2d(src, src_ld_bytes, dst, dst_ld_bytes, rows, cols_bytes, src_off=0, ds
               rows, cols_bytes, stream())
 
 
+# ----------------------------------------------------------------------------- BatchNorm prologue
+class Pending:
+    """act(BatchNorm(y)) whose statistics are known but which is NOT materialised.
+
+    A consumer that supports the BatchNorm-apply prologue (conv2d, dw3x3) reads y and forms
+    act((y - mean) * rstd*gamma + beta) as it loads it (include/rod.h, ABI 3), and its backward
+    runs the BatchNorm backward itself; `materialize` writes the tensor for any other consumer.
+    """
+    __slots__ = ('y', 'mean', 'rstd', 'gamma', 'beta', 'act', 'training')
+
+    def __init__(self, y, mean, rstd, gamma, beta, act, training):
+        self.y, self.mean, self.rstd, self.gamma, self.beta = y, mean, rstd, gamma, beta
+        self.act, self.training = act, training
+
+    @property
+    def shape(self):
+        return self.y.shape
+
+
+def _pro_args(p):
+    """The five prologue arguments of the ABI-3 entries (NULLs without a prologue)."""
+    if p is None:
+        return (None, None, None, None, 0)
+    mean, rstd, gamma, beta, act = p
+    return (mean, rstd, gamma, beta, act)
+
+
+def _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
+    """rod_bn_bwd: gradient wrt the pre-BatchNorm y from the gradient dz of act(BN(y));
+    dgamma / dbeta go to the parameters' flat-buffer slots."""
+    N, H, W, C = y.shape
+    M = N * H * W
+    dz = dz.contiguous()
+    dy = torch.empty_like(y)
+    dg = grad_slot(gamma) if need_g else None
+    db = grad_slot(beta) if need_b else None
+    if db is None:
+        db = torch.empty(C, dtype=torch.float32, device=y.device)  # the kernel always may write dbeta
+    ws = workspace(_abi.query("rod_bn_bwd_workspace", M, C), y.device)
+    _abi.call("rod_bn_bwd", dz, y, mean, rstd, gamma, beta, dy, dg, db, ws, M, C, 0, 0, 0, act, dtcode(y),
+              stream())
+    if need_g:
+        _mark_written(gamma)
+    if need_b:
+        _mark_written(beta)
+    return dy
+
+
+def _split_in(x):
+    """(tensor, gamma, beta, mean, rstd, act, training) of a plain tensor or a Pending."""
+    if isinstance(x, Pending):
+        return x.y, x.gamma, x.beta, x.mean, x.rstd, x.act, x.training
+    return x, None, None, None, None, 0, False
+
+
 # ----------------------------------------------------------------------------- depthwise
 class _DW3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, want_stats=False):
+    def forward(ctx, x, w, stride, want_stats, gamma, beta, mean, rstd, act, training):
         N, H, W, C = x.shape
         Ho, pt = same_pad(H, stride)
         Wo, pl = same_pad(W, stride)
@@ -89,10 +144,13 @@ class _DW3x3(torch.autograd.Function):
         parts = None
         if want_stats:  # BatchNorm partial statistics from the epilogue
             nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C)
-            parts = torch.empty((3, C, nparts), dtype=torch.float32, device=x.device)
-        _abi.call("rod_dw3x3_fwd", x, w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x), stream())
-        ctx.save_for_backward(x, w)
+            parts = torch.empty((nparts, 3, C), dtype=torch.float32, device=x.device)
+        pro = (mean, rstd, gamma, beta, act) if mean is not None else None
+        _abi.call("rod_dw3x3_fwd", x, *_pro_args(pro), w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x),
+                  stream())
+        ctx.save_for_backward(x, w, gamma, beta, mean, rstd)
         ctx.geo = (N, H, W, C, stride, pt, pl, Ho, Wo)
+        ctx.act, ctx.pro, ctx.training = act, pro is not None, training
         if want_stats:
             ctx.mark_non_differentiable(parts)
             ctx.set_materialize_grads(False)
@@ -101,40 +159,51 @@ class _DW3x3(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, *_):
-        x, w = ctx.saved_tensors
+        x, w, gamma, beta, mean, rstd = ctx.saved_tensors
         N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
         dy = dy.contiguous()
+        pro = (mean, rstd, gamma, beta, ctx.act) if ctx.pro else None
+        need_g = ctx.pro and gamma is not None and ctx.needs_input_grad[4]
+        need_b = ctx.pro and beta is not None and ctx.needs_input_grad[5]
         dx = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
+        if ctx.needs_input_grad[0] or need_g or need_b:
+            if ctx.pro and not ctx.training:
+                raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
+            dx = torch.empty_like(x)   # gradient wrt the dw input (the BatchNorm output when pro)
             _abi.call("rod_dw3x3_bwd_data", dy, w, dx, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x), stream())
         if ctx.needs_input_grad[1]:
             g = grad_slot(w)
             ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
-            _abi.call("rod_dw3x3_bwd_filter", x, dy, g, ws, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x), stream())
+            _abi.call("rod_dw3x3_bwd_filter", x, *_pro_args(pro), dy, g, ws, N, H, W, C, s, pt, pl, Ho, Wo,
+                      dtcode(x), stream())
             _mark_written(w)
-        return dx, None, None, None
+        if ctx.pro and dx is not None:
+            dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
+        return dx, None, None, None, None, None, None, None, None, None
 
 
 def dw3x3(x, w, stride=1, want_stats=False):
-    """Depthwise 3x3, TF-SAME (conv_blocks.py:238-247).  want_stats: also return the
-    BatchNorm partial statistics of the output (for bn_act(..., parts=))."""
+    """Depthwise 3x3, TF-SAME (conv_blocks.py:238-247).  x: tensor or Pending (the BatchNorm
+    of the layer below is then applied in the load prologue).  want_stats: also return the
+    BatchNorm partial statistics of the output (for bn_pending(..., parts=))."""
+    xt, g, b, m, r, act, tr = _split_in(x)
     if want_stats and "dwstats" in _DISABLE:
-        return _DW3x3.apply(x, w, stride, False), None
-    return _DW3x3.apply(x, w, stride, want_stats)
+        return _DW3x3.apply(xt, w, stride, False, g, b, m, r, act, tr), None
+    return _DW3x3.apply(xt, w, stride, want_stats, g, b, m, r, act, tr)
 
 
 # ----------------------------------------------------------------------------- dense conv
-def conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, stat_parts=None):
+def conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, stat_parts=None, pro=None):
     """rod_conv_fwd with its split-K workspace (allocated only when the plan splits)."""
     nb = 0 if "splitk" in _DISABLE else _abi.query("rod_conv_fwd_workspace", N, H, W, Cin, Cout, ksize)
     ws = workspace(nb, x.device) if nb else None
-    _abi.call("rod_conv_fwd", x, wt, b, y, ws, stat_parts, N, H, W, Cin, Cout, ksize, 0, 0, dtcode(x), stream())
+    _abi.call("rod_conv_fwd", x, *_pro_args(pro), wt, b, y, ws, stat_parts, N, H, W, Cin, Cout, ksize, 0, 0,
+              dtcode(x), stream())
 
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, ksize, want_stats=False):
+    def forward(ctx, x, w, b, ksize, want_stats, gamma, beta, mean, rstd, act, training):
         N, H, W, Cin = x.shape
         Cout = w.shape[0]
         assert w.shape == (Cout, ksize, ksize, Cin), (tuple(w.shape), ksize, Cin)
@@ -142,11 +211,13 @@ class _Conv(torch.autograd.Function):
         _abi.call("rod_conv_weight_prep", w, wt, Cout, Cin, ksize, 0, dtcode(x), stream())
         y = torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
         parts = None
-        if want_stats:  # BatchNorm partial statistics from the epilogue ([3][Cout][ceil(M/128)])
-            parts = torch.empty((3, Cout, -(-(N * H * W) // 128)), dtype=torch.float32, device=x.device)
-        conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, parts)
-        ctx.save_for_backward(x, w, b)
+        if want_stats:  # BatchNorm partial statistics from the epilogue ([ceil(M/128)][3][Cout])
+            parts = torch.empty((-(-(N * H * W) // 128), 3, Cout), dtype=torch.float32, device=x.device)
+        pro = (mean, rstd, gamma, beta, act) if mean is not None else None
+        conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, parts, pro)
+        ctx.save_for_backward(x, w, b, gamma, beta, mean, rstd)
         ctx.ksize = ksize
+        ctx.act, ctx.pro, ctx.training = act, pro is not None, training
         if want_stats:
             ctx.mark_non_differentiable(parts)
             ctx.set_materialize_grads(False)
@@ -155,61 +226,78 @@ class _Conv(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, *_):
-        x, w, b = ctx.saved_tensors
+        x, w, b, gamma, beta, mean, rstd = ctx.saved_tensors
         ks = ctx.ksize
         N, H, W, Cin = x.shape
         Cout = w.shape[0]
         dy = dy.contiguous()
+        pro = (mean, rstd, gamma, beta, ctx.act) if ctx.pro else None
+        need_g = ctx.pro and gamma is not None and ctx.needs_input_grad[5]
+        need_b = ctx.pro and beta is not None and ctx.needs_input_grad[6]
         dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] or need_g or need_b:
+            if ctx.pro and not ctx.training:
+                raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
             wt1 = torch.empty((Cin, ks * ks * Cout), dtype=x.dtype, device=x.device)
             _abi.call("rod_conv_weight_prep", w, wt1, Cout, Cin, ks, 1, dtcode(x), stream())
-            dx = torch.empty_like(x)
+            dx = torch.empty_like(x)   # gradient wrt the conv input (the BatchNorm output when pro)
             conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks)
         need_w = ctx.needs_input_grad[1]
-        need_b = b is not None and ctx.needs_input_grad[2]
-        if need_w or need_b:
+        need_bias = b is not None and ctx.needs_input_grad[2]
+        if need_w or need_bias:
             gw = grad_slot(w) if need_w else None
             if gw is None:  # bias-only gradient still needs a scratch dW
                 gw = torch.empty(w.shape, dtype=torch.float32, device=x.device)
-            gb = grad_slot(b) if need_b else None
+            gb = grad_slot(b) if need_bias else None
             ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, H, W, Cin, Cout, ks), x.device)
-            _abi.call("rod_conv_wgrad", x, dy, gw, gb, ws, N, H, W, Cin, Cout, ks, 0, 0, dtcode(x), stream())
+            _abi.call("rod_conv_wgrad", x, *_pro_args(pro), dy, gw, gb, ws, N, H, W, Cin, Cout, ks, 0, 0, dtcode(x),
+                      stream())
             if need_w:
                 _mark_written(w)
-            if need_b:
+            if need_bias:
                 _mark_written(b)
-        return dx, None, None, None, None
+        if ctx.pro and dx is not None:
+            dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
+        return dx, None, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, w, b=None, ksize=1, want_stats=False):
-    """slim.conv2d, stride 1, SAME (1x1 or 3x3), NHWC.  want_stats: also return the
-    BatchNorm partial statistics of the output (for bn_act(..., parts=))."""
+    """slim.conv2d, stride 1, SAME (1x1 or 3x3), NHWC.  x: tensor or Pending (BatchNorm of the
+    layer below applied in the load prologue).  want_stats: also return the BatchNorm partial
+    statistics of the output (for bn_pending(..., parts=))."""
+    xt, g, bb, m, r, act, tr = _split_in(x)
     if want_stats and "convstats" in _DISABLE:
-        return _Conv.apply(x, w, b, ksize, False), None
-    return _Conv.apply(x, w, b, ksize, want_stats)
+        return _Conv.apply(xt, w, b, ksize, False, g, bb, m, r, act, tr), None
+    return _Conv.apply(xt, w, b, ksize, want_stats, g, bb, m, r, act, tr)
 
 
 # ----------------------------------------------------------------------------- batch norm
+def bn_statistics(x, mmean, mvar, training, decay, eps=1e-3, parts=None):
+    """(mean, rstd) fp32 [C] of slim.batch_norm: batch statistics (+ moving-average update)
+    in training — from the producer's partial statistics when given — else the moving ones."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(C, dtype=torch.float32, device=x.device)
+    if "epistats" in _DISABLE:
+        parts = None
+    if training and parts is not None:  # statistics already reduced by the producer's epilogue
+        nb = _abi.query("rod_bn_finalize_workspace", parts.shape[0], C)
+        ws = workspace(nb, x.device) if nb else None
+        _abi.call("rod_bn_finalize", parts, parts.shape[0], M, C, eps, decay, mean, rstd, mmean, mvar, ws, stream())
+    elif training:
+        ws = workspace(_abi.query("rod_bn_stats_workspace", M, C), x.device)
+        _abi.call("rod_bn_stats", x, M, C, 0, eps, decay, mean, rstd, mmean, mvar, ws, dtcode(x), stream())
+    else:
+        _abi.call("rod_bn_eval_stats", mmean, mvar, eps, mean, rstd, C, stream())
+    return mean, rstd
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, mmean, mvar, act, training, decay, eps, parts):
+    def forward(ctx, x, gamma, beta, residual, mean, rstd, act, training):
         N, H, W, C = x.shape
         M = N * H * W
-        mean = torch.empty(C, dtype=torch.float32, device=x.device)
-        rstd = torch.empty(C, dtype=torch.float32, device=x.device)
-        if "epistats" in _DISABLE:
-            parts = None
-        if training and parts is not None:  # statistics already reduced by the producer's epilogue
-            nb = _abi.query("rod_bn_finalize_workspace", parts.shape[2], C)
-            ws = workspace(nb, x.device) if nb else None
-            _abi.call("rod_bn_finalize", parts, parts.shape[2], M, C, eps, decay, mean, rstd, mmean, mvar, ws,
-                      stream())
-        elif training:
-            ws = workspace(_abi.query("rod_bn_stats_workspace", M, C), x.device)
-            _abi.call("rod_bn_stats", x, M, C, 0, eps, decay, mean, rstd, mmean, mvar, ws, dtcode(x), stream())
-        else:
-            _abi.call("rod_bn_eval_stats", mmean, mvar, eps, mean, rstd, C, stream())
         y = torch.empty_like(x)
         _abi.call("rod_bn_apply", x, mean, rstd, gamma, beta, residual, y, M, C, 0, 0, 0, act, dtcode(x),
                   stream())
@@ -224,33 +312,30 @@ class _BNAct(torch.autograd.Function):
         x, mean, rstd, gamma, beta = ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
-        N, H, W, C = x.shape
-        M = N * H * W
-        dy = dy.contiguous()
-        dx = torch.empty_like(x)
         need_g = gamma is not None and ctx.needs_input_grad[1]
         need_b = beta is not None and ctx.needs_input_grad[2]
-        dg = grad_slot(gamma) if need_g else None
-        db = grad_slot(beta) if need_b else None
-        if need_b and db is None:
-            db = torch.empty(C, dtype=torch.float32, device=x.device)
-        if db is None:
-            db = torch.empty(C, dtype=torch.float32, device=x.device)  # kernel always may write dbeta
-        ws = workspace(_abi.query("rod_bn_bwd_workspace", M, C), x.device)
-        _abi.call("rod_bn_bwd", dy, x, mean, rstd, gamma, beta, dx, dg, db, ws, M, C, 0, 0, 0, ctx.act,
-                  dtcode(x), stream())
-        if need_g:
-            _mark_written(gamma)
-        if need_b:
-            _mark_written(beta)
+        dx = _bn_backward(dy, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
         dres = dy if ctx.has_res else None
-        return dx, None, None, dres, None, None, None, None, None, None, None
+        return dx, None, None, dres, None, None, None, None
+
+
+def bn_pending(x, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, parts=None):
+    """slim.batch_norm (fused) + activation, left for the consumer's load prologue."""
+    mean, rstd = bn_statistics(x, mmean, mvar, training, decay, eps, parts)
+    return Pending(x, mean, rstd, gamma, beta, act, training)
+
+
+def materialize(p, residual=None):
+    """Write act(BatchNorm(y)) (+ residual after the activation) of a Pending."""
+    if not isinstance(p, Pending):
+        return p
+    return _BNAct.apply(p.y, p.gamma, p.beta, residual, p.mean, p.rstd, p.act, p.training)
 
 
 def bn_act(x, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, residual=None, parts=None):
-    """slim.batch_norm (fused) + activation (+ residual add after the activation).
+    """slim.batch_norm (fused) + activation (+ residual add after the activation), written out.
     parts: partial statistics of x from its producer (conv2d(..., want_stats=True))."""
-    return _BNAct.apply(x, gamma, beta, residual, mmean, mvar, act, training, decay, eps, parts)
+    return materialize(bn_pending(x, gamma, beta, mmean, mvar, act, training, decay, eps, parts), residual)
 
 
 # ----------------------------------------------------------------------------- levels
@@ -408,8 +493,8 @@ class _Deconv2x2(torch.autograd.Function):
             conv_fwd_raw(dz, wt1, None, dx, N, h, wd, 4 * F, Cin, 1)
         if ctx.needs_input_grad[1]:
             ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, h, wd, Cin, 4 * F, 1), x.device)
-            _abi.call("rod_conv_wgrad", x, dz, grad_slot(w), None, ws, N, h, wd, Cin, 4 * F, 1, 0, 0, dtcode(x),
-                      stream())
+            _abi.call("rod_conv_wgrad", x, *_pro_args(None), dz, grad_slot(w), None, ws, N, h, wd, Cin, 4 * F, 1,
+                      0, 0, dtcode(x), stream())
             _mark_written(w)
         return dx, None, None, None
 

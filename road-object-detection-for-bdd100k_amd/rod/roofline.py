@@ -20,23 +20,28 @@ MI355X_F32_PEAK_TFLOPS = 157.3    # f32 MFMA / vector
 
 def cost(name, a):
     """(bytes, flops) of the call rod_<name>(*a)."""
-    if name in ("rod_dw3x3_fwd", "rod_dw3x3_bwd_data"):
-        o = 1 if name == "rod_dw3x3_fwd" else 0   # rod_dw3x3_fwd has the stat_parts pointer
-        N, H, W, C, Ho, Wo, dt = a[3 + o], a[4 + o], a[5 + o], a[6 + o], a[10 + o], a[11 + o], a[12 + o]
+    # ABI 3: rod_dw3x3_fwd / _bwd_filter / rod_conv_fwd / _wgrad carry the five BatchNorm
+    # prologue arguments after x (P = 5 positions)
+    if name == "rod_dw3x3_fwd":
+        N, H, W, C, Ho, Wo, dt = a[9], a[10], a[11], a[12], a[16], a[17], a[18]
+        es = _ES[dt]
+        return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
+    if name == "rod_dw3x3_bwd_data":
+        N, H, W, C, Ho, Wo, dt = a[3], a[4], a[5], a[6], a[10], a[11], a[12]
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
     if name == "rod_dw3x3_bwd_filter":
-        N, H, W, C, Ho, Wo, dt = a[4], a[5], a[6], a[7], a[11], a[12], a[13]
+        N, H, W, C, Ho, Wo, dt = a[9], a[10], a[11], a[12], a[16], a[17], a[18]
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
     if name == "rod_conv_fwd":
-        N, H, W, Cin, Cout, ks, dt = a[6], a[7], a[8], a[9], a[10], a[11], a[14]
+        N, H, W, Cin, Cout, ks, dt = a[11], a[12], a[13], a[14], a[15], a[16], a[19]
         es = _ES[dt]
         M = N * H * W
         K = ks * ks * Cin
-        return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[2] is not None else 0), 2 * M * K * Cout
+        return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[7] is not None else 0), 2 * M * K * Cout
     if name == "rod_conv_wgrad":
-        N, H, W, Cin, Cout, ks, dt = a[6], a[7], a[8], a[9], a[10], a[11], a[14]
+        N, H, W, Cin, Cout, ks, dt = a[10], a[11], a[12], a[13], a[14], a[15], a[18]
         es = _ES[dt]
         M = N * H * W
         K = ks * ks * Cin
@@ -55,3 +60,15 @@ def cost(name, a):
         B, A, G = a[12], a[13], a[14]
         return B * A * 56 + A * 32 + B * G * 20, 15 * G * A * B
     return 0, 0
+
+
+# C-ABI entry -> (anchor kernel launched exactly once per entry call, kernel-name substrings of
+# every kernel the entry launches) for attributing rocprofv3 PMC counters (tools/pmc_traffic.py)
+ENTRY_KERNELS = {
+    "rod_bn_bwd": ("bn_bwd_apply_kernel", ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel", "bn_bwd_apply_kernel")),
+    "rod_bn_apply": ("bn_apply_kernel", ("bn_apply_kernel",)),
+    "rod_dw3x3_fwd": ("dw3x3_fwd_kernel", ("dw3x3_fwd_kernel",)),
+    "rod_dw3x3_bwd_data": ("dw3x3_bwd_data", ("dw3x3_bwd_data",)),
+    "rod_dw3x3_bwd_filter": ("dw3x3_bwd_filter_kernel", ("dw3x3_bwd_filter_kernel",)),
+    "rod_bn_finalize": ("bn_parts_merge_kernel", ("bn_parts_merge_kernel",)),
+}

@@ -332,3 +332,68 @@ def test_sgd_clip_and_normalize(dev):
     out = ops.normalize_image(img.to(dev))
     k = np.float32(2.0 / 255.0)
     np.testing.assert_array_equal(out.cpu().numpy(), k * img.numpy().astype(np.float32) - np.float32(1.0))
+
+
+def _pending_pair(dev, dtype, shape, act, gamma, seed):
+    """Two identical leaf pre-BatchNorm tensors y (for the fused and the materialised path) and
+    the BatchNorm parameters; statistics from rod_bn_stats (no moving-average update)."""
+    g = torch.Generator().manual_seed(seed)
+    C = shape[-1]
+    y0 = (torch.randn(*shape, generator=g) * 2 + 0.7).to(dev, dtype)
+    ga = _param(torch.rand(C, generator=g) + 0.5, dev) if gamma else None
+    be = _param(torch.randn(C, generator=g) * 0.3, dev)
+    return y0, ga, be
+
+
+def _fused_vs_materialised(dev, dtype, shape, act, gamma, consumer, seed):
+    """consumer(x) on ops.Pending (BatchNorm-apply in the load prologue, BatchNorm backward in
+    the consumer's backward) against consumer(materialize(Pending)) (rod_bn_apply + the plain
+    kernel): forward bit-exact, gradients of y / gamma / beta / weights bit-exact."""
+    y0, ga, be = _pending_pair(dev, dtype, shape, act, gamma, seed)
+    outs = []
+    for fused in (True, False):
+        y = y0.clone().requires_grad_(True)
+        for p in (ga, be):
+            if p is not None:
+                p._rod_grad.zero_()
+        p = ops.bn_pending(y, ga, be, None, None, act, True, 0.9, 1e-3)
+        out, wgrad = consumer(p if fused else ops.materialize(p))
+        gy = torch.randn(out.shape, generator=torch.Generator().manual_seed(seed + 1)).to(dev, dtype)
+        out.backward(gy)
+        outs.append((out.detach().clone(), y.grad.clone(), None if ga is None else ga._rod_grad.clone(),
+                     be._rod_grad.clone(), wgrad().clone()))
+    for a, b in zip(*outs):
+        if a is not None:
+            assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('ks,Cin,Cout,NHW,act,gamma', [
+    (1, 144, 24, (2, 23, 40), ops.ROD_ACT_RELU6, True),      # project conv (dw BN prologue)
+    (1, 960, 160, (2, 3, 5), ops.ROD_ACT_RELU6, True),       # deep project: split-K path
+    (3, 128, 128, (2, 10, 18), ops.ROD_ACT_LEAKY, False),    # head 3x3 after 1x1 (beta only)
+    (1, 128, 36, (2, 10, 18), ops.ROD_ACT_LEAKY, False),     # head 1x1 -> k*A
+    (3, 36, 36, (2, 10, 18), ops.ROD_ACT_LEAKY, False),      # head 3x3 over k*A (scalar A path)
+    (3, 24, 24, (1, 3, 5), ops.ROD_ACT_LEAKY, False)])
+def test_conv_bn_prologue(dev, dtype, ks, Cin, Cout, NHW, act, gamma):
+    g = torch.Generator().manual_seed(11)
+    w = _param(torch.randn(Cout, ks, ks, Cin, generator=g) / np.sqrt(ks * ks * Cin), dev)
+    b = _param(torch.randn(Cout, generator=g) * 0.1, dev)
+
+    def consumer(x):
+        w._rod_grad.zero_()
+        return ops.conv2d(x, w, b, ks), (lambda: w._rod_grad)
+    _fused_vs_materialised(dev, dtype, NHW + (Cin,), act, gamma, consumer, 12)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('C,stride,H,W', [(96, 2, 45, 81), (144, 1, 23, 40), (32, 1, 30, 44), (36, 1, 9, 11),
+                                          (6, 2, 13, 17), (960, 1, 3, 5)])
+def test_dw_bn_prologue(dev, dtype, C, stride, H, W):
+    g = torch.Generator().manual_seed(13)
+    w = _param(torch.randn(3, 3, C, generator=g) * 0.3, dev)
+
+    def consumer(x):
+        w._rod_grad.zero_()
+        return ops.dw3x3(x, w, stride), (lambda: w._rod_grad)
+    _fused_vs_materialised(dev, dtype, (2, H, W, C), ops.ROD_ACT_RELU6, True, consumer, 14)
