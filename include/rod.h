@@ -68,7 +68,7 @@ int rod_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, v
 /* stat_parts (nullable): BatchNorm partial statistics of y ([nparts][3][C], see
  * rod_bn_finalize) with nparts = rod_dw3x3_fwd_stat_parts(), reduced in the epilogue from
  * the rounded outputs (the depthwise BatchNorm, conv_blocks.py:247 + mobilenet.py:417). */
-int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C);
+int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C, int stride, int dtype);
 int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
                   const float* pro_beta, int pro_act, const float* w, void* y, float* stat_parts, int N, int H,
                   int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);

@@ -217,6 +217,331 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x,
   }
 }
 
+// =====================================================================================
+// LDS neighbour-exchange engine (forward).
+//
+// A block owns a tile of P input columns x CVb 16-byte channel vectors (Cc = CVb*V channels)
+// and a strip of RB output rows.  Thread (p, cvb) loads ONE 16-byte vector per input row
+// (S=2: two, its column pair) — each input byte crosses the memory system once, in full
+// CVb*16-byte pixel segments — applies the BatchNorm prologue to it in registers, and
+// publishes it in an LDS row slot; its left / right taps come back from the neighbouring
+// threads' slots.  Rows stream through a 3-deep (S=2: 4-deep) register prefetch ring, the
+// three output rows in progress are rolling fp32 accumulators, and the LDS slot is double
+// buffered so each input row costs one barrier.  Halo columns (S=1: one each side, S=2: one
+// on the right) load but do not compute.  Accumulation order per output is tap (0,0) ..
+// (2,2), the order of dw3x3_fwd_kernel, so both kernels round identically.
+// =====================================================================================
+struct DwTile {
+  int CVb, P, TWo, cgroups, coltiles, RB, strips;
+};
+
+// Tile plan for a V-wide 16-byte pack: CVb a divisor of C/V (whole 128-byte pixel segments
+// preferred), P columns (<= the columns the map has), RB output rows (>= 8: the prologue / epilogue are per block) so that the grid has
+// ~1024 blocks.  Deterministic in (N, Ho, Wo, C, S, V): the statistics part count depends
+// on it.
+static DwTile dw_tile(int N, int Ho, int Wo, int C, int S, int V) {
+  DwTile t;
+  const int CV = C / V;
+  const int halo = S == 1 ? 2 : 1;
+  double best = -1.0;
+  t.CVb = 1;
+  for (int d = 1; d <= std::min(CV, 32); ++d) {
+    if (CV % d) continue;
+    const int P = std::min(256 / d, Wo + halo);
+    if (P <= halo) continue;
+    const double eff = (double)(P - halo) / P * (double)(P * d) / 256.0;
+    const double seg = (d * 16 >= 128 || d == CV) ? 1.0 : 0.8;
+    const double sc = eff * seg;
+    if (sc > best + 1e-9) {
+      best = sc;
+      t.CVb = d;
+    }
+  }
+  t.P = std::min(256 / t.CVb, Wo + halo);
+  t.TWo = t.P - halo;
+  t.cgroups = CV / t.CVb;
+  t.coltiles = cdiv(Wo, t.TWo);
+  const long base = (long)N * t.coltiles * t.cgroups;
+  const long want = std::max<long>(1, cdivl(1024, base));
+  t.RB = (int)std::min<long>(64, std::max<long>(8, cdivl(Ho, want)));
+  t.strips = cdiv(Ho, t.RB);
+  return t;
+}
+
+// blockIdx -> (x, y, z) after an XCD-aware remap: consecutive tiles (which share halo
+// rows / columns) are placed on the same XCD (the dispatcher deals blocks round-robin).
+__device__ __forceinline__ void xcd_block(int& bx, int& by, int& bz) {
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const int nb = gx * gy * gz;
+  int lin = (blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x;
+  if ((nb & 7) == 0) lin = (lin & 7) * (nb >> 3) + (lin >> 3);
+  bx = lin % gx;
+  lin /= gx;
+  by = lin % gy;
+  bz = lin / gy;
+}
+
+// One 16-byte LDS-DMA (global_load_lds_dwordx4) per lane: lane l of the wave lands at
+// lds_wave + 16*l.  Issued from inline asm so that hipcc's wait-count bookkeeping does not
+// drain it (it would put vmcnt(0) before every LDS read); completion is counted by hand
+// with s_waitcnt vmcnt(N) — loads retire in issue order, so N = DMAs issued later.
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_wave) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"((unsigned)__builtin_amdgcn_readfirstlane((int)lds_wave))
+               : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <typename T, int S, int PACT, bool STATS>
+__global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                           T* __restrict__ y, int H, int W, int C, int pt, int pl,
+                                                           int Ho, int Wo, DwTile tl, float* __restrict__ parts,
+                                                           BnPro pro) {
+  constexpr int V = Vec16<T>::N;
+  // LDS: prefetch ring of D input rows (S=2: column pairs) + the double-buffered exchange
+  // slot; the statistics merge reuses the front after the row loop
+  constexpr int XS = 2 * 256 * 16;            // double-buffered exchange slot
+  constexpr int SS = STATS ? (256 * (2 * V + 1) + 3 * 512) * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
+  T* xs = (T*)smem;
+  const int tid = threadIdx.x;
+  const int CVb = tl.CVb, P = tl.P;
+  const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
+  int bx, strip, n;
+  xcd_block(bx, strip, n);
+  const int cg = bx % tl.cgroups, ct = bx / tl.cgroups;
+  const int c = (cg * CVb + cvb) * V;
+  const int wo0 = ct * tl.TWo;
+  const int ho0 = strip * tl.RB;
+  const int ho1 = ho0 + tl.RB < Ho ? ho0 + tl.RB : Ho;
+  constexpr int HL = S == 1 ? 1 : 0;
+  const int wo = wo0 + p - HL;
+  const bool comp = p >= HL && p <= P - 2 && wo < Wo;
+  // input columns of this thread
+  const int ci0 = S == 1 ? wo0 + p - pl : 2 * (wo0 + p) - pl;
+  const bool cok0 = p < P && ci0 >= 0 && ci0 < W;
+  const bool cok1 = S == 2 && p < P && ci0 + 1 >= 0 && ci0 + 1 < W;
+
+  float wr[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+  DwIn<T, V, PACT> in;
+  in.init(pro, c);
+  const T* xn = x + (long)n * H * W * C + c;
+  T* yn = y + (long)n * Ho * Wo * C + c;
+
+  float piv[V], s1[V], s2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) piv[v] = s1[v] = s2[v] = 0.f;
+
+  auto cvt = [&](const Vec16<T>& r, bool ok, float (&o)[V]) {
+    PackV<T, V> pk;
+    pk.v = r.v;
+    in.cvt(pk, ok, o);
+    if constexpr (PACT < 0) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) o[v] = ok ? o[v] : 0.f;
+    }
+  };
+  auto publish = [&](const float (&o)[V], int buf) {
+    Vec16<T> st;
+#pragma unroll
+    for (int v = 0; v < V; ++v) st.set(v, o[v]);
+    st.store(xs + (buf * 256 + tid) * V);
+  };
+  auto emit = [&](const float (&a)[V], int ho, bool first) {
+    Vec16<T> o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) o.set(v, a[v]);
+    o.store(yn + ((long)ho * Wo + wo) * C);
+    if constexpr (STATS) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float ov = o.get(v);
+        if (first) piv[v] = ov;
+        const float d = ov - piv[v];
+        s1[v] += d;
+        s2[v] = fmaf(d, d, s2[v]);
+      }
+    }
+  };
+
+  if constexpr (S == 1) {
+    const int hi0 = ho0 - pt;
+    const int nin = ho1 - ho0 + 2;
+    Vec16<T> ring[3];
+    bool rok[3];
+    auto issue = [&](int k, int q) {
+      const int hi = hi0 + q;
+      rok[k] = cok0 && q < nin && hi >= 0 && hi < H;
+      if (rok[k]) ring[k].load(xn + ((long)hi * W + ci0) * C);
+    };
+    issue(0, 0);
+    issue(1, 1);
+    issue(2, 2);
+    float acc[3][V];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[a][v] = 0.f;
+    for (int q0 = 0; q0 < nin; q0 += 3) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int q = q0 + k;
+        const int buf = q & 1;
+        float cen[V];
+        cvt(ring[k], rok[k], cen);
+        issue(k, q + 3);
+        publish(cen, buf);
+        __syncthreads();
+        if (comp) {
+          Vec16<T> L, R;
+          L.load(xs + (buf * 256 + tid - CVb) * V);
+          R.load(xs + (buf * 256 + tid + CVb) * V);
+          // row q feeds output m = q - i with weight row i: slot (k - i) mod 3
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int sl = (k - i + 3) % 3;
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+              float a = acc[sl][v];
+              a = fmaf(L.get(v), wr[i * 3][v], a);
+              a = fmaf(cen[v], wr[i * 3 + 1][v], a);
+              a = fmaf(R.get(v), wr[i * 3 + 2][v], a);
+              acc[sl][v] = a;
+            }
+          }
+          const int sd = (k + 1) % 3;  // output m = q - 2 is complete
+          const int m = q - 2;
+          if (m >= 0 && ho0 + m < ho1) emit(acc[sd], ho0 + m, m == 0);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
+        }
+      }
+    }
+  } else {
+    const int hi0 = 2 * ho0 - pt;
+    const int nin = 2 * (ho1 - ho0) + 1;
+    Vec16<T> ring[4][2];
+    bool rok[4][2];
+    auto issue = [&](int k, int q) {
+      const int hi = hi0 + q;
+      const bool rowok = q < nin && hi >= 0 && hi < H;
+      rok[k][0] = rowok && cok0;
+      rok[k][1] = rowok && cok1;
+      if (rok[k][0]) ring[k][0].load(xn + ((long)hi * W + ci0) * C);
+      if (rok[k][1]) ring[k][1].load(xn + ((long)hi * W + ci0 + 1) * C);
+    };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) issue(k, k);
+    float acc[2][V];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[a][v] = 0.f;
+    for (int q0 = 0; q0 < nin; q0 += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = q0 + k;
+        const int buf = q & 1;
+        float c0[V], c1[V];
+        cvt(ring[k][0], rok[k][0], c0);
+        cvt(ring[k][1], rok[k][1], c1);
+        issue(k, q + 4);
+        publish(c0, buf);
+        __syncthreads();
+        if (comp) {
+          Vec16<T> R;
+          R.load(xs + (buf * 256 + tid + CVb) * V);
+          // q = q0 + k, q0 % 4 == 0: k even -> weight row 0 into output q/2 (slot k/2) and
+          // row 2 into output q/2 - 1 (slot 1 - k/2, then complete); k odd -> row 1 into
+          // output (q-1)/2 (slot k/2)
+          auto addrow = [&](int i, int sl) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+              float a = acc[sl][v];
+              a = fmaf(c0[v], wr[i * 3][v], a);
+              a = fmaf(c1[v], wr[i * 3 + 1][v], a);
+              a = fmaf(R.get(v), wr[i * 3 + 2][v], a);
+              acc[sl][v] = a;
+            }
+          };
+          if ((k & 1) == 0) {
+            const int sn = k >> 1, sd = 1 - (k >> 1);
+            addrow(2, sd);
+            const int m = (q >> 1) - 1;
+            if (m >= 0 && ho0 + m < ho1) emit(acc[sd], ho0 + m, m == 0);
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
+            addrow(0, sn);
+          } else {
+            addrow(1, k >> 1);
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (STATS) {
+    // per thread (n, mean, M2) of its rows; per channel, Chan merge over the computing
+    // columns in column order -> part (n*strips + strip)*coltiles + ct, channels of cgroup cg
+    __syncthreads();
+    float* sm = (float*)smem;
+    float* sq = sm + 256 * V;
+    float* sn = sq + 256 * V;
+    const int nr = comp ? ho1 - ho0 : 0;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float inv = nr > 0 ? 1.f / (float)nr : 0.f;
+      const float dm = s1[v] * inv;
+      sm[tid * V + v] = piv[v] + dm;
+      sq[tid * V + v] = nr > 0 ? fmaxf(s2[v] - s1[v] * dm, 0.f) : 0.f;
+    }
+    sn[tid] = (float)nr;
+    __syncthreads();
+    // two levels (runs of 8 columns, then the runs, each in column order) so the serial
+    // merge depth is ~8 + P/8 rather than P
+    const int Cc = CVb * V;
+    const int nrun = (P + 7) / 8;
+    float* l1n = sn + 256;
+    float* l1m = l1n + 512;
+    float* l1q = l1m + 512;
+    for (int e = tid; e < Cc * nrun; e += 256) {
+      const int ch = e % Cc, run = e / Cc;
+      const int cve = ch / V, v = ch - cve * V;
+      float pn = 0.f, pm = 0.f, pq = 0.f;
+      for (int pp = run * 8; pp < run * 8 + 8 && pp < P; ++pp) {
+        const int t2 = pp * CVb + cve;
+        chan_merge(pn, pm, pq, sn[t2], sm[t2 * V + v], sq[t2 * V + v]);
+      }
+      l1n[e] = pn;
+      l1m[e] = pm;
+      l1q[e] = pq;
+    }
+    __syncthreads();
+    const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+    for (int ch = tid; ch < Cc; ch += 256) {
+      float pn = 0.f, pm = 0.f, pq = 0.f;
+      for (int run = 0; run < nrun; ++run) chan_merge(pn, pm, pq, l1n[run * Cc + ch], l1m[run * Cc + ch], l1q[run * Cc + ch]);
+      store_stat_part(parts, C, part, cg * Cc + ch, pn, pm, pq);
+    }
+  }
+}
+
 // dx[n,h,w,c] = sum_{i,j} dy[n,(h+pt-i)/S,(w+pl-j)/S,c] * w[i,j,c] over exact divisions.
 // S=1: the three dy rows h+pt-i roll down in registers; S=2: direct loads (each dx pixel
 // sees 1, 2 or 4 dy pixels).
@@ -567,6 +892,40 @@ static void dw_fwd_launch(const void* x, const BnPro* pro, const float* w, void*
   }
 #undef DWF
 }
+// LDS-exchange forward: needs 16-byte packs (C % V == 0, 16-byte aligned x and y).
+template <typename T>
+static bool dw_lx_ok(const void* x, const void* y, int C) {
+  static const bool legacy = getenv("ROD_DW_LEGACY") != nullptr;  // A/B timing switch
+  return !legacy && C % Vec16<T>::N == 0 && ((((uintptr_t)x) | ((uintptr_t)y)) & 15) == 0;
+}
+static long dw_lx_parts(int N, int Ho, int Wo, int C, int S, int V) {
+  const DwTile t = dw_tile(N, Ho, Wo, C, S, V);
+  return (long)N * t.strips * t.coltiles;
+}
+template <typename T>
+static long dw_fwd_lx_launch(const void* x, const BnPro* pro, const float* w, void* y, float* parts, int N, int H,
+                             int W, int C, int S, int pt, int pl, int Ho, int Wo, hipStream_t s) {
+  const DwTile t = dw_tile(N, Ho, Wo, C, S, Vec16<T>::N);
+  const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
+  const BnPro pv = pro ? *pro : BnPro{};
+  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
+#define DWL(S_, PA, ST)                                                                                       \
+  hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, S_, PA, ST>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, \
+                     pt, pl, Ho, Wo, t, parts, pv)
+#define DWL_PA(S_, ST)                    \
+  if (pa == ROD_ACT_RELU6) DWL(S_, ROD_ACT_RELU6, ST); \
+  else if (pa == 3) DWL(S_, 3, ST);       \
+  else DWL(S_, -1, ST)
+  if (S == 1) {
+    if (parts) { DWL_PA(1, true); } else { DWL_PA(1, false); }
+  } else {
+    if (parts) { DWL_PA(2, true); } else { DWL_PA(2, false); }
+  }
+#undef DWL_PA
+#undef DWL
+  return (long)N * t.strips * t.coltiles;
+}
+
 template <typename T, int S, int V>
 static void dw_bwd_data_launch(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int pt, int pl,
                                int Ho, int Wo, hipStream_t s) {
@@ -617,13 +976,14 @@ using namespace rod;
 
 extern "C" {
 
-int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C) {
-  // the pack the bf16 / f32 launch will use for aligned pointers (the caller allocates the
-  // slab for this; a smaller pack falls back to the separate statistics pass)
-  const int V = C % 8 == 0 ? 8 : (C % 4 == 0 ? 4 : 1);
+int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C, int stride, int dtype) {
+  // exactly the parts the launch for 16-byte-aligned x / y writes: the LDS-exchange kernel
+  // when C fills 16-byte packs, else the register-strip kernel's grid
+  const int V16 = dtype == ROD_F32 ? 4 : 8;
+  if (C % V16 == 0) return (int)dw_lx_parts(N, Ho, Wo, C, stride == 2 ? 2 : 1, V16);
+  const int V = dtype == ROD_F32 ? (C % 4 == 0 ? 4 : 1) : (C % 4 == 0 ? 4 : 1);
   const dim3 g = dw_fwd_grid(N, Ho, Wo, C, V);
-  const dim3 g4 = dw_fwd_grid(N, Ho, Wo, C, C % 4 == 0 ? 4 : 1);
-  return (int)std::max(g.x * g.y * g.z, g4.x * g4.y * g4.z);
+  return (int)(g.x * g.y * g.z);
 }
 
 int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
@@ -634,18 +994,22 @@ int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, c
   hipStream_t s = ROD_STREAM(stream);
   const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
   const BnPro* pp = pro_mean ? &pro : nullptr;
-  const int nparts = rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C);
+  const int nparts = rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C, stride, dtype);
   auto run = [&](auto tag) {
     typedef decltype(tag) T;
+    if (dw_lx_ok<T>(x, y, C)) {
+      dw_fwd_lx_launch<T>(x, pp, w, y, stat_parts, N, H, W, C, stride, pad_t, pad_l, Ho, Wo, s);
+      return;
+    }
     const int pk = dw_pack<T>(x, y, C, 4);
     const int V = pk == 8 ? (sizeof(T) == 2 ? 8 : 4) : pk;
     const dim3 g = dw_fwd_grid(N, Ho, Wo, C, V);
-    // the fused statistics write g.x*g.y*g.z parts; pad the rest of the slab with empty parts
-    float* fused = stat_parts;
-    DW_SELECT(dw_fwd_launch, T, pk, x, pp, w, y, fused, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
-    const long used = (long)g.x * g.y * g.z;
-    if (stat_parts && used < nparts)
-      (void)hipMemsetAsync(stat_parts + used * 3 * C, 0, (size_t)(nparts - used) * 3 * C * sizeof(float), s);
+    // the fused statistics write one part per block; when that is not the count the caller
+    // sized the slab for (misaligned pointers, legacy switch), a separate pass writes them
+    const bool fuse = stat_parts && (long)g.x * g.y * g.z == nparts;
+    DW_SELECT(dw_fwd_launch, T, pk, x, pp, w, y, fuse ? stat_parts : nullptr, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+    if (stat_parts && !fuse)
+      ::rod::stat_parts(sizeof(T) == 4 ? ROD_F32 : ROD_BF16, y, (long)N * Ho * Wo, C, C, stat_parts, nparts, s);
   };
   if (dtype == ROD_F32) run(float{});
   else if (dtype == ROD_BF16) run(bf16_t{});

@@ -143,7 +143,7 @@ class _DW3x3(torch.autograd.Function):
         y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
         parts = None
         if want_stats:  # BatchNorm partial statistics from the epilogue
-            nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C)
+            nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C, stride, dtcode(x))
             parts = torch.empty((nparts, 3, C), dtype=torch.float32, device=x.device)
         pro = (mean, rstd, gamma, beta, act) if mean is not None else None
         _abi.call("rod_dw3x3_fwd", x, *_pro_args(pro), w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x),
