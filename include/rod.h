@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 3
+#define ROD_ABI_VERSION 4
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -72,9 +72,17 @@ int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C, int stride, int dtype
 int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
                   const float* pro_beta, int pro_act, const float* w, void* y, float* stat_parts, int N, int H,
                   int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
-/* dx = d y / d x  (DepthwiseConv2dNativeBackpropInput) */
-int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, int W, int C,
-                       int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
+/* dx = d y / d x  (DepthwiseConv2dNativeBackpropInput).
+ * gred_* (nullable, ABI 4): when x was read through a BatchNorm-apply prologue, dx is the
+ * gradient of that BatchNorm's output and the kernel also reduces its backward partial
+ * sums in the epilogue: gred_y = the pre-BatchNorm tensor (x's storage, [N,H,W,C]),
+ * gred_mean/rstd/gamma/beta/act its BatchNorm, gred_parts [nparts][2][C] with
+ * nparts = rod_dw3x3_bwd_data_gred_parts(); see rod_bn_bwd_finalize. */
+int rod_dw3x3_bwd_data_gred_parts(int N, int H, int W, int C, int stride, int dtype);
+int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, const void* gred_y, const float* gred_mean,
+                       const float* gred_rstd, const float* gred_gamma, const float* gred_beta, int gred_act,
+                       float* gred_parts, int N, int H, int W, int C, int stride, int pad_t, int pad_l,
+                       int Ho, int Wo, int dtype, void* stream);
 /* dw[3][3][C] (fp32, overwritten) (DepthwiseConv2dNativeBackpropFilter).
  * workspace: rod_dw3x3_bwd_filter_workspace() bytes. */
 size_t rod_dw3x3_bwd_filter_workspace(int N, int Ho, int Wo, int C);
@@ -121,6 +129,20 @@ int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rs
                const float* gamma, const float* beta, void* dx, float* dgamma, float* dbeta,
                void* workspace, long M, int C, int lddy, int ldx, int lddx, int act,
                int dtype, void* stream);
+/* The same backward split at its reduction (ABI 4), for a BatchNorm applied in a
+ * consumer's load prologue: the consumer's backward-data kernel (rod_conv_fwd /
+ * rod_dw3x3_bwd_data "gred_*" arguments) writes dz = d/d(act output) and, from the same
+ * registers plus the pre-BatchNorm y, the partial sums parts [nparts][2][C] =
+ * (sum g, sum g*yhat), g = dz*act'(y*scale + offset), yhat = (y - mean)*rstd (the
+ * reduction of FusedBatchNormGrad).  rod_bn_bwd_finalize merges them (f64, fixed order)
+ * into dbeta, dgamma (either may be NULL) and coef[3][C] = (rstd*gamma, mean g,
+ * mean g*yhat); rod_bn_bwd_apply writes dy = coef0*(g - coef1 - yhat*coef2) [M, C] dense,
+ * bit for bit the rod_bn_bwd result for the same sums. */
+int rod_bn_bwd_finalize(const float* parts, int nparts, long M, int C, const float* rstd,
+                        const float* gamma, float* dgamma, float* dbeta, float* coef, void* stream);
+int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, const float* coef, void* dy, long M, int C,
+                     int act, int dtype, void* stream);
 
 /* -------------------------------------- dense conv as implicit GEMM (A2 A3 A5)
  * y[m, co] = sum_k A[m, k] * wt[co, k] (+ bias[co]), fp32 accumulation,
@@ -139,16 +161,27 @@ int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rs
  * the rounded outputs (the BatchNorm that follows every conv, mobilenet.py:417,
  * catch_net.py:302) so no separate statistics pass re-reads y. */
 size_t rod_conv_fwd_workspace(int N, int H, int W, int Cin, int Cout, int ksize);
+/* gred_* (nullable, ABI 4): used as a backward-data (x = dy, wt mode 1) whose input went
+ * through a BatchNorm-apply prologue in the forward, the output is that BatchNorm's dz and
+ * the epilogue also writes its backward partial sums [ceil(M/128)][2][Cout] (gred_y = the
+ * pre-BatchNorm tensor [M, Cout], dense; see rod_bn_bwd_finalize). */
 int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
                  const float* pro_beta, int pro_act, const void* wt, const float* bias, void* y,
-                 void* workspace, float* stat_parts, int N, int H, int W, int Cin, int Cout, int ksize,
-                 int ldx, int ldy, int dtype, void* stream);
+                 void* workspace, float* stat_parts, const void* gred_y, const float* gred_mean,
+                 const float* gred_rstd, const float* gred_gamma, const float* gred_beta, int gred_act,
+                 float* gred_parts, int N, int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy,
+                 int dtype, void* stream);
 /* Weight layouts derived from the fp32 master weight w[Cout][ksize][ksize][Cin]:
  *   mode 0: forward operand      wt[co][i][j][ci]           (cast to dtype)
  *   mode 1: backward-data operand wt[ci][2-i][2-j][co]       (transposed, flipped)
  * so dx = rod_conv_fwd(dy, wt_mode1) (Conv2DBackpropInput, stride 1 SAME). */
 int rod_conv_weight_prep(const float* w, void* wt, int Cout, int Cin, int ksize, int mode,
                          int dtype, void* stream);
+/* Every weight of a step in one launch: table is a DEVICE array of n entries
+ *   struct { const float* w; void* wt; long start; int Cout, Cin, ksize, mode; }  (40 bytes)
+ * each as rod_conv_weight_prep(w, wt, Cout, Cin, ksize, mode); start = the sum of
+ * Cout*ksize*ksize*Cin over the entries before it (ascending), total = the sum over all. */
+int rod_conv_weight_prep_batch(const void* table, int n, long total, int dtype, void* stream);
 /* dw[co][k] = sum_m dy[m, co] * A[m, k]  (Conv2DBackpropFilter), fp32 out,
  * db[co] = sum_m dy[m, co] when db != NULL.  workspace: see query. */
 size_t rod_conv_wgrad_workspace(int N, int H, int W, int Cin, int Cout, int ksize);

@@ -175,47 +175,68 @@ struct MergePlan {
 };
 static MergePlan merge_plan(int C) {
   MergePlan p;
-  p.CB = C < 256 ? C : 256;
+  p.CB = C < 64 ? C : 64;   // 64 channels x 4+ part lanes per block
   p.PL = 256 / p.CB;
-  p.slice = 32 * p.PL;
+  p.slice = 64 * p.PL;      // <= 64 parts per lane per level
   return p;
 }
 
+// Parts are merged in shifted-sum form (no divisions in the loop): with a pivot k per
+// channel (the mean of the slice's first non-empty part), every part contributes
+// n, S1 = n*(mean-k), S2 = M2 + n*(mean-k)^2 in f64; lanes and then the block's part lanes
+// are added in a fixed order, and the slice's (n, mean, M2) = (n, k + S1/n, S2 - S1^2/n).
 __global__ void __launch_bounds__(256) bn_parts_merge_kernel(const float* __restrict__ parts, int nparts, int C, int CB,
                                                              int slice, float* __restrict__ out, long M, float eps,
                                                              float decay, float* __restrict__ mean,
                                                              float* __restrict__ rstd, float* __restrict__ mmean,
                                                              float* __restrict__ mvar) {
-  __shared__ double sn[256], sm[256], sq[256];
+  __shared__ double sn[256], s1[256], s2[256];
+  __shared__ float piv[256];
   const int tid = threadIdx.x;
   const int PL = 256 / CB;
   const int cl = tid % CB, pl = tid / CB;
   const int c = blockIdx.y * CB + cl;
   const bool ok = pl < PL && c < C;
-  double n = 0.0, mu = 0.0, m2 = 0.0;
-  if (ok) {
-    // all (<= 32) parts of this thread are loaded before the first merge: one latency round
-    const int b0 = blockIdx.x * slice + pl;
-    const int b1 = blockIdx.x * slice + slice < nparts ? blockIdx.x * slice + slice : nparts;
-    float vn[32], vm[32], vq[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int bb = b0 + u * PL;
-      const bool in = bb < b1;
-      const float* p = parts + (long)(in ? bb : 0) * 3 * C + c;
-      vn[u] = in ? p[0] : 0.f;
-      vm[u] = in ? p[C] : 0.f;
-      vq[u] = in ? p[2 * C] : 0.f;
+  const int b0 = blockIdx.x * slice;
+  const int b1 = b0 + slice < nparts ? b0 + slice : nparts;
+  if (pl == 0 && c < C) {  // pivot: mean of the first non-empty part of the slice
+    float k = 0.f;
+    for (int b = b0; b < b1; ++b) {
+      if (parts[(long)b * 3 * C + c] != 0.f) {
+        k = parts[(long)b * 3 * C + C + c];
+        break;
+      }
     }
-#pragma unroll
-    for (int u = 0; u < 32; ++u) chan_merge_d(n, mu, m2, (double)vn[u], (double)vm[u], (double)vq[u]);
+    piv[cl] = k;
+  }
+  __syncthreads();
+  double n = 0.0, a1 = 0.0, a2 = 0.0;
+  if (ok) {
+    const double k = (double)piv[cl];
+#pragma unroll 4
+    for (int b = b0 + pl; b < b1; b += PL) {
+      const float* p = parts + (long)b * 3 * C + c;
+      const double nb = (double)p[0];
+      const double d = (double)p[C] - k;
+      const double q = nb * d;
+      n += nb;
+      a1 += q;
+      a2 += (double)p[2 * C] + q * d;
+    }
   }
   sn[tid] = n;
-  sm[tid] = mu;
-  sq[tid] = m2;
+  s1[tid] = a1;
+  s2[tid] = a2;
   __syncthreads();
   if (ok && pl == 0) {
-    for (int l = 1; l < PL; ++l) chan_merge_d(n, mu, m2, sn[l * CB + cl], sm[l * CB + cl], sq[l * CB + cl]);
+    for (int l = 1; l < PL; ++l) {
+      n += sn[l * CB + cl];
+      a1 += s1[l * CB + cl];
+      a2 += s2[l * CB + cl];
+    }
+    const double k = (double)piv[cl];
+    const double mu = n > 0.0 ? k + a1 / n : 0.0;
+    const double m2 = n > 0.0 ? fmax(a2 - a1 * a1 / n, 0.0) : 0.0;
     if (gridDim.x > 1) {
       store_stat_part(out, C, blockIdx.x, c, (float)n, (float)mu, (float)m2);
       return;
@@ -298,7 +319,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------- backward
-template <typename T, bool VEC>
+template <typename T, bool VEC, bool PM = false>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
@@ -369,9 +390,14 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
       a += red[(l * CVb + cb) * V + v];
       b += red[(256 + l * CVb + cb) * V + v];
     }
-    const long nblk = gridDim.x;
-    slab[(long)(cg * V + v) * nblk + blockIdx.x] = a;
-    slab[((long)C + cg * V + v) * nblk + blockIdx.x] = b;
+    if constexpr (PM) {  // part-major [nparts][2][C] (rod_bn_bwd_finalize)
+      slab[(long)blockIdx.x * 2 * C + cg * V + v] = a;
+      slab[(long)blockIdx.x * 2 * C + C + cg * V + v] = b;
+    } else {
+      const long nblk = gridDim.x;
+      slab[(long)(cg * V + v) * nblk + blockIdx.x] = a;
+      slab[((long)C + cg * V + v) * nblk + blockIdx.x] = b;
+    }
   }
 }
 
@@ -537,11 +563,76 @@ static void bwd_launch(bool vec, const void* dy, const void* x, const float* mea
                        mean, rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
 }
 
+// coef[3][C] from the merged sums held in coef[C..3C) (sum g, sum g*yhat): dbeta, dgamma and
+// (rstd*gamma, mean g, mean g*yhat) in place — the coefficients bn_bwd_apply_kernel uses
+__global__ void bn_bwd_coef_kernel(long M, int C, const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                   float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sg = coef[C + c], sgx = coef[2 * C + c];
+  if (dbeta) dbeta[c] = sg;
+  if (dgamma) dgamma[c] = sgx;
+  coef[c] = gamma ? rstd[c] * gamma[c] : rstd[c];
+  coef[C + c] = (float)((double)sg / (double)M);
+  coef[2 * C + c] = (float)((double)sgx / (double)M);
+}
+
+// Backward partial sums [nparts][2][C] of g = dz*act'(u), g*yhat over exactly nparts row
+// chunks: the fallback for producers of dz that cannot fuse the reduction.
+template <typename T>
+static void gred_pass_typed(const void* dz, const void* y, const BnPro& p, long M, int C, float* parts, int nparts,
+                            hipStream_t s) {
+  const bool vec = vec_ok<T>(C, {{dz, C}, {y, C}});
+  RedPlan pl = red_plan<T>(M, C, vec);
+  pl.chunk = cdivl(M, nparts);
+  dim3 grid(nparts, pl.cgroups);
+  size_t lds = 2 * 256 * pl.V * sizeof(float);
+  if (vec)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, true>), grid, dim3(256), lds, s, (const T*)dz, (const T*)y,
+                       p.mean, p.rstd, p.gamma, p.beta, M, C, C, C, p.act, pl.CVb, pl.lanes, pl.chunk, parts);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false, true>), grid, dim3(256), lds, s, (const T*)dz, (const T*)y,
+                       p.mean, p.rstd, p.gamma, p.beta, M, C, C, C, p.act, pl.CVb, pl.lanes, pl.chunk, parts);
+}
+void gred_parts(int dtype, const void* dz, const void* y, const BnPro& p, long M, int C, float* parts, int nparts,
+                hipStream_t s) {
+  if (dtype == ROD_F32) gred_pass_typed<float>(dz, y, p, M, C, parts, nparts, s);
+  else gred_pass_typed<bf16_t>(dz, y, p, M, C, parts, nparts, s);
+}
+
 }  // namespace rod
 
 using namespace rod;
 
 extern "C" {
+
+int rod_bn_bwd_finalize(const float* parts, int nparts, long M, int C, const float* rstd, const float* gamma,
+                        float* dgamma, float* dbeta, float* coef, void* stream) {
+  ROD_CHECK_ARG(parts != nullptr && nparts > 0 && M > 0 && C > 0 && coef != nullptr && rstd != nullptr,
+                "rod_bn_bwd_finalize: bad arguments");
+  hipStream_t s = ROD_STREAM(stream);
+  slab_sum(parts, coef + C, nparts, 2L * C, s);  // f64, fixed order
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, M, C, rstd, gamma, dgamma, dbeta, coef);
+  return check_launch("rod_bn_bwd_finalize");
+}
+
+int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                     const float* beta, const float* coef, void* dy, long M, int C, int act, int dtype, void* stream) {
+  ROD_CHECK_ARG(M > 0 && C > 0 && coef != nullptr, "rod_bn_bwd_apply: bad arguments");
+  hipStream_t s = ROD_STREAM(stream);
+  ROD_DISPATCH_DTYPE(dtype, {
+    const bool vec = vec_ok<T>(C, {{dz, C}, {y, C}, {dy, C}});
+    const int V = vec ? Vec16<T>::N : 1;
+    const int blocks = const_channel_blocks(C / V, M * (C / V));
+    if (vec)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dz, (const T*)y,
+                         mean, rstd, gamma, beta, coef, (T*)dy, M, C, C, C, C, act);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false>), dim3(blocks), dim3(256), 0, s, (const T*)dz, (const T*)y,
+                         mean, rstd, gamma, beta, coef, (T*)dy, M, C, C, C, C, act);
+  });
+  return check_launch("rod_bn_bwd_apply");
+}
 
 size_t rod_bn_stats_workspace(long M, int C) {
   const int nbx = max_nbx(M, C);

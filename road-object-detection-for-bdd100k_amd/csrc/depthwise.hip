@@ -217,6 +217,50 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x,
   }
 }
 
+// GRED (backward-data kernels): BatchNorm-backward partial sums of the rounded dx against the
+// pre-BatchNorm y of the layer below (rod_common.h gred_acc), per thread, then per block into
+// part (z*gy + y)*gx + x of [nparts][2][C].
+template <int V>
+struct DwGred {
+  float sc[V], sh[V], mu[V], rs[V], sg[V], sgx[V];
+  __device__ __forceinline__ void init(const BnGred& g, int c, bool ok) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      sg[v] = sgx[v] = 0.f;
+      sc[v] = sh[v] = mu[v] = rs[v] = 0.f;
+      if (ok) gred_coef(g.p, c + v, sc[v], sh[v], mu[v], rs[v]);
+    }
+  }
+  template <typename T>
+  __device__ __forceinline__ void acc(const PackV<T, V>& dz, const T* yp, int act) {
+    PackV<T, V> yv;
+    yv.load(yp);
+#pragma unroll
+    for (int v = 0; v < V; ++v) gred_acc(dz.get(v), yv.get(v), sc[v], sh[v], mu[v], rs[v], act, sg[v], sgx[v]);
+  }
+  // block sums: threads holding channel vector cve sit at tl = (cve - tb) mod CV + k*CV
+  __device__ __forceinline__ void flush(float* red, int C, int CV, float* parts) {
+    const int tid = threadIdx.x;
+    const long tb = (long)blockIdx.x * 256;
+    const int t0mod = (int)(tb % CV);
+    const long part = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) red[tid * V + v] = q == 0 ? sg[v] : sgx[v];
+      __syncthreads();
+      for (int e = tid; e < C; e += 256) {
+        const int cve = e / V, v = e - cve * V;
+        int tl = cve - t0mod;
+        if (tl < 0) tl += CV;
+        float a = 0.f;
+        for (; tl < 256; tl += CV) a += red[tl * V + v];
+        parts[part * 2 * C + q * C + e] = a;
+      }
+      __syncthreads();
+    }
+  }
+};
+
 // =====================================================================================
 // LDS neighbour-exchange engine (forward).
 //
@@ -304,16 +348,21 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <typename T, int S, int PACT, bool STATS>
+// FLIP (S=1 only): the correlation with the flipped taps w[2-i][2-j] — the stride-1
+// backward-data (DepthwiseConv2dNativeBackpropInput) is this kernel on dy with pads
+// (2-pt, 2-pl).  GRED: the BatchNorm-backward partial sums of the rounded outputs against the
+// pre-BatchNorm y of the layer below (rod_common.h), y prefetched two rows ahead.
+template <typename T, int S, int PACT, bool STATS, bool FLIP = false, bool GRED = false>
 __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                            T* __restrict__ y, int H, int W, int C, int pt, int pl,
                                                            int Ho, int Wo, DwTile tl, float* __restrict__ parts,
-                                                           BnPro pro) {
+                                                           BnPro pro, BnGred gr = BnGred{}) {
+  static_assert(S == 1 || !(FLIP || GRED), "the backward-data form is stride 1");
   constexpr int V = Vec16<T>::N;
   // LDS: prefetch ring of D input rows (S=2: column pairs) + the double-buffered exchange
   // slot; the statistics merge reuses the front after the row loop
   constexpr int XS = 2 * 256 * 16;            // double-buffered exchange slot
-  constexpr int SS = STATS ? (256 * (2 * V + 1) + 3 * 512) * 4 : 0;
+  constexpr int SS = STATS ? (256 * (2 * V + 1) + 3 * 512) * 4 : (GRED ? 256 * 2 * V * 4 : 0);
   __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
   T* xs = (T*)smem;
   const int tid = threadIdx.x;
@@ -338,7 +387,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
 #pragma unroll
   for (int k = 0; k < 9; ++k)
 #pragma unroll
-    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+    for (int v = 0; v < V; ++v) wr[k][v] = w[(FLIP ? 8 - k : k) * C + c + v];
   DwIn<T, V, PACT> in;
   in.init(pro, c);
   const T* xn = x + (long)n * H * W * C + c;
@@ -347,6 +396,10 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
   float piv[V], s1[V], s2[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) piv[v] = s1[v] = s2[v] = 0.f;
+  DwGred<GRED ? V : 1> gd;
+  if constexpr (GRED) gd.init(gr, c, comp);
+  const T* gyn = GRED ? (const T*)gr.y + (long)n * Ho * Wo * C + c : nullptr;
+  PackV<T, V> gring[GRED ? 3 : 1];
 
   auto cvt = [&](const Vec16<T>& r, bool ok, float (&o)[V]) {
     PackV<T, V> pk;
@@ -379,6 +432,17 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
       }
     }
   };
+  auto emit_g = [&](const float (&a)[V], int ho, int gslot) {  // GRED: y of row ho is in gring[gslot]
+    PackV<T, V> o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) o.set(v, a[v]);
+    o.store(yn + ((long)ho * Wo + wo) * C);
+    if constexpr (GRED) {
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        gred_acc(o.get(v), gring[gslot].get(v), gd.sc[v], gd.sh[v], gd.mu[v], gd.rs[v], gr.p.act, gd.sg[v], gd.sgx[v]);
+    }
+  };
 
   if constexpr (S == 1) {
     const int hi0 = ho0 - pt;
@@ -393,6 +457,12 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
     issue(0, 0);
     issue(1, 1);
     issue(2, 2);
+    // GRED: y of output row m is loaded at input row q = m into slot m % 3 (two rows ahead)
+    auto gissue = [&](int k, int m) {
+      if constexpr (GRED) {
+        if (comp && ho0 + m < ho1) gring[k].load(gyn + ((long)(ho0 + m) * Wo + wo) * C);
+      }
+    };
     float acc[3][V];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
@@ -406,6 +476,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
         float cen[V];
         cvt(ring[k], rok[k], cen);
         issue(k, q + 3);
+        gissue(k, q);
         publish(cen, buf);
         __syncthreads();
         if (comp) {
@@ -427,7 +498,11 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
           }
           const int sd = (k + 1) % 3;  // output m = q - 2 is complete
           const int m = q - 2;
-          if (m >= 0 && ho0 + m < ho1) emit(acc[sd], ho0 + m, m == 0);
+          if constexpr (GRED) {
+            if (m >= 0 && ho0 + m < ho1) emit_g(acc[sd], ho0 + m, sd);
+          } else {
+            if (m >= 0 && ho0 + m < ho1) emit(acc[sd], ho0 + m, m == 0);
+          }
 #pragma unroll
           for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
         }
@@ -496,6 +571,31 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
     }
   }
 
+  if constexpr (GRED) {
+    // per channel: sum over the computing columns in column order -> part
+    // (n*strips + strip)*coltiles + ct, channels of cgroup cg
+    __syncthreads();
+    float* ga = (float*)smem;
+    float* gb = ga + 256 * V;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      ga[tid * V + v] = gd.sg[v];
+      gb[tid * V + v] = gd.sgx[v];
+    }
+    __syncthreads();
+    const int Cc = CVb * V;
+    const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+    for (int e = tid; e < Cc; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      float a = 0.f, b = 0.f;
+      for (int pp = HL; pp <= P - 2; ++pp) {
+        a += ga[(pp * CVb + cve) * V + v];
+        b += gb[(pp * CVb + cve) * V + v];
+      }
+      gr.parts[part * 2 * C + cg * Cc + e] = a;
+      gr.parts[part * 2 * C + C + cg * Cc + e] = b;
+    }
+  }
   if constexpr (STATS) {
     // per thread (n, mean, M2) of its rows; per channel, Chan merge over the computing
     // columns in column order -> part (n*strips + strip)*coltiles + ct, channels of cgroup cg
@@ -545,15 +645,20 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
 // dx[n,h,w,c] = sum_{i,j} dy[n,(h+pt-i)/S,(w+pl-j)/S,c] * w[i,j,c] over exact divisions.
 // S=1: the three dy rows h+pt-i roll down in registers; S=2: direct loads (each dx pixel
 // sees 1, 2 or 4 dy pixels).
-template <typename T, int S, int V>
+template <typename T, int S, int V, bool GRED = false>
 __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict__ dy, const float* __restrict__ w,
                                                              T* __restrict__ dx, int H, int W, int C, int pt,
-                                                             int pl, int Ho, int Wo) {
+                                                             int pl, int Ho, int Wo, BnGred gr = BnGred{}) {
   const int CV = C / V;
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cv = (int)(t % CV);
   const int wc = (int)(t / CV);
-  if (wc >= W) return;
+  __shared__ __attribute__((aligned(16))) float gred_red[GRED ? 256 * V : 1];
+  DwGred<GRED ? V : 1> gd;
+  if constexpr (GRED) gd.init(gr, cv * V, wc < W);
+  const T* gy = GRED ? (const T*)gr.y + (long)blockIdx.z * H * W * C + cv * V : nullptr;
+  // (no early return: the GRED flush barriers must be reached by every lane of every wave)
+  if (wc < W) {
   const int h0 = blockIdx.y * DW_RB;
   const int h1 = h0 + DW_RB < H ? h0 + DW_RB : H;
   const int n = blockIdx.z;
@@ -594,6 +699,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
       o.store(xn + ((long)h * W + wc) * C);
+      if constexpr (GRED) gd.template acc<T>(o, gy + ((long)h * W + wc) * C, gr.p.act);
       if (h + 1 < h1) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -631,8 +737,11 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
       o.store(xn + ((long)h * W + wc) * C);
+      if constexpr (GRED) gd.template acc<T>(o, gy + ((long)h * W + wc) * C, gr.p.act);
     }
   }
+  }  // wc < W
+  if constexpr (GRED) gd.flush(gred_red, C, CV, gr.parts);
 }
 
 // Stride-2 backward data, phase-split: with u = h + pt and v = w + pl, dx row u=2a takes dy
@@ -641,15 +750,20 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
 // dy[a-1..a][b-1..b], of which row a-1 is carried from the previous step, so each step
 // loads two dy pixels (one shared with the left neighbour via L1) and stores four.
 constexpr int DW_S2_RP = 4;  // row pairs per thread
-template <typename T, int V>
+template <typename T, int V, bool GRED = false>
 __global__ void __launch_bounds__(256) dw3x3_bwd_data_s2_kernel(const T* __restrict__ dy, const float* __restrict__ w,
                                                                 T* __restrict__ dx, int H, int W, int C, int pt,
-                                                                int pl, int Ho, int Wo, int Bc) {
+                                                                int pl, int Ho, int Wo, int Bc,
+                                                                BnGred gr = BnGred{}) {
   const int CV = C / V;
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cv = (int)(t % CV);
   const int b = (int)(t / CV);
-  if (b >= Bc) return;
+  __shared__ __attribute__((aligned(16))) float gred_red[GRED ? 256 * V : 1];
+  DwGred<GRED ? V : 1> gd;
+  if constexpr (GRED) gd.init(gr, cv * V, b < Bc);
+  const T* gy = GRED ? (const T*)gr.y + (long)blockIdx.z * H * W * C + cv * V : nullptr;
+  if (b < Bc) {  // (no early return: see dw3x3_bwd_data_kernel)
   const int a0 = blockIdx.y * DW_S2_RP;
   const int amax = (H - 1 + pt) >> 1;  // last a with a dx row
   const int a1 = a0 + DW_S2_RP - 1 < amax ? a0 + DW_S2_RP - 1 : amax;
@@ -672,10 +786,23 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_s2_kernel(const T* __restr
   };
   const int w0 = 2 * b - pl, w1 = 2 * b + 1 - pl;  // dx columns of this thread
   PackV<T, V> prev[2], cur[2], nxt[2];
+  // GRED: y of the 2x2 dx block of step a (rows 2a-pt, 2a+1-pt x columns w0, w1), one step ahead
+  PackV<T, V> yq[GRED ? 4 : 1], yn[GRED ? 4 : 1];
+  auto yload = [&](PackV<T, V>(&q)[GRED ? 4 : 1], int a) {
+    if constexpr (GRED) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int h = 2 * a + (i >> 1) - pt, ww = (i & 1) ? w1 : w0;
+        if (h >= 0 && h < H && ww >= 0 && ww < W) q[i].load(gy + ((long)h * W + ww) * C);
+      }
+    }
+  };
+  yload(yq, a0);
   load2(prev, a0 - 1);
   load2(cur, a0);
   if (a0 + 1 <= a1) load2(nxt, a0 + 1);
   for (int a = a0; a <= a1; ++a) {
+    if (a + 1 <= a1) yload(yn, a + 1);
     float o00[V], o01[V], o10[V], o11[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -687,17 +814,26 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_s2_kernel(const T* __restr
       o10[v] = fmaf(c0, wr[5][v], c1 * wr[3][v]);
       o11[v] = c1 * wr[4][v];
     }
-    auto put = [&](int h, int ww, const float (&o)[V]) {
+    auto put = [&](int h, int ww, const float (&o)[V], int i) {
       if (h < 0 || h >= H || ww < 0 || ww >= W) return;
       PackV<T, V> pk;
 #pragma unroll
       for (int v = 0; v < V; ++v) pk.set(v, o[v]);
       pk.store(xn + ((long)h * W + ww) * C);
+      if constexpr (GRED) {
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          gred_acc(pk.get(v), yq[i].get(v), gd.sc[v], gd.sh[v], gd.mu[v], gd.rs[v], gr.p.act, gd.sg[v], gd.sgx[v]);
+      }
     };
-    put(2 * a - pt, w0, o00);
-    put(2 * a - pt, w1, o01);
-    put(2 * a + 1 - pt, w0, o10);
-    put(2 * a + 1 - pt, w1, o11);
+    put(2 * a - pt, w0, o00, 0);
+    put(2 * a - pt, w1, o01, 1);
+    put(2 * a + 1 - pt, w0, o10, 2);
+    put(2 * a + 1 - pt, w1, o11, 3);
+    if constexpr (GRED) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) yq[i] = yn[i];
+    }
     if (a + 1 <= a1) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -707,6 +843,8 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_s2_kernel(const T* __restr
       if (a + 2 <= a1) load2(nxt, a + 2);
     }
   }
+  }  // b < Bc
+  if constexpr (GRED) gd.flush(gred_red, C, CV, gr.parts);
 }
 
 // Filter gradient: dw[i,j,c] = sum_{n,ho,wo} dy[n,ho,wo,c] * x[n, ho*S-pt+i, wo*S-pl+j, c].
@@ -926,21 +1064,57 @@ static long dw_fwd_lx_launch(const void* x, const BnPro* pro, const float* w, vo
   return (long)N * t.strips * t.coltiles;
 }
 
-template <typename T, int S, int V>
-static void dw_bwd_data_launch(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int pt, int pl,
-                               int Ho, int Wo, hipStream_t s) {
+// the grid of the backward-data launch (phase-split kernel for stride 2): its block count is
+// the gred part count
+static dim3 dw_bwd_data_grid(int N, int H, int W, int C, int S, int pt, int pl, int V, bool* s2k) {
   static const bool no_s2 = getenv("ROD_DEBUG_NOS2") != nullptr;  // debug bisection
-  if (S == 2 && pt <= 1 && pl <= 1 && !no_s2) {
+  *s2k = S == 2 && pt <= 1 && pl <= 1 && !no_s2;
+  if (*s2k) {
     const int Bc = (W - 1 + pl) / 2 + 1;
     const int Ar = (H - 1 + pt) / 2 + 1;
-    dim3 g2(cdiv((long)(C / V) * Bc, 256), cdiv(Ar, DW_S2_RP), N);
-    hipLaunchKernelGGL((dw3x3_bwd_data_s2_kernel<T, V>), g2, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W, C, pt,
-                       pl, Ho, Wo, Bc);
+    return dim3(cdiv((long)(C / V) * Bc, 256), cdiv(Ar, DW_S2_RP), N);
+  }
+  return dim3(cdiv((long)(C / V) * W, 256), cdiv(H, DW_RB), N);
+}
+// stride-1 backward-data on the LDS-exchange kernel: correlation of dy [N,Ho,Wo,C] with the
+// flipped taps, pads (2-pt, 2-pl), output dx [N,H,W,C]; returns the gred part count
+template <typename T>
+static long dw_bwd_data_lx_launch(const void* dy, const float* w, void* dx, const BnGred* gr, int N, int H, int W,
+                                  int C, int pt, int pl, int Ho, int Wo, hipStream_t s) {
+  const DwTile t = dw_tile(N, H, W, C, 1, Vec16<T>::N);
+  const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
+  const BnGred g = gr ? *gr : BnGred{};
+  if (gr)
+    hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, 1, -1, false, true, true>), grid, dim3(256), 0, s, (const T*)dy, w,
+                       (T*)dx, Ho, Wo, C, 2 - pt, 2 - pl, H, W, t, nullptr, BnPro{}, g);
+  else
+    hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, 1, -1, false, true, false>), grid, dim3(256), 0, s, (const T*)dy, w,
+                       (T*)dx, Ho, Wo, C, 2 - pt, 2 - pl, H, W, t, nullptr, BnPro{}, g);
+  return (long)N * t.strips * t.coltiles;
+}
+
+template <typename T, int S, int V>
+static void dw_bwd_data_launch(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int pt, int pl,
+                               int Ho, int Wo, const BnGred* gr, hipStream_t s) {
+  bool s2k;
+  const dim3 grid = dw_bwd_data_grid(N, H, W, C, S, pt, pl, V, &s2k);
+  const BnGred g = gr ? *gr : BnGred{};
+  if (s2k) {
+    const int Bc = (W - 1 + pl) / 2 + 1;
+    if (gr)
+      hipLaunchKernelGGL((dw3x3_bwd_data_s2_kernel<T, V, true>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W,
+                         C, pt, pl, Ho, Wo, Bc, g);
+    else
+      hipLaunchKernelGGL((dw3x3_bwd_data_s2_kernel<T, V, false>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H,
+                         W, C, pt, pl, Ho, Wo, Bc, g);
     return;
   }
-  dim3 grid(cdiv((long)(C / V) * W, 256), cdiv(H, DW_RB), N);
-  hipLaunchKernelGGL((dw3x3_bwd_data_kernel<T, S, V>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W, C, pt,
-                     pl, Ho, Wo);
+  if (gr)
+    hipLaunchKernelGGL((dw3x3_bwd_data_kernel<T, S, V, true>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W,
+                       C, pt, pl, Ho, Wo, g);
+  else
+    hipLaunchKernelGGL((dw3x3_bwd_data_kernel<T, S, V, false>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, H, W,
+                       C, pt, pl, Ho, Wo, g);
 }
 template <typename T, int S, int V>
 static void dw_bwd_filter_launch(const void* x, const BnPro* pro, const void* dy, float* dw, float* slab, int N, int H,
@@ -1020,17 +1194,52 @@ int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, c
   return check_launch("rod_dw3x3_fwd");
 }
 
-int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int stride,
-                       int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream) {
+static int dw_bwd_data_pack(int C, int dtype) {  // the pack dw_pack picks for 16-byte-aligned pointers
+  if (dtype == ROD_BF16 && C % 8 == 0) return 8;
+  return C % 4 == 0 ? 4 : 1;
+}
+
+int rod_dw3x3_bwd_data_gred_parts(int N, int H, int W, int C, int stride, int dtype) {
+  const int V16 = dtype == ROD_F32 ? 4 : 8;
+  if (stride == 1 && C % V16 == 0) return (int)dw_lx_parts(N, H, W, C, 1, V16);  // LDS-exchange kernel
+  const int pt = stride == 2 ? std::max((cdiv(H, 2) - 1) * 2 + 3 - H, 0) / 2 : 1;
+  const int pl = stride == 2 ? std::max((cdiv(W, 2) - 1) * 2 + 3 - W, 0) / 2 : 1;
+  const int pk = dw_bwd_data_pack(C, dtype);
+  const int V = pk == 8 ? (dtype == ROD_BF16 ? 8 : 4) : pk;
+  bool s2k;
+  const dim3 g = dw_bwd_data_grid(N, H, W, C, stride, pt, pl, V, &s2k);
+  return (int)(g.x * g.y * g.z);
+}
+
+int rod_dw3x3_bwd_data(const void* dy, const float* w, void* dx, const void* gred_y, const float* gred_mean,
+                       const float* gred_rstd, const float* gred_gamma, const float* gred_beta, int gred_act,
+                       float* gred_parts, int N, int H, int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo,
+                       int dtype, void* stream) {
   DW_ARGS_OK("rod_dw3x3_bwd_data");
+  ROD_CHECK_ARG(!gred_parts || (gred_y && gred_mean && gred_rstd), "rod_dw3x3_bwd_data: gred needs y, mean, rstd");
   hipStream_t s = ROD_STREAM(stream);
-  if (dtype == ROD_F32) {
-    const int pk = dw_pack<float>(dy, dx, C, 8);
-    DW_SELECT(dw_bwd_data_launch, float, pk, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
-  } else if (dtype == ROD_BF16) {
-    const int pk = dw_pack<bf16_t>(dy, dx, C, 8);
-    DW_SELECT(dw_bwd_data_launch, bf16_t, pk, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
-  } else {
+  const BnGred gr{gred_y, BnPro{gred_mean, gred_rstd, gred_gamma, gred_beta, gred_act}, gred_parts};
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    const int nparts = gred_parts ? rod_dw3x3_bwd_data_gred_parts(N, H, W, C, stride, dtype) : 0;
+    if (stride == 1 && dw_lx_ok<T>(dy, dx, C) && (!gred_parts || ((((uintptr_t)gred_y) & 15) == 0))) {
+      dw_bwd_data_lx_launch<T>(dy, w, dx, gred_parts ? &gr : nullptr, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
+      return;
+    }
+    const int pk = dw_pack<T>(dy, dx, C, 8);
+    const int V = pk == 8 ? (sizeof(T) == 2 ? 8 : 4) : pk;
+    bool s2k;
+    const dim3 g = dw_bwd_data_grid(N, H, W, C, stride, pad_t, pad_l, V, &s2k);
+    // fused when this launch's blocks are the parts the caller sized (aligned pointers,
+    // 16-byte-aligned y too); otherwise a separate pass
+    const bool fuse = gred_parts && (long)g.x * g.y * g.z == nparts && (((uintptr_t)gred_y) & 15) == 0;
+    const BnGred* gp = fuse ? &gr : nullptr;
+    DW_SELECT(dw_bwd_data_launch, T, pk, dy, w, dx, N, H, W, C, pad_t, pad_l, Ho, Wo, gp, s);
+    if (gred_parts && !fuse) ::rod::gred_parts(dtype, dx, gred_y, gr.p, (long)N * H * W, C, gred_parts, nparts, s);
+  };
+  if (dtype == ROD_F32) run(float{});
+  else if (dtype == ROD_BF16) run(bf16_t{});
+  else {
     set_error("rod_dw3x3_bwd_data: bad dtype %d", dtype);
     return ROD_EINVAL;
   }

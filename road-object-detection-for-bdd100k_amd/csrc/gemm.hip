@@ -196,12 +196,12 @@ __device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b
 // block 256 threads = 4 waves laid out WM x WN; tile BM x BN; wave tile (BM/WM) x (BN/WN)
 // =====================================================================================
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool SPLIT = false, bool STATS = false,
-          bool PRO = false>
+          bool PRO = false, bool GRED = false>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
                                                        const float* __restrict__ bias, T* __restrict__ Y, long M,
                                                        int H, int W, int Cin, int Cout, int ldx, int ldy,
                                                        float* __restrict__ part = nullptr, int kper = 0,
-                                                       BnPro pro = BnPro{}) {
+                                                       BnPro pro = BnPro{}, BnGred gr = BnGred{}) {
   constexpr int BM = 128;
   constexpr int WN = BN >= 64 ? 2 : 1;
   constexpr int WM = 4 / WN;
@@ -331,6 +331,21 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     const int scol = tid % BN, spart = tid / BN;
     const bool sact = STATS && spart < TPC && n0 + scol < Cout;
     float st_n = 0.f, st_mean = 0.f, st_m2 = 0.f;
+    // GRED: BatchNorm-backward sums of this tile's rounded outputs (dz, staged in Cs) against
+    // y_in; a thread owns one EV-wide column chunk and walks rows GRPP apart, so each pass of
+    // the block reads whole 16-byte row segments of y_in (coalesced, all loads independent)
+    constexpr int GCPR = BN / EV;
+    constexpr int GRPP = 256 / GCPR;
+    const int gcc = (tid % GCPR) * EV, grg = tid / GCPR;
+    const int gcol = n0 + gcc;
+    const bool gact = GRED && grg < GRPP && gcol < Cout;
+    constexpr int GV = GRED ? EV : 1;
+    float gsc[GV], gsh[GV], gmu[GV], grs[GV], gs[GV], gsx[GV];
+#pragma unroll
+    for (int v = 0; v < GV; ++v) {
+      gsc[v] = gsh[v] = gmu[v] = grs[v] = gs[v] = gsx[v] = 0.f;
+      if (GRED && gact && gcol + v < Cout) gred_coef(gr.p, gcol + v, gsc[v], gsh[v], gmu[v], grs[v]);
+    }
 #pragma unroll
     for (int h = 0; h < BM / 64; ++h) {
       __syncthreads();
@@ -347,6 +362,28 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         }
       }
       __syncthreads();
+      if constexpr (GRED) {
+        const long left = M - (m0 + h * 64);
+        const int nrows = left < 64 ? (int)left : 64;
+        if (gact) {
+          const T* yin = (const T*)gr.y + (m0 + h * 64) * ldy + gcol;
+          const bool full = gcol + EV <= Cout;
+#pragma unroll 2
+          for (int r = grg; r < nrows; r += GRPP) {
+            Vec16<T> yv, dv;
+            if (full) {
+              yv.load(yin + (long)r * ldy);
+            } else {
+#pragma unroll
+              for (int v = 0; v < EV; ++v) yv.set(v, gcol + v < Cout ? to_f32(yin[(long)r * ldy + v]) : 0.f);
+            }
+            dv.v = *(const decltype(dv.v)*)(Cs + r * LDC + gcc);
+#pragma unroll
+            for (int v = 0; v < EV; ++v)
+              gred_acc(dv.get(v), yv.get(v), gsc[v], gsh[v], gmu[v], grs[v], gr.p.act, gs[v], gsx[v]);
+          }
+        }
+      }
       if constexpr (STATS) {
         const long left = M - (m0 + h * 64);
         const int nrows = left < 64 ? (int)left : 64;
@@ -379,6 +416,26 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
           *(uint4*)dst = *(const uint4*)src;
         } else {
           for (int j = 0; j < Cout - col; ++j) dst[j] = src[j];
+        }
+      }
+    }
+    if constexpr (GRED) {
+      // per channel: the GRPP row groups of its chunk, in order -> part blockIdx.x
+      __shared__ float gsum[2][256];
+#pragma unroll
+      for (int v = 0; v < GV; ++v) {
+        __syncthreads();
+        gsum[0][tid] = gs[v];
+        gsum[1][tid] = gsx[v];
+        __syncthreads();
+        if (gact && grg == 0 && gcol + v < Cout) {
+          float a = 0.f, b = 0.f;
+          for (int q = 0; q < GRPP; ++q) {
+            a += gsum[0][q * GCPR + tid];
+            b += gsum[1][q * GCPR + tid];
+          }
+          gr.parts[(long)blockIdx.x * 2 * Cout + gcol + v] = a;
+          gr.parts[(long)blockIdx.x * 2 * Cout + Cout + gcol + v] = b;
         }
       }
     }
@@ -679,6 +736,41 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, T* __restrict__ 
   wt[idx] = from_f32<T>(w[(((long)co * ks + si) * ks + sj) * Cin + ci]);
 }
 
+// batched weight_prep: one launch over the concatenated element ranges of every table entry
+struct PrepEntry {
+  const float* w;
+  void* wt;
+  long start;
+  int Cout, Cin, ksize, mode;
+};
+static_assert(sizeof(PrepEntry) == 40, "rod_prep_entry layout");
+
+template <typename T>
+__global__ void __launch_bounds__(256) weight_prep_batch_kernel(const PrepEntry* __restrict__ tab, int n, long total) {
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n - 1;  // last entry with start <= idx
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tab[mid].start <= idx) lo = mid;
+      else hi = mid - 1;
+    }
+    const PrepEntry e = tab[lo];
+    const long i = idx - e.start;
+    T* wt = (T*)e.wt;
+    if (e.mode == 0) {
+      wt[i] = from_f32<T>(e.w[i]);
+      continue;
+    }
+    const int co = (int)(i % e.Cout);
+    long t = i / e.Cout;
+    const int j = (int)(t % e.ksize);
+    t /= e.ksize;
+    const int ii = (int)(t % e.ksize);
+    const int ci = (int)(t / e.ksize);
+    wt[i] = from_f32<T>(e.w[(((long)co * e.ksize + (e.ksize - 1 - ii)) * e.ksize + (e.ksize - 1 - j)) * e.Cin + ci]);
+  }
+}
+
 struct WgradPlan {
   int ctiles, ktiles, splits;
   long chunk;
@@ -706,10 +798,16 @@ static bool aligned16(const void* p) {
 // dynamic LDS.
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool PRO>
 static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
-                            int Cout, int ldx, int ldy, float* stats, const BnPro& pro, hipStream_t s) {
+                            int Cout, int ldx, int ldy, float* stats, const BnPro& pro, const BnGred* gr,
+                            hipStream_t s) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
   const size_t lds = PRO ? 8 * (size_t)Cin : 0;
   if constexpr (VY) {
+    if (gr) {
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO, true>), grid, dim3(256), lds, s,
+                         (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, nullptr, 0, pro, *gr);
+      return;
+    }
     if (stats) {
       hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, true, PRO>), grid, dim3(256), lds, s,
                          (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, stats, 0, pro);
@@ -727,9 +825,9 @@ static void conv_fwd_launch(const void* x, const void* wt, const float* bias, vo
 template <typename T, int KS, bool PRO>
 static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const void* wt, const float* bias, void* y,
                               long M, int H, int W, int Cin, int Cout, int ldx, int ldy, float* stats,
-                              const BnPro& pro, hipStream_t s) {
+                              const BnPro& pro, const BnGred* gr, hipStream_t s) {
 #define CF(BN_, VA_, VB_, VY_) \
-  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, s)
+  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, gr, s)
   if (va && vb && vy) {
     if (Cout <= 32) CF(32, true, true, true);
     else if (Cout <= 64) CF(64, true, true, true);
@@ -765,8 +863,8 @@ static void conv_fwd_split(const SplitPlan& p, const void* x, const void* wt, fl
 
 template <typename T>
 static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, const float* bias, void* y, void* ws,
-                           float* stats, int N, int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy,
-                           hipStream_t s) {
+                           float* stats, const BnGred* gr, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
+                           int ldy, hipStream_t s) {
   const long M = (long)N * H * W;
   const int K = ksize * ksize * Cin;
   const int eV = Vec16<T>::N;
@@ -789,15 +887,17 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
     hipLaunchKernelGGL(splitk_combine_kernel<T>, dim3(cdivl(M * Cout, 256)), dim3(256), 0, s, (const float*)part,
                        bias, (T*)y, M, Cout, ldy, sp.splits);
     if (stats) stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
+    if (gr) gred_parts(dt, y, gr->y, gr->p, M, Cout, gr->parts, nparts, s);
     return;
   }
-  if (stats && !(va && vb && vy)) {  // no fused epilogue on this path: separate statistics pass
-    conv_fwd_typed<T>(x, pro, wt, bias, y, ws, nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy, s);
-    stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
+  if ((stats || gr) && !(va && vb && vy)) {  // no fused epilogue on this path: separate pass
+    conv_fwd_typed<T>(x, pro, wt, bias, y, ws, nullptr, nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy, s);
+    if (stats) stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
+    if (gr) gred_parts(dt, y, gr->y, gr->p, M, Cout, gr->parts, nparts, s);
     return;
   }
   static const bool no_stem = getenv("ROD_DEBUG_NOSTEM") != nullptr;  // debug bisection
-  if (!pro && ksize == 3 && Cin == 3 && (Cout == 32 || Cout == 64) && vy && !no_stem) {
+  if (!pro && !gr && ksize == 3 && Cin == 3 && (Cout == 32 || Cout == 64) && vy && !no_stem) {
     if (Cout == 32)
       hipLaunchKernelGGL((stem_conv_fwd_kernel<T, 32>), dim3(cdiv(W, 128), H, N), dim3(256), 0, s, (const T*)x,
                          (const T*)wt, bias, (T*)y, H, W, ldx, ldy);
@@ -807,11 +907,11 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
     return;
   }
   if (ksize == 1) {
-    if (pro) conv_fwd_dispatch<T, 1, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
-    else conv_fwd_dispatch<T, 1, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
+    if (pro) conv_fwd_dispatch<T, 1, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
+    else conv_fwd_dispatch<T, 1, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
   } else {
-    if (pro) conv_fwd_dispatch<T, 3, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
-    else conv_fwd_dispatch<T, 3, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, s);
+    if (pro) conv_fwd_dispatch<T, 3, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
+    else conv_fwd_dispatch<T, 3, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
   }
 }
 
@@ -879,17 +979,22 @@ size_t rod_conv_fwd_workspace(int N, int H, int W, int Cin, int Cout, int ksize)
 
 int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
                  const float* pro_beta, int pro_act, const void* wt, const float* bias, void* y, void* workspace,
-                 float* stat_parts, int N, int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy, int dtype,
-                 void* stream) {
+                 float* stat_parts, const void* gred_y, const float* gred_mean, const float* gred_rstd,
+                 const float* gred_gamma, const float* gred_beta, int gred_act, float* gred_parts, int N, int H, int W,
+                 int Cin, int Cout, int ksize, int ldx, int ldy, int dtype, void* stream) {
   ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "rod_conv_fwd: bad shape");
   ROD_CHECK_ARG(ksize == 1 || ksize == 3, "rod_conv_fwd: ksize must be 1 or 3");
   if (ldx == 0) ldx = Cin;
   if (ldy == 0) ldy = Cout;
   ROD_CHECK_ARG(ldx >= Cin && ldy >= Cout, "rod_conv_fwd: leading dim too small");
   ROD_CHECK_ARG(!pro_mean || (pro_rstd && Cin <= PRO_MAXC), "rod_conv_fwd: bad BatchNorm prologue (Cin %d)", Cin);
+  ROD_CHECK_ARG(!gred_parts || (gred_y && gred_mean && gred_rstd && ldy == Cout && !stat_parts),
+                "rod_conv_fwd: gred needs y, mean, rstd, a dense output and no stat_parts");
   const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
-  ROD_DISPATCH_DTYPE(dtype, conv_fwd_typed<T>(x, pro_mean ? &pro : nullptr, wt, bias, y, workspace, stat_parts, N, H,
-                                              W, Cin, Cout, ksize, ldx, ldy, ROD_STREAM(stream)));
+  const BnGred gr{gred_y, BnPro{gred_mean, gred_rstd, gred_gamma, gred_beta, gred_act}, gred_parts};
+  ROD_DISPATCH_DTYPE(dtype, conv_fwd_typed<T>(x, pro_mean ? &pro : nullptr, wt, bias, y, workspace, stat_parts,
+                                              gred_parts ? &gr : nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy,
+                                              ROD_STREAM(stream)));
   return check_launch("rod_conv_fwd");
 }
 
@@ -901,6 +1006,14 @@ int rod_conv_weight_prep(const float* w, void* wt, int Cout, int Cin, int ksize,
   ROD_DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(weight_prep_kernel<T>, dim3(cdivl(n, 256)), dim3(256), 0,
                                                ROD_STREAM(stream), w, (T*)wt, Cout, Cin, ksize, mode));
   return check_launch("rod_conv_weight_prep");
+}
+
+int rod_conv_weight_prep_batch(const void* table, int n, long total, int dtype, void* stream) {
+  ROD_CHECK_ARG(table != nullptr && n > 0 && total > 0, "rod_conv_weight_prep_batch: bad arguments");
+  const int blocks = (int)std::min<long>(cdivl(total, 256), 4096);
+  ROD_DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(weight_prep_batch_kernel<T>, dim3(blocks), dim3(256), 0,
+                                               ROD_STREAM(stream), (const PrepEntry*)table, n, total));
+  return check_launch("rod_conv_weight_prep_batch");
 }
 
 size_t rod_conv_wgrad_workspace(int N, int H, int W, int Cin, int Cout, int ksize) {

@@ -141,6 +141,33 @@ __device__ __forceinline__ void bn_pro_affine(const BnPro& p, int c, float& sc, 
 
 // Fallback: parts of y[M, C] computed by a separate pass (batchnorm.hip).
 void stat_parts(int dtype, const void* y, long M, int C, int ld, float* parts, int nparts, hipStream_t s);
+// Fallback: BatchNorm-backward partial sums [nparts][2][C] of (g, g*yhat) from dz and the
+// pre-BatchNorm y (both [M, C] contiguous) by a separate pass (batchnorm.hip).
+void gred_parts(int dtype, const void* dz, const void* y, const BnPro& p, long M, int C, float* parts, int nparts,
+                hipStream_t s);
+
+// BatchNorm-backward reduction in a producer's epilogue ("gred"): for the BatchNorm whose
+// output z = act(y*scale + offset) a consumer read through its prologue, the kernel that
+// writes dz (that consumer's backward-data) also reads y at the same positions and sums,
+// per channel, g = dz*act'(y*scale + offset) and g*yhat, yhat = (y - mean)*rstd — the
+// arithmetic of bn_bwd_reduce_kernel, on the rounded dz it stores.
+struct BnGred {
+  const void* y;
+  BnPro p;
+  float* parts;  // [nparts][2][C]
+};
+__device__ __forceinline__ void gred_coef(const BnPro& p, int c, float& sc, float& sh, float& mu, float& rs) {
+  bn_pro_affine(p, c, sc, sh);
+  mu = p.mean[c];
+  rs = p.rstd[c];
+}
+__device__ __forceinline__ void gred_acc(float dz, float y, float sc, float sh, float mu, float rs, int act, float& sg,
+                                         float& sgx) {
+  const float d = y - mu;
+  const float g = dz * act_grad(fmaf(y, sc, sh), act);
+  sg += g;
+  sgx = fmaf(g, d * rs, sgx);
+}
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 inline long cdivl(long a, long b) { return (a + b - 1) / b; }

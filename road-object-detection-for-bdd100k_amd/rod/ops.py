@@ -20,8 +20,11 @@ from . import _abi
 from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU6  # noqa: F401
 
 _DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
-# debug bisection switches (comma list): splitk, epistats, convstats, dwstats
+# debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro
 _DISABLE = set(os.environ.get("ROD_DISABLE", "").split(","))
+# opt-in paths (comma list): gred = BatchNorm-backward reduction fused into the backward-data
+# epilogues (measured slower than the separate streaming reduce on MI355X: DESIGN.md §6)
+_ENABLE = set(os.environ.get("ROD_ENABLE", "").split(","))
 
 
 def dtcode(t: torch.Tensor) -> int:
@@ -126,6 +129,31 @@ def _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
     return dy
 
 
+def _bn_backward_parts(dz, y, mean, rstd, gamma, beta, act, parts, need_g, need_b):
+    """Finish a BatchNorm backward whose reduction the producer of dz already did in its
+    epilogue (gred partial sums): rod_bn_bwd_finalize -> rod_bn_bwd_apply."""
+    N, H, W, C = y.shape
+    M = N * H * W
+    coef = torch.empty(3 * C, dtype=torch.float32, device=y.device)
+    dg = grad_slot(gamma) if need_g else None
+    db = grad_slot(beta) if need_b else None
+    _abi.call("rod_bn_bwd_finalize", parts, parts.shape[0], M, C, rstd, gamma, dg, db, coef, stream())
+    dy = torch.empty_like(y)
+    _abi.call("rod_bn_bwd_apply", dz, y, mean, rstd, gamma, beta, coef, dy, M, C, act, dtcode(y), stream())
+    if need_g:
+        _mark_written(gamma)
+    if need_b:
+        _mark_written(beta)
+    return dy
+
+
+def _gred_args(g):
+    """The seven gred arguments (pre-BatchNorm y, mean, rstd, gamma, beta, act, parts)."""
+    if g is None:
+        return (None, None, None, None, None, 0, None)
+    return g
+
+
 def _split_in(x):
     """(tensor, gamma, beta, mean, rstd, act, training) of a plain tensor or a Pending."""
     if isinstance(x, Pending):
@@ -170,7 +198,13 @@ class _DW3x3(torch.autograd.Function):
             if ctx.pro and not ctx.training:
                 raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
             dx = torch.empty_like(x)   # gradient wrt the dw input (the BatchNorm output when pro)
-            _abi.call("rod_dw3x3_bwd_data", dy, w, dx, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x), stream())
+            gred = None
+            if ctx.pro and "gred" in _ENABLE:   # BatchNorm-backward sums in the epilogue
+                nparts = _abi.lib().rod_dw3x3_bwd_data_gred_parts(N, H, W, C, s, dtcode(x))
+                parts = torch.empty((nparts, 2, C), dtype=torch.float32, device=x.device)
+                gred = (x, mean, rstd, gamma, beta, ctx.act, parts)
+            _abi.call("rod_dw3x3_bwd_data", dy, w, dx, *_gred_args(gred), N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x),
+                      stream())
         if ctx.needs_input_grad[1]:
             g = grad_slot(w)
             ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
@@ -178,7 +212,10 @@ class _DW3x3(torch.autograd.Function):
                       dtcode(x), stream())
             _mark_written(w)
         if ctx.pro and dx is not None:
-            dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
+            if gred is not None:
+                dx = _bn_backward_parts(dx, x, mean, rstd, gamma, beta, ctx.act, gred[6], need_g, need_b)
+            else:
+                dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
         return dx, None, None, None, None, None, None, None, None, None
 
 
@@ -193,12 +230,23 @@ def dw3x3(x, w, stride=1, want_stats=False):
 
 
 # ----------------------------------------------------------------------------- dense conv
-def conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, stat_parts=None, pro=None):
+def _prep(w, mode, dtype, Cout, Cin, ks):
+    """GEMM operand layout of conv weight w (rod_conv_weight_prep): cached per parameter store
+    and refreshed in one batched launch per step; a tensor outside a store is prepared here."""
+    store = getattr(w, "_rod_store", None)
+    if store is not None and "prepcache" not in _DISABLE:
+        return store.prepped(w, mode, dtype, Cout, Cin, ks)
+    wt = torch.empty((Cout, ks * ks * Cin) if mode == 0 else (Cin, ks * ks * Cout), dtype=dtype, device=w.device)
+    _abi.call("rod_conv_weight_prep", w, wt, Cout, Cin, ks, mode, dtcode(wt), stream())
+    return wt
+
+
+def conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, stat_parts=None, pro=None, gred=None):
     """rod_conv_fwd with its split-K workspace (allocated only when the plan splits)."""
     nb = 0 if "splitk" in _DISABLE else _abi.query("rod_conv_fwd_workspace", N, H, W, Cin, Cout, ksize)
     ws = workspace(nb, x.device) if nb else None
-    _abi.call("rod_conv_fwd", x, *_pro_args(pro), wt, b, y, ws, stat_parts, N, H, W, Cin, Cout, ksize, 0, 0,
-              dtcode(x), stream())
+    _abi.call("rod_conv_fwd", x, *_pro_args(pro), wt, b, y, ws, stat_parts, *_gred_args(gred), N, H, W, Cin, Cout,
+              ksize, 0, 0, dtcode(x), stream())
 
 
 class _Conv(torch.autograd.Function):
@@ -207,8 +255,7 @@ class _Conv(torch.autograd.Function):
         N, H, W, Cin = x.shape
         Cout = w.shape[0]
         assert w.shape == (Cout, ksize, ksize, Cin), (tuple(w.shape), ksize, Cin)
-        wt = torch.empty((Cout, ksize * ksize * Cin), dtype=x.dtype, device=x.device)
-        _abi.call("rod_conv_weight_prep", w, wt, Cout, Cin, ksize, 0, dtcode(x), stream())
+        wt = _prep(w, 0, x.dtype, Cout, Cin, ksize)
         y = torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
         parts = None
         if want_stats:  # BatchNorm partial statistics from the epilogue ([ceil(M/128)][3][Cout])
@@ -238,10 +285,13 @@ class _Conv(torch.autograd.Function):
         if ctx.needs_input_grad[0] or need_g or need_b:
             if ctx.pro and not ctx.training:
                 raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
-            wt1 = torch.empty((Cin, ks * ks * Cout), dtype=x.dtype, device=x.device)
-            _abi.call("rod_conv_weight_prep", w, wt1, Cout, Cin, ks, 1, dtcode(x), stream())
+            wt1 = _prep(w, 1, x.dtype, Cout, Cin, ks)
             dx = torch.empty_like(x)   # gradient wrt the conv input (the BatchNorm output when pro)
-            conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks)
+            gred = None
+            if ctx.pro and "gred" in _ENABLE:   # BatchNorm-backward sums in the epilogue
+                parts = torch.empty((-(-(N * H * W) // 128), 2, Cin), dtype=torch.float32, device=x.device)
+                gred = (x, mean, rstd, gamma, beta, ctx.act, parts)
+            conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks, gred=gred)
         need_w = ctx.needs_input_grad[1]
         need_bias = b is not None and ctx.needs_input_grad[2]
         if need_w or need_bias:
@@ -257,7 +307,10 @@ class _Conv(torch.autograd.Function):
             if need_bias:
                 _mark_written(b)
         if ctx.pro and dx is not None:
-            dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
+            if gred is not None:
+                dx = _bn_backward_parts(dx, x, mean, rstd, gamma, beta, ctx.act, gred[6], need_g, need_b)
+            else:
+                dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
         return dx, None, None, None, None, None, None, None, None, None, None
 
 
@@ -469,8 +522,7 @@ class _Deconv2x2(torch.autograd.Function):
         F = w.shape[2]
         assert w.shape == (2, 2, F, Cin)
         x = x.contiguous()
-        wt = torch.empty((4 * F, Cin), dtype=x.dtype, device=x.device)
-        _abi.call("rod_conv_weight_prep", w, wt, 4 * F, Cin, 1, 0, dtcode(x), stream())
+        wt = _prep(w, 0, x.dtype, 4 * F, Cin, 1)
         z = torch.empty((N, h, wd, 4 * F), dtype=x.dtype, device=x.device)
         conv_fwd_raw(x, wt, None, z, N, h, wd, Cin, 4 * F, 1)
         y = torch.empty((N, ho, wo, F), dtype=x.dtype, device=x.device)
@@ -487,8 +539,7 @@ class _Deconv2x2(torch.autograd.Function):
         _abi.call("rod_space_to_depth2", dy.contiguous(), dz, N, h, wd, F, ho, wo, 0, dtcode(dy), stream())
         dx = None
         if ctx.needs_input_grad[0]:
-            wt1 = torch.empty((Cin, 4 * F), dtype=dy.dtype, device=dy.device)
-            _abi.call("rod_conv_weight_prep", w, wt1, 4 * F, Cin, 1, 1, dtcode(dy), stream())
+            wt1 = _prep(w, 1, dy.dtype, 4 * F, Cin, 1)
             dx = torch.empty_like(x)
             conv_fwd_raw(dz, wt1, None, dx, N, h, wd, 4 * F, Cin, 1)
         if ctx.needs_input_grad[1]:

@@ -52,6 +52,9 @@ class ParamStore:
         self.flat_grad = None
         self.offsets = {}
         self.device = None
+        self.version = 0          # bumped whenever parameter values change (SGD step, load)
+        self._prep = {}           # (name, mode, dtype) -> [prepped tensor, version, entry]
+        self._prep_tables = {}    # dtype -> (device table, n, total) or None when stale
 
     # ---- registration (host) ------------------------------------------------------
     def add(self, name: str, init: np.ndarray):
@@ -83,6 +86,7 @@ class ParamStore:
             p = self.flat[o:o + n].view(arr.shape).detach().requires_grad_(True)
             p._rod_grad = self.flat_grad[o:o + n].view(arr.shape)
             p._rod_name = name
+            p._rod_store = self
             self.params[name] = p
         for name, arr in self._buffers.items():
             self.buffers[name] = torch.from_numpy(arr.copy()).to(self.device)
@@ -98,6 +102,48 @@ class ParamStore:
 
     def zero_grad(self):
         self.flat_grad.zero_()
+
+    # ---- derived weight layouts (rod_conv_weight_prep) -------------------------------
+    def prepped(self, p, mode, dtype, Cout, Cin, ks):
+        """The GEMM operand layout `mode` of conv weight p in `dtype` (rod_conv_weight_prep):
+        built once, then refreshed for EVERY registered weight by one batched launch
+        (rod_conv_weight_prep_batch) the first time it is asked for after the parameters
+        changed (self.version)."""
+        from . import _abi
+        from .ops import dtcode, stream
+        key = (p._rod_name, mode, dtype)
+        e = self._prep.get(key)
+        if e is None:
+            wt = torch.empty((Cout, ks * ks * Cin) if mode == 0 else (Cin, ks * ks * Cout), dtype=dtype,
+                             device=p.device)
+            _abi.call("rod_conv_weight_prep", p, wt, Cout, Cin, ks, mode, dtcode(wt), stream())
+            self._prep[key] = [wt, self.version, (p.data_ptr(), wt.data_ptr(), Cout, Cin, ks, mode)]
+            self._prep_tables[dtype] = None
+            return wt
+        if e[1] != self.version:
+            self._refresh_prep(dtype)
+        return e[0]
+
+    def _refresh_prep(self, dtype):
+        from . import _abi
+        from .ops import dtcode, stream
+        tab = self._prep_tables.get(dtype)
+        if tab is None:
+            ents = [e for (n, m, d), e in self._prep.items() if d == dtype]
+            rec = np.zeros(len(ents), dtype=np.dtype([('w', '<u8'), ('wt', '<u8'), ('start', '<i8'), ('Cout', '<i4'),
+                                                       ('Cin', '<i4'), ('ks', '<i4'), ('mode', '<i4')]))
+            start = 0
+            for i, e in enumerate(ents):
+                wp, tp, Cout, Cin, ks, mode = e[2]
+                rec[i] = (wp, tp, start, Cout, Cin, ks, mode)
+                start += Cout * ks * ks * Cin
+            dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+            tab = (dev, len(ents), start, ents)
+            self._prep_tables[dtype] = tab
+        dev, n, total, ents = tab
+        _abi.call("rod_conv_weight_prep_batch", dev, n, total, dtcode(ents[0][0]), stream())
+        for e in ents:
+            e[1] = self.version
 
     # ---- checkpointing -------------------------------------------------------------
     def state_dict(self):
@@ -117,6 +163,7 @@ class ParamStore:
                     missing.append(n)
                     continue
                 p.copy_(sd[n].to(p.device).view(p.shape))
+        self.version += 1
         if strict and missing:
             raise KeyError(f"missing entries in checkpoint: {missing[:5]}{'...' if len(missing) > 5 else ''}")
         return missing

@@ -21,25 +21,28 @@ MI355X_F32_PEAK_TFLOPS = 157.3    # f32 MFMA / vector
 def cost(name, a):
     """(bytes, flops) of the call rod_<name>(*a)."""
     # ABI 3: rod_dw3x3_fwd / _bwd_filter / rod_conv_fwd / _wgrad carry the five BatchNorm
-    # prologue arguments after x (P = 5 positions)
+    # prologue arguments after x (P = 5 positions); ABI 4: rod_conv_fwd (after stat_parts)
+    # and rod_dw3x3_bwd_data (after dx) the seven gred arguments
     if name == "rod_dw3x3_fwd":
         N, H, W, C, Ho, Wo, dt = a[9], a[10], a[11], a[12], a[16], a[17], a[18]
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
     if name == "rod_dw3x3_bwd_data":
-        N, H, W, C, Ho, Wo, dt = a[3], a[4], a[5], a[6], a[10], a[11], a[12]
+        N, H, W, C, Ho, Wo, dt = a[10], a[11], a[12], a[13], a[17], a[18], a[19]
         es = _ES[dt]
-        return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
+        gred = es * N * H * W * C if a[9] is not None else 0   # the epilogue reads y
+        return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C + gred, 18 * N * Ho * Wo * C
     if name == "rod_dw3x3_bwd_filter":
         N, H, W, C, Ho, Wo, dt = a[9], a[10], a[11], a[12], a[16], a[17], a[18]
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
     if name == "rod_conv_fwd":
-        N, H, W, Cin, Cout, ks, dt = a[11], a[12], a[13], a[14], a[15], a[16], a[19]
+        N, H, W, Cin, Cout, ks, dt = a[18], a[19], a[20], a[21], a[22], a[23], a[26]
         es = _ES[dt]
         M = N * H * W
         K = ks * ks * Cin
-        return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[7] is not None else 0), 2 * M * K * Cout
+        gred = es * M * Cout if a[17] is not None else 0   # the gred epilogue reads y
+        return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[7] is not None else 0) + gred, 2 * M * K * Cout
     if name == "rod_conv_wgrad":
         N, H, W, Cin, Cout, ks, dt = a[10], a[11], a[12], a[13], a[14], a[15], a[18]
         es = _ES[dt]
@@ -56,6 +59,9 @@ def cost(name, a):
     if name == "rod_bn_bwd":
         M, C, dt = a[10], a[11], a[16]
         return _ES[dt] * M * C * 3, 16 * M * C  # algorithmic: read dy, read x, write dx
+    if name == "rod_bn_bwd_apply":
+        M, C, dt = a[8], a[9], a[11]
+        return _ES[dt] * M * C * 3, 8 * M * C   # read dz, read y, write dy
     if name == "rod_match_anchors":
         B, A, G = a[12], a[13], a[14]
         return B * A * 56 + A * 32 + B * G * 20, 15 * G * A * B
@@ -67,7 +73,7 @@ def cost(name, a):
 ENTRY_KERNELS = {
     "rod_bn_bwd": ("bn_bwd_apply_kernel", ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel", "bn_bwd_apply_kernel")),
     "rod_bn_apply": ("bn_apply_kernel", ("bn_apply_kernel",)),
-    "rod_dw3x3_fwd": ("dw3x3_fwd_kernel", ("dw3x3_fwd_kernel",)),
+    "rod_dw3x3_fwd": ("dw3x3_fwd_", ("dw3x3_fwd_",)),
     "rod_dw3x3_bwd_data": ("dw3x3_bwd_data", ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": ("dw3x3_bwd_filter_kernel", ("dw3x3_bwd_filter_kernel",)),
     "rod_bn_finalize": ("bn_parts_merge_kernel", ("bn_parts_merge_kernel",)),

@@ -208,6 +208,7 @@ class optimizer(object):
 
     def step(self):
         ops.sgd_clip_(self.store.flat, self.store.flat_grad, self.lr, self.clip)
+        self.store.version += 1   # derived weight layouts are refreshed (one batched launch) on next use
         self.global_step += 1
 
 

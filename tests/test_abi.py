@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().rod_abi_version() == 3
+    assert _abi.lib().rod_abi_version() == 4
 
 
 def test_invalid_arguments_raise_with_message():
@@ -28,8 +28,8 @@ def test_invalid_arguments_raise_with_message():
         _abi.call('rod_dw3x3_fwd', None, None, None, None, None, 0, None, None, None, 0, 8, 8, 8, 1, 1, 1, 8, 8, 0,
                   None)
     with pytest.raises(RuntimeError, match='ksize'):
-        _abi.call('rod_conv_fwd', None, None, None, None, None, 0, None, None, None, None, None, 1, 4, 4, 8, 8, 5, 0,
-                  0, 0, None)
+        _abi.call('rod_conv_fwd', None, None, None, None, None, 0, None, None, None, None, None,
+                  None, None, None, None, None, 0, None, 1, 4, 4, 8, 8, 5, 0, 0, 0, None)
     with pytest.raises(RuntimeError, match='dtype'):
         _abi.call('rod_conv_weight_prep', None, None, 8, 8, 1, 0, 7, None)
     with pytest.raises(RuntimeError, match='offsets'):

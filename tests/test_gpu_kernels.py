@@ -348,7 +348,10 @@ def _pending_pair(dev, dtype, shape, act, gamma, seed):
 def _fused_vs_materialised(dev, dtype, shape, act, gamma, consumer, seed):
     """consumer(x) on ops.Pending (BatchNorm-apply in the load prologue, BatchNorm backward in
     the consumer's backward) against consumer(materialize(Pending)) (rod_bn_apply + the plain
-    kernel): forward bit-exact, gradients of y / gamma / beta / weights bit-exact."""
+    kernel): forward and the consumer's weight gradient bit-exact; the gradients of y / gamma /
+    beta agree to fp32 summation order (the fused path reduces the BatchNorm-backward sums in
+    the backward-data epilogue, per 128-row tile or per block, rod_bn_bwd_finalize) — for bf16
+    dy that is at most one bf16 rounding step."""
     y0, ga, be = _pending_pair(dev, dtype, shape, act, gamma, seed)
     outs = []
     for fused in (True, False):
@@ -362,9 +365,16 @@ def _fused_vs_materialised(dev, dtype, shape, act, gamma, consumer, seed):
         out.backward(gy)
         outs.append((out.detach().clone(), y.grad.clone(), None if ga is None else ga._rod_grad.clone(),
                      be._rod_grad.clone(), wgrad().clone()))
-    for a, b in zip(*outs):
-        if a is not None:
+    for i, (a, b) in enumerate(zip(*outs)):
+        if a is None:
+            continue
+        if i in (0, 4):
             assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+        else:
+            af, bf = a.float().cpu(), b.float().cpu()
+            scale = float(bf.abs().max()) + 1e-30
+            tol = 1e-5 if (i > 1 or dtype == torch.float32) else 8e-3
+            torch.testing.assert_close(af, bf, rtol=tol, atol=tol * scale)
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])

@@ -27,7 +27,7 @@ def main():
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--out', default=None)
     ap.add_argument('--check', default=None)
-    ap.add_argument('--ops', default='fwd,fwdpro,bwd_data,bwd_filter')
+    ap.add_argument('--ops', default='fwd,fwdpro,bwd_data,bwd_data_gred,bwd_filter')
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == 'bf16' else torch.float32
     code = _abi.ROD_BF16 if a.dtype == 'bf16' else _abi.ROD_F32
@@ -58,13 +58,16 @@ def main():
                           device=dev)
         fws = _abi.query('rod_bn_finalize_workspace', nparts, C)
         fwsb = torch.empty(max(16, fws), dtype=torch.uint8, device=dev) if fws else None
+        gparts = torch.empty((_abi.lib().rod_dw3x3_bwd_data_gred_parts(N, H, W, C, S, code), 2, C), device=dev)
         io = es * (N * H * W * C + N * Ho * Wo * C)
         calls = {
             'fwd': lambda: _abi.call('rod_dw3x3_fwd', x, None, None, None, None, 0, w, y, None, N, H, W, C, S, pt,
                                      pl, Ho, Wo, code, s),
             'fwdpro': lambda: _abi.call('rod_dw3x3_fwd', x, mean, rstd, gamma, beta, 1, w, y, parts, N, H, W, C, S,
                                         pt, pl, Ho, Wo, code, s),
-            'bwd_data': lambda: _abi.call('rod_dw3x3_bwd_data', dy, w, dx, N, H, W, C, S, pt, pl, Ho, Wo, code, s),
+            'bwd_data': lambda: _abi.call('rod_dw3x3_bwd_data', dy, w, dx, None, None, None, None, None, 0, None, N, H, W, C, S, pt, pl, Ho, Wo, code, s),
+            'bwd_data_gred': lambda: _abi.call('rod_dw3x3_bwd_data', dy, w, dx, x, mean, rstd, gamma, beta, 1, gparts,
+                                               N, H, W, C, S, pt, pl, Ho, Wo, code, s),
             'bwd_filter': lambda: _abi.call('rod_dw3x3_bwd_filter', x, mean, rstd, gamma, beta, 1, dy, dw, wsb, N, H,
                                             W, C, S, pt, pl, Ho, Wo, code, s),
         }
@@ -88,7 +91,7 @@ def main():
             elif op == 'fwdpro':
                 _abi.call('rod_bn_finalize', parts, nparts, N * Ho * Wo, C, 1e-3, 0.997, mu, rs, None, None, fwsb, s)
                 results[key] = (y.float().cpu(), mu.cpu(), rs.cpu())
-            elif op == 'bwd_data':
+            elif op in ('bwd_data', 'bwd_data_gred'):
                 results[key] = dx.float().cpu()
             else:
                 results[key] = dw.cpu()
