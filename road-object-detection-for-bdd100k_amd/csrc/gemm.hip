@@ -215,7 +215,10 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   constexpr int LDC = BN + EV;
   constexpr int MAIN_BYTES = (BM + BN) * LD * sizeof(T);
   constexpr int EPI_BYTES = VY ? 64 * LDC * sizeof(T) : 0;
-  constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  // STATS final reduction scratch (reuses the staging area): 2*256*EV + 256 + 3*TPC*BN + BN floats
+  constexpr int ST_BYTES = (VY && STATS) ? (2 * 256 * EV + 256 + 3 * (256 / BN > 0 ? 256 / BN : 1) * BN + BN) * 4 : 0;
+  constexpr int SM1 = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  constexpr int SMEM = SM1 > ST_BYTES ? SM1 : ST_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   T* As = (T*)smem;
   T* Bs = As + BM * LD;
@@ -325,12 +328,11 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     }
     T* Cs = (T*)smem;
     constexpr int WROWS = BM / WM;  // rows per wave
-    // BatchNorm partial statistics of this 128-row tile (STATS): TPC threads per column
-    // walk the staged (already rounded) rows of each half; (n, mean, M2) Chan-merged
-    constexpr int TPC = 256 / BN > 0 ? 256 / BN : 1;
-    const int scol = tid % BN, spart = tid / BN;
-    const bool sact = STATS && spart < TPC && n0 + scol < Cout;
-    float st_n = 0.f, st_mean = 0.f, st_m2 = 0.f;
+    // BatchNorm partial statistics of this 128-row tile (STATS) and the gred sums (GRED) walk
+    // the staged (already rounded) rows of each half: a thread owns one EV-wide column chunk
+    // and the rows GRPP apart, reading 16-byte LDS chunks.  STATS: one pass of sums shifted by
+    // a pivot per column common to the whole tile (the mean of its first <= 8 rows, so the
+    // shifted sums do not cancel), combined over the row groups by plain addition.
     // GRED: BatchNorm-backward sums of this tile's rounded outputs (dz, staged in Cs) against
     // y_in; a thread owns one EV-wide column chunk and walks rows GRPP apart, so each pass of
     // the block reads whole 16-byte row segments of y_in (coalesced, all loads independent)
@@ -339,6 +341,12 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     const int gcc = (tid % GCPR) * EV, grg = tid / GCPR;
     const int gcol = n0 + gcc;
     const bool gact = GRED && grg < GRPP && gcol < Cout;
+    const bool sact = STATS && grg < GRPP && gcol < Cout;
+    constexpr int SVN = STATS ? EV : 1;
+    float spv[SVN], smu[SVN], sm2[SVN];  // pivot-shifted sums, then (mean, M2)
+    float scnt = 0.f;
+#pragma unroll
+    for (int v = 0; v < SVN; ++v) spv[v] = smu[v] = sm2[v] = 0.f;
     constexpr int GV = GRED ? EV : 1;
     float gsc[GV], gsh[GV], gmu[GV], grs[GV], gs[GV], gsx[GV];
 #pragma unroll
@@ -387,20 +395,32 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
       if constexpr (STATS) {
         const long left = M - (m0 + h * 64);
         const int nrows = left < 64 ? (int)left : 64;
-        if (sact && nrows > 0) {
-          float sum = 0.f, cnt = 0.f;
-          for (int r = spart; r < nrows; r += TPC) {
-            sum += to_f32(Cs[r * LDC + scol]);
-            cnt += 1.f;
-          }
-          if (cnt > 0.f) {
-            const float mu = sum / cnt;
-            float q = 0.f;
-            for (int r = spart; r < nrows; r += TPC) {
-              const float d = to_f32(Cs[r * LDC + scol]) - mu;
-              q = fmaf(d, d, q);
+        if (sact) {
+          if (h == 0) {  // the column's pivot: mean of the tile's first (up to) 8 rows, same in every thread
+            const int np = nrows < 8 ? nrows : 8;
+#pragma unroll
+            for (int v = 0; v < SVN; ++v) spv[v] = 0.f;
+            for (int r = 0; r < np; ++r) {
+              Vec16<T> pv;
+              pv.v = *(const decltype(pv.v)*)(Cs + r * LDC + gcc);
+#pragma unroll
+              for (int v = 0; v < SVN; ++v) spv[v] += pv.get(v);
             }
-            chan_merge(st_n, st_mean, st_m2, cnt, mu, q);
+            const float inv = 1.f / (float)np;
+#pragma unroll
+            for (int v = 0; v < SVN; ++v) spv[v] *= inv;
+          }
+#pragma unroll 2
+          for (int r = grg; r < nrows; r += GRPP) {
+            Vec16<T> dv;
+            dv.v = *(const decltype(dv.v)*)(Cs + r * LDC + gcc);
+#pragma unroll
+            for (int v = 0; v < SVN; ++v) {
+              const float d = dv.get(v) - spv[v];
+              smu[v] += d;
+              sm2[v] = fmaf(d, d, sm2[v]);
+            }
+            scnt += 1.f;
           }
         }
       }
@@ -440,15 +460,51 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
       }
     }
     if constexpr (STATS) {
-      __shared__ float sred[3][256];
-      sred[0][tid] = st_n;
-      sred[1][tid] = st_mean;
-      sred[2][tid] = st_m2;
+      // per column (common pivot k): the GRPP row groups -> TPC interleaved slices (stage A, all
+      // threads) -> the slices in order (stage B, one thread per column): plain sums of
+      // (v - k), (v - k)^2 and the count -> (n, k + S1/n, S2 - S1^2/n) of part blockIdx.x
+      constexpr int TPC = 256 / BN > 0 ? 256 / BN : 1;
+      float* r1 = (float*)smem;          // [256][EV]
+      float* r2 = r1 + 256 * EV;         // [256][EV]
+      float* rc = r2 + 256 * EV;         // [256]
+      float* pa = rc + 256;              // [3][TPC][BN]
+      float* pv = pa + 3 * TPC * BN;     // [BN]
       __syncthreads();
-      if (sact && spart == 0) {
-        for (int q = 1; q < TPC; ++q)
-          chan_merge(st_n, st_mean, st_m2, sred[0][q * BN + scol], sred[1][q * BN + scol], sred[2][q * BN + scol]);
-        store_stat_part(part, Cout, blockIdx.x, n0 + scol, st_n, st_mean, st_m2);
+#pragma unroll
+      for (int v = 0; v < SVN; ++v) {
+        r1[tid * EV + v] = smu[v];
+        r2[tid * EV + v] = sm2[v];
+      }
+      rc[tid] = scnt;
+      if (sact && grg == 0) {
+#pragma unroll
+        for (int v = 0; v < SVN; ++v) pv[gcc + v] = spv[v];
+      }
+      __syncthreads();
+      if (tid < TPC * BN) {
+        const int col = tid % BN, j = tid / BN;
+        const int ch = col / EV, v = col - ch * EV;
+        float a = 0.f, b = 0.f, nn = 0.f;
+        for (int q = j; q < GRPP; q += TPC) {
+          const int t2 = q * GCPR + ch;
+          a += r1[t2 * EV + v];
+          b += r2[t2 * EV + v];
+          nn += rc[t2];
+        }
+        pa[(0 * TPC + j) * BN + col] = a;
+        pa[(1 * TPC + j) * BN + col] = b;
+        pa[(2 * TPC + j) * BN + col] = nn;
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < Cout) {
+        float a = 0.f, b = 0.f, nn = 0.f;
+        for (int j = 0; j < TPC; ++j) {
+          a += pa[(0 * TPC + j) * BN + tid];
+          b += pa[(1 * TPC + j) * BN + tid];
+          nn += pa[(2 * TPC + j) * BN + tid];
+        }
+        const float dm = nn > 0.f ? a / nn : 0.f;
+        store_stat_part(part, Cout, blockIdx.x, n0 + tid, nn, pv[tid] + dm, fmaxf(b - a * dm, 0.f));
       }
     }
   } else {
