@@ -642,6 +642,209 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
   }
 }
 
+// Filter gradient on the LDS-exchange engine: dw[i][j][c] = sum dy[n,ho,wo,c] *
+// z[n, ho*S-pt+i, wo*S-pl+j, c], z = the forward's input (BatchNorm prologue applied when
+// PACT >= 0).  Input rows stream exactly as in dw3x3_fwd_lx_kernel (register ring, one LDS
+// exchange per row); dy of the thread's own output column rides a register queue loaded three
+// (S=2: five) input rows ahead; the 9 taps accumulate in fp32 registers; per block the
+// computing columns are summed per channel in column order into part (n*strips + strip)*
+// coltiles + ct of the [parts][9][C] slab (channels of cgroup cg).
+template <typename T, int S, int PACT>
+__global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                            float* __restrict__ slab, int H, int W, int C, int pt,
+                                                            int pl, int Ho, int Wo, DwTile tl, BnPro pro) {
+  constexpr int V = Vec16<T>::N;
+  constexpr int XS = 2 * 256 * 16;
+  constexpr int SS = 256 * V * 4;
+  __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
+  T* xs = (T*)smem;
+  const int tid = threadIdx.x;
+  const int CVb = tl.CVb, P = tl.P;
+  const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
+  int bx, strip, n;
+  xcd_block(bx, strip, n);
+  const int cg = bx % tl.cgroups, ct = bx / tl.cgroups;
+  const int c = (cg * CVb + cvb) * V;
+  const int wo0 = ct * tl.TWo;
+  const int ho0 = strip * tl.RB;
+  const int ho1 = ho0 + tl.RB < Ho ? ho0 + tl.RB : Ho;
+  constexpr int HL = S == 1 ? 1 : 0;
+  const int wo = wo0 + p - HL;
+  const bool comp = p >= HL && p <= P - 2 && wo < Wo;
+  const int ci0 = S == 1 ? wo0 + p - pl : 2 * (wo0 + p) - pl;
+  const bool cok0 = p < P && ci0 >= 0 && ci0 < W;
+  const bool cok1 = S == 2 && p < P && ci0 + 1 >= 0 && ci0 + 1 < W;
+  DwIn<T, V, PACT> in;
+  in.init(pro, c);
+  const T* xn = x + (long)n * H * W * C + c;
+  const T* dn = dy + (long)n * Ho * Wo * C + c;
+  const int nout = ho1 - ho0;
+
+  float acc[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
+
+  auto cvt = [&](const Vec16<T>& r, bool ok, float (&o)[V]) {
+    PackV<T, V> pk;
+    pk.v = r.v;
+    in.cvt(pk, ok, o);
+    if constexpr (PACT < 0) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) o[v] = ok ? o[v] : 0.f;
+    }
+  };
+  auto publish = [&](const float (&o)[V], int buf) {
+    Vec16<T> st;
+#pragma unroll
+    for (int v = 0; v < V; ++v) st.set(v, o[v]);
+    st.store(xs + (buf * 256 + tid) * V);
+  };
+  // dy of output row m (own column), zero outside the strip
+  auto dload = [&](Vec16<T>& d, int m) {
+    if (comp && m >= 0 && m < nout) d.load(dn + ((long)(ho0 + m) * Wo + wo) * C);
+    else {
+#pragma unroll
+      for (int v = 0; v < V; ++v) d.set(v, 0.f);
+    }
+  };
+  auto addrow = [&](int i, const Vec16<T>& d, const float (&t0)[V], const float (&t1)[V], const float (&t2)[V]) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float g = d.get(v);
+      acc[i * 3][v] = fmaf(g, t0[v], acc[i * 3][v]);
+      acc[i * 3 + 1][v] = fmaf(g, t1[v], acc[i * 3 + 1][v]);
+      acc[i * 3 + 2][v] = fmaf(g, t2[v], acc[i * 3 + 2][v]);
+    }
+  };
+
+  if constexpr (S == 1) {
+    const int hi0 = ho0 - pt;
+    const int nin = nout + 2;
+    Vec16<T> ring[3];
+    bool rok[3];
+    auto issue = [&](int k, int q) {
+      const int hi = hi0 + q;
+      rok[k] = cok0 && q < nin && hi >= 0 && hi < H;
+      if (rok[k]) ring[k].load(xn + ((long)hi * W + ci0) * C);
+    };
+    issue(0, 0);
+    issue(1, 1);
+    issue(2, 2);
+    // dy queue: d0 = output q, d1 = q-1, d2 = q-2 at input row q; f1, f2 = q+1, q+2 in flight
+    Vec16<T> d0, d1, d2, f1, f2;
+    dload(d0, 0);
+    dload(d1, -1);
+    dload(d2, -2);
+    dload(f1, 1);
+    dload(f2, 2);
+    for (int q0 = 0; q0 < nin; q0 += 3) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int q = q0 + k;
+        const int buf = q & 1;
+        float cen[V];
+        cvt(ring[k], rok[k], cen);
+        issue(k, q + 3);
+        publish(cen, buf);
+        __syncthreads();
+        if (comp) {
+          Vec16<T> L, R;
+          L.load(xs + (buf * 256 + tid - CVb) * V);
+          R.load(xs + (buf * 256 + tid + CVb) * V);
+          float l[V], r[V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            l[v] = L.get(v);
+            r[v] = R.get(v);
+          }
+          // row q is tap row i of output q - i
+          addrow(0, d0, l, cen, r);
+          addrow(1, d1, l, cen, r);
+          addrow(2, d2, l, cen, r);
+        }
+        d2 = d1;
+        d1 = d0;
+        d0 = f1;
+        f1 = f2;
+        dload(f2, q + 3);
+      }
+    }
+  } else {
+    const int hi0 = 2 * ho0 - pt;
+    const int nin = 2 * nout + 1;
+    Vec16<T> ring[4][2];
+    bool rok[4][2];
+    auto issue = [&](int k, int q) {
+      const int hi = hi0 + q;
+      const bool rowok = q < nin && hi >= 0 && hi < H;
+      rok[k][0] = rowok && cok0;
+      rok[k][1] = rowok && cok1;
+      if (rok[k][0]) ring[k][0].load(xn + ((long)hi * W + ci0) * C);
+      if (rok[k][1]) ring[k][1].load(xn + ((long)hi * W + ci0 + 1) * C);
+    };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) issue(k, k);
+    // dy queue at input row q = 2m (+1): dm1 = output m-1, dm = m; f1, f2 = m+1, m+2 in flight
+    Vec16<T> dm1, dm, f1, f2;
+    dload(dm1, -1);
+    dload(dm, 0);
+    dload(f1, 1);
+    dload(f2, 2);
+    for (int q0 = 0; q0 < nin; q0 += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = q0 + k;
+        const int buf = q & 1;
+        float c0[V], c1[V];
+        cvt(ring[k][0], rok[k][0], c0);
+        cvt(ring[k][1], rok[k][1], c1);
+        issue(k, q + 4);
+        publish(c0, buf);
+        __syncthreads();
+        if (comp) {
+          Vec16<T> R;
+          R.load(xs + (buf * 256 + tid + CVb) * V);
+          float r[V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) r[v] = R.get(v);
+          if ((k & 1) == 0) {   // q = 2m: tap row 0 of output m, tap row 2 of output m-1
+            addrow(0, dm, c0, c1, r);
+            addrow(2, dm1, c0, c1, r);
+          } else {              // q = 2m+1: tap row 1 of output m
+            addrow(1, dm, c0, c1, r);
+          }
+        }
+        if (k & 1) {  // next input row starts output m+1
+          dm1 = dm;
+          dm = f1;
+          f1 = f2;
+          dload(f2, (q >> 1) + 3);
+        }
+      }
+    }
+  }
+
+  // per channel: sum over the computing columns (column order), tap by tap
+  __syncthreads();
+  float* red = (float*)smem;
+  const int Cc = CVb * V;
+  const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+  for (int k = 0; k < 9; ++k) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) red[tid * V + v] = acc[k][v];
+    __syncthreads();
+    for (int e = tid; e < Cc; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      float a = 0.f;
+      for (int pp = HL; pp <= P - 2; ++pp) a += red[(pp * CVb + cve) * V + v];
+      slab[(part * 9 + k) * C + cg * Cc + e] = a;
+    }
+    __syncthreads();
+  }
+}
+
 // dx[n,h,w,c] = sum_{i,j} dy[n,(h+pt-i)/S,(w+pl-j)/S,c] * w[i,j,c] over exact divisions.
 // S=1: the three dy rows h+pt-i roll down in registers; S=2: direct loads (each dx pixel
 // sees 1, 2 or 4 dy pixels).
@@ -1251,6 +1454,8 @@ size_t rod_dw3x3_bwd_filter_workspace(int N, int Ho, int Wo, int C) {
   for (int V : {1, 4, 8}) {
     if (C % V) continue;
     for (int es : {2, 4}) parts = std::max(parts, dw_filter_plan(N, Ho, Wo, C, V, es).parts());
+    if (V >= 4)
+      for (int S : {1, 2}) parts = std::max(parts, dw_lx_parts(N, Ho, Wo, C, S, V));
   }
   return (size_t)parts * 9 * C * sizeof(float);
 }
@@ -1265,7 +1470,28 @@ int rod_dw3x3_bwd_filter(const void* x, const float* pro_mean, const float* pro_
   float* slab = (float*)workspace;
   const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
   const BnPro* pp = pro_mean ? &pro : nullptr;
-  if (dtype == ROD_F32) {
+  auto lx = [&](auto tag) {  // LDS-exchange kernel (16-byte packs)
+    typedef decltype(tag) T;
+    const DwTile t = dw_tile(N, Ho, Wo, C, stride, Vec16<T>::N);
+    const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
+    const BnPro pv = pp ? *pp : BnPro{};
+    const int pa = !pp ? -1 : (pp->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
+#define DWW(S_, PA)                                                                                               \
+  hipLaunchKernelGGL((dw3x3_bwdw_lx_kernel<T, S_, PA>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, H, W, \
+                     C, pad_t, pad_l, Ho, Wo, t, pv)
+    if (stride == 1) {
+      if (pa == ROD_ACT_RELU6) DWW(1, ROD_ACT_RELU6); else if (pa == 3) DWW(1, 3); else DWW(1, -1);
+    } else {
+      if (pa == ROD_ACT_RELU6) DWW(2, ROD_ACT_RELU6); else if (pa == 3) DWW(2, 3); else DWW(2, -1);
+    }
+#undef DWW
+    slab_sum(slab, dw, (int)((long)N * t.strips * t.coltiles), 9L * C, s);
+  };
+  if (dtype == ROD_F32 && dw_lx_ok<float>(x, dy, C)) {
+    lx(float{});
+  } else if (dtype == ROD_BF16 && dw_lx_ok<bf16_t>(x, dy, C)) {
+    lx(bf16_t{});
+  } else if (dtype == ROD_F32) {
     const int pk = dw_pack<float>(x, dy, C, 4);
     DW_SELECT(dw_bwd_filter_launch, float, pk, x, pp, dy, dw, slab, N, H, W, C, pad_t, pad_l, Ho, Wo, s);
   } else if (dtype == ROD_BF16) {
