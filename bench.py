@@ -47,6 +47,9 @@ def parse():
                     help='per-entry HBM bytes per launch from rocprofv3 PMC passes (tools/pmc_traffic.py)')
     ap.add_argument('--cpu-baseline', dest='cpu_baseline', action='store_true', default=True)
     ap.add_argument('--no-cpu-baseline', dest='cpu_baseline', action='store_false')
+    ap.add_argument('--kernel-steps', dest='kernel_steps', type=int, default=2,
+                    help='extra steps AFTER the timed region with the north-star kernels probed '
+                         '("kernels" in the JSON: dw3x3 / pw GEMM / BN-backward rooflines); 0 = off')
     ap.add_argument('--inference', dest='inference', action='store_true', default=True)
     ap.add_argument('--no-inference', dest='inference', action='store_false')
     return ap.parse_args()
@@ -115,6 +118,41 @@ def inference_fps(args, dev, dtype, batch=32, steps=5, warmup=2):
             'mAP@0.5': None, 'mAP_note': 'no BDD100K data or trained checkpoint on the box (synthetic inputs)'}
 
 
+NORTH_STAR = ('rod_dw3x3_fwd', 'rod_dw3x3_bwd_data', 'rod_dw3x3_bwd_filter', 'rod_conv_fwd', 'rod_conv_wgrad',
+              'rod_bn_bwd')
+
+
+def kernel_rooflines(tr, batch, steps, dtype):
+    """Per-entry rooflines of the north-star kernels (depthwise 3x3, the pointwise / 3x3 GEMMs,
+    the BatchNorm backward), timed with HIP events around every call of `steps` extra training
+    steps run after the timed region (so the headline number carries no probe overhead).
+    Aggregate over all calls of the entry, and its single most expensive call shape."""
+    from rod import _abi, roofline
+    _abi.PROBE.arm(NORTH_STAR)
+    for _ in range(steps):
+        tr.step(*batch)
+    torch.cuda.synchronize()
+    _abi.PROBE.disarm()
+    agg = _abi.PROBE.table()
+    by_shape = _abi.PROBE.table(by_shape=True)
+    peak_tf = roofline.MI355X_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else roofline.MI355X_F32_PEAK_TFLOPS
+    out = {}
+    for name in NORTH_STAR:
+        if name not in agg:
+            continue
+        n, ms, b, fl = agg[name]
+        top = max(((k, v) for k, v in by_shape.items() if k[0] == name), key=lambda kv: kv[1][1])
+        tn, tms, tb, tfl = top[1]
+        gbs, tgbs = b / ms / 1e6, tb / tms / 1e6
+        out[name] = {'launches_per_step': n // steps, 'ms_per_step': round(ms / steps, 3),
+                     'alg_GBps': round(gbs, 1), 'hbm_frac': round(gbs / roofline.MI355X_HBM_PEAK_GBS, 4),
+                     'alg_TFLOPs': round(fl / ms / 1e9, 2), 'mfma_frac': round(fl / ms / 1e9 / peak_tf, 5),
+                     'top_call': {'args': list(top[0][1]), 'avg_us': round(1e3 * tms / tn, 1),
+                                  'alg_GBps': round(tgbs, 1), 'hbm_frac': round(tgbs / roofline.MI355X_HBM_PEAK_GBS, 4),
+                                  'alg_TFLOPs': round(tfl / tms / 1e9, 2)}}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -163,6 +201,9 @@ def main():
     table = _abi.PROBE.table()
     n_launch, ms, byts, flops = table.get(args.probe, (0, 0.0, 0, 0))
     loss_val = float(losses[0].item())
+    kernels = None
+    if args.kernel_steps > 0 and world == 1:
+        kernels = kernel_rooflines(tr, batch, args.kernel_steps, dtype)
     if args.probe_table and rank == 0:
         # per-entry live timing (every call bracketed by events; the step itself is slower
         # in this mode, so ms_per_step of such a run is not a bench number)
@@ -219,6 +260,8 @@ def main():
             'loss': round(loss_val, 5),
             'roofline': rl,
         }
+        if kernels is not None:
+            out['kernels'] = kernels
         if args.inference and world == 1:
             out['inference'] = inference_fps(args, dev, dtype)
         if args.cpu_baseline and world == 1:

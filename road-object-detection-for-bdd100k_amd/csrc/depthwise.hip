@@ -352,11 +352,10 @@ __device__ __forceinline__ void lds_barrier() {
 // backward-data (DepthwiseConv2dNativeBackpropInput) is this kernel on dy with pads
 // (2-pt, 2-pl).  GRED: the BatchNorm-backward partial sums of the rounded outputs against the
 // pre-BatchNorm y of the layer below (rod_common.h), y prefetched two rows ahead.
-template <typename T, int S, int PACT, bool STATS, bool FLIP = false, bool GRED = false>
-__global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                           T* __restrict__ y, int H, int W, int C, int pt, int pl,
-                                                           int Ho, int Wo, DwTile tl, float* __restrict__ parts,
-                                                           BnPro pro, BnGred gr = BnGred{}) {
+template <typename T, int S, int PACT, bool STATS, bool FLIP, bool GRED>
+__device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float* __restrict__ w, T* __restrict__ y,
+                                           int H, int W, int C, int pt, int pl, int Ho, int Wo, const DwTile& tl,
+                                           float* __restrict__ parts, const BnPro& pro, const BnGred& gr) {
   static_assert(S == 1 || !(FLIP || GRED), "the backward-data form is stride 1");
   constexpr int V = Vec16<T>::N;
   // LDS: prefetch ring of D input rows (S=2: column pairs) + the double-buffered exchange
@@ -640,6 +639,21 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__
       store_stat_part(parts, C, part, cg * Cc + ch, pn, pm, pq);
     }
   }
+}
+
+template <typename T, int S, int PACT, bool STATS>
+__global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                           T* __restrict__ y, int H, int W, int C, int pt, int pl,
+                                                           int Ho, int Wo, DwTile tl, float* __restrict__ parts,
+                                                           BnPro pro) {
+  dw_lx_body<T, S, PACT, STATS, false, false>(x, w, y, H, W, C, pt, pl, Ho, Wo, tl, parts, pro, BnGred{});
+}
+// stride-1 backward-data (DepthwiseConv2dNativeBackpropInput): the body with flipped taps
+template <typename T, bool GRED>
+__global__ void __launch_bounds__(256) dw3x3_bwd_data_lx_kernel(const T* __restrict__ dy, const float* __restrict__ w,
+                                                                T* __restrict__ dx, int Ho, int Wo, int C, int pt,
+                                                                int pl, int H, int W, DwTile tl, BnGred gr) {
+  dw_lx_body<T, 1, -1, false, true, GRED>(dy, w, dx, Ho, Wo, C, pt, pl, H, W, tl, nullptr, BnPro{}, gr);
 }
 
 // Filter gradient on the LDS-exchange engine: dw[i][j][c] = sum dy[n,ho,wo,c] *
@@ -1288,11 +1302,11 @@ static long dw_bwd_data_lx_launch(const void* dy, const float* w, void* dx, cons
   const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
   const BnGred g = gr ? *gr : BnGred{};
   if (gr)
-    hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, 1, -1, false, true, true>), grid, dim3(256), 0, s, (const T*)dy, w,
-                       (T*)dx, Ho, Wo, C, 2 - pt, 2 - pl, H, W, t, nullptr, BnPro{}, g);
+    hipLaunchKernelGGL((dw3x3_bwd_data_lx_kernel<T, true>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, Ho, Wo,
+                       C, 2 - pt, 2 - pl, H, W, t, g);
   else
-    hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, 1, -1, false, true, false>), grid, dim3(256), 0, s, (const T*)dy, w,
-                       (T*)dx, Ho, Wo, C, 2 - pt, 2 - pl, H, W, t, nullptr, BnPro{}, g);
+    hipLaunchKernelGGL((dw3x3_bwd_data_lx_kernel<T, false>), grid, dim3(256), 0, s, (const T*)dy, w, (T*)dx, Ho, Wo,
+                       C, 2 - pt, 2 - pl, H, W, t, g);
   return (long)N * t.strips * t.coltiles;
 }
 

@@ -68,13 +68,16 @@ def cost(name, a):
     return 0, 0
 
 
-# C-ABI entry -> (anchor kernel launched exactly once per entry call, kernel-name substrings of
-# every kernel the entry launches) for attributing rocprofv3 PMC counters (tools/pmc_traffic.py)
+# C-ABI entry -> (kernel-name substrings of which exactly one launches once per entry call,
+# substrings of every kernel the entry launches) for attributing rocprofv3 PMC counters
+# (tools/pmc_traffic.py); shared helper kernels (slab_sum, splitk_combine) are not attributed
 ENTRY_KERNELS = {
-    "rod_bn_bwd": ("bn_bwd_apply_kernel", ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel", "bn_bwd_apply_kernel")),
-    "rod_bn_apply": ("bn_apply_kernel", ("bn_apply_kernel",)),
-    "rod_dw3x3_fwd": ("dw3x3_fwd_", ("dw3x3_fwd_",)),
-    "rod_dw3x3_bwd_data": ("dw3x3_bwd_data", ("dw3x3_bwd_data",)),
-    "rod_dw3x3_bwd_filter": ("dw3x3_bwd_filter_kernel", ("dw3x3_bwd_filter_kernel",)),
-    "rod_bn_finalize": ("bn_parts_merge_kernel", ("bn_parts_merge_kernel",)),
+    "rod_bn_bwd": (("bn_bwd_apply_kernel",), ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel", "bn_bwd_apply_kernel")),
+    "rod_bn_apply": (("bn_apply_kernel",), ("bn_apply_kernel",)),
+    "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
+    "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
+    "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),
+    "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
+    "rod_conv_fwd": (("conv_fwd_kernel", "stem_conv_fwd_kernel"), ("conv_fwd_kernel", "stem_conv_fwd_kernel")),
+    "rod_bn_finalize": (("bn_parts_merge_kernel",), ("bn_parts_merge_kernel",)),
 }

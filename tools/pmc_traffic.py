@@ -5,7 +5,7 @@ Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section)
   * on gfx950 FETCH_SIZE reports 1/2 of the bytes of a wide (16 B/lane) coalesced
     streaming read -> doubled; WRITE_SIZE is exact for 16 B/lane stores.
 An entry's traffic per launch = sum over its kernels (rod/roofline.py ENTRY_KERNELS) of
-the corrected bytes / launches of its anchor kernel (one per entry call).
+the corrected bytes / launches of its anchor kernels (one launch per entry call).
 
 usage: python tools/pmc_traffic.py <fetch csv> <write csv> <out.json> [train_range batch H W dtype]
 (the bench configuration both passes ran; bench.py only uses the file for that configuration)
@@ -39,8 +39,8 @@ def main():
            'fetch_csv': sys.argv[1], 'write_csv': sys.argv[2], 'entries': {},
            'config': [sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7]), sys.argv[8]]
            if len(sys.argv) > 8 else ['REFINE', 8, 720, 1280, 'bf16']}
-    for entry, (anchor, kernels) in ENTRY_KERNELS.items():
-        n = sum(c for k, (c, _) in fetch.items() if anchor in k)
+    for entry, (anchors, kernels) in ENTRY_KERNELS.items():
+        n = sum(c for k, (c, _) in fetch.items() if any(a in k for a in anchors))
         if n == 0:
             continue
         rd = sum(b for k, (_, b) in fetch.items() if any(s in k for s in kernels)) * 2.0
