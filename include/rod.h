@@ -265,6 +265,29 @@ size_t rod_softmax_ce_hnm_workspace(int B, int A, int L);
 int rod_softmax_ce_hnm(const void* logits, const int* det_lbl, const int* det_pos, const float* iou,
                        const int* lvl_off, int L, float bs, float* out, void* grad, void* workspace,
                        int B, int A, int K, int dtype, void* stream);
+/* The same, split at its exchange points for data parallelism (the reference
+ * selects negatives over the WHOLE batch, net_tools.py:557-587).  Per rank, on its B images:
+ *   rod_hnm_rows        -> counts[2] = (n_pos, n_neg) of its rows  [caller: all-reduce SUM]
+ *   rod_hnm_begin       -> state (k from the global counts, B_global = the global batch)
+ *   for shift = 24, 16, 8, 0:
+ *     rod_hnm_radix_hist -> hist[256] of its rows                 [caller: all-reduce SUM]
+ *     rod_hnm_radix_scan -> the next digit of the k-th smallest nvalue (clears hist)
+ *   rod_hnm_loss        -> out / grad of its rows; bs = the GLOBAL batch; out[6] counts
+ *                          this rank's selected negatives
+ * counts (int[2]), state (int[8]) and hist (unsigned[256]) are caller-owned device arrays;
+ * every call is stream-ordered (the all-reduces go on the same stream).  Integer sums make
+ * k and the threshold bit-identical to rod_softmax_ce_hnm on the concatenated batch.
+ * workspace: rod_hnm_workspace() bytes (per rank, kept from rod_hnm_rows to rod_hnm_loss). */
+size_t rod_hnm_workspace(int B, int A, int L);
+int rod_hnm_rows(const void* logits, const int* det_pos, void* workspace, int* counts, int B, int A,
+                 int K, int L, int dtype, void* stream);
+int rod_hnm_begin(const int* counts, int B_global, int* state, unsigned* hist, void* stream);
+int rod_hnm_radix_hist(const void* workspace, int B, int A, int L, int shift, const int* state,
+                       unsigned* hist, void* stream);
+int rod_hnm_radix_scan(int shift, int* state, unsigned* hist, void* stream);
+int rod_hnm_loss(const void* logits, const int* det_lbl, const int* det_pos, const float* iou,
+                 const int* lvl_off, int L, float bs, const int* state, float* out, void* grad,
+                 void* workspace, int B, int A, int K, int dtype, void* stream);
 
 /* ------------------------------------------------ post-processing (A15)
  * detected_bboxes (net_tools.py:739-758) for every image and class 1..K-1: select

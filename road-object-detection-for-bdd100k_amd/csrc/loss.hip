@@ -300,6 +300,44 @@ __global__ void hnm_finalize_kernel(const double* __restrict__ slab, int nb, con
   }
 }
 
+// data-parallel split (rod_hnm_*): the per-rank counts, then k from the all-reduced counts
+__global__ void hnm_sum_counts_kernel(const int* __restrict__ cnt_slab, int nb, int* __restrict__ counts) {
+  __shared__ int s[2][256];
+  int np = 0, nn = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    np += cnt_slab[2 * i];
+    nn += cnt_slab[2 * i + 1];
+  }
+  s[0][threadIdx.x] = np;
+  s[1][threadIdx.x] = nn;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      s[0][threadIdx.x] += s[0][threadIdx.x + w];
+      s[1][threadIdx.x] += s[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    counts[0] = s[0][0];
+    counts[1] = s[1][0];
+  }
+}
+__global__ void hnm_begin_kernel(const int* __restrict__ counts, int B, int* __restrict__ state,
+                                 unsigned* __restrict__ hist) {
+  hist[threadIdx.x] = 0u;
+  if (threadIdx.x == 0) {
+    int k = (int)(3.0f * (float)counts[0]) + B;  // the same arithmetic as hnm_count_kernel
+    k = min(k, counts[1]);
+    state[0] = k;
+    state[1] = 0;
+    state[2] = k;
+    state[3] = counts[0];
+    state[4] = counts[1];
+    state[5] = state[6] = state[7] = 0;
+  }
+}
+
 static int hnm_blocks(long R) { return (int)std::min<long>(cdivl(R, 256), 2048); }
 
 static HnmWs carve(void* ws, long R, int B, int L, int nb) {
@@ -361,6 +399,68 @@ int rod_softmax_ce_hnm(const void* logits, const int* det_lbl, const int* det_po
     hipLaunchKernelGGL(hnm_finalize_kernel, dim3(1), dim3(256), 0, s, w.loss_slab, nb, w.state, bs, out);
   });
   return check_launch("rod_softmax_ce_hnm");
+}
+
+// ---- data-parallel split: per-rank rows, exchange points are counts[2] and hist[256] ----
+size_t rod_hnm_workspace(int B, int A, int L) { return rod_softmax_ce_hnm_workspace(B, A, L); }
+
+int rod_hnm_rows(const void* logits, const int* det_pos, void* workspace, int* counts, int B, int A, int K, int L,
+                 int dtype, void* stream) {
+  ROD_CHECK_ARG(B > 0 && A > 0 && K > 1 && K <= HNM_K && workspace && counts, "rod_hnm_rows: bad arguments");
+  const long R = (long)B * A;
+  const int nb = hnm_blocks(R);
+  HnmWs w = carve(workspace, R, B, L, nb);
+  hipStream_t s = ROD_STREAM(stream);
+  ROD_DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(hnm_rows_kernel<T>, dim3(nb), dim3(256), 0, s, (const T*)logits,
+                                               det_pos, R, K, w.nval, w.cnt_slab));
+  hipLaunchKernelGGL(hnm_sum_counts_kernel, dim3(1), dim3(256), 0, s, w.cnt_slab, nb, counts);
+  return check_launch("rod_hnm_rows");
+}
+
+int rod_hnm_begin(const int* counts, int B_global, int* state, unsigned* hist, void* stream) {
+  ROD_CHECK_ARG(counts && state && hist && B_global > 0, "rod_hnm_begin: bad arguments");
+  hipLaunchKernelGGL(hnm_begin_kernel, dim3(1), dim3(256), 0, ROD_STREAM(stream), counts, B_global, state, hist);
+  return check_launch("rod_hnm_begin");
+}
+
+int rod_hnm_radix_hist(const void* workspace, int B, int A, int L, int shift, const int* state, unsigned* hist,
+                       void* stream) {
+  ROD_CHECK_ARG(workspace && state && hist && (shift == 0 || shift == 8 || shift == 16 || shift == 24),
+                "rod_hnm_radix_hist: bad arguments");
+  const long R = (long)B * A;
+  const int nb = hnm_blocks(R);
+  HnmWs w = carve((void*)workspace, R, B, L, nb);
+  hipLaunchKernelGGL(radix_hist_kernel, dim3(nb), dim3(256), 0, ROD_STREAM(stream), w.nval, R, shift, state, hist);
+  return check_launch("rod_hnm_radix_hist");
+}
+
+int rod_hnm_radix_scan(int shift, int* state, unsigned* hist, void* stream) {
+  ROD_CHECK_ARG(state && hist, "rod_hnm_radix_scan: bad arguments");
+  hipLaunchKernelGGL(radix_scan_kernel, dim3(1), dim3(256), 0, ROD_STREAM(stream), shift, state, hist);
+  return check_launch("rod_hnm_radix_scan");
+}
+
+int rod_hnm_loss(const void* logits, const int* det_lbl, const int* det_pos, const float* iou, const int* lvl_off,
+                 int L, float bs, const int* state, float* out, void* grad, void* workspace, int B, int A, int K,
+                 int dtype, void* stream) {
+  ROD_CHECK_ARG(B > 0 && A > 0 && K > 1 && K <= HNM_K, "rod_hnm_loss: bad shape (K <= 16)");
+  ROD_CHECK_ARG(L >= 1 && L <= HNM_MAXL && lvl_off, "rod_hnm_loss: bad levels");
+  ROD_CHECK_ARG(lvl_off[0] == 0 && lvl_off[L] == A, "rod_hnm_loss: level offsets must span [0, A]");
+  ROD_CHECK_ARG(workspace && out && state, "rod_hnm_loss: workspace/out/state NULL");
+  HnmLevels lv;
+  lv.L = L;
+  for (int i = 0; i <= HNM_MAXL; ++i) lv.off[i] = i <= L ? lvl_off[i] : A;
+  const long R = (long)B * A;
+  const int nb = hnm_blocks(R);
+  HnmWs w = carve(workspace, R, B, L, nb);
+  hipStream_t s = ROD_STREAM(stream);
+  ROD_DISPATCH_DTYPE(dtype, {
+    hipLaunchKernelGGL(iou_group_kernel, dim3(B * L), dim3(256), 0, s, iou, lv, A, w.gstat);
+    hipLaunchKernelGGL(hnm_loss_kernel<T>, dim3(nb), dim3(256), 0, s, (const T*)logits, det_lbl, det_pos, iou, w.nval,
+                       w.gstat, state, lv, R, A, K, 1.0f / bs, (T*)grad, w.loss_slab);
+    hipLaunchKernelGGL(hnm_finalize_kernel, dim3(1), dim3(256), 0, s, w.loss_slab, nb, state, bs, out);
+  });
+  return check_launch("rod_hnm_loss");
 }
 
 }  // extern "C"

@@ -76,5 +76,11 @@ class GradReducer(object):
             b['work'].wait()
         self.reset()
 
+    def hnm_allreduce(self, tensors):
+        """In-place SUM of small device int32 tensors over the ranks, on the compute stream
+        (the hard-negative exchange of net_tools.det_clf_loss)."""
+        for t in tensors:
+            dist.all_reduce(t, group=self.group)
+
     def launched(self):
         return sum(1 for b in self.buckets if b['work'] is not None)

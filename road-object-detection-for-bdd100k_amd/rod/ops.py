@@ -667,6 +667,72 @@ def softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, bs):
     return _SoftmaxCEHNM.apply(logits, det_lbl, det_pos, iou, lvl_off, bs)
 
 
+def hnm_lockstep(shards, lvl_off, bs, B_global, allreduce, want_grad=True):
+    """Hard-negative mining over a batch split into shards: rod_hnm_* for every
+    shard in lock step, `allreduce(list_of_int32_tensors)` summing each exchange tensor over
+    ALL shards of the global batch (in place) at the two exchange points — the counts, then
+    the four 256-bin radix histograms.  In data-parallel training each process holds one
+    shard and allreduce is an RCCL all-reduce on the compute stream; the sums are integers,
+    so k and the threshold equal the single-process ones bit for bit.
+    shards: [(logits [B,A,K], det_lbl, det_pos, iou)]; returns [(out [8], grad or None)]."""
+    L = len(lvl_off) - 1
+    lo = np.ascontiguousarray(lvl_off, dtype=np.int32)
+    st = []
+    for (logits, lbl, pos, iou) in shards:
+        B, A, K = logits.shape
+        dev = logits.device
+        ws = workspace(_abi.query("rod_hnm_workspace", B, A, L), dev)
+        counts = torch.empty(2, dtype=torch.int32, device=dev)
+        state = torch.empty(8, dtype=torch.int32, device=dev)
+        hist = torch.empty(256, dtype=torch.int32, device=dev)
+        logits = logits.contiguous()
+        _abi.call("rod_hnm_rows", logits, pos, ws, counts, B, A, K, L, dtcode(logits), stream())
+        st.append((logits, lbl, pos, iou, ws, counts, state, hist, B, A, K))
+    allreduce([x[5] for x in st])
+    for x in st:
+        _abi.call("rod_hnm_begin", x[5], int(B_global), x[6], x[7], stream())
+    for shift in (24, 16, 8, 0):
+        for x in st:
+            _abi.call("rod_hnm_radix_hist", x[4], x[8], x[9], L, shift, x[6], x[7], stream())
+        allreduce([x[7] for x in st])
+        for x in st:
+            _abi.call("rod_hnm_radix_scan", shift, x[6], x[7], stream())
+    res = []
+    for (logits, lbl, pos, iou, ws, counts, state, hist, B, A, K) in st:
+        out = torch.empty(8, dtype=torch.float32, device=logits.device)
+        grad = torch.empty_like(logits) if want_grad else None
+        _abi.call("rod_hnm_loss", logits, lbl, pos, iou, lo, L, float(bs), state, out, grad, ws, B, A, K,
+                  dtcode(logits), stream())
+        res.append((out, grad))
+    return res
+
+
+class _SoftmaxCEHNMDP(torch.autograd.Function):
+    """softmax_ce_hnm for one data-parallel shard (hnm_lockstep with the process group)."""
+
+    @staticmethod
+    def forward(ctx, logits, det_lbl, det_pos, iou, lvl_off, bs, B_global, allreduce):
+        ((out, grad),) = hnm_lockstep([(logits, det_lbl, det_pos, iou)], lvl_off, bs, B_global, allreduce,
+                                      want_grad=ctx.needs_input_grad[0])
+        ctx.save_for_backward(grad)
+        ctx.set_materialize_grads(False)
+        ctx.mark_non_differentiable(out)
+        return out, out[2]
+
+    @staticmethod
+    def backward(ctx, g_vec, g_loss):
+        (grad,) = ctx.saved_tensors
+        if g_loss is None:
+            return None, None, None, None, None, None, None, None
+        return grad, None, None, None, None, None, None, None
+
+
+def softmax_ce_hnm_dp(logits, det_lbl, det_pos, iou, lvl_off, bs, B_global, allreduce):
+    """softmax_ce_hnm with the hard negatives selected over the GLOBAL batch of a data-parallel
+    job (allreduce: in-place SUM of a list of device int32 tensors over the ranks)."""
+    return _SoftmaxCEHNMDP.apply(logits, det_lbl, det_pos, iou, lvl_off, bs, B_global, allreduce)
+
+
 def select_topk_nms(probs, boxes, select_threshold, top_k, keep_top_k, nms_threshold):
     B, A, K = probs.shape
     dev = probs.device

@@ -9,7 +9,8 @@ Data-parallel: one process per GPU, the per-image batch sharded across ranks; th
 flat gradient buffer is all-reduced (sum) over RCCL and losses are normalised by the
 GLOBAL batch so the sum equals the single-process gradient (the reference divides by
 bs, net_tools.py:513).  Clipping happens after the reduction (net_tools.py:649).
-BatchNorm statistics are per rank (documented deviation).
+BatchNorm statistics are per rank (documented deviation); the hard negatives are
+selected over the global batch (counts + radix histograms all-reduced, ops.hnm_lockstep).
 """
 from __future__ import annotations
 
@@ -54,6 +55,9 @@ class Trainer:
         self.reducer = reducer
         if reducer is not None and hasattr(reducer, 'attach'):
             reducer.attach(store)  # buckets over the trainable parameters (rod.ddp)
+        # hard negatives over the global batch (net_tools.py:557-587)
+        net_tools.HNM_EXCHANGE = (reducer.hnm_allreduce, world_size) \
+            if world_size > 1 and reducer is not None and hasattr(reducer, 'hnm_allreduce') else None
         self.train_range = train_range
         self.fix_refine = fix_refine
 

@@ -243,6 +243,12 @@ def det_groundtruth(refine_out, offset_gt, cbboxes, refine_labels, refine_pos_ma
     return res
 
 
+# Data-parallel exchange for the hard-negative selection: None (single process) or
+# (allreduce(list of device int32 tensors, in-place SUM over ranks), world_size); set by
+# rod.trainer.Trainer when it runs under torch.distributed.
+HNM_EXCHANGE = None
+
+
 def det_clf_loss(refine_out, clf_out, det_out, det_groundtruth, det_pos_mask, det_labels, iou_all_layers,
                  dtype=torch.float32, scale=None, targets=None):
     """(det_loss, clf_loss) (net_tools.py:519-623): masked smooth-L1 on the ODM offsets and
@@ -262,7 +268,11 @@ def det_clf_loss(refine_out, clf_out, det_out, det_groundtruth, det_pos_mask, de
     pred = ops.levels_concat(det_out, 4)
     dvec, det_loss_one = ops.smooth_l1_masked(pred, det_gt, det_pos, lvl_off, scale)
     logits = ops.levels_concat(clf_out, config.total_obj_n)
-    cvec, clf_loss = ops.softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, scale)
+    if HNM_EXCHANGE is not None:   # data parallel: hard negatives over the global batch (§8e)
+        allreduce, world = HNM_EXCHANGE
+        cvec, clf_loss = ops.softmax_ce_hnm_dp(logits, det_lbl, det_pos, iou, lvl_off, scale, B * world, allreduce)
+    else:
+        cvec, clf_loss = ops.softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, scale)
     det_clf_loss.last_stats = cvec
     det_clf_loss.last_det_per_layer = dvec
     return det_loss_one, clf_loss

@@ -164,6 +164,50 @@ def test_det_targets_and_hnm_loss(dev):
     np.testing.assert_allclose(dd.grad.cpu().numpy(), ref['g_det'], rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize('ranks', [1, 2, 4])
+def test_hnm_data_parallel_exchange(dev, ranks):
+    """the batch split over `ranks` shards (emulated in one process; the exchange
+    sums the int32 counts / histograms over the shards as RCCL all-reduce does across GPUs).
+    k, the k-th smallest nvalue and the negative mask equal the single-process ones bit for bit;
+    the per-shard gradients are the rows of the full-batch gradient; the loss sums match."""
+    from utils import net_tools as nt
+    from utils.common_tools import cornerBboxes_2_centerBboxes
+    from rod.data import synthetic_boxes
+    H, W, B = 300, 300, 4
+    rng, anchors, tab, A = _setup(H, W, B, 3)
+    corner, labels, n = synthetic_boxes(B, seed=12)
+    tg = nt.refine_groundtruth(anchors, cornerBboxes_2_centerBboxes(torch.from_numpy(corner).to(dev)),
+                               torch.from_numpy(labels).to(dev), config.refine_method.JACCARD_BIGGER,
+                               n_boxes=torch.from_numpy(n).to(dev))
+    rgt = tg.flat[0].cpu().numpy()
+    ro_d = torch.from_numpy((rgt + rng.normal(0, 0.15, rgt.shape)).astype(f32)).to(dev)
+    dgt, dpos, dlbl, iou = ops.det_targets(tg.table.center, ro_d, tg.flat[0], tg.flat[1], tg.flat[2], tg.flat[3],
+                                           tab.lvl_off, config.det_pos_jac_val_all_layers)
+    logits = torch.from_numpy(rng.normal(0, 2.0, (B, A, 11)).astype(f32)).to(dev)
+    ld = logits.clone().requires_grad_(True)
+    full, clf = ops.softmax_ce_hnm(ld, dlbl, dpos, iou, tab.lvl_off, float(B))
+    clf.backward()
+    full = full.cpu().numpy()
+
+    def exchange(ts):       # in-place SUM over the shards (what dist.all_reduce does over ranks)
+        tot = ts[0].clone()
+        for t in ts[1:]:
+            tot += t
+        for t in ts:
+            t.copy_(tot)
+    per = B // ranks
+    sl = [slice(r * per, (r + 1) * per) for r in range(ranks)]
+    shards = [(logits[s].contiguous(), dlbl[s].contiguous(), dpos[s].contiguous(), iou[s].contiguous()) for s in sl]
+    res = ops.hnm_lockstep(shards, tab.lvl_off, float(B), B, exchange)
+    outs = np.stack([o.cpu().numpy() for o, _ in res])
+    assert (outs[:, 3] == full[3]).all() and (outs[:, 5] == full[5]).all() and (outs[:, 4] == full[4]).all()
+    assert int(outs[:, 6].sum()) == int(full[6])
+    np.testing.assert_allclose(outs[:, 0].sum(), full[0], rtol=1e-5)
+    np.testing.assert_allclose(outs[:, 1].sum(), full[1], rtol=1e-5)
+    g = torch.cat([gr for _, gr in res]).cpu().numpy()
+    np.testing.assert_array_equal(g, ld.grad.cpu().numpy())
+
+
 @pytest.mark.parametrize('sel,nms,top_k,keep', [(0.1, 0.4, 400, 200), (0.3, 0.4, 400, 200), (0.02, 0.45, 64, 16)])
 def test_select_topk_nms_bit_exact(dev, sel, nms, top_k, keep):
     rng, anchors, tab, A = _setup(300, 300, 2, 5)
