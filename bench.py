@@ -40,6 +40,8 @@ def parse():
     ap.add_argument('--width', type=int, default=1280)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--train_range', default='REFINE', choices=['REFINE', 'ALL'])
+    ap.add_argument('--no-fix-refine', dest='fix_refine', action='store_false', default=True,
+                    help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
     ap.add_argument('--probe', default='rod_bn_bwd', help='C-ABI entry reported in "roofline" (dominant)')
     ap.add_argument('--probe-table', dest='probe_table', default=None,
                     help='time EVERY librod call and write a per-entry table (JSON) here (analysis only)')
@@ -174,7 +176,7 @@ def main():
         from rod.ddp import GradReducer
         reducer = GradReducer(world)  # bucketed RCCL all-reduce, launched during backward
     tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
-                 world_size=world, reducer=reducer)
+                 world_size=world, reducer=reducer, fix_refine=args.fix_refine)
     batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED + rank)
 
     for _ in range(args.warmup):
@@ -256,7 +258,8 @@ def main():
             'config': {'workload': f'{args.train_range} train step (train.py), MobileNet-v2 RefineDet, '
                                    f'{args.height}x{args.width}, {args.batch} images/GPU',
                        'global_batch': args.batch * world, 'img_hw': [args.height, args.width],
-                       'train_range': args.train_range, 'parallelism': f'dp{world}'},
+                       'train_range': args.train_range, 'parallelism': f'dp{world}',
+                       **({} if args.train_range == 'REFINE' else {'fix_refine': args.fix_refine})},
             'loss': round(loss_val, 5),
             'roofline': rl,
         }

@@ -206,12 +206,13 @@ int rod_match_anchors(const float* anc_corner, const float* anc_center, const in
 /* Masked smooth-L1 (net_tools.py:478-516): per-level sums of
  * smooth_l1((target - pred)*mask) / scale written to loss_lvl[0..L-1] and their
  * sum (accumulated in level order) to loss_lvl[L] (fp32, device, L+1 entries),
- * and grad = d(sum/scale)/d pred when grad != NULL.  pred [B,A,4] in dtype,
- * target fp32 [B,A,4], mask int [B,A]. */
+ * and grad = d(sum/scale)/d pred when grad != NULL; grad_target (nullable, fp32) =
+ * d(sum/scale)/d target = -grad (the ODM target det_gt depends on refine_out when the refine
+ * net is trained, net_tools.py:471).  pred [B,A,4] in dtype, target fp32 [B,A,4], mask int [B,A]. */
 size_t rod_smoothl1_workspace(int B, int A);
 int rod_smoothl1_masked(const void* pred, const float* target, const int* mask,
                         const int* lvl_off, int L, float scale, float* loss_lvl, void* grad,
-                        void* workspace, int B, int A, int dtype, void* stream);
+                        float* grad_target, void* workspace, int B, int A, int dtype, void* stream);
 
 /* Box conversions on [n,4] fp32 (utils/common_tools.py:16-56):
  * to_center=1: (ymin,xmin,ymax,xmax) -> (cy,cx,h,w); 0: the inverse. */
@@ -253,6 +254,21 @@ int rod_det_targets(const float* anc_center, const void* refine_out, const float
                     const float* cbox, const int* label, const int* refine_pos, const int* lvl_off,
                     const float* thr, int L, float* det_gt, int* det_pos, int* det_lbl, float* iou,
                     int B, int A, int dtype, void* stream);
+/* Backward of rod_det_targets wrt refine_out, for training the refine net through the ODM
+ * loss (train.py fix_refine=False; the reference has no stop-gradient, net_tools.py:459-471):
+ * g_refine_out = -g_det_gt * det_pos + d iou / d refine_out * g_iou (decode -> corners ->
+ * jaccard with TF's max/min gradient rules).  g_det_gt / g_iou fp32 nullable; output in the
+ * refine_out dtype, overwritten. */
+int rod_det_targets_bwd(const float* anc_center, const void* refine_out, const float* cbox,
+                        const int* det_pos, const float* g_det_gt, const float* g_iou,
+                        void* g_refine_out, int B, int A, int dtype, void* stream);
+/* d clf_loss / d iou through the per-(image, level) IoU focal factor (net_tools.py:590-607:
+ * tf.nn.moments standardisation, min-shift, max-normalise, ^4; reduce_min/max gradients
+ * split over ties as TF does), for the positives' cross-entropy recomputed from logits.
+ * g_iou fp32 [B*A] overwritten. */
+int rod_iou_factor_bwd(const void* logits, const int* det_lbl, const int* det_pos, const float* iou,
+                       const int* lvl_off, int L, float bs, float* g_iou, int B, int A, int K,
+                       int dtype, void* stream);
 /* probs[r, k] = softmax(logits[r, :]) over K <= 16 classes, fp32 out (slim.softmax). */
 int rod_softmax(const void* logits, float* probs, long rows, int K, int dtype, void* stream);
 /* Classification half of det_clf_loss with global hard-negative mining (net_tools.py:551-615),

@@ -160,8 +160,8 @@ def resize_bilinear_legacy(x, size):
     tr = x[:, :, y0][:, :, :, x1]
     bl = x[:, :, y1][:, :, :, x0]
     br = x[:, :, y1][:, :, :, x1]
-    fx_ = fx[None, None, None, :]
-    fy_ = fy[None, None, :, None]
+    fx_ = fx[None, None, None, :].to(x.device, x.dtype)
+    fy_ = fy[None, None, :, None].to(x.device, x.dtype)
     top = tl + (tr - tl) * fx_
     bot = bl + (br - bl) * fx_
     return top + (bot - top) * fy_

@@ -189,3 +189,72 @@ def voc_ap(tp, fp, scores, n_gt, voc07=True):
     for i in range(len(p) - 2, -1, -1):
         p[i] = max(p[i], p[i + 1])
     return sum(p[i + 1] * (r[i + 1] - r[i]) for i in range(len(p) - 1))
+
+
+def odm_losses_torch(anc_center, lvl_off, refine_out, det_out, logits, refine_gt, cbox, refine_pos, det_pos, det_lbl,
+                     negmask, bs):
+    """Differentiable restatement (PyTorch-CPU, any float dtype; test infrastructure) of the
+    ALL-mode losses when the refine net is trained (train.py:144-166, fix_refine=False):
+    refine_loss (net_tools.py:492-516), det_groundtruth (431-475: det_gt and iou depend on
+    refine_out, no stop-gradient) and det_clf_loss (519-623: smooth-L1, sparse softmax CE,
+    IoU focal factor through tf.nn.moments / reduce_min / reduce_max / pow).  The integer
+    decisions (det_pos, det_lbl, the hard-negative mask) are inputs (constants), as they are
+    non-differentiable in the reference.  TF gradient rules are kept: maximum / minimum send
+    the gradient to their first argument on ties (where), reduce_min / reduce_max split it
+    evenly over ties (torch amin / amax do the same), moments' variance uses
+    stop_gradient(mean).  Tensors [B, A, .]; returns (refine_loss, det_loss, clf_loss)."""
+    import torch
+    T = refine_out.dtype
+    ro, do, lg = refine_out, det_out, logits
+    B, A, K = lg.shape
+    ac = torch.from_numpy(np.asarray(anc_center)).to(T)
+    t = lambda a: torch.from_numpy(np.asarray(a)).to(T)
+    rgt, cb = t(refine_gt), t(cbox)
+    rpos, dpos = t(refine_pos)[..., None], t(det_pos)[..., None]
+
+    def tmax(a, b):
+        return torch.where(a >= b, a, b)
+
+    def tmin(a, b):
+        return torch.where(a <= b, a, b)
+
+    def smooth_l1(x):
+        ax = torch.abs(x)
+        return 0.5 * ((ax - 1) * tmin(ax, torch.ones_like(ax)) + ax)
+    refine_loss = smooth_l1((rgt - ro) * rpos).sum() / bs
+    # decode -> corners -> jaccard against the matched GT box
+    cy = ro[..., 0] * ac[:, 2] + ac[:, 0]
+    cx = ro[..., 1] * ac[:, 3] + ac[:, 1]
+    h = torch.exp(ro[..., 2]) * ac[:, 2]
+    w = torch.exp(ro[..., 3]) * ac[:, 3]
+    ay0, ax0, ay1, ax1 = cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2
+    gy0, gx0 = cb[..., 0] - cb[..., 2] / 2, cb[..., 1] - cb[..., 3] / 2
+    gy1, gx1 = cb[..., 0] + cb[..., 2] / 2, cb[..., 1] + cb[..., 3] / 2
+    vol_a = (ax1 - ax0) * (ay1 - ay0)
+    zero = torch.zeros_like(ay0)
+    ih = tmax(tmin(ay1, gy1) - tmax(ay0, gy0), zero)
+    iw = tmax(tmin(ax1, gx1) - tmax(ax0, gx0), zero)
+    inter = ih * iw
+    iou = inter / (vol_a - inter + (gy1 - gy0) * (gx1 - gx0))
+    det_gt = (rgt - ro) * dpos
+    det_loss = smooth_l1((det_gt - do) * dpos).sum() / bs
+    # IoU focal factor per (image, level)
+    fs = []
+    for l in range(len(lvl_off) - 1):
+        u = iou[:, lvl_off[l]:lvl_off[l + 1]]
+        mean = u.mean(1, keepdim=True)
+        var = ((u - mean.detach()) ** 2).mean(1, keepdim=True)
+        z = (u - mean) / torch.sqrt(var + 1e-8)
+        z = z + (0. - z.amin(1, keepdim=True))
+        z = z / (z.amax(1, keepdim=True) + 1e-8)
+        fs.append(z ** 4)
+    iouf = torch.cat(fs, 1)
+    lsm = torch.log_softmax(lg, -1)
+    lab = torch.from_numpy(np.asarray(det_lbl, np.int64))
+    ce_lab = -lsm.gather(-1, lab[..., None])[..., 0]
+    ce0 = -lsm[..., 0]
+    pm = t(det_pos)
+    nm = t(np.asarray(negmask).reshape(B, A))
+    pos_loss = (ce_lab * pm * iouf).sum() / bs
+    neg_loss = (ce0 * nm).sum() / bs
+    return refine_loss, det_loss, neg_loss / 2 + pos_loss

@@ -216,6 +216,66 @@ __global__ void det_targets_kernel(const float* __restrict__ anc_center, const T
   }
 }
 
+// Backward of det_targets wrt refine_out (train.py fix_refine=False; no stop-gradient in the
+// reference): det_gt = (refine_gt - refine_out)*pos (net_tools.py:471) gives -g_det_gt*pos;
+// iou = jaccard(corner(decode(anchor, refine_out)), corner(cbox)) (459-465) gives the chain
+// below with TF's gradient rules (maximum -> the first argument when x >= y, minimum -> when
+// x <= y, max(., 0) passes at >= 0).  The forward is recomputed with det_targets_kernel's
+// exact operations.
+template <typename T>
+__global__ void det_targets_bwd_kernel(const float* __restrict__ anc_center, const T* __restrict__ refine_out,
+                                       const float* __restrict__ cbox, const int* __restrict__ det_pos,
+                                       const float* __restrict__ g_det_gt, const float* __restrict__ g_iou,
+                                       T* __restrict__ g_ro, long BA, int A) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < BA; i += (long)gridDim.x * blockDim.x) {
+    const int a = (int)(i % A);
+    const f32x4 az = *(const f32x4*)(anc_center + (long)a * 4);
+    float ro[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ro[k] = to_f32(refine_out[i * 4 + k]);
+    const float cy = ro[0] * az[2] + az[0], cx = ro[1] * az[3] + az[1];
+    const float h = exp_cr(ro[2]) * az[2], w = exp_cr(ro[3]) * az[3];
+    const float ay0 = cy - h / 2.f, ax0 = cx - w / 2.f, ay1 = cy + h / 2.f, ax1 = cx + w / 2.f;
+    const f32x4 gz = *(const f32x4*)(cbox + i * 4);
+    const float gy0 = gz[0] - gz[2] / 2.f, gx0 = gz[1] - gz[3] / 2.f;
+    const float gy1 = gz[0] + gz[2] / 2.f, gx1 = gz[1] + gz[3] / 2.f;
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    const float G = g_iou ? g_iou[i] : 0.f;
+    if (G != 0.f) {
+      const float vol_a = (ax1 - ax0) * (ay1 - ay0);
+      const float ihr = fminf(ay1, gy1) - fmaxf(ay0, gy0);
+      const float iwr = fminf(ax1, gx1) - fmaxf(ax0, gx0);
+      const float ih = fmaxf(ihr, 0.f), iw = fmaxf(iwr, 0.f);
+      const float inter = ih * iw;
+      const float uni = vol_a - inter + (gy1 - gy0) * (gx1 - gx0);
+      const float q = G * inter / (uni * uni);
+      const float d_inter = G / uni + q;  // d iou/d inter, with union = vol_a - inter + vol_g
+      const float d_vol = -q;
+      const float d_ih = ihr >= 0.f ? d_inter * iw : 0.f;
+      const float d_iw = iwr >= 0.f ? d_inter * ih : 0.f;
+      float d_ay1 = ay1 <= gy1 ? d_ih : 0.f, d_ay0 = ay0 >= gy0 ? -d_ih : 0.f;
+      float d_ax1 = ax1 <= gx1 ? d_iw : 0.f, d_ax0 = ax0 >= gx0 ? -d_iw : 0.f;
+      d_ax1 += d_vol * (ay1 - ay0);
+      d_ax0 -= d_vol * (ay1 - ay0);
+      d_ay1 += d_vol * (ax1 - ax0);
+      d_ay0 -= d_vol * (ax1 - ax0);
+      const float d_cy = d_ay0 + d_ay1, d_h = (d_ay1 - d_ay0) / 2.f;
+      const float d_cx = d_ax0 + d_ax1, d_w = (d_ax1 - d_ax0) / 2.f;
+      g[0] = d_cy * az[2];
+      g[1] = d_cx * az[3];
+      g[2] = d_h * h;
+      g[3] = d_w * w;
+    }
+    if (g_det_gt) {
+      const float pm = (float)det_pos[i];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] -= g_det_gt[i * 4 + k] * pm;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g_ro[i * 4 + k] = from_f32<T>(g[k]);
+  }
+}
+
 // ---------------------------------------------------------------- softmax over K classes
 template <typename T>
 __global__ void softmax_kernel(const T* __restrict__ logits, float* __restrict__ probs, long rows, int K) {
@@ -323,6 +383,17 @@ int rod_det_targets(const float* anc_center, const void* refine_out, const float
                                                ROD_STREAM(stream), anc_center, (const T*)refine_out, refine_gt, cbox,
                                                label, refine_pos, lv, det_gt, det_pos, det_lbl, iou, BA, A));
   return check_launch("rod_det_targets");
+}
+
+int rod_det_targets_bwd(const float* anc_center, const void* refine_out, const float* cbox, const int* det_pos,
+                        const float* g_det_gt, const float* g_iou, void* g_refine_out, int B, int A, int dtype,
+                        void* stream) {
+  ROD_CHECK_ARG(B > 0 && A > 0 && g_refine_out, "rod_det_targets_bwd: bad arguments");
+  const long BA = (long)B * A;
+  ROD_DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(det_targets_bwd_kernel<T>, dim3(ew_grid(BA)), dim3(256), 0,
+                                               ROD_STREAM(stream), anc_center, (const T*)refine_out, cbox, det_pos,
+                                               g_det_gt, g_iou, (T*)g_refine_out, BA, A));
+  return check_launch("rod_det_targets_bwd");
 }
 
 int rod_softmax(const void* logits, float* probs, long rows, int K, int dtype, void* stream) {

@@ -338,6 +338,138 @@ __global__ void hnm_begin_kernel(const int* __restrict__ counts, int B, int* __r
   }
 }
 
+// d clf_loss / d iou through the IoU focal factor (net_tools.py:590-607), the path that
+// exists when refine_out is trained (train.py fix_refine=False; the reference applies no
+// stop-gradient).  One block per (image, level) group, f64 sums, TF's gradient rules:
+//   pos_loss = sum CE*pos*f / bs, f = w^4, w = zz/den, den = max(zz) + 1e-8, zz = z - min(z),
+//   z = (u - mean)/sqrt(var + 1e-8) with tf.nn.moments (variance of stop_gradient(mean));
+//   reduce_min / reduce_max split their gradient evenly over the tied elements.
+// Recomputes the forward statistics with iou_group_kernel's exact float operations so the
+// tie tests select the same elements.  g_iou [B*A] fp32 is written (0 for no gradient).
+template <typename T>
+__global__ void __launch_bounds__(256) iou_factor_bwd_kernel(const T* __restrict__ logits, const int* __restrict__ lbl,
+                                                             const int* __restrict__ pos, const float* __restrict__ iou,
+                                                             HnmLevels lv, int A, int K, float inv_bs,
+                                                             float* __restrict__ g_iou) {
+  __shared__ double sd[4][256];
+  __shared__ float smin[256], smax[256];
+  const int g = blockIdx.x;
+  const int b = g / lv.L, l = g - b * lv.L;
+  const long r0 = (long)b * A + lv.off[l];
+  const int n = lv.off[l + 1] - lv.off[l];
+  const int tid = threadIdx.x;
+  auto block_sum = [&](double v0, double v1, double v2, double v3, double (&o)[4]) {
+    __syncthreads();
+    sd[0][tid] = v0;
+    sd[1][tid] = v1;
+    sd[2][tid] = v2;
+    sd[3][tid] = v3;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (tid < w)
+        for (int j = 0; j < 4; ++j) sd[j][tid] += sd[j][tid + w];
+      __syncthreads();
+    }
+    for (int j = 0; j < 4; ++j) o[j] = sd[j][0];
+  };
+  // forward statistics (iou_group_kernel)
+  double s = 0.0;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = tid; i < n; i += 256) {
+    const float u = iou[r0 + i];
+    s += (double)u;
+    mn = fminf(mn, u);
+    mx = fmaxf(mx, u);
+  }
+  smin[tid] = mn;
+  smax[tid] = mx;
+  double o4[4];
+  block_sum(s, 0.0, 0.0, 0.0, o4);
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) {
+      smin[tid] = fminf(smin[tid], smin[tid + w]);
+      smax[tid] = fmaxf(smax[tid], smax[tid + w]);
+    }
+    __syncthreads();
+  }
+  const float mean = (float)(o4[0] / (double)n);
+  const float umin = smin[0], umax = smax[0];
+  double v = 0.0;
+  for (int i = tid; i < n; i += 256) {
+    const float d = iou[r0 + i] - mean;
+    v += (double)(d * d);
+  }
+  block_sum(v, 0.0, 0.0, 0.0, o4);
+  const float var = (float)(o4[0] / (double)n);
+  const float sdev = sqrtf(var + 1e-8f);
+  const float zmin = (umin - mean) / sdev;
+  const float zzmax = (umax - mean) / sdev + (0.f - zmin);
+  const float den = zzmax + 1e-8f;
+  // pass A: a_i = dL/dw_i = G_i * 4 w^3 (G_i = CE_i * pos_i / bs) -> g_iou (scratch);
+  // sums a*zz (den), tie counts of max(zz) and min(z)
+  double saz = 0.0, cmax = 0.0, cmin = 0.0;
+  for (int i = tid; i < n; i += 256) {
+    const long r = r0 + i;
+    const float u = iou[r];
+    const float z = (u - mean) / sdev;
+    const float zz = z + (0.f - zmin);
+    const float w = zz / den;
+    float a = 0.f;
+    if (pos[r] != 0) {
+      const T* x = logits + r * K;
+      float m = to_f32(x[0]);
+      for (int k = 1; k < K; ++k) m = fmaxf(m, to_f32(x[k]));
+      float se = 0.f;
+      for (int k = 0; k < K; ++k) se += exp_cr(to_f32(x[k]) - m);
+      const float ce = log_cr(se) - (to_f32(x[lbl[r]]) - m);
+      a = ce * inv_bs * (4.f * powf(w, 3.f));
+    }
+    g_iou[r] = a;
+    saz += (double)a * (double)zz;
+    cmax += zz == zzmax ? 1.0 : 0.0;
+    cmin += z == zmin ? 1.0 : 0.0;
+  }
+  block_sum(saz, cmax, cmin, 0.0, o4);
+  const double dden = -o4[0] / ((double)den * (double)den);
+  const double tmax = dden / o4[1];   // reduce_max: split over the ties
+  const double ncmin = o4[2];
+  // pass B: dzz_i = a_i/den + [zz_i max] tmax; sum dzz (-> d min(z))
+  double sdzz = 0.0;
+  for (int i = tid; i < n; i += 256) {
+    const long r = r0 + i;
+    const float u = iou[r];
+    const float z = (u - mean) / sdev;
+    const float zz = z + (0.f - zmin);
+    double dzz = (double)g_iou[r] / (double)den + (zz == zzmax ? tmax : 0.0);
+    g_iou[r] = (float)dzz;
+    sdzz += dzz;
+  }
+  block_sum(sdzz, 0.0, 0.0, 0.0, o4);
+  const double tmin = -o4[0] / ncmin;   // d min(z) = -sum dzz, split over the ties
+  // pass C: g_i = dL/dz_i; sums g and g*(u - mean)
+  double sg = 0.0, sgu = 0.0;
+  for (int i = tid; i < n; i += 256) {
+    const long r = r0 + i;
+    const float u = iou[r];
+    const float z = (u - mean) / sdev;
+    const double gi = (double)g_iou[r] + (z == zmin ? tmin : 0.0);
+    g_iou[r] = (float)gi;
+    sg += gi;
+    sgu += gi * (double)(u - mean);
+  }
+  block_sum(sg, sgu, 0.0, 0.0, o4);
+  // z = (u - mean)/s, s = sqrt(var + 1e-8), var = mean((u - stop_gradient(mean))^2)
+  const double sd_ = (double)sdev;
+  const double dsdev = -o4[1] / (sd_ * sd_);
+  const double cmean = -o4[0] / sd_ / (double)n;
+  for (int i = tid; i < n; i += 256) {
+    const long r = r0 + i;
+    const double gi = (double)g_iou[r];
+    const double du = gi / sd_ + cmean + dsdev * (double)(iou[r] - mean) / ((double)n * sd_);
+    g_iou[r] = (float)du;
+  }
+}
+
 static int hnm_blocks(long R) { return (int)std::min<long>(cdivl(R, 256), 2048); }
 
 static HnmWs carve(void* ws, long R, int B, int L, int nb) {
@@ -399,6 +531,21 @@ int rod_softmax_ce_hnm(const void* logits, const int* det_lbl, const int* det_po
     hipLaunchKernelGGL(hnm_finalize_kernel, dim3(1), dim3(256), 0, s, w.loss_slab, nb, w.state, bs, out);
   });
   return check_launch("rod_softmax_ce_hnm");
+}
+
+int rod_iou_factor_bwd(const void* logits, const int* det_lbl, const int* det_pos, const float* iou,
+                       const int* lvl_off, int L, float bs, float* g_iou, int B, int A, int K, int dtype,
+                       void* stream) {
+  ROD_CHECK_ARG(B > 0 && A > 0 && K > 1 && K <= HNM_K && g_iou, "rod_iou_factor_bwd: bad arguments");
+  ROD_CHECK_ARG(L >= 1 && L <= HNM_MAXL && lvl_off && lvl_off[0] == 0 && lvl_off[L] == A,
+                "rod_iou_factor_bwd: bad levels");
+  HnmLevels lv;
+  lv.L = L;
+  for (int i = 0; i <= HNM_MAXL; ++i) lv.off[i] = i <= L ? lvl_off[i] : A;
+  ROD_DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(iou_factor_bwd_kernel<T>, dim3(B * L), dim3(256), 0,
+                                               ROD_STREAM(stream), (const T*)logits, det_lbl, det_pos, iou, lv, A, K,
+                                               1.0f / bs, g_iou));
+  return check_launch("rod_iou_factor_bwd");
 }
 
 // ---- data-parallel split: per-rank rows, exchange points are counts[2] and hist[256] ----

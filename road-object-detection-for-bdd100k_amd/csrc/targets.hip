@@ -131,8 +131,8 @@ __global__ void __launch_bounds__(256) match_anchors_kernel(const float* __restr
 template <typename T>
 __global__ void __launch_bounds__(256) smoothl1_kernel(const T* __restrict__ pred, const float* __restrict__ target,
                                                        const int* __restrict__ mask, LevelInfo li, float inv_scale,
-                                                       T* __restrict__ grad, float* __restrict__ slab, int B, int A,
-                                                       int nbx) {
+                                                       T* __restrict__ grad, float* __restrict__ grad_t,
+                                                       float* __restrict__ slab, int B, int A, int nbx) {
   __shared__ float red[4];
   const int l = blockIdx.y;
   const int Al = li.off[l + 1] - li.off[l];
@@ -157,6 +157,10 @@ __global__ void __launch_bounds__(256) smoothl1_kernel(const T* __restrict__ pre
     if (grad) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) grad[o * 4 + c] = from_f32<T>(gv[c]);
+    }
+    if (grad_t) {  // d/d target = -d/d pred (the ODM target depends on refine_out, 471)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) grad_t[o * 4 + c] = -gv[c];
     }
   }
   s = warp_sum(s);
@@ -267,8 +271,8 @@ size_t rod_smoothl1_workspace(int B, int A) {
 }
 
 int rod_smoothl1_masked(const void* pred, const float* target, const int* mask, const int* lvl_off, int L,
-                        float scale, float* loss_lvl, void* grad, void* workspace, int B, int A, int dtype,
-                        void* stream) {
+                        float scale, float* loss_lvl, void* grad, float* grad_target, void* workspace, int B, int A,
+                        int dtype, void* stream) {
   ROD_CHECK_ARG(B > 0 && A > 0, "rod_smoothl1_masked: bad shape");
   ROD_CHECK_ARG(scale != 0.f, "rod_smoothl1_masked: scale must be non-zero");
   ROD_CHECK_ARG(workspace && loss_lvl, "rod_smoothl1_masked: workspace/loss_lvl NULL");
@@ -280,7 +284,7 @@ int rod_smoothl1_masked(const void* pred, const float* target, const int* mask, 
   hipStream_t s = ROD_STREAM(stream);
   ROD_DISPATCH_DTYPE(dtype, {
     hipLaunchKernelGGL(smoothl1_kernel<T>, dim3(nbx, L), dim3(256), 0, s, (const T*)pred, target, mask, li, inv,
-                       (T*)grad, (float*)workspace, B, A, nbx);
+                       (T*)grad, grad_target, (float*)workspace, B, A, nbx);
   });
   hipLaunchKernelGGL(level_sum_finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nbx, L, scale,
                      loss_lvl);

@@ -439,22 +439,23 @@ class _SmoothL1(torch.autograd.Function):
         L = len(lvl_off) - 1
         loss = torch.empty(L + 1, dtype=torch.float32, device=pred.device)
         grad = torch.empty_like(pred) if ctx.needs_input_grad[0] else None
+        grad_t = torch.empty_like(target) if ctx.needs_input_grad[1] else None
         ws = workspace(_abi.query("rod_smoothl1_workspace", B, A), pred.device)
         _abi.call("rod_smoothl1_masked", pred, target, mask, np.ascontiguousarray(lvl_off, dtype=np.int32), L,
-                  float(scale), loss, grad, ws, B, A, dtcode(pred), stream())
-        ctx.save_for_backward(grad)
+                  float(scale), loss, grad, grad_t, ws, B, A, dtcode(pred), stream())
+        ctx.save_for_backward(grad, grad_t)
         ctx.set_materialize_grads(False)
         ctx.mark_non_differentiable(loss)
         return loss, loss[L]
 
     @staticmethod
     def backward(ctx, g_vec, g_tot):
-        (grad,) = ctx.saved_tensors
+        grad, grad_t = ctx.saved_tensors
         if g_tot is None:
             return None, None, None, None, None
         # the total is the training loss and its seed is 1 (graph.backward); any other
         # upstream weight would need a scale kernel, which no caller of the reference uses
-        return grad, None, None, None, None
+        return grad, grad_t, None, None, None
 
 
 def smooth_l1_masked(pred, target, mask, lvl_off, scale):
@@ -616,17 +617,61 @@ def decode(anc_center, off_a, off_b=None, to_corner=False):
     return out
 
 
-def det_targets(anc_center, refine_out, refine_gt, cbox, label, refine_pos, lvl_off, thr):
+def _det_targets_raw(anc_center, refine_out, refine_gt, cbox, label, refine_pos, lvl_off, thr):
     B, A = refine_out.shape[0], refine_out.shape[1]
     dev = refine_out.device
     det_gt = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
     det_pos = torch.empty((B, A), dtype=torch.int32, device=dev)
     det_lbl = torch.empty((B, A), dtype=torch.int32, device=dev)
     iou = torch.empty((B, A), dtype=torch.float32, device=dev)
-    _abi.call("rod_det_targets", anc_center, refine_out.contiguous(), refine_gt, cbox, label, refine_pos,
+    _abi.call("rod_det_targets", anc_center, refine_out, refine_gt, cbox, label, refine_pos,
               np.ascontiguousarray(lvl_off, dtype=np.int32), np.ascontiguousarray(thr, dtype=np.float32),
               len(lvl_off) - 1, det_gt, det_pos, det_lbl, iou, B, A, dtcode(refine_out), stream())
     return det_gt, det_pos, det_lbl, iou
+
+
+class _DetTargets(torch.autograd.Function):
+    """det_groundtruth (net_tools.py:431-475) differentiable wrt refine_out: det_gt and iou
+    depend on it (no stop-gradient in the reference); the masks and labels do not."""
+
+    @staticmethod
+    def forward(ctx, refine_out, anc_center, refine_gt, cbox, label, refine_pos, lvl_off, thr):
+        det_gt, det_pos, det_lbl, iou = _det_targets_raw(anc_center, refine_out, refine_gt, cbox, label, refine_pos,
+                                                         lvl_off, thr)
+        ctx.save_for_backward(refine_out, anc_center, cbox, det_pos)
+        ctx.mark_non_differentiable(det_pos, det_lbl)
+        ctx.set_materialize_grads(False)
+        return det_gt, det_pos, det_lbl, iou
+
+    @staticmethod
+    def backward(ctx, g_gt, g_pos, g_lbl, g_iou):
+        refine_out, anc_center, cbox, det_pos = ctx.saved_tensors
+        if g_gt is None and g_iou is None:
+            return (None,) * 8
+        B, A = refine_out.shape[0], refine_out.shape[1]
+        g_ro = torch.empty_like(refine_out)
+        _abi.call("rod_det_targets_bwd", anc_center, refine_out, cbox, det_pos,
+                  None if g_gt is None else g_gt.contiguous(), None if g_iou is None else g_iou.contiguous(), g_ro,
+                  B, A, dtcode(refine_out), stream())
+        return (g_ro,) + (None,) * 7
+
+
+def det_targets(anc_center, refine_out, refine_gt, cbox, label, refine_pos, lvl_off, thr):
+    """(det_gt, det_pos, det_lbl, iou); differentiable wrt refine_out when it requires grad."""
+    ro = refine_out.contiguous()
+    if torch.is_grad_enabled() and ro.requires_grad:
+        return _DetTargets.apply(ro, anc_center, refine_gt, cbox, label, refine_pos, lvl_off, thr)
+    return _det_targets_raw(anc_center, ro, refine_gt, cbox, label, refine_pos, lvl_off, thr)
+
+
+def _iou_factor_grad(logits, det_lbl, det_pos, iou, lvl_off, bs):
+    """d clf_loss / d iou through the IoU focal factor (rod_iou_factor_bwd)."""
+    B, A, K = logits.shape
+    g = torch.empty((B, A), dtype=torch.float32, device=logits.device)
+    _abi.call("rod_iou_factor_bwd", logits, det_lbl, det_pos, iou.contiguous(),
+              np.ascontiguousarray(lvl_off, dtype=np.int32), len(lvl_off) - 1, float(bs), g, B, A, K,
+              dtcode(logits), stream())
+    return g
 
 
 def softmax(logits, K):
@@ -647,18 +692,21 @@ class _SoftmaxCEHNM(torch.autograd.Function):
         _abi.call("rod_softmax_ce_hnm", logits.contiguous(), det_lbl, det_pos, iou,
                   np.ascontiguousarray(lvl_off, dtype=np.int32), L, float(bs), out, grad, ws, B, A, K,
                   dtcode(logits), stream())
-        ctx.save_for_backward(grad)
+        ctx.save_for_backward(grad, logits, det_lbl, det_pos, iou)
+        ctx.hnm = (lvl_off, bs)
         ctx.set_materialize_grads(False)
         ctx.mark_non_differentiable(out)
         return out, out[2]
 
     @staticmethod
     def backward(ctx, g_vec, g_loss):
-        (grad,) = ctx.saved_tensors
+        grad, logits, det_lbl, det_pos, iou = ctx.saved_tensors
         if g_loss is None:
             return None, None, None, None, None, None
-        # clf_loss enters the training loss with weight 1 (net_tools.det_clf_loss)
-        return grad, None, None, None, None, None
+        # clf_loss enters the training loss with weight 1 (net_tools.det_clf_loss); the IoU
+        # factor passes gradient to iou when refine_out is trained (fix_refine=False)
+        g_iou = _iou_factor_grad(logits, det_lbl, det_pos, iou, *ctx.hnm) if ctx.needs_input_grad[3] else None
+        return grad, None, None, g_iou, None, None
 
 
 def softmax_ce_hnm(logits, det_lbl, det_pos, iou, lvl_off, bs):
@@ -714,17 +762,19 @@ class _SoftmaxCEHNMDP(torch.autograd.Function):
     def forward(ctx, logits, det_lbl, det_pos, iou, lvl_off, bs, B_global, allreduce):
         ((out, grad),) = hnm_lockstep([(logits, det_lbl, det_pos, iou)], lvl_off, bs, B_global, allreduce,
                                       want_grad=ctx.needs_input_grad[0])
-        ctx.save_for_backward(grad)
+        ctx.save_for_backward(grad, logits, det_lbl, det_pos, iou)
+        ctx.hnm = (lvl_off, bs)
         ctx.set_materialize_grads(False)
         ctx.mark_non_differentiable(out)
         return out, out[2]
 
     @staticmethod
     def backward(ctx, g_vec, g_loss):
-        (grad,) = ctx.saved_tensors
+        grad, logits, det_lbl, det_pos, iou = ctx.saved_tensors
         if g_loss is None:
             return None, None, None, None, None, None, None, None
-        return grad, None, None, None, None, None, None, None
+        g_iou = _iou_factor_grad(logits, det_lbl, det_pos, iou, *ctx.hnm) if ctx.needs_input_grad[3] else None
+        return grad, None, None, g_iou, None, None, None, None
 
 
 def softmax_ce_hnm_dp(logits, det_lbl, det_pos, iou, lvl_off, bs, B_global, allreduce):

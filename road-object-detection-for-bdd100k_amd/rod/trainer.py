@@ -43,10 +43,6 @@ class Trainer:
                                                    net_tools.init_anchor(layer_n))
         self.table = net_tools.anchor_table(self.anchors, self.device)
         store = self.net.store
-        if train_range is config.train_range.ALL and not fix_refine:
-            raise NotImplementedError(
-                'ALL with fix_refine=False needs the gradient through the ODM IoU factor into refine_out '
-                '(net_tools.py:590-599); not built yet (DESIGN.md, "next")')
         if train_range is config.train_range.ALL and fix_refine:
             import re
             pat = re.compile(r'^((?!(backbone|refine)).)*$')   # train.py:160-163
@@ -62,6 +58,15 @@ class Trainer:
         self.fix_refine = fix_refine
 
     def step(self, img_u8, gt_corner, gt_labels, gt_n):
+        losses = self.losses(img_u8, gt_corner, gt_labels, gt_n)
+        graph.backward(losses[0])
+        if self.reducer is not None:
+            self.reducer(self.net.store.flat_grad)
+        self.opt.step()
+        return losses
+
+    def losses(self, img_u8, gt_corner, gt_labels, gt_n):
+        """Forward of one step: (training loss, [refine, det, clf] in ALL mode)."""
         x = ops.normalize_image(img_u8, self.dtype)                 # (2/255)x - 1
         center = cornerBboxes_2_centerBboxes(gt_corner)              # train.py:109
         tg = net_tools.refine_groundtruth(self.anchors, center, gt_labels, config.refine_method.JACCARD_BIGGER,
@@ -73,14 +78,19 @@ class Trainer:
             losses = (loss,)
         else:
             refine_out, det_out, clf_out = out
-            r_loss = net_tools.refine_loss(refine_out, tg[0], tg[3], targets=tg, scale=scale)
-            dgt = net_tools.det_groundtruth(refine_out, tg[0], tg[1], tg[2], tg[3], self.anchors, targets=tg)
+            self.last_out = out
+            rflat = [None, None]
+            if not self.fix_refine:
+                # refine_out feeds the refine loss AND the ODM targets / IoU factor (train.py:144-151,
+                # total_loss = refine + det + clf): one concatenation, two aliases whose gradients
+                # meet in rod_add
+                rflat = list(graph.fork(ops.levels_concat(refine_out, 4), 2))
+            r_loss = net_tools.refine_loss(refine_out, tg[0], tg[3], targets=tg, scale=scale, refine_flat=rflat[0])
+            dgt = net_tools.det_groundtruth(refine_out, tg[0], tg[1], tg[2], tg[3], self.anchors, targets=tg,
+                                            refine_flat=rflat[1])
             d_loss, c_loss = net_tools.det_clf_loss(refine_out, clf_out, det_out, dgt, dgt[1], dgt[2], dgt[3],
                                                     scale=scale)
             loss = graph.scalar_sum(d_loss, c_loss) if self.fix_refine else graph.scalar_sum(r_loss, d_loss, c_loss)
             losses = (loss, r_loss, d_loss, c_loss)
-        graph.backward(loss)
-        if self.reducer is not None:
-            self.reducer(self.net.store.flat_grad)
-        self.opt.step()
+            self.last_targets = (tg, dgt)
         return losses

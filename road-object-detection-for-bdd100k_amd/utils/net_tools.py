@@ -161,7 +161,8 @@ def smooth_l1(x):
     raise NotImplementedError('smooth_l1 is fused into refine_loss / det_clf_loss kernels')
 
 
-def refine_loss(refine_out, refine_groundtruth, refine_pos_mask, dtype=torch.float32, targets=None, scale=None):
+def refine_loss(refine_out, refine_groundtruth, refine_pos_mask, dtype=torch.float32, targets=None, scale=None,
+                refine_flat=None):
     """sum_l sum smooth_l1((gt - out) * mask) / bs (net_tools.py:492-516).
 
     `targets` (the RefineTargets returned by refine_groundtruth) lets the kernel read
@@ -172,7 +173,8 @@ def refine_loss(refine_out, refine_groundtruth, refine_pos_mask, dtype=torch.flo
     """
     B = refine_out[0].shape[0]
     scale = float(B) if scale is None else float(scale)
-    pred = ops.levels_concat(refine_out, 4)
+    # refine_flat: the concatenated refine_out when the caller shares it between losses
+    pred = ops.levels_concat(refine_out, 4) if refine_flat is None else refine_flat
     if targets is not None:
         gt_flat, _, _, pos_flat = targets.flat
         lvl_off = targets.table.lvl_off
@@ -220,12 +222,12 @@ def _flat_levels(tensors, k, table):
 
 
 def det_groundtruth(refine_out, offset_gt, cbboxes, refine_labels, refine_pos_mask, anchors, scope="det_encode",
-                    targets=None):
+                    targets=None, refine_flat=None):
     """ODM targets (net_tools.py:431-475).  Returns (det_gt, det_pos_mask, det_labels, iou)
     as per-layer views [B, fh, fw, A, 4|1] / iou [B, fh, fw, A]; the concatenated buffers
     are attached as `.flat` for the fused loss kernels."""
     tab = targets.table if targets is not None else anchor_table(anchors, refine_out[0].device)
-    ro = ops.levels_concat(refine_out, 4)
+    ro = ops.levels_concat(refine_out, 4) if refine_flat is None else refine_flat
     if targets is not None:
         rgt, cbox, lbl, rpos = targets.flat
     else:
@@ -234,7 +236,9 @@ def det_groundtruth(refine_out, offset_gt, cbboxes, refine_labels, refine_pos_ma
         cbox = _flat_levels(cbboxes, 4, tab).float()
         lbl = _flat_levels(refine_labels, 1, tab).view(B, -1)
         rpos = _flat_levels(refine_pos_mask, 1, tab).view(B, -1)
-    det_gt, det_pos, det_lbl, iou = ops.det_targets(tab.center, ro.detach(), rgt, cbox, lbl, rpos, tab.lvl_off,
+    # differentiable wrt refine_out (det_gt and iou; no stop-gradient in the reference) when it
+    # requires grad, i.e. when the refine net is trained (train.py fix_refine=False)
+    det_gt, det_pos, det_lbl, iou = ops.det_targets(tab.center, ro, rgt, cbox, lbl, rpos, tab.lvl_off,
                                                     config.det_pos_jac_val_all_layers[:len(tab.shapes)])
     res = RefineTargets(tab.split(det_gt, 4), tab.split(det_pos[..., None], 1), tab.split(det_lbl[..., None], 1),
                         tab.split(iou, 0))
