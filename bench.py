@@ -40,6 +40,9 @@ def parse():
     ap.add_argument('--width', type=int, default=1280)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--train_range', default='REFINE', choices=['REFINE', 'ALL'])
+    ap.add_argument('--augment', action='store_true', default=False,
+                    help='each step starts from raw 720x1280 uint8 frames through the GPU training augmentation '
+                         '(process_raw_data_train: random crop / resize / flip / colour, fused normalisation)')
     ap.add_argument('--no-fix-refine', dest='fix_refine', action='store_false', default=True,
                     help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
     ap.add_argument('--probe', default='rod_bn_bwd', help='C-ABI entry reported in "roofline" (dominant)')
@@ -178,9 +181,14 @@ def main():
     tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
                  world_size=world, reducer=reducer, fix_refine=args.fix_refine)
     batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED + rank)
+    source = None
+    if args.augment:
+        from rod.dataio import AugmentedSource
+        source = AugmentedSource(args.batch, (args.height, args.width), dev, dtype, seed=SEED + rank, n_distinct=2)
+    next_batch = (lambda: next(source)) if source is not None else (lambda: batch)
 
     for _ in range(args.warmup):
-        tr.step(*batch)
+        tr.step(*next_batch())
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -188,7 +196,7 @@ def main():
     _abi.PROBE.arm('*' if args.probe_table else args.probe)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        losses = tr.step(*batch)
+        losses = tr.step(*next_batch())
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -259,6 +267,7 @@ def main():
                                    f'{args.height}x{args.width}, {args.batch} images/GPU',
                        'global_batch': args.batch * world, 'img_hw': [args.height, args.width],
                        'train_range': args.train_range, 'parallelism': f'dp{world}',
+                       'augment': bool(args.augment),
                        **({} if args.train_range == 'REFINE' else {'fix_refine': args.fix_refine})},
             'loss': round(loss_val, 5),
             'roofline': rl,

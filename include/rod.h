@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 4
+#define ROD_ABI_VERSION 5
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -60,6 +60,33 @@ const char* rod_last_error(void);
 int rod_normalize_image(const void* img_u8, void* out, long n, int out_dtype, void* stream);
 /* dst = src converted between storage dtypes (tf.cast). */
 int rod_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, void* stream);
+
+/* ------------------------------------------------ training augmentation (A17)
+ * process_raw_data_train (utils/data_pileline_tools.py:76-108) on a batch of decoded uint8
+ * RGB images of any sizes: image b is src_hw[b] = (H, W) pixels at byte offset src_off[b] of
+ * src (rows of 3*W bytes).  Per image, with parameters sampled on the host:
+ *   crop[b]   = (y0, x0, h, w)   tf.slice window of sample_distorted_bounding_box (process.py:117-127)
+ *   mode[b]   = (flip, ordering) random_flip_left_right (tf_image.py:281-305); colour ordering
+ *               0..3 of distort_color(fast_mode=False) (process.py:59-77), -1 = no colour ops
+ *   colour[b] = (brightness delta, saturation factor, contrast factor)
+ * out[b] = colour(flip(resize_bilinear_legacy(crop(src_b), Ho x Wo))) on the 0-255 scale, no
+ * clamping (process.py:79), then (2/255)x - 1 when normalize != 0 (train.py:126), stored in
+ * dtype as [B, Ho, Wo, 3].  Contrast uses the per-image channel mean of the image it receives.
+ * prepare_data_test (data_pileline_tools.py:18-43) is crop = whole image, mode = (0, -1).
+ * workspace: rod_augment_workspace(B, Ho, Wo) bytes.  out 16-byte aligned. */
+size_t rod_augment_workspace(int B, int Ho, int Wo);
+int rod_augment_images(const void* src, const int64_t* src_off, const int32_t* src_hw, const int32_t* crop,
+                       const int32_t* mode, const float* colour, void* workspace, void* out, int B, int Ho, int Wo,
+                       int normalize, int dtype, void* stream);
+/* Box side of the same step, boxes [B][G][4] (ymin, xmin, ymax, xmax), first n[b] valid:
+ * bboxes_resize to ref[b] (the crop as a normalised box, bboxes.py:139-163), keep boxes whose
+ * intersection / own area with [0,0,1,1] is > threshold (bboxes_filter_overlap, bboxes.py:408-428;
+ * 0.3 = BBOX_CROP_OVERLAP, process.py:6) compacted in order (tf.boolean_mask), flip when
+ * mode[b][0] (tf_image.py:284-289; mode may be NULL), clip to [0,1] (data_pileline_tools.py:106-107).
+ * Outputs padded with zeros past n_out[b]. */
+int rod_augment_boxes(const float* boxes, const int32_t* labels, const int32_t* n, const float* ref,
+                      const int32_t* mode, float* boxes_out, int32_t* labels_out, int32_t* n_out, int B, int G,
+                      float threshold, void* stream);
 
 /* --------------------------------------------------- depthwise 3x3 (A1)
  * slim.separable_conv2d(num_outputs=None, depth_multiplier=1), padding SAME

@@ -68,6 +68,64 @@ def normalize_image(img_u8: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
     return out
 
 
+def _device_i(a, dev, dtype):
+    """Small host parameter array -> device, pinned + non-blocking (no stream sync)."""
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dtype)
+    if dev.type == 'cuda':
+        t = t.pin_memory()
+    return t.to(dev, non_blocking=True)
+
+
+def augment_images(src, crop, mode, colour, out_hw, dtype=torch.float32, normalize=False, src_hw=None,
+                   src_off=None):
+    """rod_augment_images: crop -> legacy bilinear resize -> flip -> colour chain [-> (2/255)x-1]
+    (data_pileline_tools.py:76-108, train.py:126).  src: uint8 [B, H, W, 3] device tensor, or a
+    flat uint8 buffer with per-image src_hw [B, 2] / src_off [B] (host arrays).  crop [B, 4],
+    mode [B, 2], colour [B, 3]: host arrays of the sampled parameters."""
+    dev = src.device
+    if src_hw is None:
+        B, H, W, _ = src.shape
+        src_hw = np.tile(np.array([H, W], np.int32), (B, 1))
+        src_off = np.arange(B, dtype=np.int64) * (H * W * 3)
+    B = len(src_hw)
+    Ho, Wo = int(out_hw[0]), int(out_hw[1])
+    crop = np.asarray(crop, np.int32).reshape(B, 4)
+    hw = np.asarray(src_hw, np.int64).reshape(B, 2)
+    if (crop[:, :2] < 0).any() or (crop[:, 2:] <= 0).any() or (crop[:, 0] + crop[:, 2] > hw[:, 0]).any() or \
+            (crop[:, 1] + crop[:, 3] > hw[:, 1]).any():
+        raise ValueError('augment_images: crop window outside the source image')
+    if int((hw[:, 0] * hw[:, 1] * 3).max()) >= 2 ** 31:
+        raise ValueError('augment_images: a source image exceeds 2 GiB')
+    if int((np.asarray(src_off, np.int64) + hw[:, 0] * hw[:, 1] * 3).max()) > src.numel():
+        raise ValueError('augment_images: source offsets exceed the buffer')
+    out = torch.empty((B, Ho, Wo, 3), dtype=dtype, device=dev)
+    ws = workspace(_abi.query('rod_augment_workspace', B, Ho, Wo), dev)
+    _abi.call('rod_augment_images', src, _device_i(src_off, dev, torch.int64), _device_i(src_hw, dev, torch.int32),
+              _device_i(crop, dev, torch.int32), _device_i(np.asarray(mode, np.int32), dev, torch.int32),
+              _device_i(np.asarray(colour, np.float32), dev, torch.float32), ws, out, B, Ho, Wo,
+              int(bool(normalize)), dtcode(out), stream())
+    return out
+
+
+def augment_boxes(boxes, labels, n, ref, mode=None, threshold=0.3):
+    """rod_augment_boxes: bboxes_resize -> bboxes_filter_overlap -> flip -> clip (process.py:130-134,
+    tf_image.py:284-289, data_pileline_tools.py:106-107).  boxes [B, G, 4] / labels [B, G] / n [B]
+    as device tensors or host arrays; ref [B, 4], mode [B, 2] host arrays.  Returns device
+    (boxes, labels, n), zero-padded past n."""
+    dev = boxes.device if torch.is_tensor(boxes) else torch.device('cuda')
+    b = boxes if torch.is_tensor(boxes) else _device_i(np.asarray(boxes, np.float32), dev, torch.float32)
+    lab = labels if torch.is_tensor(labels) else _device_i(np.asarray(labels, np.int32), dev, torch.int32)
+    nn = n if torch.is_tensor(n) else _device_i(np.asarray(n, np.int32), dev, torch.int32)
+    B, G = b.shape[0], b.shape[1]
+    bo = torch.empty_like(b)
+    lo = torch.empty_like(lab)
+    no = torch.empty_like(nn)
+    md = None if mode is None else _device_i(np.asarray(mode, np.int32), dev, torch.int32)
+    _abi.call('rod_augment_boxes', b.contiguous(), lab.contiguous(), nn, _device_i(np.asarray(ref, np.float32), dev,
+              torch.float32), md, bo, lo, no, B, G, float(threshold), stream())
+    return bo, lo, no
+
+
 def cast(x: torch.Tensor, dtype) -> torch.Tensor:
     if x.dtype == dtype:
         return x

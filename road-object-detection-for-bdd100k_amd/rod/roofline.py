@@ -23,6 +23,10 @@ def cost(name, a):
     # ABI 3: rod_dw3x3_fwd / _bwd_filter / rod_conv_fwd / _wgrad carry the five BatchNorm
     # prologue arguments after x (P = 5 positions); ABI 4: rod_conv_fwd (after stat_parts)
     # and rod_dw3x3_bwd_data (after dx) the seven gred arguments
+    if name == "rod_augment_images":
+        # written network input + one uint8 sample per output value read (the crop is resampled)
+        B, Ho, Wo, dt = a[8], a[9], a[10], a[12]
+        return (_ES[dt] + 1) * B * Ho * Wo * 3, 0
     if name == "rod_dw3x3_fwd":
         N, H, W, C, Ho, Wo, dt = a[9], a[10], a[11], a[12], a[16], a[17], a[18]
         es = _ES[dt]

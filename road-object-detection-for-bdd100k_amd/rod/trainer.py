@@ -67,7 +67,10 @@ class Trainer:
 
     def losses(self, img_u8, gt_corner, gt_labels, gt_n):
         """Forward of one step: (training loss, [refine, det, clf] in ALL mode)."""
-        x = ops.normalize_image(img_u8, self.dtype)                 # (2/255)x - 1
+        if img_u8.is_floating_point():   # already (2/255)x - 1 (fused into rod_augment_images)
+            x = ops.cast(img_u8, self.dtype)
+        else:
+            x = ops.normalize_image(img_u8, self.dtype)             # (2/255)x - 1
         center = cornerBboxes_2_centerBboxes(gt_corner)              # train.py:109
         tg = net_tools.refine_groundtruth(self.anchors, center, gt_labels, config.refine_method.JACCARD_BIGGER,
                                           n_boxes=gt_n)

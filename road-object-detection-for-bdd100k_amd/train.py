@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
     ap.add_argument('--dataset_dir', default='./dataset/bdd100k_TfRecord/')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--augment', type=str2bool, default=True,
+                    help='process_raw_data_train on the GPU (random crop / flip / colour); False = raw batches')
     return ap.parse_args(argv)
 
 
@@ -117,7 +119,8 @@ def main(argv=None):
             logger.info('TF variables init success...')
     trainer.opt.global_step = step0
     logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
-    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, seed=1000 * rank + F.seed)
+    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, seed=1000 * rank + F.seed,
+                         augment_dtype=dtype if F.augment else None)
 
     os.makedirs(F.summary_dir, exist_ok=True)
     summ = open(os.path.join(F.summary_dir, 'train_rank%d.jsonl' % rank), 'a') if rank == 0 else None

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().rod_abi_version() == 4
+    assert _abi.lib().rod_abi_version() == 5
 
 
 def test_invalid_arguments_raise_with_message():

@@ -27,6 +27,8 @@ for step in "$@"; do
     benchfast) run benchfast 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchall) run benchall 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-cpu-baseline --no-inference ;;
     benchallfr) run benchallfr 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-fix-refine --no-cpu-baseline --no-inference ;;
+    benchaug) run benchaug 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_aug.json ;;
+    benchaug2) run benchaug2 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference ;;
     cli) run cli_train 300 python road-object-detection-for-bdd100k_amd/train.py --train_range=ALL --batch_size=2 --max_number_of_steps=4 --log_every_n_steps=2 --save_every_n_steps=4 --checkpoint_refine=None --train_dir=gpurun_out/ckpt --summary_dir=gpurun_out/summ &&
          run cli_eval 300 python road-object-detection-for-bdd100k_amd/evaluate.py --checkpoint_path=gpurun_out/ckpt --batch_size=2 --num_images=6 --eval_dir=gpurun_out/eval &&
          run cli_predict 300 python road-object-detection-for-bdd100k_amd/predict.py --checkpoint_all=gpurun_out/ckpt/mobilenet_v2.model --batch_size=2 --num_batches=2 --output=gpurun_out/pred.json ;;
