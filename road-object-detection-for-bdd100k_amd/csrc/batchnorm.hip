@@ -35,7 +35,9 @@ static RedPlan red_plan(long M, int C, bool vec) {
   r.CVb = cdiv(r.CV, r.cgroups);
   r.lanes = 256 / r.CVb;
   const long want = std::max<long>(1, 1024 / r.cgroups);
-  const long minchunk = (long)r.lanes * 16;
+  // >= 16 rows per lane; 4 on small narrow tensors (C <= 256, M*C <= 4M), whose launches are
+  // latency-bound (measured, tools/bn_bench.py)
+  const long minchunk = (long)r.lanes * (C <= 256 && M * C <= (4L << 20) ? 4 : 16);
   r.chunk = std::max<long>(cdivl(M, want), minchunk);
   r.nbx = (int)cdivl(M, r.chunk);
   return r;
@@ -304,16 +306,33 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
   float sc[V], sh[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) bn_affine(mean, rstd, gamma, beta, c + v, sc[v], sh[v]);
-  for (long r = t0 / CV; r < M; r += rstep) {
-    float xv[V], rv[V];
-    load_v<T, VEC>(x + r * ldx + c, xv);
-    if constexpr (RES) load_v<T, VEC>(res + r * ldr + c, rv);
+  auto row = [&](float (&xv)[V], const float (&rv)[V]) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float z = act_fwd(fmaf(xv[v], sc[v], sh[v]), act);
       if constexpr (RES) z = z + rv[v];
       xv[v] = z;
     }
+  };
+  long r = t0 / CV;
+  for (; r + 3 * rstep < M; r += 4 * rstep) {  // four rows in flight per thread
+    float xa[4][V], ra[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      load_v<T, VEC>(x + (r + u * rstep) * ldx + c, xa[u]);
+      if constexpr (RES) load_v<T, VEC>(res + (r + u * rstep) * ldr + c, ra[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      row(xa[u], ra[u]);
+      store_v<T, VEC>(y + (r + u * rstep) * ldy + c, xa[u]);
+    }
+  }
+  for (; r < M; r += rstep) {
+    float xv[V], rv[V];
+    load_v<T, VEC>(x + r * ldx + c, xv);
+    if constexpr (RES) load_v<T, VEC>(res + r * ldr + c, rv);
+    row(xv, rv);
     store_v<T, VEC>(y + r * ldy + c, xv);
   }
 }
@@ -450,10 +469,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
     mg[v] = coef[C + c + v];
     mgx[v] = coef[2 * C + c + v];
   }
-  for (long r = t0 / CV; r < M; r += rstep) {
-    float xv[V], gv[V];
-    load_v<T, VEC>(x + r * ldx + c, xv);
-    load_v<T, VEC>(dy + r * lddy + c, gv);
+  auto row = [&](float (&xv)[V], const float (&gv)[V]) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float d = xv[v] - mu[v];
@@ -461,6 +477,28 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
       const float g = gv[v] * act_grad(z, act);
       xv[v] = a[v] * (g - mg[v] - (d * rs[v]) * mgx[v]);
     }
+  };
+  long r = t0 / CV;
+  // four rows per iteration, loads first: the small-M launches give each thread only a few
+  // rows, so memory-level parallelism per thread decides their speed
+  for (; r + 3 * rstep < M; r += 4 * rstep) {
+    float xa[4][V], ga[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      load_v<T, VEC>(x + (r + u * rstep) * ldx + c, xa[u]);
+      load_v<T, VEC>(dy + (r + u * rstep) * lddy + c, ga[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      row(xa[u], ga[u]);
+      store_v<T, VEC>(dx + (r + u * rstep) * lddx + c, xa[u]);
+    }
+  }
+  for (; r < M; r += rstep) {
+    float xv[V], gv[V];
+    load_v<T, VEC>(x + r * ldx + c, xv);
+    load_v<T, VEC>(dy + r * lddy + c, gv);
+    row(xv, gv);
     store_v<T, VEC>(dx + r * lddx + c, xv);
   }
 }
@@ -477,6 +515,10 @@ static bool vec_ok(int C, std::initializer_list<std::pair<const void*, int>> buf
   return true;
 }
 
+// Threads for the row-streaming apply kernels: >= ~8 rows per thread on large tensors (the
+// per-thread coefficient loads amortised), but at least 256 blocks' worth on small ones.
+static long apply_threads(long total) { return std::max(total / 8, std::min(total, 256L * 256)); }
+
 static int max_nbx(long M, int C) {
   int a = red_plan<float>(M, C, false).nbx;
   int b = red_plan<float>(M, C, C % 4 == 0).nbx;
@@ -489,7 +531,7 @@ static void apply_launch(bool vec, const void* x, const float* mean, const float
                          const float* beta, const void* res, void* y, long M, int C, int ldx, int ldr, int ldy,
                          int act, hipStream_t s) {
   const int V = vec ? Vec16<T>::N : 1;
-  const int blocks = const_channel_blocks(C / V, M * (C / V));
+  const int blocks = const_channel_blocks(C / V, apply_threads(M * (C / V)));
 #define LA(VE, RE)                                                                                            \
   hipLaunchKernelGGL((bn_apply_kernel<T, VE, RE>), dim3(blocks), dim3(256), 0, s, (const T*)x, mean, rstd, gamma, \
                      beta, (const T*)res, (T*)y, M, C, ldx, ldr, ldy, act)
@@ -554,7 +596,8 @@ static void bwd_launch(bool vec, const void* dy, const void* x, const float* mea
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 4)), dim3(256), 0, s, slab, pl.nbx, M, C, rstd, gamma,
                      dgamma, dbeta, coef);
   const int V = pl.V;
-  const int blocks = const_channel_blocks(C / V, M * (C / V));
+  // >= ~8 rows per thread so the per-thread coefficient loads (7 x V floats) are amortised
+  const int blocks = const_channel_blocks(C / V, apply_threads(M * (C / V)));
   if (vec)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dy, (const T*)x, mean,
                        rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
@@ -623,7 +666,7 @@ int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const flo
   ROD_DISPATCH_DTYPE(dtype, {
     const bool vec = vec_ok<T>(C, {{dz, C}, {y, C}, {dy, C}});
     const int V = vec ? Vec16<T>::N : 1;
-    const int blocks = const_channel_blocks(C / V, M * (C / V));
+    const int blocks = const_channel_blocks(C / V, apply_threads(M * (C / V)));
     if (vec)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dz, (const T*)y,
                          mean, rstd, gamma, beta, coef, (T*)dy, M, C, C, C, C, act);
