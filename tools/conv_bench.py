@@ -26,6 +26,7 @@ def main():
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--out', default=None)
     ap.add_argument('--check', default=None)
+    ap.add_argument('--ops', default='fwd_plain,fwd_stats,bwd_data,wgrad')
     a = ap.parse_args()
     dt = torch.bfloat16
     dev = 'cuda'
@@ -58,12 +59,15 @@ def main():
         K = ks * ks * Cin
         io_f = 2 * (M * Cin + M * Cout)
         calls = {
+            'fwd_plain': (lambda: ops.conv_fwd_raw(x, wt0, None, y, N, H, W, Cin, Cout, ks), io_f),
             'fwd_stats': (lambda: ops.conv_fwd_raw(x, wt0, None, y, N, H, W, Cin, Cout, ks, parts, pro), io_f),
             'bwd_data': (lambda: ops.conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks), io_f),
             'wgrad': (lambda: _abi.call('rod_conv_wgrad', x, *ops._pro_args(pro), dy, dw, None, wws, N, H, W, Cin,
                                         Cout, ks, 0, 0, 1, s), io_f),
         }
         for op, (fn, io) in calls.items():
+            if op not in a.ops.split(','):
+                continue
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -80,6 +84,8 @@ def main():
             if op == 'fwd_stats':
                 _abi.call('rod_bn_finalize', parts, parts.shape[0], M, Cout, 1e-3, 0.997, mu, rs, None, None, fws, s)
                 res[key] = (y.float().cpu(), mu.cpu(), rs.cpu())
+            elif op == 'fwd_plain':
+                pass
             elif op == 'bwd_data':
                 res[key] = (dx.float().cpu(),)
             else:
