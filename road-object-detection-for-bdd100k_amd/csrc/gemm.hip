@@ -215,8 +215,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   constexpr int LDC = BN + EV;
   constexpr int MAIN_BYTES = (BM + BN) * LD * sizeof(T);
   constexpr int EPI_BYTES = VY ? 64 * LDC * sizeof(T) : 0;
-  // STATS final reduction scratch (reuses the staging area): 2*256*EV + 256 + 3*TPC*BN + BN floats
-  constexpr int ST_BYTES = (VY && STATS) ? (2 * 256 * EV + 256 + 3 * (256 / BN > 0 ? 256 / BN : 1) * BN + BN) * 4 : 0;
+  constexpr int ST_BYTES = 0;
   constexpr int SM1 = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   constexpr int SMEM = SM1 > ST_BYTES ? SM1 : ST_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -341,12 +340,75 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     const int gcc = (tid % GCPR) * EV, grg = tid / GCPR;
     const int gcol = n0 + gcc;
     const bool gact = GRED && grg < GRPP && gcol < Cout;
-    const bool sact = STATS && grg < GRPP && gcol < Cout;
-    constexpr int SVN = STATS ? EV : 1;
-    float spv[SVN], smu[SVN], sm2[SVN];  // pivot-shifted sums, then (mean, M2)
-    float scnt = 0.f;
+    // STATS from the accumulators, before staging: a column of a 16x16 MFMA tile lives in the
+    // four lanes l, l^16, l^32, l^48 (rows 4(l>>4)+r).  Per wave and column: pivot = mean of the
+    // wave strip's first (up to) 8 valid rows, then sums of (v - pivot), (v - pivot)^2 over the
+    // strip's valid rows (v = the output rounded to T), combined across the four lane groups by
+    // shuffles -> (n, mean, M2) per wave; the WM waves are Chan-merged in order at the end.
+    // per-wave (count, mean, M2) of each column: [WM][3][BN] floats in their own LDS (written
+    // here, read after the staging loop, whose barriers order the two)
+    __shared__ float wst[(VY && STATS) ? WM * 3 * BN : 1];
+    if constexpr (STATS) {
+      const int lg = lane >> 4;
+      // rows of this wave's strip still inside M (all of them except in the last tile)
+      const long left_l = M - (m0 + wm * WROWS);
+      const int left = left_l > WROWS ? WROWS : (left_l < 0 ? 0 : (int)left_l);
 #pragma unroll
-    for (int v = 0; v < SVN; ++v) spv[v] = smu[v] = sm2[v] = 0.f;
+      for (int b = 0; b < NT; ++b) {
+        float p = 0.f, pc = 0.f;
+        if (lg < 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (lg * 4 + r < left) {
+              p += to_f32(from_f32<T>(acc[0][b][r] + bv[b]));
+              pc += 1.f;
+            }
+          }
+        }
+        p += __shfl_xor(p, 16, 64);
+        pc += __shfl_xor(pc, 16, 64);
+        p = __shfl(p, lane & 15, 64);
+        pc = __shfl(pc, lane & 15, 64);
+        const float piv = pc > 0.f ? p / pc : 0.f;
+        float s1 = 0.f, s2 = 0.f, n = 0.f;
+        if (left == WROWS) {  // full strip: no row checks
+#pragma unroll
+          for (int a = 0; a < MT; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float d = to_f32(from_f32<T>(acc[a][b][r] + bv[b])) - piv;
+              s1 += d;
+              s2 = fmaf(d, d, s2);
+            }
+          n = (float)(MT * 4);
+        } else {
+#pragma unroll
+          for (int a = 0; a < MT; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (a * 16 + lg * 4 + r < left) {
+                const float d = to_f32(from_f32<T>(acc[a][b][r] + bv[b])) - piv;
+                s1 += d;
+                s2 = fmaf(d, d, s2);
+                n += 1.f;
+              }
+            }
+        }
+        s1 += __shfl_xor(s1, 16, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        n += __shfl_xor(n, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        n += __shfl_xor(n, 32, 64);
+        if (lane < 16) {
+          const float dm = n > 0.f ? s1 / n : 0.f;
+          const int cl = wn * (BN / WN) + b * 16 + lane;
+          wst[(wm * 3 + 0) * BN + cl] = n;
+          wst[(wm * 3 + 1) * BN + cl] = piv + dm;
+          wst[(wm * 3 + 2) * BN + cl] = fmaxf(s2 - s1 * dm, 0.f);
+        }
+      }
+    }
     constexpr int GV = GRED ? EV : 1;
     float gsc[GV], gsh[GV], gmu[GV], grs[GV], gs[GV], gsx[GV];
 #pragma unroll
@@ -392,38 +454,6 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
           }
         }
       }
-      if constexpr (STATS) {
-        const long left = M - (m0 + h * 64);
-        const int nrows = left < 64 ? (int)left : 64;
-        if (sact) {
-          if (h == 0) {  // the column's pivot: mean of the tile's first (up to) 8 rows, same in every thread
-            const int np = nrows < 8 ? nrows : 8;
-#pragma unroll
-            for (int v = 0; v < SVN; ++v) spv[v] = 0.f;
-            for (int r = 0; r < np; ++r) {
-              Vec16<T> pv;
-              pv.v = *(const decltype(pv.v)*)(Cs + r * LDC + gcc);
-#pragma unroll
-              for (int v = 0; v < SVN; ++v) spv[v] += pv.get(v);
-            }
-            const float inv = 1.f / (float)np;
-#pragma unroll
-            for (int v = 0; v < SVN; ++v) spv[v] *= inv;
-          }
-#pragma unroll 2
-          for (int r = grg; r < nrows; r += GRPP) {
-            Vec16<T> dv;
-            dv.v = *(const decltype(dv.v)*)(Cs + r * LDC + gcc);
-#pragma unroll
-            for (int v = 0; v < SVN; ++v) {
-              const float d = dv.get(v) - spv[v];
-              smu[v] += d;
-              sm2[v] = fmaf(d, d, sm2[v]);
-            }
-            scnt += 1.f;
-          }
-        }
-      }
       constexpr int CPR = BN / EV;  // 16-byte chunks per row
       for (int idx = tid; idx < 64 * CPR; idx += 256) {
         const int rr = idx / CPR, cc = (idx - rr * CPR) * EV;
@@ -460,51 +490,20 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
       }
     }
     if constexpr (STATS) {
-      // per column (common pivot k): the GRPP row groups -> TPC interleaved slices (stage A, all
-      // threads) -> the slices in order (stage B, one thread per column): plain sums of
-      // (v - k), (v - k)^2 and the count -> (n, k + S1/n, S2 - S1^2/n) of part blockIdx.x
-      constexpr int TPC = 256 / BN > 0 ? 256 / BN : 1;
-      float* r1 = (float*)smem;          // [256][EV]
-      float* r2 = r1 + 256 * EV;         // [256][EV]
-      float* rc = r2 + 256 * EV;         // [256]
-      float* pa = rc + 256;              // [3][TPC][BN]
-      float* pv = pa + 3 * TPC * BN;     // [BN]
-      __syncthreads();
-#pragma unroll
-      for (int v = 0; v < SVN; ++v) {
-        r1[tid * EV + v] = smu[v];
-        r2[tid * EV + v] = sm2[v];
-      }
-      rc[tid] = scnt;
-      if (sact && grg == 0) {
-#pragma unroll
-        for (int v = 0; v < SVN; ++v) pv[gcc + v] = spv[v];
-      }
-      __syncthreads();
-      if (tid < TPC * BN) {
-        const int col = tid % BN, j = tid / BN;
-        const int ch = col / EV, v = col - ch * EV;
-        float a = 0.f, b = 0.f, nn = 0.f;
-        for (int q = j; q < GRPP; q += TPC) {
-          const int t2 = q * GCPR + ch;
-          a += r1[t2 * EV + v];
-          b += r2[t2 * EV + v];
-          nn += rc[t2];
-        }
-        pa[(0 * TPC + j) * BN + col] = a;
-        pa[(1 * TPC + j) * BN + col] = b;
-        pa[(2 * TPC + j) * BN + col] = nn;
-      }
-      __syncthreads();
+      const float* st = wst;
       if (tid < BN && n0 + tid < Cout) {
-        float a = 0.f, b = 0.f, nn = 0.f;
-        for (int j = 0; j < TPC; ++j) {
-          a += pa[(0 * TPC + j) * BN + tid];
-          b += pa[(1 * TPC + j) * BN + tid];
-          nn += pa[(2 * TPC + j) * BN + tid];
+        float n = st[tid], mu = st[BN + tid], m2 = st[2 * BN + tid];
+        for (int w = 1; w < WM; ++w) {  // Chan merge in wave order
+          const float nb = st[(w * 3) * BN + tid];
+          if (nb <= 0.f) continue;
+          const float mb = st[(w * 3 + 1) * BN + tid], m2b = st[(w * 3 + 2) * BN + tid];
+          const float nn = n + nb;
+          const float d = mb - mu;
+          mu = mu + d * (nb / nn);
+          m2 = m2 + m2b + d * d * (n * nb / nn);
+          n = nn;
         }
-        const float dm = nn > 0.f ? a / nn : 0.f;
-        store_stat_part(part, Cout, blockIdx.x, n0 + tid, nn, pv[tid] + dm, fmaxf(b - a * dm, 0.f));
+        store_stat_part(part, Cout, blockIdx.x, n0 + tid, n, mu, m2);
       }
     }
   } else {
