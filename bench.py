@@ -163,9 +163,16 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # RCCL ('nccl') is the product path; ROD_DIST_BACKEND=gloo rehearses the N>1 path with
+    # several ranks sharing the GPUs of a smaller box (device = LOCAL_RANK mod device count)
+    backend = os.environ.get('ROD_DIST_BACKEND', 'nccl')
     if world > 1:
+        local = local % torch.cuda.device_count() if backend != 'nccl' else local
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            torch.distributed.init_process_group(backend)
     dev = torch.device('cuda', local)
     import config
     from rod import _abi, roofline
@@ -268,6 +275,7 @@ def main():
                        'global_batch': args.batch * world, 'img_hw': [args.height, args.width],
                        'train_range': args.train_range, 'parallelism': f'dp{world}',
                        'augment': bool(args.augment),
+                       **({'dist_backend': 'rccl' if backend == 'nccl' else backend} if world > 1 else {}),
                        **({} if args.train_range == 'REFINE' else {'fix_refine': args.fix_refine})},
             'loss': round(loss_val, 5),
             'roofline': rl,
