@@ -622,6 +622,132 @@ __global__ void __launch_bounds__(256) stem_conv_fwd_kernel(const T* __restrict_
   }
 }
 
+constexpr int SW_TW = 128;  // stem kernels: pixels per block row
+constexpr int SW_LD = 40;   // stem kernels: LDS row (elements), 80 B
+
+// =====================================================================================
+// stem forward on MFMA (bf16, Cout = 32): a block makes 128 consecutive pixels of one image
+// row.  Each thread gathers 16 taps of one pixel's 3x3x3 patch (as stem_wgrad_kernel) into
+// an im2col tile Xs[128][32] (taps 27..31 zero); wave w multiplies pixels [32w, 32w+32) by
+// the [32 taps][32 co] weights held in registers (2 x 2 16x16x32 MFMAs: A rows = pixels read
+// straight from Xs, B = Wt rows), adds the bias, rounds, and stages the [128][32] tile in
+// LDS so each thread stores 32 contiguous bytes.  STATS (W % 128 == 0, so the block is
+// exactly the 128-row tile blockIdx of the rod_conv_fwd stat_parts contract): per channel,
+// 8 lanes x 16 pixels of pivot-shifted sums of the rounded outputs, xor-shuffle combined.
+// =====================================================================================
+// Taps [16*HALF, 16*HALF + 16) of pixel (n, y, xx)'s 3x3x3 SAME patch (tap = (r*3 + c)*3 + ci;
+// taps >= 27 and padding read as zero).  HALF is a template argument so every tap's
+// (r, c, ci) folds to constants; callers make it wave-uniform.
+template <int HALF>
+__device__ __forceinline__ void stem_gather(const unsigned short* __restrict__ Xu, long nH, int y, int xx, int H,
+                                            int W, int ldx, unsigned short (&tv)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = HALF * 16 + j;
+    unsigned short v = 0;
+    if (k < 27) {
+      const int r = k / 9, c = (k / 3) % 3, ci = k % 3;
+      const int iy = y + r - 1, ix = xx + c - 1;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W && xx < W)
+        v = Xu[((nH + iy) * W + ix) * ldx + ci];
+    }
+    tv[j] = v;
+  }
+}
+
+template <bool STATS>
+__global__ void __launch_bounds__(256) stem_fwd_mfma_kernel(const bf16_t* __restrict__ X,
+                                                            const bf16_t* __restrict__ Wt,
+                                                            const float* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                            float* __restrict__ stats, int H, int W, int ldx,
+                                                            int ldy, int rb) {
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[SW_TW * SW_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ys[SW_TW * SW_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int x0 = blockIdx.x * SW_TW, n = blockIdx.z;
+  const int ya = blockIdx.y * rb;
+  const int yz = ya + rb < H ? ya + rb : H;
+  const int px = tid >> 1, half = tid & 1;  // output store: pixel, 16-channel half
+  const int xx = x0 + px;
+  const bool inx = xx < W;
+  const int pg = tid & 127, hg = tid >> 7;  // gather: pixel, wave-uniform tap half
+  typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+  unsigned short tv[16];
+  auto gather = [&](int y) {
+    if (hg) stem_gather<1>((const unsigned short*)X, (long)n * H, y, x0 + pg, H, W, ldx, tv);
+    else stem_gather<0>((const unsigned short*)X, (long)n * H, y, x0 + pg, H, W, ldx, tv);
+  };
+  const int g = lane >> 4, i = lane & 15;
+  bf16x8 fb[2];  // B[k = 8g + j][co = ct*16 + i] = Wt[co][k]
+  float bv[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * g + j;
+      fb[ct][j] = k < 27 ? Wt[(ct * 16 + i) * 27 + k] : (bf16_t)0.f;
+    }
+    bv[ct] = bias ? bias[ct * 16 + i] : 0.f;
+  }
+  if (ya < yz) gather(ya);
+  for (int y = ya; y < yz; ++y) {
+    __syncthreads();
+    {
+      u16x8 t0, t1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        t0[j] = tv[j];
+        t1[j] = tv[8 + j];
+      }
+      *(u16x8*)(Xs + pg * SW_LD + hg * 16) = t0;
+      *(u16x8*)(Xs + pg * SW_LD + hg * 16 + 8) = t1;
+    }
+    __syncthreads();
+    if (y + 1 < yz) gather(y + 1);  // next row's patch loads in flight under this row
+    const int m0 = wave * 32;
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const bf16x8 fa = *(const bf16x8*)(Xs + (m0 + pt * 16 + i) * SW_LD + 8 * g);
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[ct], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ys[(m0 + pt * 16 + g * 4 + r) * SW_LD + ct * 16 + i] = (bf16_t)(acc[r] + bv[ct]);
+      }
+    }
+    __syncthreads();
+    if (inx) {
+      bf16_t* dst = Y + (((long)n * H + y) * W + xx) * ldy + half * 16;
+      *(bf16x8*)dst = *(const bf16x8*)(Ys + px * SW_LD + half * 16);
+      *(bf16x8*)(dst + 8) = *(const bf16x8*)(Ys + px * SW_LD + half * 16 + 8);
+    }
+    if constexpr (STATS) {
+      const int c = tid >> 3, sub = tid & 7;
+      const float k = (float)Ys[c];  // pivot: pixel 0 of the tile
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float d = (float)Ys[(sub * 16 + j) * SW_LD + c] - k;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      if (sub == 0) {
+        const long tile = (((long)n * H + y) * W + x0) / SW_TW;
+        const double nb = (double)SW_TW;
+        const double m2 = (double)s2 - (double)s1 * (double)s1 / nb;
+        store_stat_part(stats, 32, tile, c, (float)nb, (float)((double)k + (double)s1 / nb),
+                        (float)(m2 > 0.0 ? m2 : 0.0));
+      }
+    }
+  }
+}
+
 // =====================================================================================
 // weight gradient: part[s][co][k] = sum_{m in split s} dy[m, co] * A[m, k]
 // tile 64 (co) x 64 (k); rows staged m-major in LDS and read transposed
@@ -637,13 +763,16 @@ __device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
   return __builtin_bit_cast(bf16x4, r);
 }
 
+// RPT row chunks per thread per step (bf16: 2, so a block keeps two 32-row steps of loads in
+// flight per barrier pair; the kernel is load-latency bound at <= 8 resident blocks per CU)
 template <typename T, int KS, bool VA, bool VD, int CIN = 0, bool PRO = false>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X, const T* __restrict__ DY,
                                                          float* __restrict__ part, long M, int H, int W, int Cin,
                                                          int Cout, int ldx, int lddy, long chunk, int ktiles,
                                                          BnPro pro = BnPro{}) {
-  __shared__ __attribute__((aligned(16))) T Ds[BK * WG_LD];  // [m][co]
-  __shared__ __attribute__((aligned(16))) T Xs[BK * WG_LD];  // [m][k]
+  constexpr int RPT = sizeof(T) == 2 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) T Ds[RPT * BK * WG_LD];  // [m][co]
+  __shared__ __attribute__((aligned(16))) T Xs[RPT * BK * WG_LD];  // [m][k]
   extern __shared__ float pro_lds[];  // PRO: [Cin][2] prologue table (dynamic LDS)
   if constexpr (PRO) {
     stage_pro(pro_lds, pro, Cin);
@@ -669,9 +798,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.f;
 
-  Chunk8<T> rd, rx;
-  auto load_step = [&](long m) {
-    const long row = m + lr;
+  Chunk8<T> rdv[RPT], rxv[RPT];
+  auto load_one = [&](long row, Chunk8<T>& rd, Chunk8<T>& rx) {
     // dy[row, co0+lc .. +7]
     if (row >= me || co0 + lc >= Cout) {
       rd.zero();
@@ -685,32 +813,41 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
     rs.init(X, row < me ? row : M, M, H, W, ldx);
     rs.template load<VA, PRO>(rx, k0 + lc, K, Cin, H, W, ldx, pro_lds, pro.act);
   };
+  auto load_step = [&](long m) {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) load_one(m + lr + u * BK, rdv[u], rxv[u]);
+  };
 
   if (mb < me) load_step(mb);
-  for (long m = mb; m < me; m += BK) {
+  for (long m = mb; m < me; m += RPT * BK) {
     __syncthreads();
-    rd.store_lds(Ds + lr * WG_LD + lc);
-    if constexpr (PRO) {
-      RowSrc<T, KS, CIN> rp;  // (pro_pending only needs KS)
-      rp.template pro_pending<PRO>(rx, k0 + lc, Cin, pro_lds, pro.act);
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      rdv[u].store_lds(Ds + (lr + u * BK) * WG_LD + lc);
+      if constexpr (PRO) {
+        RowSrc<T, KS, CIN> rp;  // (pro_pending only needs KS)
+        rp.template pro_pending<PRO>(rxv[u], k0 + lc, Cin, pro_lds, pro.act);
+      }
+      rxv[u].store_lds(Xs + (lr + u * BK) * WG_LD + lc);
     }
-    rx.store_lds(Xs + lr * WG_LD + lc);
     __syncthreads();
-    if (m + BK < me) load_step(m + BK);
+    if (m + RPT * BK < me) load_step(m + RPT * BK);
+#pragma unroll
+    for (int u = 0; u < RPT; ++u)
     if constexpr (sizeof(T) == 2) {
       // A operand (rows = co): lane needs Ds[8g+j][co]; B (cols = k): Xs[8g+j][k]
       const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         const int cb = wm * 32 + a * 16;
-        const bf16x4 lo = tr_read((const bf16_t*)Ds + (8 * g + q) * WG_LD + cb + 4 * p);
-        const bf16x4 hi = tr_read((const bf16_t*)Ds + (8 * g + 4 + q) * WG_LD + cb + 4 * p);
+        const bf16x4 lo = tr_read((const bf16_t*)Ds + (u * BK + 8 * g + q) * WG_LD + cb + 4 * p);
+        const bf16x4 hi = tr_read((const bf16_t*)Ds + (u * BK + 8 * g + 4 + q) * WG_LD + cb + 4 * p);
         bf16x8 fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const int kb = wn * 32 + b * 16;
-          const bf16x4 l2 = tr_read((const bf16_t*)Xs + (8 * g + q) * WG_LD + kb + 4 * p);
-          const bf16x4 h2 = tr_read((const bf16_t*)Xs + (8 * g + 4 + q) * WG_LD + kb + 4 * p);
+          const bf16x4 l2 = tr_read((const bf16_t*)Xs + (u * BK + 8 * g + q) * WG_LD + kb + 4 * p);
+          const bf16x4 h2 = tr_read((const bf16_t*)Xs + (u * BK + 8 * g + 4 + q) * WG_LD + kb + 4 * p);
           bf16x8 fb = {l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[a][b], 0, 0, 0);
         }
@@ -720,7 +857,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
       const int i = lane & 15, q = lane >> 4;
 #pragma unroll
       for (int kk = 0; kk < BK / 4; ++kk) {
-        const int mr = kk * 4 + q;
+        const int mr = u * BK + kk * 4 + q;
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           const float av = ((const float*)Ds)[mr * WG_LD + wm * 32 + a * 16 + i];
@@ -747,6 +884,132 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
         if (co < Cout) out[(long)co * K + k] = acc[a][b][r];
       }
     }
+}
+
+// =====================================================================================
+// stem weight gradient (3x3 / stride 1 / SAME, Cin = 3, Cout = 32, bf16):
+// part[blk][co][k] = sum over the block's pixels of dy[px, co] * im2col[px, k], k = 27 taps.
+// A block owns 128 consecutive pixels of one image row for RB image rows.  Per row, each
+// thread loads 32 bytes of dy (one pixel, 16 channels) and gathers its 16 taps of that
+// pixel's 3x3x3 patch (contiguous 9-element runs of the three input rows; SAME padding
+// and x >= W read as zero), so the [128][32] dy tile and the [128][32] im2col tile (taps
+// 27..31 zero) are built in LDS with one 16-byte store per 8 values; the next row's loads
+// are issued before the MFMAs of the current one.  Wave w contracts pixels [32w, 32w+32)
+// with 2 x 2 16x16x32 bf16 MFMAs (co tiles x tap tiles, operands read transposed with
+// ds_read_b64_tr_b16 as in conv_wgrad_kernel); the four waves' tiles are summed in LDS in
+// a fixed order and the block writes its 32 x 27 partial (summed by slab_sum).
+// =====================================================================================
+
+struct StemWgradPlan {
+  int xb, yb, rb, nblk;
+};
+static StemWgradPlan stem_wgrad_plan(int N, int H, int W) {
+  StemWgradPlan p;
+  p.xb = cdiv(W, SW_TW);
+  const long segs = (long)N * H * p.xb;
+  p.rb = (int)std::max<long>(1, cdivl(segs, 2048));  // <= ~2048 partials
+  p.yb = cdiv(H, p.rb);
+  p.nblk = N * p.yb * p.xb;
+  return p;
+}
+
+__global__ void __launch_bounds__(256) stem_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
+                                                         float* __restrict__ part, int H, int W, int ldx, int lddy,
+                                                         int rb) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * SW_TW * SW_LD];  // Ds [px][co] | Xs [px][tap]
+  bf16_t* Ds = lds;
+  bf16_t* Xs = lds + SW_TW * SW_LD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int x0 = blockIdx.x * SW_TW;
+  const int n = blockIdx.z;
+  const int ya = blockIdx.y * rb;
+  const int yz = ya + rb < H ? ya + rb : H;
+  const int px = tid >> 1, half = tid & 1;  // dy loader: pixel, 16-channel half
+  const int xx = x0 + px;
+  const bool inx = xx < W;
+  const int pg = tid & 127, hg = tid >> 7;  // gather: pixel, wave-uniform tap half
+
+  bf16x8 d0, d1;
+  unsigned short tv[16];
+  const unsigned short* Xu = (const unsigned short*)X;
+  auto load_row = [&](int y) {
+    if (inx) {
+      const bf16_t* src = DY + (((long)n * H + y) * W + xx) * lddy + half * 16;
+      d0 = *(const bf16x8*)src;
+      d1 = *(const bf16x8*)(src + 8);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d0[j] = d1[j] = (bf16_t)0.f;
+    }
+    if (hg) stem_gather<1>(Xu, (long)n * H, y, x0 + pg, H, W, ldx, tv);
+    else stem_gather<0>(Xu, (long)n * H, y, x0 + pg, H, W, ldx, tv);
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.f;
+
+  if (ya < yz) load_row(ya);
+  for (int y = ya; y < yz; ++y) {
+    __syncthreads();
+    *(bf16x8*)(Ds + px * SW_LD + half * 16) = d0;
+    *(bf16x8*)(Ds + px * SW_LD + half * 16 + 8) = d1;
+    {
+      typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+      u16x8 t0, t1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        t0[j] = tv[j];
+        t1[j] = tv[8 + j];
+      }
+      *(u16x8*)(Xs + pg * SW_LD + hg * 16) = t0;
+      *(u16x8*)(Xs + pg * SW_LD + hg * 16 + 8) = t1;
+    }
+    __syncthreads();
+    if (y + 1 < yz) load_row(y + 1);
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int m0 = wave * 32;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const bf16x4 lo = tr_read(Ds + (m0 + 8 * g + q) * SW_LD + a * 16 + 4 * p);
+      const bf16x4 hi = tr_read(Ds + (m0 + 8 * g + 4 + q) * SW_LD + a * 16 + 4 * p);
+      bf16x8 fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const bf16x4 l2 = tr_read(Xs + (m0 + 8 * g + q) * SW_LD + b * 16 + 4 * p);
+        const bf16x4 h2 = tr_read(Xs + (m0 + 8 * g + 4 + q) * SW_LD + b * 16 + 4 * p);
+        bf16x8 fb = {l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[a][b], 0, 0, 0);
+      }
+    }
+  }
+  // fixed-order sum of the four waves' 32 x 32 tiles: red[wave][co][tap]
+  __syncthreads();
+  float* red = (float*)lds;  // 4 * 32 * 32 floats = 16 KB <= 20 KB
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = a * 16 + (lane >> 4) * 4 + r, k = b * 16 + (lane & 15);
+        red[(wave * 32 + co) * 32 + k] = acc[a][b][r];
+      }
+  __syncthreads();
+  const long blk = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  float* out = part + blk * 32 * 27;
+  for (int e = tid; e < 32 * 27; e += 256) {
+    const int co = e / 27, k = e - co * 27;
+    float s = red[co * 32 + k];
+    s += red[(32 + co) * 32 + k];
+    s += red[(64 + co) * 32 + k];
+    s += red[(96 + co) * 32 + k];
+    out[e] = s;
+  }
 }
 
 __global__ void split_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int splits, long n) {
@@ -930,6 +1193,24 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
   const int nparts = (int)cdivl(M, 128);
   const int dt = sizeof(T) == 4 ? ROD_F32 : ROD_BF16;
   const BnPro pv = pro ? *pro : BnPro{};
+  static const bool old_stem_fwd = getenv("ROD_DEBUG_OLDSTEMFWD") != nullptr;  // A/B against the VALU kernel
+  if constexpr (sizeof(T) == 2) {
+    if (!pro && !gr && ksize == 3 && Cin == 3 && Cout == 32 && vy && !old_stem_fwd) {
+      const bool fuse = stats != nullptr && W % SW_TW == 0;  // block == stat tile
+      // rows per block: >= ~4 blocks' worth per CU of rows, pipelined within a block
+      const int xb = cdiv(W, SW_TW);
+      const int rb = (int)std::max<long>(1, std::min<long>(8, (long)N * H * xb / 8192));
+      const dim3 grid(xb, cdiv(H, rb), N);
+      if (fuse)
+        hipLaunchKernelGGL(stem_fwd_mfma_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wt,
+                           bias, (bf16_t*)y, stats, H, W, ldx, ldy, rb);
+      else
+        hipLaunchKernelGGL(stem_fwd_mfma_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wt,
+                           bias, (bf16_t*)y, nullptr, H, W, ldx, ldy, rb);
+      if (stats && !fuse) stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
+      return;
+    }
+  }
   if (ws != nullptr && sp.splits > 1 && va && vb) {
     float* part = (float*)ws;
     if (ksize == 1) {
@@ -998,7 +1279,19 @@ static void wgrad_typed(const void* x, const BnPro* pro, const void* dy, float* 
   const bool va = aligned16<T>(x) && (ldx % eV == 0) && (ksize == 1 ? true : (Cin % 8 == 0));
   const bool vd = aligned16<T>(dy) && (lddy % eV == 0);
   const BnPro pv = pro ? *pro : BnPro{};
-  if (!pro && ksize == 3 && Cin == 3 && vd) {
+  static const bool old_stem = getenv("ROD_DEBUG_OLDSTEMWG") != nullptr;  // A/B against the generic kernel
+  bool stem = false;
+  if constexpr (sizeof(T) == 2) {
+    if (!pro && ksize == 3 && Cin == 3 && Cout == 32 && vd && !old_stem) {
+      const StemWgradPlan sp = stem_wgrad_plan(N, H, W);
+      hipLaunchKernelGGL(stem_wgrad_kernel, dim3(sp.xb, sp.yb, N), dim3(256), 0, s, (const bf16_t*)x,
+                         (const bf16_t*)dy, part, H, W, ldx, lddy, sp.rb);
+      p.splits = sp.nblk;
+      stem = true;
+    }
+  }
+  if (stem) {
+  } else if (!pro && ksize == 3 && Cin == 3 && vd) {
     dim3 grid(p.ctiles * p.ktiles, p.splits);
     hipLaunchKernelGGL((conv_wgrad_kernel<T, 3, false, true, 3>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy,
                        part, M, H, W, Cin, Cout, ldx, lddy, p.chunk, p.ktiles, pv);
@@ -1075,6 +1368,7 @@ size_t rod_conv_wgrad_workspace(int N, int H, int W, int Cin, int Cout, int ksiz
   const long M = (long)N * H * W;
   WgradPlan p = wgrad_plan(M, Cin, Cout, ksize);
   const long K = (long)ksize * ksize * Cin;
+  if (ksize == 3 && Cin == 3 && Cout == 32) p.splits = std::max(p.splits, stem_wgrad_plan(N, H, W).nblk);
   size_t part = (size_t)p.splits * Cout * K * sizeof(float);
   long cchunk = std::max<long>(64, cdivl(M, 512));
   size_t cs = (size_t)cdivl(M, cchunk) * Cout * sizeof(float);

@@ -18,7 +18,8 @@ from rod import _abi, ops  # noqa: E402
 # L12 expand, stem, head 3x3, head 1x1
 SHAPES = [(8, 720, 1280, 16, 96, 1, 0), (8, 360, 640, 96, 24, 1, 1), (8, 360, 640, 24, 144, 1, 0),
           (8, 360, 640, 144, 24, 1, 1), (8, 180, 320, 32, 192, 1, 0), (8, 90, 160, 64, 384, 1, 0),
-          (8, 90, 160, 384, 64, 1, 1), (8, 90, 160, 128, 128, 3, 2), (8, 90, 160, 64, 128, 1, 0)]
+          (8, 90, 160, 384, 64, 1, 1), (8, 90, 160, 128, 128, 3, 2), (8, 90, 160, 64, 128, 1, 0),
+          (8, 720, 1280, 3, 32, 3, 0)]
 
 
 def main():
@@ -27,13 +28,15 @@ def main():
     ap.add_argument('--out', default=None)
     ap.add_argument('--check', default=None)
     ap.add_argument('--ops', default='fwd_plain,fwd_stats,bwd_data,wgrad')
+    ap.add_argument('--shapes', default=None, help='comma-separated SHAPES indices (default all)')
     a = ap.parse_args()
     dt = torch.bfloat16
     dev = 'cuda'
     g = torch.Generator(device=dev).manual_seed(0)
     s = ops.stream()
     res, tot = {}, {}
-    for (N, H, W, Cin, Cout, ks, act) in SHAPES:
+    sel = [SHAPES[int(i)] for i in a.shapes.split(',')] if a.shapes else SHAPES
+    for (N, H, W, Cin, Cout, ks, act) in sel:
         M = N * H * W
         x = torch.randn((N, H, W, Cin), device=dev, generator=g).to(dt)
         dy = torch.randn((N, H, W, Cout), device=dev, generator=g).to(dt)
@@ -67,6 +70,8 @@ def main():
         }
         for op, (fn, io) in calls.items():
             if op not in a.ops.split(','):
+                continue
+            if op == 'bwd_data' and Cin == 3:  # the stem has no backward-data (input = image)
                 continue
             fn()
             torch.cuda.synchronize()
