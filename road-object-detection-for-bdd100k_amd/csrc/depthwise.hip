@@ -21,6 +21,7 @@ template <> struct PackV<float, 4> {
   __device__ __forceinline__ float get(int i) const { return v[i]; }
   __device__ __forceinline__ void set(int i, float a) { v[i] = a; }
   __device__ __forceinline__ void store(float* p) const { *(f32x4*)p = v; }
+  __device__ __forceinline__ void store_out(float* p) const { ROD_ST_OUT((f32x4*)p, v); }
 };
 template <> struct PackV<bf16_t, 4> {
   bf16x4 v;
@@ -29,6 +30,7 @@ template <> struct PackV<bf16_t, 4> {
   __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
   __device__ __forceinline__ void set(int i, float a) { v[i] = (bf16_t)a; }
   __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x4*)p = v; }
+  __device__ __forceinline__ void store_out(bf16_t* p) const { ROD_ST_OUT((bf16x4*)p, v); }
 };
 template <> struct PackV<bf16_t, 8> {
   bf16x8 v;
@@ -40,6 +42,7 @@ template <> struct PackV<bf16_t, 8> {
   __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
   __device__ __forceinline__ void set(int i, float a) { v[i] = (bf16_t)a; }
   __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x8*)p = v; }
+  __device__ __forceinline__ void store_out(bf16_t* p) const { ROD_ST_OUT((bf16x8*)p, v); }
 };
 template <typename T> struct PackV<T, 1> {
   T v;
@@ -48,6 +51,7 @@ template <typename T> struct PackV<T, 1> {
   __device__ __forceinline__ float get(int) const { return to_f32(v); }
   __device__ __forceinline__ void set(int, float a) { v = from_f32<T>(a); }
   __device__ __forceinline__ void store(T* p) const { *p = v; }
+  __device__ __forceinline__ void store_out(T* p) const { *p = v; }
 };
 
 constexpr int DW_RB = 8;  // output rows per thread (forward / backward-data strips)
@@ -155,7 +159,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(const T* __restrict__ x,
       PackV<T, V> o;
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
-      o.store(yn + ((long)ho * Wo + wo) * C);
+      o.store_out(yn + ((long)ho * Wo + wo) * C);
       if constexpr (STATS) {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -419,7 +423,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
     Vec16<T> o;
 #pragma unroll
     for (int v = 0; v < V; ++v) o.set(v, a[v]);
-    o.store(yn + ((long)ho * Wo + wo) * C);
+    o.store_out(yn + ((long)ho * Wo + wo) * C);
     if constexpr (STATS) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
@@ -435,7 +439,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
     PackV<T, V> o;
 #pragma unroll
     for (int v = 0; v < V; ++v) o.set(v, a[v]);
-    o.store(yn + ((long)ho * Wo + wo) * C);
+    o.store_out(yn + ((long)ho * Wo + wo) * C);
     if constexpr (GRED) {
 #pragma unroll
       for (int v = 0; v < V; ++v)
@@ -915,7 +919,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
       PackV<T, V> o;
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
-      o.store(xn + ((long)h * W + wc) * C);
+      o.store_out(xn + ((long)h * W + wc) * C);
       if constexpr (GRED) gd.template acc<T>(o, gy + ((long)h * W + wc) * C, gr.p.act);
       if (h + 1 < h1) {
 #pragma unroll
@@ -953,7 +957,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_kernel(const T* __restrict
       PackV<T, V> o;
 #pragma unroll
       for (int v = 0; v < V; ++v) o.set(v, acc[v]);
-      o.store(xn + ((long)h * W + wc) * C);
+      o.store_out(xn + ((long)h * W + wc) * C);
       if constexpr (GRED) gd.template acc<T>(o, gy + ((long)h * W + wc) * C, gr.p.act);
     }
   }
@@ -1036,7 +1040,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_s2_kernel(const T* __restr
       PackV<T, V> pk;
 #pragma unroll
       for (int v = 0; v < V; ++v) pk.set(v, o[v]);
-      pk.store(xn + ((long)h * W + ww) * C);
+      pk.store_out(xn + ((long)h * W + ww) * C);
       if constexpr (GRED) {
 #pragma unroll
         for (int v = 0; v < V; ++v)

@@ -463,7 +463,8 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         const T* src = Cs + rr * LDC + cc;
         T* dst = Y + row * ldy + col;
         if (col + EV <= Cout) {
-          *(uint4*)dst = *(const uint4*)src;
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          ROD_ST_OUT((u32x4*)dst, *(const u32x4*)src);
         } else {
           for (int j = 0; j < Cout - col; ++j) dst[j] = src[j];
         }
@@ -719,8 +720,8 @@ __global__ void __launch_bounds__(256) stem_fwd_mfma_kernel(const bf16_t* __rest
     __syncthreads();
     if (inx) {
       bf16_t* dst = Y + (((long)n * H + y) * W + xx) * ldy + half * 16;
-      *(bf16x8*)dst = *(const bf16x8*)(Ys + px * SW_LD + half * 16);
-      *(bf16x8*)(dst + 8) = *(const bf16x8*)(Ys + px * SW_LD + half * 16 + 8);
+      ROD_ST_OUT((bf16x8*)dst, *(const bf16x8*)(Ys + px * SW_LD + half * 16));
+      ROD_ST_OUT((bf16x8*)(dst + 8), *(const bf16x8*)(Ys + px * SW_LD + half * 16 + 8));
     }
     if constexpr (STATS) {
       const int c = tid >> 3, sub = tid & 7;

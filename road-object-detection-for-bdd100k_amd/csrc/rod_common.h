@@ -36,12 +36,21 @@ template <> __device__ __forceinline__ float from_f32<float>(float v) { return v
 template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) { return (bf16_t)v; }
 
 // 16-byte vector of T: 4 x f32 or 8 x bf16.
+// Global stores of kernel outputs that are streamed (written once, read by a later launch):
+// ROD_NT_OUT builds mark them non-temporal.
+#ifdef ROD_NT_OUT
+#define ROD_ST_OUT(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define ROD_ST_OUT(p, v) (*(p) = (v))
+#endif
+
 template <typename T> struct Vec16;
 template <> struct Vec16<float> {
   static constexpr int N = 4;
   f32x4 v;
   __device__ __forceinline__ void load(const float* p) { v = *(const f32x4*)p; }
   __device__ __forceinline__ void store(float* p) const { *(f32x4*)p = v; }
+  __device__ __forceinline__ void store_out(float* p) const { ROD_ST_OUT((f32x4*)p, v); }
   __device__ __forceinline__ float get(int i) const { return v[i]; }
   __device__ __forceinline__ void set(int i, float x) { v[i] = x; }
 };
@@ -50,6 +59,7 @@ template <> struct Vec16<bf16_t> {
   bf16x8 v;
   __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x8*)p; }
   __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x8*)p = v; }
+  __device__ __forceinline__ void store_out(bf16_t* p) const { ROD_ST_OUT((bf16x8*)p, v); }
   __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
   __device__ __forceinline__ void set(int i, float x) { v[i] = (bf16_t)x; }
 };
