@@ -782,9 +782,19 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
   const int K = KS * KS * Cin;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves of 32x32
-  const int co0 = (blockIdx.x / ktiles) * WG_T;
-  const int k0 = (blockIdx.x % ktiles) * WG_T;
-  const long mb = (long)blockIdx.y * chunk;
+  // XCD-aware order: the gridDim.x tiles of one row split run on one XCD (the hardware
+  // deals blocks to the 8 XCDs round-robin by linear id), so the dy / x rows the tiles share
+  // are fetched into that XCD's L2 once (wgrad_plan makes the split count a multiple of 8)
+  int tile = blockIdx.x, split = blockIdx.y;
+  if (gridDim.x > 1 && (gridDim.y & 7) == 0) {
+    const long pl = blockIdx.x + (long)blockIdx.y * gridDim.x;
+    const long q = pl >> 3;
+    tile = (int)(q % gridDim.x);
+    split = (int)((q / gridDim.x) * 8 + (pl & 7));
+  }
+  const int co0 = (tile / ktiles) * WG_T;
+  const int k0 = (tile % ktiles) * WG_T;
+  const long mb = (long)split * chunk;
   const long me = mb + chunk < M ? mb + chunk : M;
 
   // each thread stages one 8-wide chunk of a Ds row and one of an Xs row per step
@@ -872,7 +882,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
     }
   }
   // write the partial tile: rows co, cols k
-  float* out = part + (long)blockIdx.y * Cout * K;
+  float* out = part + (long)split * Cout * K;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1105,6 +1115,9 @@ static WgradPlan wgrad_plan(long M, int Cin, int Cout, int ks) {
   chunk = cdivl(chunk, BK) * BK;
   p.chunk = chunk;
   p.splits = (int)cdivl(M, chunk);
+  // several tiles share each row split: a multiple of 8 splits lets the kernel keep them on
+  // one XCD (splits past M are empty and write zero partials)
+  if (tiles > 1 && p.splits >= 8) p.splits = (p.splits + 7) / 8 * 8;
   return p;
 }
 

@@ -63,7 +63,7 @@ def test_depthwise(dev, dtype, C, stride, H, W):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('ks,Cin,Cout,NHW', [(1, 16, 96, None), (1, 96, 24, None), (1, 64, 128, None), (1, 40, 66, None),
-                                             (3, 3, 32, None), (3, 128, 128, None), (3, 24, 24, None), (3, 99, 99, None),
+                                             (3, 3, 32, None), (3, 3, 32, (1, 5, 128)), (3, 128, 128, None), (3, 24, 24, None), (3, 99, 99, None),
                                              (1, 320, 1920, None), (1, 24, 144, (2, 45, 80)), (1, 32, 192, (2, 23, 40)),
                                              (1, 96, 160, (2, 23, 40)), (1, 64, 256, (1, 30, 41)),
                                              (3, 36, 36, (2, 3, 5)), (1, 1920, 320, (2, 3, 5)),
@@ -158,7 +158,7 @@ def test_batchnorm(dev, dtype, act, C, gamma, res):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('ks,Cin,Cout,NHW', [(1, 16, 96, (2, 45, 80)), (3, 128, 128, (2, 3, 5)), (3, 36, 36, (2, 10, 18)),
-                                             (1, 64, 256, (1, 30, 41)), (3, 3, 32, (1, 20, 30)),
+                                             (1, 64, 256, (1, 30, 41)), (3, 3, 32, (1, 20, 30)), (3, 3, 32, (2, 9, 256)),
                                              (1, 320, 1920, (2, 3, 5)), (1, 24, 144, (2, 23, 40))])
 def test_conv_epilogue_bn_stats(dev, dtype, ks, Cin, Cout, NHW):
     """BatchNorm statistics reduced in the conv epilogue (rod_conv_fwd stat_parts ->
