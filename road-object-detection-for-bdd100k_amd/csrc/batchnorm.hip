@@ -167,7 +167,7 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 
 // Merge of part-major partial statistics, one level: block (s, g) merges parts
 // [s*slice, (s+1)*slice) of channels [g*CB, (g+1)*CB) — PL = 256/CB part lanes per channel,
-// <= 32 serial f64 Chan merges per thread on coalesced rows, then a fixed-order LDS tree
+// <= 16 serial part loads per thread (1024-thread blocks) on coalesced rows, then a fixed-order LDS tree
 // over the lanes — into part s of `out`.  When a single part remains (gridDim.x == 1) the
 // same block finishes: mean, rstd and the moving-average update.
 __device__ __forceinline__ void chan_merge_d(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
@@ -185,14 +185,16 @@ __device__ __forceinline__ void chan_merge_d(double& n, double& mean, double& m2
   n = nt;
 }
 
+constexpr int MERGE_T = 1024;  // threads per merge block
+
 struct MergePlan {
   int CB, PL, slice;
 };
 static MergePlan merge_plan(int C) {
   MergePlan p;
-  p.CB = C < 64 ? C : 64;   // 64 channels x 4+ part lanes per block
-  p.PL = 256 / p.CB;
-  p.slice = 64 * p.PL;      // <= 64 parts per lane per level
+  p.CB = C < 64 ? C : 64;   // 64 channels x 16+ part lanes per block
+  p.PL = MERGE_T / p.CB;
+  p.slice = 16 * p.PL;      // <= 16 parts per lane per level: short dependent load chains
   return p;
 }
 
@@ -200,15 +202,15 @@ static MergePlan merge_plan(int C) {
 // channel (the mean of the slice's first non-empty part), every part contributes
 // n, S1 = n*(mean-k), S2 = M2 + n*(mean-k)^2 in f64; lanes and then the block's part lanes
 // are added in a fixed order, and the slice's (n, mean, M2) = (n, k + S1/n, S2 - S1^2/n).
-__global__ void __launch_bounds__(256) bn_parts_merge_kernel(const float* __restrict__ parts, int nparts, int C, int CB,
+__global__ void __launch_bounds__(MERGE_T) bn_parts_merge_kernel(const float* __restrict__ parts, int nparts, int C, int CB,
                                                              int slice, float* __restrict__ out, long M, float eps,
                                                              float decay, float* __restrict__ mean,
                                                              float* __restrict__ rstd, float* __restrict__ mmean,
                                                              float* __restrict__ mvar) {
-  __shared__ double sn[256], s1[256], s2[256];
-  __shared__ float piv[256];
+  __shared__ double sn[MERGE_T], s1[MERGE_T], s2[MERGE_T];
+  __shared__ float piv[64];
   const int tid = threadIdx.x;
-  const int PL = 256 / CB;
+  const int PL = MERGE_T / CB;
   const int cl = tid % CB, pl = tid / CB;
   const int c = blockIdx.y * CB + cl;
   const bool ok = pl < PL && c < C;
@@ -285,7 +287,7 @@ static void finalize_launch(const float* parts, int nparts, long M, int C, float
   int k = 0;
   while (true) {
     const int S = cdiv(nparts, p.slice);
-    hipLaunchKernelGGL(bn_parts_merge_kernel, dim3(S, cdiv(C, p.CB)), dim3(256), 0, s, parts, nparts, C, p.CB, p.slice,
+    hipLaunchKernelGGL(bn_parts_merge_kernel, dim3(S, cdiv(C, p.CB)), dim3(MERGE_T), 0, s, parts, nparts, C, p.CB, p.slice,
                        S > 1 ? buf[k] : nullptr, M, eps, decay, mean, rstd, mm, mv);
     if (S == 1) break;
     parts = buf[k];
@@ -443,13 +445,26 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   if (c >= C) return;
   const float* pa = slab + (long)c * nblk;
   const float* pb = slab + ((long)C + c) * nblk;
-  double a = 0.0, b = 0.0;
-  for (int k = lane; k < nblk; k += 64) {
-    a += (double)pa[k];
-    b += (double)pb[k];
+  // four independent chains per lane: the slab loads of a wave are issued 8 at a time
+  // instead of one dependent f64 add per load round trip
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+  int k = lane;
+  for (; k + 192 < nblk; k += 256) {
+    a0 += (double)pa[k];
+    a1 += (double)pa[k + 64];
+    a2 += (double)pa[k + 128];
+    a3 += (double)pa[k + 192];
+    b0 += (double)pb[k];
+    b1 += (double)pb[k + 64];
+    b2 += (double)pb[k + 128];
+    b3 += (double)pb[k + 192];
   }
-  const double sg = wave_sum_f64(a);
-  const double sgx = wave_sum_f64(b);
+  for (; k < nblk; k += 64) {
+    a0 += (double)pa[k];
+    b0 += (double)pb[k];
+  }
+  const double sg = wave_sum_f64((a0 + a1) + (a2 + a3));
+  const double sgx = wave_sum_f64((b0 + b1) + (b2 + b3));
   if (lane != 0) return;
   if (dbeta) dbeta[c] = (float)sg;
   if (dgamma) dgamma[c] = (float)sgx;
