@@ -349,6 +349,13 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     // here, read after the staging loop, whose barriers order the two)
     __shared__ float wst[(VY && STATS) ? WM * 3 * BN : 1];
     if constexpr (STATS) {
+      // round once, in place: the statistics and the staging below use the stored values
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[a][b][r] = to_f32(from_f32<T>(acc[a][b][r] + bv[b]));
       const int lg = lane >> 4;
       // rows of this wave's strip still inside M (all of them except in the last tile)
       const long left_l = M - (m0 + wm * WROWS);
@@ -360,7 +367,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             if (lg * 4 + r < left) {
-              p += to_f32(from_f32<T>(acc[0][b][r] + bv[b]));
+              p += acc[0][b][r];
               pc += 1.f;
             }
           }
@@ -369,14 +376,15 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         pc += __shfl_xor(pc, 16, 64);
         p = __shfl(p, lane & 15, 64);
         pc = __shfl(pc, lane & 15, 64);
-        const float piv = pc > 0.f ? p / pc : 0.f;
+        // full strips: pc = 8 and the division is an exact scaling
+        const float piv = left >= 8 ? p * 0.125f : (pc > 0.f ? p / pc : 0.f);
         float s1 = 0.f, s2 = 0.f, n = 0.f;
         if (left == WROWS) {  // full strip: no row checks
 #pragma unroll
           for (int a = 0; a < MT; ++a)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float d = to_f32(from_f32<T>(acc[a][b][r] + bv[b])) - piv;
+              const float d = acc[a][b][r] - piv;
               s1 += d;
               s2 = fmaf(d, d, s2);
             }
@@ -387,7 +395,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               if (a * 16 + lg * 4 + r < left) {
-                const float d = to_f32(from_f32<T>(acc[a][b][r] + bv[b])) - piv;
+                const float d = acc[a][b][r] - piv;
                 s1 += d;
                 s2 = fmaf(d, d, s2);
                 n += 1.f;
@@ -401,7 +409,8 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         s2 += __shfl_xor(s2, 32, 64);
         n += __shfl_xor(n, 32, 64);
         if (lane < 16) {
-          const float dm = n > 0.f ? s1 / n : 0.f;
+          static_assert((WROWS & (WROWS - 1)) == 0, "wave strip must be a power of two");
+          const float dm = left == WROWS ? s1 * (1.0f / WROWS) : (n > 0.f ? s1 / n : 0.f);
           const int cl = wn * (BN / WN) + b * 16 + lane;
           wst[(wm * 3 + 0) * BN + cl] = n;
           wst[(wm * 3 + 1) * BN + cl] = piv + dm;
@@ -428,7 +437,8 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
           const int cl = wn * (BN / WN) + b * 16 + (lane & 15);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            Cs[(r_tile - h * 64 + (lane >> 4) * 4 + r) * LDC + cl] = from_f32<T>(acc[a][b][r] + bv[b]);
+            Cs[(r_tile - h * 64 + (lane >> 4) * 4 + r) * LDC + cl] =
+                from_f32<T>(STATS ? acc[a][b][r] : acc[a][b][r] + bv[b]);  // STATS: already rounded
         }
       }
       __syncthreads();
