@@ -1042,16 +1042,37 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, float* __res
 }
 
 // column sums of dy[M, C] (row stride ld): slab [nblk][C] then reduce
+// (bias gradients of the head convs, whose C is 24..36: all 256 threads work — 256 / C row
+// lanes per column, four independent chains per lane, lanes added in a fixed order)
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ dy, long M, int C, int ld, long chunk,
                                                      float* __restrict__ slab) {
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  const int CB = C < 256 ? C : 256;
+  const int lanes = 256 / CB;
+  const int cl = tid % CB, ln = tid / CB;
+  const int c = blockIdx.y * 256 + cl;
   const long r0 = (long)blockIdx.x * chunk;
   const long r1 = r0 + chunk < M ? r0 + chunk : M;
-  float s = 0.f;
-  for (long r = r0; r < r1; ++r) s += to_f32(dy[r * ld + c]);
-  slab[(long)blockIdx.x * C + c] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (ln < lanes && c < C) {
+    long r = r0 + ln;
+    for (; r + 3L * lanes < r1; r += 4L * lanes) {
+      s0 += to_f32(dy[r * ld + c]);
+      s1 += to_f32(dy[(r + lanes) * ld + c]);
+      s2 += to_f32(dy[(r + 2L * lanes) * ld + c]);
+      s3 += to_f32(dy[(r + 3L * lanes) * ld + c]);
+    }
+    for (; r < r1; r += lanes) s0 += to_f32(dy[r * ld + c]);
+  }
+  red[tid] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ln == 0 && c < C) {
+    float t = 0.f;
+    for (int l = 0; l < lanes; ++l) t += red[l * CB + cl];
+    slab[(long)blockIdx.x * C + c] = t;
+  }
 }
 
 template <typename T>

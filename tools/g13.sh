@@ -1,5 +1,5 @@
 #!/bin/bash
-# gpu tests + bench (1024-thread statistics merge)
+# gpu tests + bench + short kernel trace
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp
 O=gpurun_out
