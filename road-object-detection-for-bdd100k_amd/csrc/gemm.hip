@@ -226,8 +226,20 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const long m0 = (long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // XCD-aware order when Cout spans several N tiles (Cout > 256): the host pads gridDim.x to a
+  // multiple of 8 and the N tiles of one M tile run on one XCD, so its A rows are fetched into
+  // that XCD's L2 once; padding blocks exit before any barrier
+  long mt = blockIdx.x;
+  int nt = blockIdx.y;
+  if (!SPLIT && gridDim.y > 1 && (gridDim.x & 7) == 0) {
+    const long pl = blockIdx.x + (long)blockIdx.y * gridDim.x;
+    const long q = pl >> 3;
+    nt = (int)(q % gridDim.y);
+    mt = (q / gridDim.y) * 8 + (pl & 7);
+    if (mt * BM >= M) return;
+  }
+  const long m0 = mt * BM;
+  const int n0 = nt * BN;
   const int kc = (tid & 3) * 8;
 
   RowSrc<T, KS> rows[ACH];
@@ -495,8 +507,8 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
             a += gsum[0][q * GCPR + tid];
             b += gsum[1][q * GCPR + tid];
           }
-          gr.parts[(long)blockIdx.x * 2 * Cout + gcol + v] = a;
-          gr.parts[(long)blockIdx.x * 2 * Cout + Cout + gcol + v] = b;
+          gr.parts[mt * 2 * Cout + gcol + v] = a;
+          gr.parts[mt * 2 * Cout + Cout + gcol + v] = b;
         }
       }
     }
@@ -514,7 +526,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
           m2 = m2 + m2b + d * d * (n * nb / nn);
           n = nn;
         }
-        store_stat_part(part, Cout, blockIdx.x, n0 + tid, n, mu, m2);
+        store_stat_part(part, Cout, mt, n0 + tid, n, mu, m2);
       }
     }
   } else {
@@ -1164,6 +1176,7 @@ static void conv_fwd_launch(const void* x, const void* wt, const float* bias, vo
                             int Cout, int ldx, int ldy, float* stats, const BnPro& pro, const BnGred* gr,
                             hipStream_t s) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
+  if (grid.y > 1) grid.x = (grid.x + 7) / 8 * 8;  // XCD-aware N-tile order (see the kernel)
   const size_t lds = PRO ? 8 * (size_t)Cin : 0;
   if constexpr (VY) {
     if (gr) {
