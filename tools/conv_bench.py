@@ -19,7 +19,8 @@ from rod import _abi, ops  # noqa: E402
 SHAPES = [(8, 720, 1280, 16, 96, 1, 0), (8, 360, 640, 96, 24, 1, 1), (8, 360, 640, 24, 144, 1, 0),
           (8, 360, 640, 144, 24, 1, 1), (8, 180, 320, 32, 192, 1, 0), (8, 90, 160, 64, 384, 1, 0),
           (8, 90, 160, 384, 64, 1, 1), (8, 90, 160, 128, 128, 3, 2), (8, 90, 160, 64, 128, 1, 0),
-          (8, 720, 1280, 3, 32, 3, 0)]
+          (8, 720, 1280, 3, 32, 3, 0), (8, 45, 80, 96, 576, 1, 0), (8, 45, 80, 576, 96, 1, 1),
+          (8, 23, 40, 160, 960, 1, 0)]
 
 
 def main():
