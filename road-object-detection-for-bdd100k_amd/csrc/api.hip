@@ -98,6 +98,12 @@ __global__ void cast_kernel(const S* __restrict__ src, D* __restrict__ dst, long
   for (; i < n; i += stride) dst[i] = from_f32<D>(to_f32(src[i]));
 }
 
+// tf.clip_by_value = minimum(maximum(g, -clip), clip) with Eigen's scalar max/min
+// (a < b ? b : a / b < a ? b : a): a NaN gradient stays NaN and poisons the variable, as in TF.
+__device__ __forceinline__ float clip_tf(float g, float clip) {
+  return g != g ? g : fminf(fmaxf(g, -clip), clip);
+}
+
 __global__ void sgd_clip_kernel(float* __restrict__ p, const float* __restrict__ g, long n, float lr,
                                 float clip) {
   long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -108,12 +114,12 @@ __global__ void sgd_clip_kernel(float* __restrict__ p, const float* __restrict__
       f32x4 gv = *(const f32x4*)(g + i);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float c = fminf(fmaxf(gv[j], -clip), clip);  // tf.clip_by_value
+        float c = clip_tf(gv[j], clip);               // tf.clip_by_value
         pv[j] = pv[j] - lr * c;                       // ApplyGradientDescent: var -= alpha * delta
       }
       *(f32x4*)(p + i) = pv;
     } else {
-      for (long k = i; k < n; ++k) p[k] = p[k] - lr * fminf(fmaxf(g[k], -clip), clip);
+      for (long k = i; k < n; ++k) p[k] = p[k] - lr * clip_tf(g[k], clip);
     }
   }
 }

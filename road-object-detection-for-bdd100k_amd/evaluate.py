@@ -21,6 +21,10 @@ import config  # noqa: E402
 from utils.common_tools import logger  # noqa: E402
 
 
+def str2bool(v):
+    return v if isinstance(v, bool) else str(v).lower() in ('1', 'true', 't', 'yes', 'y')
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument('--backbone_name', default='mobilenet_v2')
@@ -41,14 +45,23 @@ def parse(argv=None):
     ap.add_argument('--img_width', type=int, default=config.img_size[1])
     ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
     ap.add_argument('--dataset_dir', default='./dataset/bdd100k_TfRecord/')
+    ap.add_argument('--synthetic', type=str2bool, default=False,
+                    help='run on synthetic BDD-shaped batches (no dataset needed); results are not real '
+                         'metrics.  Without it a missing dataset or checkpoint is an error')
     return ap.parse_args(argv)
 
 
 def latest_checkpoint(path, backbone):
+    """A torch checkpoint (train.py writes <train_dir>/<backbone>.model) or a TF-1.x tensor
+    bundle (<prefix>.index + .data-*), as a directory or a file prefix."""
+    from rod.checkpoint import exists
     if os.path.isdir(path):
         cand = os.path.join(path, backbone + '.model')
-        return cand if os.path.exists(cand) else None
-    return path if os.path.exists(path) else None
+        if exists(cand):
+            return cand
+        from rod.checkpoint import tf_latest_checkpoint
+        return tf_latest_checkpoint(path)
+    return path if exists(path) else None
 
 
 def main(argv=None):
@@ -56,8 +69,7 @@ def main(argv=None):
     logger.info('Asserting parameters')
     assert F.backbone_name in config.supported_backbone_name
     from nets.catch_net import CatchNet, factory
-    from rod import ops
-    from rod.dataio import make_source
+    from rod.dataio import make_source, network_input
     from utils import net_tools
     from utils.common_tools import cornerBboxes_2_centerBboxes  # noqa: F401
     import utils.tf_extended as tfe
@@ -75,13 +87,17 @@ def main(argv=None):
     net = CatchNet(F.backbone_name, config_dict, dev)
     ckpt = latest_checkpoint(F.checkpoint_path, F.backbone_name)
     if ckpt is not None:
-        sd = torch.load(ckpt, map_location='cpu', weights_only=True)
-        net.store.load_state_dict(sd['variables'])
+        from rod.checkpoint import load_variables
+        load_variables(net.store, ckpt)
         logger.info('Evaluating %s' % ckpt)
-    else:
-        logger.warning('no checkpoint at %r: evaluating randomly initialised weights', F.checkpoint_path)
+    elif F.synthetic:
+        logger.warning('--synthetic: no checkpoint at %r, evaluating randomly initialised weights',
+                       F.checkpoint_path)
+    else:   # tf.train.latest_checkpoint(...) -> None makes the reference's restore fail
+        raise FileNotFoundError('no checkpoint under %r (evaluate.py:221-224)' % F.checkpoint_path)
     logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
-    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, split='train')
+    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, split='train', synthetic=F.synthetic,
+                         dtype=dtype, num_readers=F.num_readers, max_images=F.num_images)
 
     num_batches = math.ceil(F.num_images / float(F.batch_size))
     state = None
@@ -90,7 +106,7 @@ def main(argv=None):
     with torch.no_grad():
         for _ in range(num_batches):
             img, gboxes, glabels, gn = next(source)
-            x = ops.normalize_image(img, dtype)
+            x = network_input(img, dtype)
             refine_out, det_out, clf_out = factory(x, F.backbone_name, False, config_dict, dtype,
                                                    net=net).get_output()
             probs = net_tools.class_probabilities(clf_out)
@@ -112,6 +128,8 @@ def main(argv=None):
         logger.info('AP_VOC07/%d %.6f  AP_VOC12/%d %.6f' % (c, aps07[c], c, aps12[c]))
     mAP07 = sum(aps07.values()) / len(aps07)
     mAP12 = sum(aps12.values()) / len(aps12)
+    if F.synthetic:
+        logger.warning('--synthetic: the AP values below are over synthetic ground truth, not a BDD100K result')
     print('AP_VOC07/mAP[%s]' % mAP07)
     print('AP_VOC12/mAP[%s]' % mAP12)
     elapsed = time.time() - start
@@ -121,7 +139,8 @@ def main(argv=None):
     with open(os.path.join(F.eval_dir, 'eval.json'), 'w') as f:
         import json
         json.dump({'AP_VOC07': aps07, 'AP_VOC12': aps12, 'mAP_VOC07': mAP07, 'mAP_VOC12': mAP12,
-                   'num_batches': num_batches, 'seconds': elapsed}, f)
+                   'num_batches': num_batches, 'seconds': elapsed, 'synthetic': bool(F.synthetic),
+                   'checkpoint': ckpt}, f)
     return mAP07, mAP12
 
 

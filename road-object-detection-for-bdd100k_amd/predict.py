@@ -44,6 +44,9 @@ def parse(argv=None):
     ap.add_argument('--img_width', type=int, default=config.img_size[1])
     ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
     ap.add_argument('--dataset_dir', default='./dataset/bdd100k_TfRecord/')
+    ap.add_argument('--synthetic', type=str2bool, default=False,
+                    help='run on synthetic BDD-shaped batches (no dataset needed); results are not real '
+                         'metrics.  Without it a missing dataset or checkpoint is an error')
     ap.add_argument('--output', default=None, help='write detections of the last batch as JSON')
     return ap.parse_args(argv)
 
@@ -61,8 +64,8 @@ class Predictor(object):
                             'merge_method': config.merge_method.ADD, 'train_range': config.train_range.ALL}
         self.net = CatchNet('mobilenet_v2', self.config_dict, device, seed)
         if checkpoint is not None:
-            sd = torch.load(checkpoint, map_location='cpu', weights_only=True)
-            self.net.store.load_state_dict(sd['variables'])
+            from rod.checkpoint import load_variables
+            load_variables(self.net.store, checkpoint)
         self.anchors = net_tools.anchors_all_layer(config.img_size, config.feat_sizes(config.img_size),
                                                    net_tools.init_anchor(6))
         self.dtype = dtype
@@ -72,9 +75,9 @@ class Predictor(object):
     @torch.no_grad()
     def __call__(self, img_u8):
         from nets.catch_net import factory
-        from rod import ops
         from utils import net_tools
-        x = ops.normalize_image(img_u8, self.dtype)
+        from rod.dataio import network_input
+        x = network_input(img_u8, self.dtype)
         refine_out, det_out, clf_out = factory(x, 'mobilenet_v2', False, self.config_dict, self.dtype,
                                                net=self.net).get_output()
         probs = net_tools.class_probabilities(clf_out)                                     # predict.py:127-128
@@ -89,13 +92,18 @@ def main(argv=None):
     from rod.dataio import make_source
     dev = torch.device('cuda', 0)
     dtype = torch.bfloat16 if F.dtype == 'bf16' else torch.float32
-    ckpt = F.checkpoint_all if F.checkpoint_all and os.path.exists(F.checkpoint_all) else None
+    from rod.checkpoint import exists
+    ckpt = F.checkpoint_all if F.checkpoint_all and exists(F.checkpoint_all) else None
     if ckpt is None:
-        logger.warning('checkpoint %r not found: predicting with randomly initialised weights', F.checkpoint_all)
+        if not F.synthetic:   # the reference's saver.restore fails (predict.py:143-146)
+            raise FileNotFoundError('checkpoint %r not found (pass --synthetic to predict with random weights)'
+                                    % F.checkpoint_all)
+        logger.warning('--synthetic: checkpoint %r not found, predicting with random weights', F.checkpoint_all)
     pred = Predictor((F.img_height, F.img_width), dev, dtype, ckpt, F.select_threshold, F.nms_threshold, F.top_k,
                      F.keep_top_k)
     logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
-    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev)
+    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, synthetic=F.synthetic, dtype=dtype,
+                         num_readers=F.num_readers)
     t0 = time.time()
     for _ in range(F.num_batches):
         img, _, _, _ = next(source)

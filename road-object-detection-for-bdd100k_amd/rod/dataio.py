@@ -1,15 +1,21 @@
 """Batch sources for the CLIs.
 
 The reference reads BDD100K TFRecords through slim's DatasetDataProvider
-(dataset/bdd100k.py, utils/data_pileline_tools.py).  TFRecord + JPEG ingest is the
-first "next" row of SURVEY.md §8(f) and is not built yet; until then every CLI runs on
-synthetic BDD-shaped batches (rod.data) and says so in its log.  The source yields
-device tensors already at the network resolution:
-    img uint8 [B, H, W, 3], corner boxes fp32 [B, G, 4], labels int32 [B, G], n int32 [B]
+(dataset/bdd100k.py, dataset/pascalvoc_common.py:40-107, utils/data_pileline_tools.py:18-69).
+`TFRecordSource` is that reader: the record scan and checksums are native (librodio), JPEG
+decode runs on a host thread pool (`num_readers` threads, as the reference's reader threads),
+and the per-image preprocessing runs on the GPU (rod_augment_images / rod_augment_boxes):
+process_raw_data_train for training, the bilinear resize of prepare_data_test otherwise.
+
+Every source yields device tensors at the network resolution:
+    img [B, H, W, 3] (uint8, or already (2/255)x-1 normalised in the compute dtype — see
+    `network_input`), corner boxes fp32 [B, G, 4], labels int32 [B, G], n int32 [B]
+Synthetic BDD-shaped batches (rod.data) only with an explicit `synthetic=True`.
 """
 import glob
 import logging
 import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -68,14 +74,128 @@ class AugmentedSource(object):
         return self.aug(img, corner, labels, n, dtype=self.dtype)
 
 
-def make_source(dataset_dir, batch_size, img_size, device, split='train', seed=SEED, augment_dtype=None):
+def network_input(img, dtype):
+    """(2/255)*img - 1 in `dtype` (train.py:126, evaluate.py:117) of a source batch."""
+    from rod import ops
+    if img.is_floating_point():   # the GPU preprocessing already normalised it
+        return ops.cast(img, dtype)
+    return ops.normalize_image(img, dtype)
+
+
+class TFRecordSource(object):
+    """DatasetDataProvider + prepare_data_train / prepare_data_test over TFRecord files of the
+    schema of dataset/pascalvoc_common.py:75-88.
+
+    train=True: records in a seeded random order, reshuffled every epoch (shuffle=True at
+    train.py:106), each image through process_raw_data_train (random crop / resize / flip /
+    colour, data_pileline_tools.py:71-108) on the GPU, normalised into `dtype`.
+    train=False: file order (shuffle=False, evaluate.py:103), resize to img_size only
+    (data_pileline_tools.py:39-40), normalised into `dtype`; boxes unchanged.  The number of
+    ground-truth boxes varies per image: batches are zero-padded to the largest count
+    (dynamic_pad=True, evaluate.py:109-114) with the counts in n."""
+
+    def __init__(self, files, batch_size, img_size, device, dtype, train=True, seed=SEED, num_readers=4,
+                 verify=True, max_images=None):
+        from rod import tfrecord
+        if not files:
+            raise FileNotFoundError('no TFRecord files')
+        self.files = [tfrecord.TFRecordFile(f, verify=verify) for f in files]
+        self.index = [(fi, ri) for fi, f in enumerate(self.files) for ri in range(len(f))]
+        if max_images is not None:
+            self.index = self.index[:max_images]
+        if not self.index:
+            raise ValueError('the TFRecord files hold no records')
+        self.batch_size, self.img_size, self.device, self.dtype = batch_size, tuple(img_size), device, dtype
+        self.train = train
+        self.rng = np.random.default_rng(seed)
+        self.order = self.rng.permutation(len(self.index)) if train else np.arange(len(self.index))
+        self.pos = 0
+        self.epoch = 0
+        self.pool = ThreadPoolExecutor(max_workers=max(1, int(num_readers)))
+        self.aug = None
+        if train:
+            from utils.data_pileline_tools import TrainAugmenter
+            self.aug = TrainAugmenter(self.img_size, seed=seed)
+
+    def __len__(self):
+        return len(self.index)
+
+    def __iter__(self):
+        return self
+
+    def _load(self, k):
+        from rod import tfrecord
+        fi, ri = self.index[k]
+        enc, fmt, shape, boxes, labels, _, _ = tfrecord.decode_detection_example(self.files[fi][ri])
+        img = tfrecord.decode_image(enc, fmt)
+        return img, boxes, labels
+
+    def _take(self):
+        ks = []
+        for _ in range(self.batch_size):
+            if self.pos == len(self.order):
+                self.pos = 0
+                self.epoch += 1
+                if self.train:
+                    self.order = self.rng.permutation(len(self.index))
+            ks.append(int(self.order[self.pos]))
+            self.pos += 1
+        return ks
+
+    def __next__(self):
+        from rod import ops
+        items = list(self.pool.map(self._load, self._take()))
+        B = len(items)
+        G = max(1, max(len(b) for _, b, _ in items))
+        boxes = np.zeros((B, G, 4), np.float32)
+        labels = np.zeros((B, G), np.int32)
+        n = np.zeros(B, np.int32)
+        hw = np.zeros((B, 2), np.int32)
+        offs = np.zeros(B, np.int64)
+        tot = 0
+        for b, (img, bx, lb) in enumerate(items):
+            g = len(bx)
+            boxes[b, :g], labels[b, :g], n[b] = bx, lb, g
+            hw[b] = img.shape[:2]
+            offs[b] = tot
+            tot += img.size
+        flat = torch.empty(tot, dtype=torch.uint8, pin_memory=self.device.type == 'cuda')
+        fl = flat.numpy()
+        for b, (img, _, _) in enumerate(items):
+            fl[offs[b]:offs[b] + img.size] = img.reshape(-1)
+        src = flat.to(self.device, non_blocking=True)
+        if self.train:
+            crop, ref, mode, colour = self.aug.sample(hw, boxes, n)
+            x = ops.augment_images(src, crop, mode, colour, self.img_size, dtype=self.dtype, normalize=True,
+                                   src_hw=hw, src_off=offs)
+            bo, lo, no = ops.augment_boxes(boxes, labels, n, ref, mode, threshold=0.3)
+            return x, bo, lo, no
+        crop = np.concatenate([np.zeros((B, 2), np.int32), hw], 1)
+        mode = np.tile(np.array([0, -1], np.int32), (B, 1))
+        x = ops.augment_images(src, crop, mode, np.zeros((B, 3), np.float32), self.img_size, dtype=self.dtype,
+                               normalize=True, src_hw=hw, src_off=offs)
+        dev = lambda a: torch.from_numpy(a).to(self.device)
+        return x, dev(boxes), dev(labels), dev(n)
+
+
+def make_source(dataset_dir, batch_size, img_size, device, split='train', seed=SEED, augment_dtype=None,
+                synthetic=False, dtype=torch.float32, num_readers=4, max_images=None):
     """augment_dtype: training batches go through the GPU augmentation pipeline and come out
-    normalised in this dtype; None = network-resolution uint8 batches (eval / predict / bench)."""
-    files = tfrecord_files(dataset_dir, split) if dataset_dir else []
-    if files:
-        raise NotImplementedError('TFRecord/JPEG ingest (SURVEY.md §8f rank 1) is not built yet; found %d files in %s'
-                                  % (len(files), dataset_dir))
-    log.warning('no BDD100K TFRecords under %r: using synthetic BDD-shaped batches (rod.data)', dataset_dir)
+    normalised in this dtype; None = network-resolution uint8 batches (eval / predict / bench).
+    synthetic: run on synthetic BDD-shaped batches (rod.data) — only when asked for explicitly;
+    a missing dataset is an error, as in the reference (its reader fails on an empty pattern)."""
+    if synthetic:
+        log.warning('--synthetic: using synthetic BDD-shaped batches (rod.data), not %r', dataset_dir)
+    else:
+        files = tfrecord_files(dataset_dir, split) if dataset_dir else []
+        if files:
+            log.info('reading %d TFRecord file(s) from %s', len(files), dataset_dir)
+            train = augment_dtype is not None
+            return TFRecordSource(files, batch_size, img_size, torch.device(device),
+                                  augment_dtype if train else dtype, train=train, seed=seed, num_readers=num_readers,
+                                  max_images=max_images)
+        raise FileNotFoundError('no bdd100k_%s_*.tfrecord under %r (pass --synthetic to run on synthetic '
+                                'BDD-shaped batches)' % (split, dataset_dir))
     if augment_dtype is not None:
         return AugmentedSource(batch_size, img_size, device, augment_dtype, seed)
     return SyntheticSource(batch_size, img_size, device, seed)

@@ -56,21 +56,27 @@ def parse(argv=None):
     ap.add_argument('--img_width', type=int, default=config.img_size[1])
     ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
     ap.add_argument('--dataset_dir', default='./dataset/bdd100k_TfRecord/')
+    ap.add_argument('--synthetic', type=str2bool, default=False,
+                    help='run on synthetic BDD-shaped batches (no dataset needed); results are not real '
+                         'metrics.  Without it a missing dataset or checkpoint is an error')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--save_format', default='torch', choices=['torch', 'tf'],
+                    help='checkpoint format: torch file, or a TF-1.x tensor bundle the reference can restore')
     ap.add_argument('--augment', type=str2bool, default=True,
                     help='process_raw_data_train on the GPU (random crop / flip / colour); False = raw batches')
     return ap.parse_args(argv)
 
 
 def load_ckpt(store, path, names_regex=None):
-    sd = torch.load(path, map_location='cpu', weights_only=True)
-    store.load_state_dict(sd['variables'], strict=names_regex is None, names_regex=names_regex)
-    return int(sd.get('global_step', 0))
+    """saver.restore (train.py:188, 282) / restore_saver of backbone.+|refine.+ (155-158, 191-193):
+    a torch checkpoint written by this CLI or a TF-1.x tensor bundle of the reference."""
+    from rod.checkpoint import load_variables
+    return load_variables(store, path, names_regex=names_regex)
 
 
-def save_ckpt(store, path, step):
-    os.makedirs(os.path.dirname(path) or '.', exist_ok=True)
-    torch.save({'variables': store.state_dict(), 'global_step': step}, path)
+def save_ckpt(store, path, step, fmt='torch'):
+    from rod.checkpoint import save_variables
+    save_variables(store, path, step, fmt)
 
 
 def main(argv=None):
@@ -120,7 +126,8 @@ def main(argv=None):
     trainer.opt.global_step = step0
     logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
     source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, seed=1000 * rank + F.seed,
-                         augment_dtype=dtype if F.augment else None)
+                         augment_dtype=dtype if F.augment else None, synthetic=F.synthetic, dtype=dtype,
+                         num_readers=F.num_readers)
 
     os.makedirs(F.summary_dir, exist_ok=True)
     summ = open(os.path.join(F.summary_dir, 'train_rank%d.jsonl' % rank), 'a') if rank == 0 else None
@@ -129,7 +136,12 @@ def main(argv=None):
     while True:
         start = time.time()
         losses = trainer.step(*next(source))
-        vals = [float(l.item()) for l in losses]  # the reference's sess.run returns host values too
+        if world > 1:   # each rank holds its shard's sum / global batch: the global loss is their sum
+            lv = torch.stack([l.detach().float().reshape(()) for l in losses])
+            torch.distributed.all_reduce(lv)
+            vals = lv.tolist()
+        else:
+            vals = [float(l.item()) for l in losses]  # the reference's sess.run returns host values too
         t = round(time.time() - start, 3)
         current_step = trainer.opt.global_step - 1
         if F.log_every_n_steps is not None:
@@ -156,7 +168,7 @@ def main(argv=None):
         if F.save_every_n_steps is not None and current_step % F.save_every_n_steps == F.save_every_n_steps - 1 \
                 and rank == 0:
             logger.info('Saving model...')
-            save_ckpt(store, os.path.join(F.train_dir, F.backbone_name + '.model'), current_step + 1)
+            save_ckpt(store, os.path.join(F.train_dir, F.backbone_name + '.model'), current_step + 1, F.save_format)
             logger.info('Save model sucess...')
         if F.max_number_of_steps is not None and current_step >= F.max_number_of_steps:
             logger.info('Exit training...')

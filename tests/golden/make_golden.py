@@ -2,6 +2,10 @@
 where /root/reference exists).  Never imported by tests; its outputs are committed:
 
   ref_anchors_<H>x<W>.npz   init_anchor + anchors_all_layer outputs (net_tools.py:21-142)
+  ref_anchor_geom_<H>x<W>.npz  the float32 anchor corners and recomputed centres / sizes the
+                            reference itself builds inside refine_groundtruth (JACCARD_BIGGER,
+                            net_tools.py:385-395) and decode_locations_one_layer
+                            (net_tools.py:202-223), captured from the stub's call records
   ref_spec.json             MobileNet-v2 spec params (mobilenet_v2.py:57-86) and
                             _make_divisible samples (conv_blocks.py:50-57)
 
@@ -45,6 +49,38 @@ def tf_same_chain(h, w, strides):
         h, w = -(-h // s), -(-w // s)
         out.append((h, w))
     return out
+
+
+def capture_geometry(nt, anc, H, W):
+    """Run the reference's refine_groundtruth (JACCARD_BIGGER) and decode_locations_one_layer
+    under the stub: their numpy anchor arithmetic runs for real and its results arrive as
+    arguments of the mocked tf calls (tf.stack of the corners; the offset-tensor mock's
+    __mul__ / __add__ with anchor_h / anchor_w / anchor_cy / anchor_cx)."""
+    from unittest import mock as _m
+    import config as ref_config
+    tf = nt.tf
+    tf.reset_mock()
+    tf.while_loop.side_effect = lambda cond, body, loop_vars, **kw: tuple(_m.MagicMock() for _ in loop_vars)
+    center = _m.MagicMock()          # a [G, 4] tensor in the graph; only the anchors are numpy
+    nt.refine_groundtruth(anc, center, np.array([1]), ref_config.refine_method.JACCARD_BIGGER)
+    corners = [c.args[0] for c in tf.stack.call_args_list
+               if isinstance(c.args[0], (list, tuple)) and len(c.args[0]) == 4 and
+               all(isinstance(a, np.ndarray) for a in c.args[0])]
+    assert len(corners) == len(anc), len(corners)
+    arrs = {}
+    for l, layer in enumerate(anc):
+        arrs['corner_%d' % l] = np.stack(corners[l], -1)
+        tf.reset_mock()
+        off = _m.MagicMock()
+        off.get_shape.return_value.as_list.return_value = [1, -1, 4]
+        nt.decode_locations_one_layer(layer, off)
+        r = tf.reshape.return_value.__getitem__.return_value
+        muls = [c.args[0] for c in r.__mul__.call_args_list]
+        adds = [c.args[0] for c in r.__mul__.return_value.__add__.call_args_list]
+        assert len(muls) == 2 and len(adds) == 2
+        arrs['center_%d' % l] = np.stack([adds[0], adds[1], muls[0], muls[1]], -1)   # (cy, cx, h, w)
+    tf.while_loop.side_effect = None
+    np.savez_compressed(os.path.join(OUT, 'ref_anchor_geom_%dx%d.npz' % (H, W)), **arrs)
 
 
 def main():
@@ -97,6 +133,7 @@ def main():
             arrs['feat_%d' % i] = np.array(feats['layer_%d' % (i + 1)])
         arrs['n_anchor'] = np.array([v.shape[0] for v in init.values()])
         np.savez_compressed(os.path.join(OUT, 'ref_anchors_%dx%d.npz' % (H, W)), **arrs)
+        capture_geometry(nt, anc, H, W)
     print('golden fixtures written to', OUT)
 
 

@@ -85,3 +85,54 @@ def test_config_surface(golden_dir):
     assert config.total_obj_n == spec['total_obj_n']
     assert config.train_range.REFINE.value == 0 and config.train_range.ALL.value == 1
     assert config.refine_method.JACCARD_BIGGER.value == 1
+
+
+def _geom(golden_dir, H, W):
+    return np.load(os.path.join(golden_dir, 'ref_anchor_geom_%dx%d.npz' % (H, W)))
+
+
+@pytest.mark.parametrize('H,W', SIZES)
+def test_anchor_geometry_matches_reference(golden_dir, H, W):
+    """The float32 anchor corners and the centres / sizes recomputed from them, as the
+    reference computes them inside refine_groundtruth (net_tools.py:385-395) and
+    decode_locations_one_layer (202-223): oracle and product tables bit-identical."""
+    import config
+    import utils.net_tools as nt
+    g = _geom(golden_dir, H, W)
+    old = config.img_size
+    config.img_size = (H, W)
+    try:
+        anc = nt.anchors_all_layer((H, W), config.feat_sizes((H, W)), nt.init_anchor(6))
+    finally:
+        config.img_size = old
+    tab = nt.AnchorTable(anc, 'cpu')
+    ref_corner = np.concatenate([g['corner_%d' % l].reshape(-1, 4) for l in range(6)])
+    ref_center = np.concatenate([g['center_%d' % l] for l in range(6)])
+    np.testing.assert_array_equal(tab.corner_np, ref_corner)
+    np.testing.assert_array_equal(tab.center_np, ref_center)
+    for l, layer in enumerate(anc):
+        np.testing.assert_array_equal(np.stack(oa.anchor_corners(layer), -1), g['corner_%d' % l])
+        np.testing.assert_array_equal(np.stack(oa.anchor_centers(layer), -1).reshape(-1, 4), g['center_%d' % l])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('H,W', SIZES)
+def test_device_anchor_tables_match_reference(golden_dir, dev, H, W):
+    """The anchor tables the kernels read (uploaded to HBM once per resolution) against the
+    reference's own numbers: anchors_all_layer and the JACCARD_BIGGER / decode geometry."""
+    import config
+    import utils.net_tools as nt
+    g, gg = _load(golden_dir, H, W), _geom(golden_dir, H, W)
+    old = config.img_size
+    config.img_size = (H, W)
+    try:
+        anc = nt.anchors_all_layer((H, W), config.feat_sizes((H, W)), nt.init_anchor(6))
+    finally:
+        config.img_size = old
+    for l, (y, x, h, w) in enumerate(anc):
+        for name, arr in zip('yxhw', (y, x, h, w)):
+            np.testing.assert_array_equal(arr, g['%s_%d' % (name, l)])
+    tab = nt.AnchorTable(anc, dev)
+    np.testing.assert_array_equal(tab.corner.cpu().numpy(),
+                                  np.concatenate([gg['corner_%d' % l].reshape(-1, 4) for l in range(6)]))
+    np.testing.assert_array_equal(tab.center.cpu().numpy(), np.concatenate([gg['center_%d' % l] for l in range(6)]))

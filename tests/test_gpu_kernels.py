@@ -328,6 +328,16 @@ def test_sgd_clip_and_normalize(dev):
     ops.sgd_clip_(pd, gd, 1e-2, 5.0)
     ref = (p.numpy() - np.float32(1e-2) * np.clip(gr.numpy(), -5, 5)).astype(np.float32)
     np.testing.assert_array_equal(pd.cpu().numpy(), ref)
+    # tf.clip_by_value keeps a NaN gradient NaN (Eigen max/min), so the variable turns NaN;
+    # +-inf clip to +-5 (vector body and the scalar tail both)
+    for n in (8, 7):
+        p2 = torch.ones(n)
+        g2 = torch.tensor([float('nan'), float('inf'), -float('inf'), 1.0, 0.5, -7.0, float('nan'), 2.0][:n])
+        pd2 = p2.to(dev)
+        ops.sgd_clip_(pd2, g2.to(dev), 0.5, 5.0)
+        got = pd2.cpu().numpy()
+        assert np.isnan(got[0]) and (n < 7 or np.isnan(got[6]))
+        np.testing.assert_array_equal(got[1:6], np.float32([1 - 2.5, 1 + 2.5, 0.5, 0.75, 1 + 2.5]))
     img = torch.randint(0, 256, (2, 5, 7, 3), dtype=torch.uint8, generator=g)
     out = ops.normalize_image(img.to(dev))
     k = np.float32(2.0 / 255.0)
