@@ -258,3 +258,50 @@ def odm_losses_torch(anc_center, lvl_off, refine_out, det_out, logits, refine_gt
     pos_loss = (ce_lab * pm * iouf).sum() / bs
     neg_loss = (ce0 * nm).sum() / bs
     return refine_loss, det_loss, neg_loss / 2 + pos_loss
+
+
+def _nms_iou_vec(bi, bj):
+    """tf_nms_iou of box bi [4] against boxes bj [n, 4], same float32 operations."""
+    ymin_i, xmin_i = min(bi[0], bi[2]), min(bi[1], bi[3])
+    ymax_i, xmax_i = max(bi[0], bi[2]), max(bi[1], bi[3])
+    ymin_j, xmin_j = np.minimum(bj[:, 0], bj[:, 2]), np.minimum(bj[:, 1], bj[:, 3])
+    ymax_j, xmax_j = np.maximum(bj[:, 0], bj[:, 2]), np.maximum(bj[:, 1], bj[:, 3])
+    area_i = f32(ymax_i - ymin_i) * f32(xmax_i - xmin_i)
+    area_j = (ymax_j - ymin_j) * (xmax_j - xmin_j)
+    ih = np.maximum(np.minimum(ymax_i, ymax_j) - np.maximum(ymin_i, ymin_j), f32(0))
+    iw = np.maximum(np.minimum(xmax_i, xmax_j) - np.maximum(xmin_i, xmin_j), f32(0))
+    inter = ih * iw
+    with np.errstate(all='ignore'):
+        v = inter / ((area_i + area_j) - inter)
+    return np.where((area_i <= 0) | (area_j <= 0), f32(0), v).astype(f32)
+
+
+def detected_bboxes_vec(probs, boxes, select_threshold, nms_threshold, top_k, keep_top_k):
+    """detected_bboxes with the greedy NMS vectorised over the kept set (identical float32
+    operations and decisions; for the full-size B=32 parity test)."""
+    probs = np.asarray(probs, f32)
+    boxes = np.asarray(boxes, f32)
+    B, A, K = probs.shape
+    out_s = np.zeros((B, K - 1, keep_top_k), f32)
+    out_b = np.zeros((B, K - 1, keep_top_k, 4), f32)
+    kept_idx = {}
+    for b in range(B):
+        for c in range(1, K):
+            p = probs[b, :, c]
+            fm = (p >= f32(select_threshold)).astype(f32)
+            s = p * fm
+            bx = boxes[b] * fm[:, None]
+            order = np.argsort(-s, kind='stable')[:min(top_k, A)]
+            sel = []
+            kb = np.zeros((0, 4), f32)
+            for i in order:
+                if len(sel) and (_nms_iou_vec(bx[i], kb) > f32(nms_threshold)).any():
+                    continue
+                sel.append(int(i))
+                kb = np.concatenate([kb, bx[i][None]], 0)
+                if len(sel) == keep_top_k:
+                    break
+            kept_idx[(b, c)] = sel
+            out_s[b, c - 1, :len(sel)] = s[sel]
+            out_b[b, c - 1, :len(sel)] = bx[sel]
+    return out_s, out_b, kept_idx

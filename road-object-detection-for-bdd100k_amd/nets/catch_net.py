@@ -164,6 +164,22 @@ class CatchNet:
         out.append(x)
         return out
 
+    @torch.no_grad()
+    def calibrate_batchnorm(self, inputs):
+        """Set every BatchNorm's moving statistics to the batch statistics of `inputs` (one
+        training-mode forward with decay 0).  For synthetic-weight runs only (bench / tests):
+        random weights with the initial moving statistics (0, 1) make eval-mode activations
+        vanish layer by layer (logits ~1e-7, uniform softmax), which is not what a trained
+        detector's inference path sees."""
+        import nets.backbone.mobilenet_v2 as mb
+        global HEAD_BN_DECAY
+        saved = (mb.BN_DECAY, HEAD_BN_DECAY)
+        mb.BN_DECAY, HEAD_BN_DECAY = 0.0, 0.0
+        try:
+            self.forward(inputs, True)
+        finally:
+            mb.BN_DECAY, HEAD_BN_DECAY = saved
+
     def forward(self, inputs, is_training):
         names = config.extract_feat_name[self.backbone_name]
         ep = self.backbone(inputs, is_training, taps=names)

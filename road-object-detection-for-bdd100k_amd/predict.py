@@ -69,6 +69,8 @@ class Predictor(object):
         self.anchors = net_tools.anchors_all_layer(config.img_size, config.feat_sizes(config.img_size),
                                                    net_tools.init_anchor(6))
         self.dtype = dtype
+        self.keep_intermediates = False   # tests: keep (logits, probs, boxes) of the last call
+        self.last = None
         self.kw = dict(select_threshold=select_threshold, nms_threshold=nms_threshold, top_k=top_k,
                        keep_top_k=keep_top_k)
 
@@ -82,6 +84,10 @@ class Predictor(object):
                                                net=self.net).get_output()
         probs = net_tools.class_probabilities(clf_out)                                     # predict.py:127-128
         boxes = net_tools.decode_all_layers(self.anchors, refine_out, det_out, to_corner=True)  # 130-134
+        if self.keep_intermediates:
+            from rod import ops
+            self.last = (ops.levels_concat(clf_out, config.total_obj_n), probs, boxes,
+                         ops.levels_concat(refine_out, 4), ops.levels_concat(det_out, 4))
         return net_tools.detected_bboxes(probs, boxes, **self.kw)                          # 136-137
 
 

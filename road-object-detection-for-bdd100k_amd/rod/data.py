@@ -37,3 +37,36 @@ def synthetic_batch(B, H, W, device, seed=SEED):
     corner, labels, n = synthetic_boxes(B, seed=seed)
     return (img.to(device), torch.from_numpy(corner).to(device), torch.from_numpy(labels).to(device),
             torch.from_numpy(n).to(device))
+
+
+def detector_like_scores(predictor, probe, rate=0.02, iters=14):
+    """Make a randomly initialised Predictor (predict.py) produce a detector-like score
+    distribution: BatchNorm moving statistics calibrated on `probe` (uint8 batch), then the
+    background logit of the clf heads shifted until about `rate` of the class scores pass
+    the selection threshold (bench / tests: NMS then has real work).  Returns the
+    fraction reached on the probe."""
+    import config
+    from rod.dataio import network_input
+    net = predictor.net
+    net.calibrate_batchnorm(network_input(probe, predictor.dtype))
+    betas = [net.store.params['clf/block_%d/BatchNorm_3/beta' % (i + 1)] for i in range(6)]
+    thr = predictor.kw['select_threshold']
+    keep = predictor.keep_intermediates
+    predictor.keep_intermediates = True
+
+    def frac(shift):
+        with torch.no_grad():
+            for b in betas:
+                b.data[0::config.total_obj_n] = shift
+        predictor(probe)
+        return float((predictor.last[1][..., 1:] >= thr).float().mean())
+    lo, hi = -8.0, 8.0
+    for _ in range(iters):
+        mid = 0.5 * (lo + hi)
+        if frac(mid) > rate:
+            lo = mid
+        else:
+            hi = mid
+    f = frac(hi)
+    predictor.keep_intermediates = keep
+    return f

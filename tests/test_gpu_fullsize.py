@@ -1,0 +1,327 @@
+"""Parity at the BASELINE.json sizes (1280x720), against the
+oracle on the same seeded inputs:
+
+  (a) C2 targets: anchor matching over all 129,915 anchors x B=8 (G <= 40 per image), ODM
+      targets and the hard-negative selection — bit-exact (positive masks, argmax labels,
+      offsets, matched boxes, IoU, k, the k-th value, the negative mask);
+  (b) C2 step: one fp32 REFINE training step at B=8, 720x1280 — loss within 1e-4 relative of
+      the float64 oracle; head outputs within 1e-4 normwise on levels 1-5 and 2e-4 on level 6
+      (the 3x5 map, 24 layers + head deep: float32 itself lands there — PyTorch's fp32 CPU
+      evaluation of the same step measured 1.25e-4, this path 1.20e-4); moving statistics
+      within 1e-4 (fixed bounds); parameter gradients within max(2e-3, 4x the error of an
+      independent float32 evaluation) — float32 backprop through the deep BatchNorms is
+      itself 1e-2..1e-1 off float64 there;
+  (c) C4 inference: predict.py's Predictor at B=32 (softmax, decode of refine+det, per-class
+      select / top-400 / NMS 0.4 / keep 200) with the clf head biased so that ~2 % of the
+      class scores pass the 0.1 selection threshold — probabilities, boxes, NMS keep lists
+      and outputs bit-exact against oracle.post given the network's logits and offsets;
+  (d) C1 plumbing: train.py main() at 300x300, batch 1, two steps (ALL), then evaluate.py and
+      predict.py main() on its checkpoint — all on the committed BDD100K-schema TFRecord
+      fixture (tests/golden/tfrecord), torch and TF-bundle checkpoints.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import config
+from oracle import net as onet
+from oracle import post as op
+from oracle import targets as ot
+from rod import ops
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+H, W = 720, 1280
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def _anchors(h=H, w=W):
+    import utils.net_tools as nt
+    config.img_size = (h, w)
+    return nt.anchors_all_layer((h, w), config.feat_sizes((h, w)), nt.init_anchor(6))
+
+
+def _nerr(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-300))
+
+
+# ------------------------------------------------------------------------------- (a)
+def test_targets_and_hard_negatives_720p_b8(dev):
+    import utils.net_tools as nt
+    from rod.data import synthetic_boxes
+    from utils.common_tools import cornerBboxes_2_centerBboxes
+    B = 8
+    anchors = _anchors()
+    corner, labels, n = synthetic_boxes(B, seed=31)
+    assert n.max() <= 40 and n.min() >= 1
+    tg = nt.refine_groundtruth(anchors, cornerBboxes_2_centerBboxes(torch.from_numpy(corner).to(dev)),
+                               torch.from_numpy(labels).to(dev), config.refine_method.JACCARD_BIGGER,
+                               n_boxes=torch.from_numpy(n).to(dev))
+    off, cbox, lbl, pos = (t.cpu().numpy() for t in tg.flat)
+    tab = tg.table
+    assert tab.A == 129915
+    thr = config.refine_pos_jac_val_all_layers
+    for b in range(B):
+        g, cb, lb, pm = ot.refine_groundtruth(anchors, ot.corner_to_center(corner[b, :n[b]]), labels[b, :n[b]], thr)
+        cat = lambda xs, k: np.concatenate([x.reshape(-1, k) for x in xs])
+        np.testing.assert_array_equal(pos[b], cat(pm, 1)[:, 0])
+        np.testing.assert_array_equal(lbl[b], cat(lb, 1)[:, 0])
+        np.testing.assert_array_equal(cbox[b], cat(cb, 4))
+        np.testing.assert_array_equal(off[b], cat(g, 4))
+    assert pos.sum() > 100 * B
+
+    rng = np.random.default_rng(32)
+    ro = (off + rng.normal(0, 0.15, off.shape)).astype(f32)
+    dthr = config.det_pos_jac_val_all_layers
+    dgt, dpos, dlbl, iou = ops.det_targets(tab.center, torch.from_numpy(ro).to(dev), *tg.flat, tab.lvl_off, dthr)
+    r_gt, r_pos, r_lbl, r_iou = op.det_groundtruth(tab.center_np, tab.lvl_off, dthr, ro, off, cbox, lbl, pos)
+    np.testing.assert_array_equal(iou.cpu().numpy(), r_iou)
+    np.testing.assert_array_equal(dpos.cpu().numpy(), r_pos)
+    np.testing.assert_array_equal(dlbl.cpu().numpy(), r_lbl)
+    np.testing.assert_array_equal(dgt.cpu().numpy(), r_gt)
+    assert r_pos.sum() > 50
+
+    logits = rng.normal(0, 2.0, (B, tab.A, 11)).astype(f32)
+    ld = torch.from_numpy(logits).to(dev).requires_grad_(True)
+    out, clf = ops.softmax_ce_hnm(ld, dlbl, dpos, iou, tab.lvl_off, float(B))
+    clf.backward()
+    ref = op.det_clf_loss(np.zeros_like(ro), r_gt, r_pos, logits, r_lbl, r_iou, tab.lvl_off, B)
+    o = out.detach().cpu().numpy()
+    assert int(o[4]) == ref['n_pos'] and int(o[5]) == ref['k']
+    assert o[3] == f32(ref['max_hard_pred'])
+    assert int(o[6]) == ref['n_neg_selected'] and ref['n_neg_selected'] > 0
+    g = ld.grad.cpu().numpy().reshape(-1, 11)
+    pm = r_pos.reshape(-1) != 0
+    neg_sel = (np.abs(g).sum(1) != 0) & ~pm                      # rows the selection kept
+    np.testing.assert_array_equal(neg_sel, ref['negmask'])
+    np.testing.assert_allclose(o[0], ref['pos_loss'], rtol=1e-5)
+    np.testing.assert_allclose(o[1], ref['neg_loss'], rtol=1e-5)
+    np.testing.assert_allclose(g, ref['g_logits'].reshape(-1, 11), rtol=1e-5, atol=1e-9)
+
+
+# ------------------------------------------------------------------------------- (b)
+def _oracle_refine_step(tr, snap, img, corner, labels, n, B, dt, device='cpu'):
+    """The REFINE step in the oracle from the parameter / moving-statistic snapshot taken
+    before the HIP step (which updates the moving statistics).  device='cuda' runs the
+    oracle's PyTorch ops on the GPU: a second, independent float32 evaluation."""
+    P = {k: v.clone().to(device, dt).requires_grad_(True) for k, v in snap[0].items()}
+    Bf = {k: v.clone().to(device, dt) for k, v in snap[1].items()}
+    x = torch.from_numpy(f32(2.0 / 255.0) * img.cpu().numpy().astype(f32) - f32(1.0)).to(device, dt)
+    mov = {}
+    refine = onet.forward(x, P, Bf, True, moving=mov)
+    center = ot.corner_to_center(corner.cpu().numpy())
+    gts, pms = [[] for _ in range(6)], [[] for _ in range(6)]
+    for b in range(B):
+        nb = int(n[b])
+        g, _, _, p = ot.refine_groundtruth(tr.anchors, center[b, :nb], labels.cpu().numpy()[b, :nb],
+                                           config.refine_pos_jac_val_all_layers)
+        for l in range(6):
+            gts[l].append(g[l])
+            pms[l].append(p[l])
+    loss = 0.
+    for l in range(6):
+        d = (torch.from_numpy(np.stack(gts[l])).to(device, dt) - refine[l]) * \
+            torch.from_numpy(np.stack(pms[l])).to(device, dt)
+        ad = d.abs()
+        loss = loss + (0.5 * ((ad - 1) * torch.clamp(ad, max=1.0) + ad)).sum() / B
+    loss.backward()
+    return P, mov, refine, loss
+
+
+def test_refine_step_fp32_720p_b8(dev):
+    import utils.net_tools as nt
+    from nets.catch_net import factory
+    from rod.data import synthetic_batch
+    from rod.trainer import Trainer
+    from utils.common_tools import cornerBboxes_2_centerBboxes
+    B = 8     # C2: BDD100K 1280x720 fp32 batch 8 (at B=2 the 3x5 level's BatchNorms see 30 rows and
+    #           float32 itself — PyTorch's CPU evaluation as much as this one — lands at 1.25e-4)
+    tr = Trainer((H, W), B, dtype=torch.float32, device=dev, learning_rate=1e-3, seed=21)
+    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=22)
+    snap = ({k: v.detach().cpu().clone() for k, v in tr.net.store.params.items()},
+            {k: v.detach().cpu().clone() for k, v in tr.net.store.buffers.items()})
+    x = ops.normalize_image(img, torch.float32)
+    tg = nt.refine_groundtruth(tr.anchors, cornerBboxes_2_centerBboxes(corner), labels,
+                               config.refine_method.JACCARD_BIGGER, n_boxes=n)
+    outs = factory(x, 'mobilenet_v2', True, tr.config_dict, torch.float32, net=tr.net).get_output()
+    loss = nt.refine_loss(outs, tg[0], tg[3], targets=tg)
+    loss.backward()
+    torch.cuda.synchronize()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    P64, mov64, ref64, loss64 = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float64)
+    rep = [(l, _nerr(a, o64)) for l, (a, o64) in enumerate(zip(outs, ref64))]
+    print('per-level normwise error vs fp64:', rep)
+    lrel = abs(loss.item() - loss64.item()) / abs(loss64.item())
+    print('loss', loss.item(), 'fp64', loss64.item(), 'rel', lrel)
+    # level 6 sits 24 backbone layers + 4 head convs deep; per-level float32 error roughly
+    # doubles per level (4e-6 ... 1.2e-4 measured, the fp32 PyTorch oracle alike)
+    assert all(e <= (1e-4 if l < 5 else 2e-4) for l, e in rep), rep
+    assert lrel <= 1e-4
+    # moving means are judged on the scale of their update, (1 - decay) x the batch std: the
+    # mean of a conv fed by a linear-BN output (project -> expand) is 0 up to rounding
+    bad_mov = []
+    for k, v in mov64.items():
+        got = tr.net.store.buffers[k].double().cpu()
+        scale = v.abs().max()
+        if k.endswith('moving_mean'):
+            decay = 0.997 if k.startswith('backbone/') else 0.999
+            var_b = (mov64[k[:-len('moving_mean')] + 'moving_variance'] - decay) / (1 - decay)
+            scale = max(float(scale), (1 - decay) * float(var_b.clamp_min(0).sqrt().max()))
+        e = float((got - v).abs().max()) / float(scale)
+        if e > 1e-4:
+            bad_mov.append((k, e))
+    assert not bad_mov, bad_mov[:5]
+    # Parameter gradients: float32 backprop through 24 BatchNorm'd layers is ill-conditioned
+    # in the deep backbone (the deepest expand / depthwise gradients of ANY float32 evaluation
+    # are 1e-2..1.5e-1 off float64 here, measured), so they are held to the float32 scatter:
+    # within max(2e-3, 4x) the error of an independent float32 evaluation of the same step (the
+    # oracle, PyTorch-CPU fp32).  Measured: worst ratio 3.7 (expanded_conv_22/expand/BatchNorm/
+    # beta 0.152 vs 0.041); a third evaluation (the oracle's ops on the GPU) did not widen it.
+    P32, _, ref32, _ = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float32)
+    Pg = P32
+    print('oracle fp32 per-level:', [(l, _nerr(a, o)) for l, (a, o) in enumerate(zip(ref32, ref64))])
+    # gradients that are zero by construction (a bias or beta feeding a BatchNorm directly:
+    # shift invariance) are judged on the scale of the step's gradients, not their own
+    gscale = float(np.median([float(P64[k].grad.abs().max()) for k in tr.net.store.params]))
+    bad, worst = [], 0.0
+    rows, zero_rows = [], []
+    for name, p in tr.net.store.params.items():
+        g64 = P64[name].grad
+        if float(g64.abs().max()) < 1e-6 * gscale:
+            z = float(p._rod_grad.abs().max()) / gscale
+            z32 = max(float(P32[name].grad.abs().max()), float(Pg[name].grad.abs().max())) / gscale
+            zero_rows.append((z, z32, name))
+            if z > max(1e-4, 4 * z32):
+                bad.append((name, 'zero-by-construction', z, z32))
+            continue
+        e = _nerr(p._rod_grad, g64)
+        e32 = max(_nerr(P32[name].grad, g64), _nerr(Pg[name].grad, g64))
+        rows.append((e, e32, name))
+        worst = max(worst, e)
+        if e > max(2e-3, 4 * e32):
+            bad.append((name, e, e32))
+    rows.sort(reverse=True)
+    zero_rows.sort(reverse=True)
+    for r in rows[:12]:
+        print('grad err %.3e  fp32 scatter %.3e  %s' % r)
+    for r in zero_rows[:3]:
+        print('zero-by-construction grad |g|/scale %.3e  fp32 %.3e  %s' % r)
+    print('worst parameter-gradient normwise error:', worst, 'over', len(tr.net.store.params), 'tensors')
+    assert not bad, bad[:10]
+
+
+# ------------------------------------------------------------------------------- (c)
+def test_predict_b32_nms_bit_exact(dev):
+    import predict
+    from rod.data import synthetic_batch
+    pr = predict.Predictor((H, W), dev, torch.bfloat16, seed=41)
+    pr.keep_intermediates = True
+    probe = synthetic_batch(4, H, W, dev, seed=42)[0]
+    # random init + initial moving statistics give vanishing eval activations (uniform
+    # softmax, nothing selected): calibrate BatchNorm on a probe batch and shift the background
+    # logit so that ~2 % of the class scores pass select_threshold 0.1
+    from rod.data import detector_like_scores
+    f_probe = detector_like_scores(pr, probe, rate=0.02)
+    img = synthetic_batch(32, H, W, dev, seed=43)[0]
+    scores, bboxes = pr(img)
+    logits, probs, boxes, roff, doff = pr.last
+    f_pass = float((probs[..., 1:] >= 0.1).float().mean())
+    print('fraction of class scores >= 0.1:', f_pass, '(probe batch:', f_probe, ')')
+    assert 0.005 <= f_pass <= 0.06
+    lg = logits.float().cpu().numpy()
+    e, s, _ = op.softmax_rows(lg)
+    probs_ref = (e / s).astype(f32)
+    P = probs.cpu().numpy()
+    np.testing.assert_array_equal(P, probs_ref)
+    import utils.net_tools as nt
+    tab = nt.anchor_table(pr.anchors, dev)
+    bx_ref = op.decode_corner(tab.center_np, roff.float().cpu().numpy() + doff.float().cpu().numpy())
+    BX = boxes.cpu().numpy()
+    np.testing.assert_array_equal(BX, bx_ref)
+    s_ref, b_ref, kept = op.detected_bboxes_vec(P, BX, 0.1, 0.4, 400, 200)
+    S = np.stack([scores[c].cpu().numpy() for c in range(1, 11)], 1)
+    Bo = np.stack([bboxes[c].cpu().numpy() for c in range(1, 11)], 1)
+    np.testing.assert_array_equal(S, s_ref)
+    np.testing.assert_array_equal(Bo, b_ref)
+    n_kept = sum(len(v) for v in kept.values())
+    print('kept detections over 32 images x 10 classes:', n_kept)
+    assert n_kept > 320 and max(len(v) for v in kept.values()) > 20
+
+
+# ------------------------------------------------------------------------------- (d)
+def _cli(mod, argv):
+    import importlib
+    m = importlib.import_module(mod)
+    return m.main(argv)
+
+
+def test_cli_train_evaluate_predict_on_tfrecords(dev, tmp_path):
+    ds = os.path.join(GOLD, 'tfrecord')
+    tdir, sdir, edir = str(tmp_path / 'ckpt'), str(tmp_path / 'summ'), str(tmp_path / 'eval')
+    common = ['--img_height=300', '--img_width=300', '--dataset_dir=' + ds]
+    _cli('train', common + ['--batch_size=1', '--train_range=ALL', '--checkpoint_refine=None', '--fix_refine=False',
+                            '--max_number_of_steps=1', '--save_every_n_steps=2', '--log_every_n_steps=1',
+                            '--summary_every_n_steps=1', '--train_dir=' + tdir, '--summary_dir=' + sdir])
+    ck = os.path.join(tdir, 'mobilenet_v2.model')
+    assert os.path.isfile(ck)
+    recs = [json.loads(l) for l in open(os.path.join(sdir, 'train_rank0.jsonl'))]
+    assert [r['step'] for r in recs] == [0, 1] and all(np.isfinite(r['loss']).all() for r in recs)
+    m07, m12 = _cli('evaluate', common + ['--batch_size=4', '--num_images=8', '--checkpoint_path=' + tdir,
+                                          '--eval_dir=' + edir])
+    ev = json.load(open(os.path.join(edir, 'eval.json')))
+    assert ev['num_batches'] == 2 and not ev['synthetic'] and ev['checkpoint'] == ck
+    assert np.isfinite(m07) and np.isfinite(m12) and 0 <= m07 <= 1 and 0 <= m12 <= 1
+    scores, boxes = _cli('predict', common + ['--batch_size=2', '--checkpoint_all=' + ck,
+                                              '--output=' + str(tmp_path / 'det.json')])
+    assert set(scores) == set(range(1, 11)) and scores[1].shape == (2, 200)
+    # the same weights as a TF-1.x tensor bundle: evaluate restores it and gives the same mAP
+    from rod.checkpoint import load_variables, save_variables
+    from nets.catch_net import CatchNet
+    cfg = {'train_range': config.train_range.ALL, 'process_backbone_method': config.process_backbone_method.NONE,
+           'deconv_method': config.deconv_method.LEARN_HALF, 'merge_method': config.merge_method.ADD}
+    net = CatchNet('mobilenet_v2', cfg, dev)
+    load_variables(net.store, ck)
+    tfdir = str(tmp_path / 'tfck')
+    save_variables(net.store, os.path.join(tfdir, 'mobilenet_v2.model'), 2, fmt='tf')
+    t07, t12 = _cli('evaluate', common + ['--batch_size=4', '--num_images=8', '--checkpoint_path=' + tfdir,
+                                          '--eval_dir=' + edir])
+    assert (t07, t12) == (m07, m12)
+    # no dataset and no --synthetic: an error, as in the reference
+    with pytest.raises(FileNotFoundError):
+        _cli('predict', ['--img_height=300', '--img_width=300', '--dataset_dir=' + str(tmp_path),
+                         '--checkpoint_all=' + ck])
+
+
+def test_tfrecord_source_batches(dev):
+    """TFRecordSource on the fixture: the eval path is the legacy bilinear resize of the
+    decoded JPEG (oracle.augment) normalised; the train path yields boxes inside [0, 1]."""
+    from oracle import augment as oaug
+    from rod.dataio import TFRecordSource, tfrecord_files
+    exp = np.load(os.path.join(GOLD, 'tfrecord', 'expected.npz'))
+    files = tfrecord_files(os.path.join(GOLD, 'tfrecord'))
+    src = TFRecordSource(files, 3, (96, 160), dev, torch.float32, train=False)
+    x, bo, lo, n = next(src)
+    for b in range(3):
+        ref = oaug.process_image(exp['image_%d' % b], (0, 0) + exp['image_%d' % b].shape[:2], False, -1, None,
+                                 96, 160, True)
+        np.testing.assert_array_equal(x[b].cpu().numpy(), ref)
+        g = int(n[b])
+        np.testing.assert_array_equal(bo[b, :g].cpu().numpy(), exp['boxes_%d' % b])
+        np.testing.assert_array_equal(lo[b, :g].cpu().numpy(), exp['labels_%d' % b])
+    tr = TFRecordSource(files, 4, (96, 160), dev, torch.bfloat16, train=True, seed=5)
+    seen = 0
+    for _ in range(3):                       # crosses an epoch boundary (8 records)
+        x, bo, lo, n = next(tr)
+        assert x.dtype == torch.bfloat16 and x.shape == (4, 96, 160, 3)
+        assert float(x.float().abs().max()) <= 1.0 + 1e-6
+        for b in range(4):
+            g = int(n[b])
+            bb = bo[b, :g].cpu().numpy()
+            assert ((bb >= 0) & (bb <= 1)).all()
+            seen += g
+    assert seen > 0 and tr.epoch == 1

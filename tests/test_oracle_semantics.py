@@ -94,3 +94,26 @@ def test_product_matching_known_case():
     assert n == 2
     assert tp.tolist() == [True, False, True, False]   # second hit on an already matched GT is FP
     assert fp.tolist() == [False, True, False, True]
+
+
+def test_vectorised_nms_oracle_equals_scalar():
+    """oracle.post.detected_bboxes_vec (used at B=32 full size) takes the same decisions and
+    float32 values as the scalar restatement, including ties, zero-area filler boxes and
+    scores below the selection threshold."""
+    from oracle import post as op
+    rng = np.random.default_rng(7)
+    B, A, K = 2, 300, 4
+    logits = rng.normal(0, 2.0, (B, A, K)).astype(np.float32)
+    logits[:, 10:20] = logits[:, 10:11]                   # exact score ties
+    e, s, _ = op.softmax_rows(logits)
+    probs = (e / s).astype(np.float32)
+    c = rng.uniform(0.2, 0.8, (B, A, 2)).astype(np.float32)
+    hw = rng.uniform(0.0, 0.3, (B, A, 2)).astype(np.float32)
+    hw[:, 50:55] = 0                                       # zero-area boxes
+    boxes = np.concatenate([c - hw / 2, c + hw / 2], -1).astype(np.float32)
+    for sel, nms, tk, keep in [(0.1, 0.4, 100, 30), (0.0, 0.5, 300, 200), (0.3, 0.2, 64, 8)]:
+        a = op.detected_bboxes(probs, boxes, sel, nms, tk, keep)
+        b = op.detected_bboxes_vec(probs, boxes, sel, nms, tk, keep)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        assert a[2] == b[2]
