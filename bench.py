@@ -45,7 +45,9 @@ def parse():
                          '(process_raw_data_train: random crop / resize / flip / colour, fused normalisation)')
     ap.add_argument('--no-fix-refine', dest='fix_refine', action='store_false', default=True,
                     help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
-    ap.add_argument('--probe', default='rod_bn_bwd', help='C-ABI entry reported in "roofline" (dominant)')
+    ap.add_argument('--probe', default='rod_bn_bwd_reduce,rod_bn_bwd_apply',
+                    help='C-ABI entry (or comma list, aggregated as one kernel family) reported in "roofline": '
+                         'default the BatchNorm backward (reduce + apply), the family VERDICT r1 names')
     ap.add_argument('--probe-table', dest='probe_table', default=None,
                     help='time EVERY librod call and write a per-entry table (JSON) here (analysis only)')
     ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'),
@@ -124,7 +126,7 @@ def inference_fps(args, dev, dtype, batch=32, steps=5, warmup=2):
 
 
 NORTH_STAR = ('rod_dw3x3_fwd', 'rod_dw3x3_bwd_data', 'rod_dw3x3_bwd_filter', 'rod_conv_fwd', 'rod_conv_wgrad',
-              'rod_bn_bwd')
+              'rod_pw_bwd', 'rod_bn_bwd_reduce', 'rod_bn_bwd_apply', 'rod_bn_bwd')
 
 
 def kernel_rooflines(tr, batch, steps, dtype):
@@ -200,7 +202,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    _abi.PROBE.arm('*' if args.probe_table else args.probe)
+    probe_set = [p for p in args.probe.split(',') if p]
+    _abi.PROBE.arm('*' if args.probe_table else probe_set)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = tr.step(*next_batch())
@@ -216,7 +219,10 @@ def main():
         elapsed = float(t.item())
 
     table = _abi.PROBE.table()
-    n_launch, ms, byts, flops = table.get(args.probe, (0, 0.0, 0, 0))
+    n_launch, ms, byts, flops = 0, 0.0, 0, 0
+    for p in probe_set:
+        e = table.get(p, (0, 0.0, 0, 0))
+        n_launch, ms, byts, flops = n_launch + e[0], ms + e[1], byts + e[2], flops + e[3]
     loss_val = float(losses[0].item())
     kernels = None
     if args.kernel_steps > 0 and world == 1:
@@ -255,12 +261,16 @@ def main():
         traffic, tsrc = None, None
         if args.traffic and os.path.exists(args.traffic):
             tj = json.load(open(args.traffic))
-            te = tj.get('entries', {}).get(args.probe)
-            if te is not None and tj.get('config') == [args.train_range, args.batch, args.height, args.width, args.dtype]:
-                traffic = round(te['bytes_per_launch'])
+            tes = [tj.get('entries', {}).get(p) for p in probe_set]
+            if all(te is not None for te in tes) and \
+                    tj.get('config') == [args.train_range, args.batch, args.height, args.width, args.dtype]:
+                # per launch of the family: total PMC bytes of its entries / their launches
+                traffic = round(sum(te['bytes_per_launch'] * te['launches'] for te in tes) /
+                                max(1, sum(te['launches'] for te in tes)))
                 tsrc = os.path.relpath(args.traffic, ROOT)
         rl.update({'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, PMC)', 'traffic_source': tsrc,
-                   'alg_bytes_per_launch': byts // max(n_launch, 1), 'kernel': args.probe, 'launches_per_step': n_launch // max(args.steps, 1),
+                   'alg_bytes_per_launch': byts // max(n_launch, 1), 'kernel': args.probe.replace(',', ' + '),
+                   'launches_per_step': n_launch // max(args.steps, 1),
                    'avg_launch_us': round(per_launch_ms * 1e3, 2), 'alg_bytes_per_step': byts // max(args.steps, 1),
                    'alg_flops_per_step': flops // max(args.steps, 1)})
         imgs = args.batch * world * args.steps

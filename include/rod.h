@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 5
+#define ROD_ABI_VERSION 6
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -170,6 +170,14 @@ int rod_bn_bwd_finalize(const float* parts, int nparts, long M, int C, const flo
 int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, const float* coef, void* dy, long M, int C,
                      int act, int dtype, void* stream);
+/* The reduction of FusedBatchNormGrad (ref mobilenet.py:417-420; catch_net.py:302) without
+ * the apply pass (ABI 5): reads dz and the pre-BatchNorm y once, writes dbeta, dgamma
+ * (either may be NULL) and coef[3][C] as rod_bn_bwd_finalize.  The consumer of coef applies
+ * dy = coef0*(g - coef1 - yhat*coef2) as it loads (rod_pw_bwd), so dy never crosses HBM.
+ * workspace: rod_bn_bwd_workspace(M, C) bytes. */
+int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const float* rstd,
+                      const float* gamma, const float* beta, float* dgamma, float* dbeta, float* coef,
+                      void* workspace, long M, int C, int act, int dtype, void* stream);
 
 /* -------------------------------------- dense conv as implicit GEMM (A2 A3 A5)
  * y[m, co] = sum_k A[m, k] * wt[co, k] (+ bias[co]), fp32 accumulation,
@@ -216,6 +224,27 @@ int rod_conv_wgrad(const void* x, const float* pro_mean, const float* pro_rstd, 
                    const float* pro_beta, int pro_act, const void* dy, float* dw, float* db,
                    void* workspace, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
                    int lddy, int dtype, void* stream);
+
+/* -------------------------------------- fused 1x1-conv backward through its BatchNorm (ABI 5)
+ * The backward of  z = act(BN(y)), y = conv1x1(a) + bias,  a = act_x(BN_x(x)) or x, in ONE
+ * pass over the rows (ref: Conv2DBackpropInput + Conv2DBackpropFilter + FusedBatchNormGrad of
+ * slim.conv2d + slim.batch_norm, conv_blocks.py:263-294, catch_net.py:301-304):
+ *   dy = coef0*(dz*act'(y*sc + sh) - coef1 - yhat*coef2)   (coef from rod_bn_bwd_reduce,
+ *        rounded to bf16 as rod_bn_bwd_apply would store it, kept in LDS only)
+ *   dx = dy . W            (W = the mode-1 operand wt1[Cin][Cout], bf16) -> dx [M, Cin]
+ *   dw = a^T . dy  -> dw fp32 [Cout][Cin] (overwritten), db = sum_m dy (when db != NULL)
+ * a = the conv input with the optional BatchNorm-apply prologue (xmean NULL => none).  One
+ * read of dz, y and x, one write of dx: the dy tensor of the unfused path (write + 3 reads)
+ * does not exist.  bf16 only; rod_pw_bwd_supported() tells which (Cin, Cout) it takes (Cin,
+ * Cout multiples of 8, Cin*Cout <= 16384, Cin <= 192, Cout <= 512).  dx may be NULL (input
+ * gradient not needed).  workspace: rod_pw_bwd_workspace() bytes. */
+int rod_pw_bwd_supported(int Cin, int Cout, int dtype);
+size_t rod_pw_bwd_workspace(long M, int Cin, int Cout);
+int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+               const float* beta, int act, const float* coef, const void* x, const float* xmean,
+               const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+               void* dx, float* dw, float* db, void* workspace, long M, int Cin, int Cout, int dtype,
+               void* stream);
 
 /* ------------------------------------------------ targets and losses
  * Anchor matching, JACCARD_BIGGER (utils/net_tools.py:270-428, branch 382-421).

@@ -762,6 +762,32 @@ size_t rod_bn_bwd_workspace(long M, int C) {
   return (size_t)max_nbx(M, C) * 2 * C * sizeof(float) + (size_t)3 * C * sizeof(float) + 16;
 }
 
+// reduce + finalize only: (dgamma, dbeta, coef[3][C]) for a consumer that applies the
+// BatchNorm backward itself (rod_pw_bwd; the apply pass is never written out)
+int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                      const float* beta, float* dgamma, float* dbeta, float* coef, void* workspace, long M, int C,
+                      int act, int dtype, void* stream) {
+  ROD_CHECK_ARG(M > 0 && C > 0 && coef != nullptr, "rod_bn_bwd_reduce: bad arguments");
+  ROD_CHECK_ARG(workspace != nullptr, "rod_bn_bwd_reduce: workspace is NULL");
+  hipStream_t s = ROD_STREAM(stream);
+  float* slab = (float*)workspace;
+  ROD_DISPATCH_DTYPE(dtype, {
+    const bool vec = vec_ok<T>(C, {{dz, C}, {y, C}});
+    RedPlan pl = red_plan<T>(M, C, vec);
+    dim3 grid(pl.nbx, pl.cgroups);
+    size_t lds = 2 * 256 * pl.V * sizeof(float);
+    if (vec)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), grid, dim3(256), lds, s, (const T*)dz, (const T*)y, mean,
+                         rstd, gamma, beta, M, C, C, C, act, pl.CVb, pl.lanes, pl.chunk, slab);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), grid, dim3(256), lds, s, (const T*)dz, (const T*)y, mean,
+                         rstd, gamma, beta, M, C, C, C, act, pl.CVb, pl.lanes, pl.chunk, slab);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 4)), dim3(256), 0, s, slab, pl.nbx, M, C, rstd, gamma,
+                       dgamma, dbeta, coef);
+  });
+  return check_launch("rod_bn_bwd_reduce");
+}
+
 int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma,
                const float* beta, void* dx, float* dgamma, float* dbeta, void* workspace, long M, int C, int lddy,
                int ldx, int lddx, int act, int dtype, void* stream) {

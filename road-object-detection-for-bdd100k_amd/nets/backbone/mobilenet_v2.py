@@ -76,20 +76,13 @@ class MobilenetV2:
         self.store.add_buffer(name + '/moving_mean', np.zeros(c, np.float32))
         self.store.add_buffer(name + '/moving_variance', np.ones(c, np.float32))
 
-    def _bn_act(self, x, name, act, training, residual=None, parts=None, pending=False):
-        """BatchNorm + activation (+ residual).  pending: leave it to the single consumer's
-        load prologue (ops.Pending) instead of writing it out."""
+    def _bn_args(self, name):
         P, B = self.store.params, self.store.buffers
-        p = ops.bn_pending(x, P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'],
-                           B[name + '/moving_variance'], act, training, BN_DECAY, BN_EPS, parts)
-        return p if pending and residual is None else ops.materialize(p, residual)
+        return P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'], B[name + '/moving_variance']
 
-    @staticmethod
-    def _conv(x, w, ks, training):
-        """conv whose epilogue also reduces the following BatchNorm's statistics (training)."""
-        if training:
-            return ops.conv2d(x, w, None, ks, want_stats=True)
-        return ops.conv2d(x, w, None, ks), None
+    def _conv_bn(self, x, w, ks, name, act, training):
+        """conv + BatchNorm(+act) as one node (ops.conv2d_bn), left Pending (owned)."""
+        return ops.conv2d_bn(x, w, None, ks, *self._bn_args(name), act, training, BN_DECAY, BN_EPS)
 
     def __call__(self, x, is_training, final_endpoint=None, taps=None):
         """Returns the endpoint dict {'layer_1': ..., 'layer_24': ...} (mobilenet.py:275-281).
@@ -102,32 +95,29 @@ class MobilenetV2:
         # The stem, expand and depthwise BatchNorms each feed exactly one consumer (the next
         # depthwise or project conv), so they stay Pending and are applied in that consumer's
         # load prologue; the project BatchNorm (+ residual) is written out as the endpoint.
+        # Each conv and its BatchNorm are one autograd node (ops.conv2d_bn / dw3x3_bn) whose
+        # backward runs the BatchNorm backward with the conv's own (fused for 1x1 where it pays).
         fuse = 'bnpro' not in ops._DISABLE
+        keep = (lambda p: p) if fuse else ops.materialize
         for (idx, kind, s, cin, inner, cout, res, sc) in self.plan:
             base = '%s/%s' % (self.scope, sc)
             name = 'layer_%d' % idx
             tapped = name in taps or final_endpoint == name
             if kind == 'conv':
-                x, st = self._conv(x, P[base + '/weights'], 3, is_training)
-                x = self._bn_act(x, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st,
-                                 pending=fuse and not tapped)
+                x = self._conv_bn(x, P[base + '/weights'], 3, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training)
+                x = ops.materialize(x) if tapped else keep(x)
             else:
                 inp = None
                 if res:
                     inp, x = graph.fork(x, 2)
                 if inner > cin:
-                    x, st = self._conv(x, P[base + '/expand/weights'], 1, is_training)
-                    x = self._bn_act(x, base + '/expand/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st,
-                                     pending=fuse)
-                if is_training:
-                    x, st = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s, want_stats=True)
-                else:
-                    x, st = ops.dw3x3(x, P[base + '/depthwise/depthwise_weights'], s), None
-                x = self._bn_act(x, base + '/depthwise/BatchNorm', ops.ROD_ACT_RELU6, is_training, parts=st,
-                                 pending=fuse)
-                x, st = self._conv(x, P[base + '/project/weights'], 1, is_training)
-                x = self._bn_act(x, base + '/project/BatchNorm', ops.ROD_ACT_NONE, is_training,
-                                 residual=inp, parts=st)
+                    x = keep(self._conv_bn(x, P[base + '/expand/weights'], 1, base + '/expand/BatchNorm',
+                                           ops.ROD_ACT_RELU6, is_training))
+                x = keep(ops.dw3x3_bn(x, P[base + '/depthwise/depthwise_weights'], s,
+                                      *self._bn_args(base + '/depthwise/BatchNorm'), ops.ROD_ACT_RELU6, is_training,
+                                      BN_DECAY, BN_EPS))
+                x = ops.materialize(self._conv_bn(x, P[base + '/project/weights'], 1, base + '/project/BatchNorm',
+                                                  ops.ROD_ACT_NONE, is_training), inp)
             last = final_endpoint == name or idx == self.plan[-1][0]
             if name in taps and not last:
                 end_points[name], x = graph.fork(x, 2)

@@ -112,12 +112,11 @@ class CatchNet:
                            act, training, HEAD_BN_DECAY, HEAD_BN_EPS, parts)
         return p if pending and 'bnpro' not in ops._DISABLE else ops.materialize(p)
 
-    @staticmethod
-    def _conv(x, w, b, ks, training):
-        """conv(+bias) whose epilogue also reduces the following BatchNorm's statistics."""
-        if training:
-            return ops.conv2d(x, w, b, ks, want_stats=True)
-        return ops.conv2d(x, w, b, ks), None
+    def _conv_bn(self, x, w, b, ks, name, training, act=ops.ROD_ACT_LEAKY):
+        """conv(+bias) + BatchNorm (beta only) + leaky as one node (ops.conv2d_bn), Pending."""
+        P, B = self.store.params, self.store.buffers
+        return ops.conv2d_bn(x, w, b, ks, None, P[name + '/beta'], B[name + '/moving_mean'],
+                             B[name + '/moving_variance'], act, training, HEAD_BN_DECAY, HEAD_BN_EPS)
 
     def head_out(self, feats, scope, k, training):
         """__det_out / __clf_out (catch_net.py:276-342)."""
@@ -130,9 +129,10 @@ class CatchNet:
                 for ks in (1, 3):
                     cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
                     bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
-                    x, st = self._conv(x, P[cname + '/weights'], P[cname + '/biases'], ks, training)
+                    x = self._conv_bn(x, P[cname + '/weights'], P[cname + '/biases'], ks, bname, training)
                     # the first three BatchNorms feed only the next conv of the head
-                    x = self._bn(x, bname, training, parts=st, pending=n < 3)
+                    if n == 3 or 'bnpro' in ops._DISABLE:
+                        x = ops.materialize(x)
                     n += 1
             B_, fh, fw, _ = x.shape
             outs.append(x.view(B_, fh, fw, self.n_anchor[i], k))
@@ -148,8 +148,8 @@ class CatchNet:
         for i in range(n):
             base = 'deconv/block_%d' % (i + 1)
             if i == 0:
-                x, st = self._conv(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1, training)
-                x = self._bn(x, base + '/BatchNorm', training, parts=st)
+                x = ops.materialize(self._conv_bn(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1,
+                                                  base + '/BatchNorm', training))
             else:
                 B_, h, w, _ = layers[i].shape
                 x_out, x_up, x_rs = xs

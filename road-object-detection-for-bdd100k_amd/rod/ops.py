@@ -147,11 +147,14 @@ class Pending:
     act((y - mean) * rstd*gamma + beta) as it loads it (include/rod.h, ABI 3), and its backward
     runs the BatchNorm backward itself; `materialize` writes the tensor for any other consumer.
     """
-    __slots__ = ('y', 'mean', 'rstd', 'gamma', 'beta', 'act', 'training')
+    __slots__ = ('y', 'mean', 'rstd', 'gamma', 'beta', 'act', 'training', 'owned')
 
-    def __init__(self, y, mean, rstd, gamma, beta, act, training):
+    def __init__(self, y, mean, rstd, gamma, beta, act, training, owned=False):
         self.y, self.mean, self.rstd, self.gamma, self.beta = y, mean, rstd, gamma, beta
         self.act, self.training = act, training
+        # owned: y is the output of a producer node (_ConvBN / _DWBN) that runs this
+        # BatchNorm's backward itself; the consumer hands back d/d(act output) unchanged
+        self.owned = owned
 
     @property
     def shape(self):
@@ -187,6 +190,38 @@ def _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
     return dy
 
 
+def bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
+    """rod_bn_bwd_reduce: the BatchNorm-backward sums of (dz, y) -> coef [3, C] for a consumer
+    that applies dy itself; dgamma / dbeta go to the parameters' flat-buffer slots."""
+    C = y.shape[-1]
+    M = y.numel() // C
+    coef = torch.empty(3 * C, dtype=torch.float32, device=y.device)
+    dg = grad_slot(gamma) if need_g else None
+    db = grad_slot(beta) if need_b else None
+    ws = workspace(_abi.query("rod_bn_bwd_workspace", M, C), y.device)
+    _abi.call("rod_bn_bwd_reduce", dz, y, mean, rstd, gamma, beta, dg, db, coef, ws, M, C, act, dtcode(y), stream())
+    if need_g:
+        _mark_written(gamma)
+    if need_b:
+        _mark_written(beta)
+    return coef
+
+
+def pw_bwd_supported(Cin, Cout, dtype):
+    return "pwbwd" not in _DISABLE and bool(_abi.lib().rod_pw_bwd_supported(int(Cin), int(Cout), _DT[dtype]))
+
+
+def pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, want_dx, dw, db):
+    """rod_pw_bwd: dx (or None), dw / db written in place (fp32 [Cout, Cin] / [Cout])."""
+    Cin, Cout = x.shape[-1], y.shape[-1]
+    M = y.numel() // Cout
+    dx = torch.empty_like(x) if want_dx else None
+    ws = workspace(_abi.query("rod_pw_bwd_workspace", M, Cin, Cout), y.device)
+    _abi.call("rod_pw_bwd", dz, y, mean, rstd, gamma, beta, act, coef, x, *_pro_args(xpro), wt1 if want_dx else None,
+              dx, dw, db, ws, M, Cin, Cout, dtcode(y), stream())
+    return dx
+
+
 def _bn_backward_parts(dz, y, mean, rstd, gamma, beta, act, parts, need_g, need_b):
     """Finish a BatchNorm backward whose reduction the producer of dz already did in its
     epilogue (gred partial sums): rod_bn_bwd_finalize -> rod_bn_bwd_apply."""
@@ -213,16 +248,21 @@ def _gred_args(g):
 
 
 def _split_in(x):
-    """(tensor, gamma, beta, mean, rstd, act, training) of a plain tensor or a Pending."""
+    """(tensor, gamma, beta, mean, rstd, act, training, owned) of a plain tensor or a Pending.
+    An owned Pending's gamma / beta are passed detached: its producer writes their gradients."""
     if isinstance(x, Pending):
-        return x.y, x.gamma, x.beta, x.mean, x.rstd, x.act, x.training
-    return x, None, None, None, None, 0, False
+        if x.owned:
+            det = lambda t: None if t is None else t.detach()
+            return x.y, det(x.gamma), det(x.beta), x.mean, x.rstd, x.act, x.training, True
+        return x.y, x.gamma, x.beta, x.mean, x.rstd, x.act, x.training, False
+    return x, None, None, None, None, 0, False, False
 
 
 # ----------------------------------------------------------------------------- depthwise
 class _DW3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, want_stats, gamma, beta, mean, rstd, act, training):
+    def forward(ctx, x, w, stride, want_stats, gamma, beta, mean, rstd, act, training, owned=False):
+        ctx.owned = owned
         N, H, W, C = x.shape
         Ho, pt = same_pad(H, stride)
         Wo, pl = same_pad(W, stride)
@@ -257,7 +297,7 @@ class _DW3x3(torch.autograd.Function):
                 raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
             dx = torch.empty_like(x)   # gradient wrt the dw input (the BatchNorm output when pro)
             gred = None
-            if ctx.pro and "gred" in _ENABLE:   # BatchNorm-backward sums in the epilogue
+            if ctx.pro and "gred" in _ENABLE and not ctx.owned:   # BatchNorm-backward sums in the epilogue
                 nparts = _abi.lib().rod_dw3x3_bwd_data_gred_parts(N, H, W, C, s, dtcode(x))
                 parts = torch.empty((nparts, 2, C), dtype=torch.float32, device=x.device)
                 gred = (x, mean, rstd, gamma, beta, ctx.act, parts)
@@ -269,22 +309,22 @@ class _DW3x3(torch.autograd.Function):
             _abi.call("rod_dw3x3_bwd_filter", x, *_pro_args(pro), dy, g, ws, N, H, W, C, s, pt, pl, Ho, Wo,
                       dtcode(x), stream())
             _mark_written(w)
-        if ctx.pro and dx is not None:
+        if ctx.pro and dx is not None and not ctx.owned:
             if gred is not None:
                 dx = _bn_backward_parts(dx, x, mean, rstd, gamma, beta, ctx.act, gred[6], need_g, need_b)
             else:
                 dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
-        return dx, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None
 
 
 def dw3x3(x, w, stride=1, want_stats=False):
     """Depthwise 3x3, TF-SAME (conv_blocks.py:238-247).  x: tensor or Pending (the BatchNorm
     of the layer below is then applied in the load prologue).  want_stats: also return the
     BatchNorm partial statistics of the output (for bn_pending(..., parts=))."""
-    xt, g, b, m, r, act, tr = _split_in(x)
+    xt, g, b, m, r, act, tr, own = _split_in(x)
     if want_stats and "dwstats" in _DISABLE:
-        return _DW3x3.apply(xt, w, stride, False, g, b, m, r, act, tr), None
-    return _DW3x3.apply(xt, w, stride, want_stats, g, b, m, r, act, tr)
+        return _DW3x3.apply(xt, w, stride, False, g, b, m, r, act, tr, own), None
+    return _DW3x3.apply(xt, w, stride, want_stats, g, b, m, r, act, tr, own)
 
 
 # ----------------------------------------------------------------------------- dense conv
@@ -309,7 +349,8 @@ def conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ksize, stat_parts=None, pro=No
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, ksize, want_stats, gamma, beta, mean, rstd, act, training):
+    def forward(ctx, x, w, b, ksize, want_stats, gamma, beta, mean, rstd, act, training, owned=False):
+        ctx.owned = owned
         N, H, W, Cin = x.shape
         Cout = w.shape[0]
         assert w.shape == (Cout, ksize, ksize, Cin), (tuple(w.shape), ksize, Cin)
@@ -346,7 +387,7 @@ class _Conv(torch.autograd.Function):
             wt1 = _prep(w, 1, x.dtype, Cout, Cin, ks)
             dx = torch.empty_like(x)   # gradient wrt the conv input (the BatchNorm output when pro)
             gred = None
-            if ctx.pro and "gred" in _ENABLE:   # BatchNorm-backward sums in the epilogue
+            if ctx.pro and "gred" in _ENABLE and not ctx.owned:   # BatchNorm-backward sums in the epilogue
                 parts = torch.empty((-(-(N * H * W) // 128), 2, Cin), dtype=torch.float32, device=x.device)
                 gred = (x, mean, rstd, gamma, beta, ctx.act, parts)
             conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks, gred=gred)
@@ -364,22 +405,22 @@ class _Conv(torch.autograd.Function):
                 _mark_written(w)
             if need_bias:
                 _mark_written(b)
-        if ctx.pro and dx is not None:
+        if ctx.pro and dx is not None and not ctx.owned:
             if gred is not None:
                 dx = _bn_backward_parts(dx, x, mean, rstd, gamma, beta, ctx.act, gred[6], need_g, need_b)
             else:
                 dx = _bn_backward(dx, x, mean, rstd, gamma, beta, ctx.act, need_g, need_b)
-        return dx, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, w, b=None, ksize=1, want_stats=False):
     """slim.conv2d, stride 1, SAME (1x1 or 3x3), NHWC.  x: tensor or Pending (BatchNorm of the
     layer below applied in the load prologue).  want_stats: also return the BatchNorm partial
     statistics of the output (for bn_pending(..., parts=))."""
-    xt, g, bb, m, r, act, tr = _split_in(x)
+    xt, g, bb, m, r, act, tr, own = _split_in(x)
     if want_stats and "convstats" in _DISABLE:
-        return _Conv.apply(xt, w, b, ksize, False, g, bb, m, r, act, tr), None
-    return _Conv.apply(xt, w, b, ksize, want_stats, g, bb, m, r, act, tr)
+        return _Conv.apply(xt, w, b, ksize, False, g, bb, m, r, act, tr, own), None
+    return _Conv.apply(xt, w, b, ksize, want_stats, g, bb, m, r, act, tr, own)
 
 
 # ----------------------------------------------------------------------------- batch norm
@@ -440,6 +481,9 @@ def materialize(p, residual=None):
     """Write act(BatchNorm(y)) (+ residual after the activation) of a Pending."""
     if not isinstance(p, Pending):
         return p
+    if p.owned:
+        det = lambda t: None if t is None else t.detach()
+        return _BNApplyOwned.apply(p.y, residual, p.mean, p.rstd, det(p.gamma), det(p.beta), p.act)
     return _BNAct.apply(p.y, p.gamma, p.beta, residual, p.mean, p.rstd, p.act, p.training)
 
 
@@ -447,6 +491,198 @@ def bn_act(x, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, residual
     """slim.batch_norm (fused) + activation (+ residual add after the activation), written out.
     parts: partial statistics of x from its producer (conv2d(..., want_stats=True))."""
     return materialize(bn_pending(x, gamma, beta, mmean, mvar, act, training, decay, eps, parts), residual)
+
+
+# ----------------------------------------------------------------------------- conv / dw + BatchNorm nodes
+# A conv (or depthwise conv) and the slim.batch_norm that follows it are ONE autograd node
+# whose output is an owned Pending: consumers apply the BatchNorm in their load prologue and
+# hand back d/d(act(BN(y))) untouched; this node's backward runs the BatchNorm backward and
+# the conv backward together, so a 1x1 conv can take the fused rod_pw_bwd path (dy never
+# written) and the others at least skip nothing they did before.
+
+def _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, act, coef):
+    C = y.shape[-1]
+    dy = torch.empty_like(y)
+    _abi.call("rod_bn_bwd_apply", dz.contiguous(), y, mean, rstd, gamma, beta, coef, dy, y.numel() // C, C, act,
+              dtcode(y), stream())
+    return dy
+
+
+def _needs(p):
+    return p is not None and p.requires_grad
+
+
+# fused 1x1 backward where it measured faster than the unfused chain (tools/pwbwd_bench.py):
+# the expand-shaped convs (Cout >= 2 Cin) on >= 200k rows
+def _pw_fused_ok(M, Cin, Cout, dtype):
+    return M >= 200_000 and Cout >= 2 * Cin and pw_bwd_supported(Cin, Cout, dtype)
+
+
+def _conv_bwd_from_dy(x, w, b, ks, dy, pro, need_dx):
+    """rod_conv_fwd (mode-1 weights) for dx and rod_conv_wgrad for dw / db from a dense dy."""
+    N, H, W, Cin = x.shape
+    Cout = w.shape[0]
+    dx = None
+    if need_dx:
+        wt1 = _prep(w, 1, x.dtype, Cout, Cin, ks)
+        dx = torch.empty_like(x)
+        conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks)
+    need_w, need_bias = _needs(w), _needs(b)
+    if need_w or need_bias:
+        gw = grad_slot(w) if need_w else torch.empty(w.shape, dtype=torch.float32, device=x.device)
+        gb = grad_slot(b) if need_bias else None
+        ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, H, W, Cin, Cout, ks), x.device)
+        _abi.call("rod_conv_wgrad", x, *_pro_args(pro), dy, gw, gb, ws, N, H, W, Cin, Cout, ks, 0, 0, dtcode(x),
+                  stream())
+        if need_w:
+            _mark_written(w)
+        if need_bias:
+            _mark_written(b)
+    return dx
+
+
+class _ConvBN(torch.autograd.Function):
+    """slim.conv2d (1x1 / 3x3, stride 1, SAME, optional bias) + slim.batch_norm as one node.
+    obn = (gamma, beta, moving_mean, moving_var, act, training, decay, eps); ipro = the input's
+    BatchNorm prologue (mean, rstd, gamma, beta, act) when the input is an owned Pending."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, ks, ipro, obn):
+        gamma, beta, mm, mv, act, training, decay, eps = obn
+        N, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        assert w.shape == (Cout, ks, ks, Cin), (tuple(w.shape), ks, Cin)
+        wt = _prep(w, 0, x.dtype, Cout, Cin, ks)
+        y = torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
+        parts = None
+        if training:
+            parts = torch.empty((-(-(N * H * W) // 128), 3, Cout), dtype=torch.float32, device=x.device)
+        conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ks, parts, ipro)
+        mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
+        ctx.save_for_backward(x, w, b, y, mean, rstd)
+        ctx.ks, ctx.ipro, ctx.gb, ctx.act, ctx.training = ks, ipro, (gamma, beta), act, training
+        ctx.mark_non_differentiable(mean, rstd)
+        ctx.set_materialize_grads(False)
+        return y, mean, rstd
+
+    @staticmethod
+    def backward(ctx, dz, *_):
+        if dz is None:
+            return None, None, None, None, None, None
+        if not ctx.training:
+            raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
+        x, w, b, y, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.gb
+        N, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        M = N * H * W
+        dz = dz.contiguous()
+        coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+        need_dx = ctx.needs_input_grad[0]
+        if ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w) or _needs(b)):
+            gw = grad_slot(w) if _needs(w) else torch.empty((Cout, Cin), dtype=torch.float32, device=y.device)
+            gb = grad_slot(b) if _needs(b) else None
+            wt1 = _prep(w, 1, x.dtype, Cout, Cin, 1) if need_dx else None
+            dx = pw_bwd(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, need_dx, gw, gb)
+            if _needs(w):
+                _mark_written(w)
+            if _needs(b):
+                _mark_written(b)
+        else:
+            dy = _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, ctx.act, coef)
+            dx = _conv_bwd_from_dy(x, w, b, ctx.ks, dy, ctx.ipro, need_dx)
+        return dx, None, None, None, None, None
+
+
+class _DWBN(torch.autograd.Function):
+    """DepthwiseConv2dNative 3x3 (TF-SAME, stride s) + slim.batch_norm as one node
+    (conv_blocks.py:238-247); the input may be an owned Pending (ipro)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, ipro, obn):
+        gamma, beta, mm, mv, act, training, decay, eps = obn
+        N, H, W, C = x.shape
+        Ho, pt = same_pad(H, stride)
+        Wo, pl = same_pad(W, stride)
+        y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        parts = None
+        if training:
+            nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C, stride, dtcode(x))
+            parts = torch.empty((nparts, 3, C), dtype=torch.float32, device=x.device)
+        _abi.call("rod_dw3x3_fwd", x, *_pro_args(ipro), w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x),
+                  stream())
+        mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
+        ctx.save_for_backward(x, w, y, mean, rstd)
+        ctx.geo = (N, H, W, C, stride, pt, pl, Ho, Wo)
+        ctx.ipro, ctx.gb, ctx.act, ctx.training = ipro, (gamma, beta), act, training
+        ctx.mark_non_differentiable(mean, rstd)
+        ctx.set_materialize_grads(False)
+        return y, mean, rstd
+
+    @staticmethod
+    def backward(ctx, dz, *_):
+        if dz is None:
+            return None, None, None, None, None
+        if not ctx.training:
+            raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
+        x, w, y, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.gb
+        N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
+        coef = bn_bwd_reduce(dz.contiguous(), y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+        dy = _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, ctx.act, coef)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _abi.call("rod_dw3x3_bwd_data", dy, w, dx, *_gred_args(None), N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x),
+                      stream())
+        if _needs(w):
+            ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
+            _abi.call("rod_dw3x3_bwd_filter", x, *_pro_args(ctx.ipro), dy, grad_slot(w), ws, N, H, W, C, s, pt, pl,
+                      Ho, Wo, dtcode(x), stream())
+            _mark_written(w)
+        return dx, None, None, None, None
+
+
+def _in_pro(x):
+    """(tensor, prologue tuple or None) of a node input: plain tensor or owned Pending."""
+    if isinstance(x, Pending):
+        if not x.owned:
+            raise ValueError("conv2d_bn / dw3x3_bn take plain tensors or owned Pendings")
+        det = lambda t: None if t is None else t.detach()
+        return x.y, (x.mean, x.rstd, det(x.gamma), det(x.beta), x.act)
+    return x, None
+
+
+def conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3):
+    """slim.conv2d + slim.batch_norm(+act), left Pending (owned) for the consumer's prologue."""
+    xt, ipro = _in_pro(x)
+    y, mean, rstd = _ConvBN.apply(xt, w, b, ksize, ipro, (gamma, beta, mmean, mvar, act, training, decay, eps))
+    return Pending(y, mean, rstd, gamma, beta, act, training, owned=True)
+
+
+def dw3x3_bn(x, w, stride, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3):
+    """depthwise 3x3 + slim.batch_norm(+act), left Pending (owned)."""
+    xt, ipro = _in_pro(x)
+    y, mean, rstd = _DWBN.apply(xt, w, stride, ipro, (gamma, beta, mmean, mvar, act, training, decay, eps))
+    return Pending(y, mean, rstd, gamma, beta, act, training, owned=True)
+
+
+class _BNApplyOwned(torch.autograd.Function):
+    """Write act(BN(y)) (+ residual) of an owned Pending; the producer node does the BatchNorm
+    backward, so the gradient passes through to y (and to the residual) unchanged."""
+
+    @staticmethod
+    def forward(ctx, y, residual, mean, rstd, gamma, beta, act):
+        N, H, W, C = y.shape
+        out = torch.empty_like(y)
+        _abi.call("rod_bn_apply", y, mean, rstd, gamma, beta, residual, out, N * H * W, C, 0, 0, 0, act, dtcode(y),
+                  stream())
+        ctx.has_res = residual is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, (g if ctx.has_res else None), None, None, None, None, None
 
 
 # ----------------------------------------------------------------------------- levels

@@ -8,6 +8,8 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
   bn_stats             : es*M*C;  bn_apply: es*M*C*(2 + residual)
   bn_bwd               : es*M*C*3 (read dy, read x, write dx; the reduce+apply split re-reads
                          dy and x, so achieved/peak also shows that avoidable re-read)
+  bn_bwd_reduce        : es*M*C*2 (read dz, read y);  bn_bwd_apply: es*M*C*3
+  pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product
   match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
 """
 
@@ -66,6 +68,15 @@ def cost(name, a):
     if name == "rod_bn_bwd_apply":
         M, C, dt = a[8], a[9], a[11]
         return _ES[dt] * M * C * 3, 8 * M * C   # read dz, read y, write dy
+    if name == "rod_bn_bwd_reduce":
+        M, C, dt = a[10], a[11], a[13]
+        return _ES[dt] * M * C * 2, 6 * M * C   # read dz, read y
+    if name == "rod_pw_bwd":
+        M, Cin, Cout, dt = a[19], a[20], a[21], a[22]
+        es = _ES[dt]
+        want_dx = a[15] is not None
+        byts = es * (2 * M * Cout + M * Cin + (M * Cin if want_dx else 0)) + Cout * Cin * (es + 4)
+        return byts, 2 * M * Cin * Cout * (2 if want_dx else 1) + 10 * M * Cout
     if name == "rod_match_anchors":
         B, A, G = a[12], a[13], a[14]
         return B * A * 56 + A * 32 + B * G * 20, 15 * G * A * B
@@ -78,6 +89,9 @@ def cost(name, a):
 ENTRY_KERNELS = {
     "rod_bn_bwd": (("bn_bwd_apply_kernel",), ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel", "bn_bwd_apply_kernel")),
     "rod_bn_apply": (("bn_apply_kernel",), ("bn_apply_kernel",)),
+    "rod_bn_bwd_reduce": (("bn_bwd_reduce_kernel",), ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel")),
+    "rod_bn_bwd_apply": (("bn_bwd_apply_kernel",), ("bn_bwd_apply_kernel",)),
+    "rod_pw_bwd": (("pw_bwd_kernel",), ("pw_bwd_kernel",)),
     "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),

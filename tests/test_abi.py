@@ -20,7 +20,9 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().rod_abi_version() == 5
+    import re
+    want = int(re.search(r'#define ROD_ABI_VERSION (\d+)', open(_abi.HEADER_PATH).read()).group(1))
+    assert _abi.lib().rod_abi_version() == want
 
 
 def test_invalid_arguments_raise_with_message():
