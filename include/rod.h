@@ -225,6 +225,32 @@ int rod_conv_wgrad(const void* x, const float* pro_mean, const float* pro_rstd, 
                    void* workspace, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
                    int lddy, int dtype, void* stream);
 
+/* -------------------------------------- fused inverted-residual block, inference (ABI 6)
+ * out = BN_p(project(relu6(BN_d(dw3x3_s(relu6(BN_e(expand(x)))))))) (+ x when residual)
+ * — expanded_conv (ref conv_blocks.py:163-312) with eval-mode BatchNorms (mean / rstd from
+ * rod_bn_eval_stats; gamma / beta as in rod_bn_apply), in ONE kernel: the expanded tensor
+ * stays in LDS (chunks of 32 channels).  we = expand weights [inner][Cin]
+ * and wp = project weights [Cout][inner] in bf16 (rod_conv_weight_prep mode 0), wd fp32
+ * [3][3][inner].  x [N,H,W,Cin] -> out [N,ceil(H/s),ceil(W/s),Cout], bf16, TF-SAME padding.
+ * Bit-identical to the unfused chain rod_conv_fwd -> rod_dw3x3_fwd -> rod_conv_fwd ->
+ * rod_bn_apply (same roundings, same MFMA k order) where those run without split-K.
+ * rod_ir_block_supported: stride 1 with Cin, Cout <= 160; stride 2 with Cin <= 96,
+ * Cout <= 320; channels multiples of 8; residual only for stride 1 and Cin == Cout. */
+int rod_ir_block_supported(int Cin, int inner, int Cout, int stride, int residual, int dtype);
+int rod_ir_block_fwd(const void* x, const void* we, const float* e_mean, const float* e_rstd,
+                     const float* e_gamma, const float* e_beta, const float* wd, const float* d_mean,
+                     const float* d_rstd, const float* d_gamma, const float* d_beta, const void* wp,
+                     const float* p_mean, const float* p_rstd, const float* p_gamma, const float* p_beta,
+                     int residual, void* y, int N, int H, int W, int Cin, int inner, int Cout, int stride,
+                     int dtype, void* stream);
+/* Variant switch (process-wide; returns the previous value): 1 (default) runs a persistent
+ * launch — every chunk's parameters resident in LDS, each workgroup walking tiles with the
+ * next tile's input window in flight — wherever those parameters fit in LDS; 0 always runs
+ * one tile per workgroup.  Both give identical output. */
+int rod_ir_block_set_mode(int mode);
+/* 1 when the block runs the persistent variant (all of its parameters fit in LDS). */
+int rod_ir_block_persistent(int Cin, int inner, int Cout, int stride, int residual, int dtype);
+
 /* -------------------------------------- fused 1x1-conv backward through its BatchNorm (ABI 5)
  * The backward of  z = act(BN(y)), y = conv1x1(a) + bias,  a = act_x(BN_x(x)) or x, in ONE
  * pass over the rows (ref: Conv2DBackpropInput + Conv2DBackpropFilter + FusedBatchNormGrad of

@@ -9,6 +9,7 @@ and ReLU6, except the linear projection; no conv has a bias.
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 from rod import graph, ops
 from rod.params import trunc_normal
@@ -80,6 +81,11 @@ class MobilenetV2:
         P, B = self.store.params, self.store.buffers
         return P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'], B[name + '/moving_variance']
 
+    def _eval_bn(self, name):
+        """(mean, rstd, gamma, beta) of an eval-mode BatchNorm (moving statistics)."""
+        g, b, mm, mv = self._bn_args(name)
+        return (*ops.eval_stats(mm, mv, BN_EPS), g, b)
+
     def _conv_bn(self, x, w, ks, name, act, training):
         """conv + BatchNorm(+act) as one node (ops.conv2d_bn), left Pending (owned)."""
         return ops.conv2d_bn(x, w, None, ks, *self._bn_args(name), act, training, BN_DECAY, BN_EPS)
@@ -106,6 +112,13 @@ class MobilenetV2:
             if kind == 'conv':
                 x = self._conv_bn(x, P[base + '/weights'], 3, base + '/BatchNorm', ops.ROD_ACT_RELU6, is_training)
                 x = ops.materialize(x) if tapped else keep(x)
+            elif (not is_training and inner > cin and torch.is_tensor(x) and x.dtype == torch.bfloat16 and
+                  ops.ir_block_preferred(cin, inner, cout, s, res, x.dtype)):
+                # inference: the whole block in one kernel, the expanded tensor never in HBM
+                x = ops.ir_block_fwd(x, P[base + '/expand/weights'], self._eval_bn(base + '/expand/BatchNorm'),
+                                     P[base + '/depthwise/depthwise_weights'],
+                                     self._eval_bn(base + '/depthwise/BatchNorm'), P[base + '/project/weights'],
+                                     self._eval_bn(base + '/project/BatchNorm'), s, res)
             else:
                 inp = None
                 if res:

@@ -685,6 +685,55 @@ class _BNApplyOwned(torch.autograd.Function):
         return g, (g if ctx.has_res else None), None, None, None, None, None
 
 
+# ----------------------------------------------------------------------------- fused IR block (inference)
+def ir_block_supported(Cin, inner, Cout, stride, residual, dtype):
+    return "irblock" not in _DISABLE and bool(_abi.lib().rod_ir_block_supported(
+        int(Cin), int(inner), int(Cout), int(stride), int(bool(residual)), _DT[dtype]))
+
+
+def ir_block_preferred(Cin, inner, Cout, stride, residual, dtype):
+    """Whether the eval backbone should take the fused block: where it measured faster than
+    the unfused chain on MI355X (tools/irblock_bench.py, HIP-graph replay, b8 720p / 1080p;
+    DESIGN.md §N1) — the persistent variant (parameters resident in LDS) at stride 1, or at
+    stride 2 on a 16-channel input.  Elsewhere (the deep blocks' parameters do not fit in LDS,
+    the stride-2 blocks with wider inputs) the unfused chain is faster."""
+    if not ir_block_supported(Cin, inner, Cout, stride, residual, dtype):
+        return False
+    if "irblock_all" in _ENABLE:
+        return True
+    pers = bool(_abi.lib().rod_ir_block_persistent(int(Cin), int(inner), int(Cout), int(stride),
+                                                      int(bool(residual)), _DT[dtype]))
+    return pers and (stride == 1 or Cin <= 16)
+
+
+def ir_block_set_mode(mode):
+    """rod_ir_block_set_mode: 1 = persistent resident-parameter launch where it fits (default),
+    0 = one tile per workgroup.  Returns the previous mode."""
+    return int(_abi.lib().rod_ir_block_set_mode(int(mode)))
+
+
+def eval_stats(mmean, mvar, eps):
+    C = mmean.numel()
+    mean = torch.empty(C, dtype=torch.float32, device=mmean.device)
+    rstd = torch.empty(C, dtype=torch.float32, device=mmean.device)
+    _abi.call("rod_bn_eval_stats", mmean, mvar, eps, mean, rstd, C, stream())
+    return mean, rstd
+
+
+def ir_block_fwd(x, we, bn_e, wd, bn_d, wp, bn_p, stride, residual):
+    """rod_ir_block_fwd: expand -> BN+ReLU6 -> dw3x3 -> BN+ReLU6 -> project -> BN (+ x), one
+    launch (inference).  we / wp: fp32 master weights [inner,1,1,Cin] / [Cout,1,1,inner];
+    bn_*: (mean, rstd, gamma, beta) eval statistics."""
+    N, H, W, Cin = x.shape
+    inner, Cout = we.shape[0], wp.shape[0]
+    wet = _prep(we, 0, x.dtype, inner, Cin, 1)
+    wpt = _prep(wp, 0, x.dtype, Cout, inner, 1)
+    y = torch.empty((N, -(-H // stride), -(-W // stride), Cout), dtype=x.dtype, device=x.device)
+    _abi.call("rod_ir_block_fwd", x.contiguous(), wet, *bn_e, wd, *bn_d, wpt, *bn_p, int(bool(residual)), y, N, H, W,
+              Cin, inner, Cout, int(stride), dtcode(x), stream())
+    return y
+
+
 # ----------------------------------------------------------------------------- levels
 class _LevelsConcat(torch.autograd.Function):
     """[B, fh, fw, A*k] per level -> [B, sum(fh*fw*A), k] (tf.concat of reshaped levels)."""

@@ -43,3 +43,20 @@ def test_workspace_queries_are_host_only():
     assert _abi.query('rod_bn_stats_workspace', 1000, 64) > 0
     assert _abi.query('rod_conv_wgrad_workspace', 2, 16, 16, 32, 64, 3) >= 4 * 64 * 9 * 32
     assert _abi.query('rod_dw3x3_bwd_filter_workspace', 2, 8, 8, 96) >= 4 * 9 * 96
+
+
+def test_ir_block_policy_is_host_only():
+    """The fused-block support / persistent-variant queries run on the host, and the eval
+    backbone's preference picks the blocks measured faster fused."""
+    import torch
+
+    from nets.backbone.mobilenet_v2 import layer_plan
+    from rod import ops
+    bf16 = torch.bfloat16
+    picked = [idx for (idx, kind, s, cin, inner, cout, res, sc) in layer_plan()
+              if kind == 'ir' and inner > cin and ops.ir_block_preferred(cin, inner, cout, s, res, bf16)]
+    assert picked == [3, 4, 6, 7], picked
+    assert ops.ir_block_supported(64, 384, 64, 1, True, bf16)
+    assert not _abi.lib().rod_ir_block_persistent(64, 384, 64, 1, 1, 1)    # parameters exceed LDS
+    assert _abi.lib().rod_ir_block_persistent(32, 192, 32, 1, 1, 1)
+    assert not ops.ir_block_preferred(24, 144, 24, 1, True, torch.float32)

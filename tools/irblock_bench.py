@@ -1,0 +1,114 @@
+"""Time the fused inference inverted-residual block (rod_ir_block_fwd) against the unfused
+librod eval chain on the backbone's blocks at 1280x720 and 1920x1080 (bf16, batch 8), with
+the fused launch's HBM GB/s (input + output + weights) and MFMA TFLOP/s (expand incl. halo
+recompute + project; depthwise on VALU not counted).
+Usage: python tools/irblock_bench.py [--iters 20] [--res 720 1080] [--json out.json]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'road-object-detection-for-bdd100k_amd'))
+import torch  # noqa: E402
+
+from rod import ops  # noqa: E402
+
+bf16 = torch.bfloat16
+
+
+def blocks(H, W):
+    from nets.backbone.mobilenet_v2 import layer_plan
+    out, h, w = [], H, W
+    for (idx, kind, s, cin, inner, cout, res, sc) in layer_plan():
+        if kind == 'ir' and inner > cin and ops.ir_block_supported(cin, inner, cout, s, res, bf16):
+            out.append((idx, cin, inner, cout, s, res, h, w))
+        h, w = -(-h // s), -(-w // s)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--res', type=int, nargs='+', default=[720, 1080])
+    ap.add_argument('--json', default=None)
+    a = ap.parse_args()
+    dev = torch.device('cuda')
+    allrows = {}
+    for R in a.res:
+        H, W = (720, 1280) if R == 720 else (1080, 1920)
+        rows = []
+        for (idx, cin, inner, cout, s, res, h, w) in blocks(H, W):
+            N = a.batch
+            x = torch.randn(N, h, w, cin, device=dev).to(bf16)
+            we = torch.randn(inner, 1, 1, cin, device=dev) * 0.2
+            wd = torch.randn(3, 3, inner, device=dev) * 0.3
+            wp = torch.randn(cout, 1, 1, inner, device=dev) * 0.1
+            ones = lambda c: torch.ones(c, device=dev)
+            zeros = lambda c: torch.zeros(c, device=dev)
+            ev = [(zeros(c), ones(c), ones(c), zeros(c)) for c in (inner, inner, cout)]
+
+            def fused():
+                ops.ir_block_fwd(x, we, ev[0], wd, ev[1], wp, ev[2], s, res)
+
+            def fused_tile():   # the mode is read at launch: fixed while capturing
+                old = ops.ir_block_set_mode(0)
+                ops.ir_block_fwd(x, we, ev[0], wd, ev[1], wp, ev[2], s, res)
+                ops.ir_block_set_mode(old)
+
+            def unfused():
+                pe = ops.conv2d_bn(x, we, None, 1, ones(inner), zeros(inner), zeros(inner), ones(inner),
+                                   ops.ROD_ACT_RELU6, False, 0.997, 1e-3)
+                pd = ops.dw3x3_bn(pe, wd, s, ones(inner), zeros(inner), zeros(inner), ones(inner), ops.ROD_ACT_RELU6,
+                                  False, 0.997, 1e-3)
+                pp = ops.conv2d_bn(pd, wp, None, 1, ones(cout), zeros(cout), zeros(cout), ones(cout),
+                                   ops.ROD_ACT_NONE, False, 0.997, 1e-3)
+                ops.materialize(pp, x if res else None)
+            t = {}
+            with torch.no_grad():
+                for name, fn in (('fused', fused), ('fused_tile', fused_tile), ('unfused', unfused)):
+                    # replayed as a HIP graph: GPU time, not the Python dispatch of the unfused chain
+                    for _ in range(3):
+                        fn()
+                    torch.cuda.synchronize()
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph):
+                        for _ in range(a.iters):
+                            fn()
+                    graph.replay()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    e0.record()
+                    graph.replay()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    t[name] = e0.elapsed_time(e1) / a.iters * 1e3
+                    del graph
+            ho, wo = -(-h // s), -(-w // s)
+            byts = 2 * (N * h * w * cin + N * ho * wo * cout) + 2 * inner * (cin + cout) + 36 * inner
+            tw, th = (16, 8) if s == 1 else (8, 8)
+            iw, ih = (tw + 2, th + 2) if s == 1 else (2 * tw + 1, 2 * th + 1)
+            ntile = N * -(-ho // th) * -(-wo // tw)
+            flops = 2.0 * ntile * (ih * iw * cin * inner + th * tw * inner * cout)
+            alg_flops = 2.0 * N * (h * w * cin * inner + ho * wo * inner * cout) + 18.0 * N * ho * wo * inner
+            r = {'layer': idx, 'shape': [N, h, w, cin, inner, cout, s, int(res)],
+                 'fused_us': round(t['fused'], 1), 'tile_us': round(t['fused_tile'], 1),
+                 'unfused_us': round(t['unfused'], 1),
+                 'speedup': round(t['unfused'] / t['fused'], 2),
+                 'fused_GBps': round(byts / t['fused'] / 1e3, 1),
+                 'fused_mfma_TFLOPs': round(flops / t['fused'] / 1e6, 1),
+                 'alg_TFLOPs': round(alg_flops / t['fused'] / 1e6, 1)}
+            rows.append(r)
+            print(R, json.dumps(r), flush=True)
+        tot = {'fused_us': round(sum(r['fused_us'] for r in rows), 1),
+               'tile_us': round(sum(r['tile_us'] for r in rows), 1),
+               'unfused_us': round(sum(r['unfused_us'] for r in rows), 1)}
+        print(R, 'total', json.dumps(tot), flush=True)
+        allrows[R] = {'blocks': rows, 'total': tot}
+    if a.json:
+        json.dump(allrows, open(a.json, 'w'), indent=1)
+
+
+if __name__ == '__main__':
+    main()
