@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 6
+#define ROD_ABI_VERSION 7
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -392,10 +392,15 @@ int rod_hnm_loss(const void* logits, const int* det_lbl, const int* det_pos, con
  * (p >= select_threshold), top_k sort (score desc, ties by index), greedy NMS (IoU >
  * nms_threshold, tf.image.non_max_suppression semantics), zero-pad to keep_top_k.
  * probs fp32 [B,A,K]; boxes fp32 corner [B,A,4];
- * out_scores [B,K-1,keep_top_k], out_boxes [B,K-1,keep_top_k,4]; top_k, keep_top_k <= 1024. */
+ * out_scores [B,K-1,keep_top_k], out_boxes [B,K-1,keep_top_k,4]; top_k, keep_top_k <= 1024.
+ * workspace (ABI 7; rod_select_topk_nms_workspace bytes, may be NULL): with it and
+ * select_threshold > 0 (K - 1 <= 32) probs is read ONCE, row-wise, and every class's selected
+ * scores are compacted into per-(image, class) candidate lists that are sorted / radix-selected
+ * on their own; otherwise each (image, class) reads its probs column directly.  Same output. */
+size_t rod_select_topk_nms_workspace(int B, int A, int K);
 int rod_select_topk_nms(const float* probs, const float* boxes, int B, int A, int K,
                         float select_threshold, int top_k, int keep_top_k, float nms_threshold,
-                        float* out_scores, float* out_boxes, void* stream);
+                        float* out_scores, float* out_boxes, void* workspace, void* stream);
 
 /* ------------------------------------------------ optimiser (A14)
  * Plain SGD with clip by value (net_tools.py:645-651):

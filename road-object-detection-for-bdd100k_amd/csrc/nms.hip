@@ -8,9 +8,19 @@
 //            min/max-normalised corners, 0 if either area <= 0 (bboxes.py:182)
 //   pad      zero-pad the kept scores/boxes to keep_top_k (tensors.py:59-86)
 //
-// The top_k threshold is an exact in-workgroup 4 x 8-bit radix select on the (non-negative)
-// f32 score bits; candidates are compacted in index order (ties resolved by index), then
-// bitonic-sorted by (score desc, index asc) in LDS.  Compiled with -ffp-contract=off.
+// Two implementations with identical output:
+//  * compacted (select_threshold > 0, workspace given — the CLIs' 0.1 / 0.3): ONE row-wise,
+//    coalesced pass over probs appends every selected (nonzero) score of every class as a
+//    64-bit key (~score bits, anchor index) to a per-(image, class) list
+//    (nms_compact_kernel); then one workgroup per (image, class) sorts its list in LDS (or,
+//    past 4096 candidates, radix-selects the top_k-th key over the list first) and runs the
+//    greedy NMS (nms_select_kernel).  The entries top_k would take beyond the selected ones
+//    have score 0 and a zeroed box (p < threshold): zero area, they suppress nothing and are
+//    output as the zero padding — so they need not be materialised.
+//  * direct (any threshold): per (image, class) an exact in-workgroup 4 x 8-bit radix select
+//    on the (non-negative) f32 score bits read column-wise from probs; candidates compacted in
+//    index order (ties resolved by index), then bitonic-sorted by (score desc, index asc).
+// Compiled with -ffp-contract=off.
 #include <math.h>
 
 #include "rod_common.h"
@@ -207,21 +217,219 @@ __global__ void __launch_bounds__(NMS_T) select_topk_nms_kernel(const float* __r
   }
 }
 
+
+// ----------------------------------------------------------------- compacted implementation
+constexpr int NMS_CT = 2048;     // anchors per compaction workgroup (8 per thread)
+constexpr int NMS_SORT = 4096;   // candidate lists up to this size are sorted whole in LDS
+constexpr int NMS_MAXC = 32;     // classes per launch (K - 1)
+
+__global__ void nms_zero_kernel(unsigned* p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
+
+__global__ void __launch_bounds__(256) nms_compact_kernel(const float* __restrict__ probs, int A, int K,
+                                                          float sel_thr, unsigned* __restrict__ counts,
+                                                          unsigned long long* __restrict__ keys) {
+  __shared__ unsigned lcnt[NMS_MAXC], lbase[NMS_MAXC];
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int C = K - 1;
+  const long base = (long)b * A;
+  const int a0 = blockIdx.x * NMS_CT;
+  const unsigned long long lower = lane ? (~0ull >> (64 - lane)) : 0ull;
+  if (tid < C) lcnt[tid] = 0u;
+  __syncthreads();
+  // pass 1: candidates per class in this tile
+  for (int u = 0; u < NMS_CT / 256; ++u) {
+    const int a = a0 + u * 256 + tid;
+    for (int c = 1; c <= C; ++c) {
+      const bool cand = a < A && __float_as_uint(sel_score(probs, base + a, K, c, sel_thr)) != 0u;
+      const unsigned long long m = __ballot(cand);
+      if (lane == 0 && m) atomicAdd(&lcnt[c - 1], (unsigned)__popcll(m));
+    }
+  }
+  __syncthreads();
+  if (tid < C) {
+    lbase[tid] = lcnt[tid] ? atomicAdd(&counts[b * C + tid], lcnt[tid]) : 0u;
+    lcnt[tid] = 0u;
+  }
+  __syncthreads();
+  // pass 2 (rows now in L1/L2): append keys; list order is irrelevant (sorted later)
+  for (int u = 0; u < NMS_CT / 256; ++u) {
+    const int a = a0 + u * 256 + tid;
+    for (int c = 1; c <= C; ++c) {
+      const unsigned bits = a < A ? __float_as_uint(sel_score(probs, base + a, K, c, sel_thr)) : 0u;
+      const bool cand = bits != 0u;
+      const unsigned long long m = __ballot(cand);
+      if (!m) continue;
+      unsigned off = 0;
+      if (lane == 0) off = atomicAdd(&lcnt[c - 1], (unsigned)__popcll(m));
+      off = __shfl(off, 0);
+      if (cand)
+        keys[((long)b * C + (c - 1)) * A + lbase[c - 1] + off + __popcll(m & lower)] =
+            ((unsigned long long)(~bits) << 32) | (unsigned)a;
+    }
+  }
+}
+
+// bitonic sort (ascending) of key[0..P), P a power of two <= NMS_SORT, 1024 threads
+__device__ void lds_bitonic(unsigned long long* key, int P) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < P; i += NMS_T) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const unsigned long long ki = key[i], kj = key[j];
+          if ((ki > kj) == up) {
+            key[i] = kj;
+            key[j] = ki;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NMS_T) nms_select_kernel(const float* __restrict__ probs,
+                                                           const float* __restrict__ boxes, int A, int K,
+                                                           float sel_thr, int top_k, int keep_k, float nms_thr,
+                                                           const unsigned* __restrict__ counts,
+                                                           const unsigned long long* __restrict__ keys,
+                                                           float* __restrict__ out_scores,
+                                                           float* __restrict__ out_boxes) {
+  __shared__ unsigned long long key[NMS_SORT];
+  __shared__ unsigned hist[256];
+  __shared__ unsigned long long sh64[2];
+  __shared__ unsigned shn[1];
+  __shared__ float bx[NMS_T][4];
+  __shared__ float sc[NMS_T];
+  __shared__ unsigned char dead[NMS_T];
+  __shared__ int kept_idx[NMS_T];
+
+  const int b = blockIdx.y, c = blockIdx.x + 1, C = K - 1, tid = threadIdx.x;
+  const long base = (long)b * A;
+  const int k = min(top_k, A);
+  const int n = (int)counts[b * C + c - 1];
+  const unsigned long long* list = keys + ((long)b * C + (c - 1)) * A;
+  int m;
+  if (n <= NMS_SORT) {
+    int P = 64;
+    while (P < n) P <<= 1;
+    for (int i = tid; i < P; i += NMS_T) key[i] = i < n ? list[i] : ~0ull;
+    __syncthreads();
+    lds_bitonic(key, P);
+    m = min(n, k);
+  } else {
+    // k-th smallest key (keys are distinct: the index is part of the key), 8 x 8-bit digits
+    unsigned long long prefix = 0;
+    unsigned rank = (unsigned)k;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      const unsigned long long hmask = shift >= 56 ? 0ull : (~0ull << (shift + 8));
+      for (int i = tid; i < 256; i += NMS_T) hist[i] = 0u;
+      __syncthreads();
+      for (int i = tid; i < n; i += NMS_T) {
+        const unsigned long long v = list[i];
+        if ((v & hmask) == (prefix & hmask)) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        unsigned acc = 0;
+        int d = 0;
+        for (; d < 256; ++d) {
+          if (acc + hist[d] >= rank) break;
+          acc += hist[d];
+        }
+        sh64[0] = prefix | ((unsigned long long)d << shift);
+        sh64[1] = rank - acc;
+      }
+      __syncthreads();
+      prefix = sh64[0];
+      rank = (unsigned)sh64[1];
+      __syncthreads();
+    }
+    // the k keys <= the k-th, in any order, then sorted
+    if (tid == 0) shn[0] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += NMS_T) {
+      const unsigned long long v = list[i];
+      if (v <= prefix) key[atomicAdd(&shn[0], 1u)] = v;
+    }
+    __syncthreads();
+    int P = 64;
+    while (P < k) P <<= 1;
+    for (int i = k + tid; i < P; i += NMS_T) key[i] = ~0ull;
+    __syncthreads();
+    lds_bitonic(key, P);
+    m = k;
+  }
+  // gather the m candidates (score desc, index asc), boxes masked as the reference
+  if (tid < m) {
+    const int a = (int)(key[tid] & 0xFFFFFFFFu);
+    const float p = probs[(base + a) * K + c];
+    const float fm = p >= sel_thr ? 1.f : 0.f;
+    sc[tid] = p * fm;
+    const float* bp = boxes + (base + a) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bx[tid][q] = bp[q] * fm;
+    dead[tid] = 0;
+  }
+  __syncthreads();
+  int kept = 0;
+  for (int i = 0; i < m && kept < keep_k; ++i) {
+    if (dead[i]) continue;  // uniform: dead[] only changes between barriers
+    if (tid == 0) kept_idx[kept] = i;
+    ++kept;
+    for (int j = i + 1 + tid; j < m; j += NMS_T)
+      if (!dead[j] && tf_iou(bx[i], bx[j]) > nms_thr) dead[j] = 1;
+    __syncthreads();
+  }
+  __syncthreads();
+  float* os = out_scores + ((long)b * C + (c - 1)) * keep_k;
+  float* ob = out_boxes + ((long)b * C + (c - 1)) * keep_k * 4;
+  for (int j = tid; j < keep_k; j += NMS_T) {
+    const bool kk = j < kept;
+    const int i = kk ? kept_idx[j] : 0;
+    os[j] = kk ? sc[i] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ob[j * 4 + q] = kk ? bx[i][q] : 0.f;
+  }
+}
+
+static size_t nms_counts_bytes(int B, int K) { return ((size_t)B * (K - 1) * sizeof(unsigned) + 255) / 256 * 256; }
+
 }  // namespace rod
 
 using namespace rod;
 
 extern "C" {
 
+size_t rod_select_topk_nms_workspace(int B, int A, int K) {
+  if (B <= 0 || A <= 0 || K < 2) return 0;
+  return nms_counts_bytes(B, K) + (size_t)B * (K - 1) * A * sizeof(unsigned long long);
+}
+
 int rod_select_topk_nms(const float* probs, const float* boxes, int B, int A, int K, float select_threshold,
                         int top_k, int keep_top_k, float nms_threshold, float* out_scores, float* out_boxes,
-                        void* stream) {
+                        void* workspace, void* stream) {
   ROD_CHECK_ARG(B > 0 && A > 0 && K > 1, "rod_select_topk_nms: bad shape");
   ROD_CHECK_ARG(top_k > 0 && top_k <= NMS_T, "rod_select_topk_nms: top_k must be in [1, %d]", NMS_T);
   ROD_CHECK_ARG(keep_top_k > 0 && keep_top_k <= NMS_T, "rod_select_topk_nms: keep_top_k must be in [1, %d]", NMS_T);
   ROD_CHECK_ARG(B <= 65535, "rod_select_topk_nms: B too large");
-  hipLaunchKernelGGL(select_topk_nms_kernel, dim3(K - 1, B), dim3(NMS_T), 0, ROD_STREAM(stream), probs, boxes, A, K,
-                     select_threshold, top_k, keep_top_k, nms_threshold, out_scores, out_boxes);
+  hipStream_t s = ROD_STREAM(stream);
+  if (workspace && select_threshold > 0.f && K - 1 <= NMS_MAXC) {
+    unsigned* counts = (unsigned*)workspace;
+    unsigned long long* keys = (unsigned long long*)((char*)workspace + nms_counts_bytes(B, K));
+    hipLaunchKernelGGL(nms_zero_kernel, dim3(cdiv((long)B * (K - 1), 256)), dim3(256), 0, s, counts, B * (K - 1));
+    hipLaunchKernelGGL(nms_compact_kernel, dim3(cdiv(A, NMS_CT), B), dim3(256), 0, s, probs, A, K, select_threshold,
+                       counts, keys);
+    hipLaunchKernelGGL(nms_select_kernel, dim3(K - 1, B), dim3(NMS_T), 0, s, probs, boxes, A, K, select_threshold,
+                       top_k, keep_top_k, nms_threshold, counts, keys, out_scores, out_boxes);
+  } else {
+    hipLaunchKernelGGL(select_topk_nms_kernel, dim3(K - 1, B), dim3(NMS_T), 0, s, probs, boxes, A, K,
+                       select_threshold, top_k, keep_top_k, nms_threshold, out_scores, out_boxes);
+  }
   return check_launch("rod_select_topk_nms");
 }
 

@@ -73,11 +73,15 @@ class Predictor(object):
         self.last = None
         self.kw = dict(select_threshold=select_threshold, nms_threshold=nms_threshold, top_k=top_k,
                        keep_top_k=keep_top_k)
+        # the whole forward + decode + NMS is captured once per input shape as a HIP graph and
+        # replayed (no per-kernel host dispatch); re-captured when the parameters change
+        self.use_graph = device.type == 'cuda' and os.environ.get('ROD_PREDICT_GRAPH', '1') != '0'
+        self._graph = None
 
-    @torch.no_grad()
-    def __call__(self, img_u8):
+    def _forward(self, img_u8):
         from nets.catch_net import factory
         from utils import net_tools
+        from rod import ops
         from rod.dataio import network_input
         x = network_input(img_u8, self.dtype)
         refine_out, det_out, clf_out = factory(x, 'mobilenet_v2', False, self.config_dict, self.dtype,
@@ -85,10 +89,34 @@ class Predictor(object):
         probs = net_tools.class_probabilities(clf_out)                                     # predict.py:127-128
         boxes = net_tools.decode_all_layers(self.anchors, refine_out, det_out, to_corner=True)  # 130-134
         if self.keep_intermediates:
-            from rod import ops
             self.last = (ops.levels_concat(clf_out, config.total_obj_n), probs, boxes,
                          ops.levels_concat(refine_out, 4), ops.levels_concat(det_out, 4))
-        return net_tools.detected_bboxes(probs, boxes, **self.kw)                          # 136-137
+        kw = self.kw                                                                        # 136-137
+        thr = 0.0 if kw['select_threshold'] is None else kw['select_threshold']
+        return ops.select_topk_nms(probs, boxes, thr, kw['top_k'], kw['keep_top_k'], kw['nms_threshold'])
+
+    @torch.no_grad()
+    def __call__(self, img_u8):
+        """detected_bboxes of the batch: ({c: scores [B, keep_top_k]}, {c: boxes [B, keep_top_k, 4]})."""
+        if not self.use_graph or self.keep_intermediates:
+            scores, boxes = self._forward(img_u8)
+        else:
+            key = (tuple(img_u8.shape), img_u8.dtype, self.net.store.version)
+            if self._graph is None or self._graph[0] != key:
+                self._graph = None
+                static_in = img_u8.clone()
+                self._forward(static_in)          # first run: weight layouts, anchor table, workspaces
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    out = self._forward(static_in)
+                self._graph = (key, g, static_in, out)
+            _, g, static_in, out = self._graph
+            static_in.copy_(img_u8)
+            g.replay()
+            scores, boxes = out[0].clone(), out[1].clone()
+        K = scores.shape[1] + 1
+        return ({c: scores[:, c - 1] for c in range(1, K)}, {c: boxes[:, c - 1] for c in range(1, K)})
 
 
 def main(argv=None):

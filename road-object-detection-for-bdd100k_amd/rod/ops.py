@@ -1126,11 +1126,14 @@ def softmax_ce_hnm_dp(logits, det_lbl, det_pos, iou, lvl_off, bs, B_global, allr
     return _SoftmaxCEHNMDP.apply(logits, det_lbl, det_pos, iou, lvl_off, bs, B_global, allreduce)
 
 
-def select_topk_nms(probs, boxes, select_threshold, top_k, keep_top_k, nms_threshold):
+def select_topk_nms(probs, boxes, select_threshold, top_k, keep_top_k, nms_threshold, compact=True):
+    """rod_select_topk_nms.  compact: pass the candidate-list workspace (one row-wise pass over
+    probs; used when select_threshold > 0) — False forces the direct column-wise kernel."""
     B, A, K = probs.shape
     dev = probs.device
     scores = torch.empty((B, K - 1, keep_top_k), dtype=torch.float32, device=dev)
     bxs = torch.empty((B, K - 1, keep_top_k, 4), dtype=torch.float32, device=dev)
+    ws = workspace(_abi.query("rod_select_topk_nms_workspace", B, A, K), dev) if compact else None
     _abi.call("rod_select_topk_nms", probs.contiguous(), boxes.contiguous(), B, A, K, float(select_threshold),
-              int(top_k), int(keep_top_k), float(nms_threshold), scores, bxs, stream())
+              int(top_k), int(keep_top_k), float(nms_threshold), scores, bxs, ws, stream())
     return scores, bxs

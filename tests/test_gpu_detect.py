@@ -220,7 +220,41 @@ def test_select_topk_nms_bit_exact(dev, sel, nms, top_k, keep):
     off = rng.normal(0, 0.2, (B, A, 4)).astype(f32)
     boxes = op.decode_corner(tab.center_np, off)
     s_ref, b_ref, kept = op.detected_bboxes(probs_ref, boxes, sel, nms, top_k, keep)
-    sd, bd = ops.select_topk_nms(pd, torch.from_numpy(boxes).to(dev), sel, top_k, keep, nms)
+    for compact in (True, False):   # candidate-list and direct implementations
+        sd, bd = ops.select_topk_nms(pd, torch.from_numpy(boxes).to(dev), sel, top_k, keep, nms, compact=compact)
+        np.testing.assert_array_equal(sd.cpu().numpy(), s_ref)
+        np.testing.assert_array_equal(bd.cpu().numpy(), b_ref)
+    assert sum(len(v) for v in kept.values()) > 0
+
+
+@pytest.mark.parametrize('case', ['many', 'ties', 'few', 'none'])
+def test_select_topk_nms_candidate_lists(dev, case):
+    """The candidate-list NMS (radix-select path past 4096 candidates per class, tied
+    scores, fewer candidates than top_k, no candidate at all) against the oracle."""
+    rng, anchors, tab, A = _setup(300, 300, 2, 5)
+    B, K = 2, 11
+    if case == 'many':      # most scores pass 0.1 in classes 1-2: lists far over 4096
+        logits = rng.normal(0, 0.3, (B, A, K)).astype(f32)
+        logits[..., 1:3] += 2.0
+    elif case == 'ties':    # quantised logits: massive exact ties in score
+        logits = np.round(rng.normal(0, 1.5, (B, A, K))).astype(f32)
+    elif case == 'few':
+        logits = rng.normal(0, 1.0, (B, A, K)).astype(f32)
+        logits[..., 0] += 4.0
+    else:
+        logits = np.zeros((B, A, K), f32)
+        logits[..., 0] = 10.0
+    e, s, _ = op.softmax_rows(logits)
+    probs_ref = (e / s).astype(f32)
+    pd = ops.softmax(torch.from_numpy(logits).to(dev), K)
+    off = rng.normal(0, 0.2, (B, A, 4)).astype(f32)
+    boxes = op.decode_corner(tab.center_np, off)
+    s_ref, b_ref, kept = op.detected_bboxes(probs_ref, boxes, 0.1, 0.4, 400, 200)
+    sd, bd = ops.select_topk_nms(pd, torch.from_numpy(boxes).to(dev), 0.1, 400, 200, 0.4)
     np.testing.assert_array_equal(sd.cpu().numpy(), s_ref)
     np.testing.assert_array_equal(bd.cpu().numpy(), b_ref)
-    assert sum(len(v) for v in kept.values()) > 0
+    n_sel = int((probs_ref[..., 1:] >= 0.1).sum(1).max())
+    if case == 'many':
+        assert n_sel > 4096
+    if case == 'none':
+        assert n_sel == 0 and not sd.any()

@@ -251,6 +251,14 @@ def test_predict_b32_nms_bit_exact(dev):
     n_kept = sum(len(v) for v in kept.values())
     print('kept detections over 32 images x 10 classes:', n_kept)
     assert n_kept > 320 and max(len(v) for v in kept.values()) > 20
+    # the HIP-graph replay (the default predict path) gives the same detections, twice
+    pr.keep_intermediates = False
+    assert pr.use_graph
+    for _ in range(2):
+        sg, bg = pr(img)
+        for c in range(1, 11):
+            assert torch.equal(sg[c], scores[c]) and torch.equal(bg[c], bboxes[c])
+    assert pr._graph is not None
 
 
 # ------------------------------------------------------------------------------- (d)
