@@ -45,6 +45,8 @@ def parse():
                          '(process_raw_data_train: random crop / resize / flip / colour, fused normalisation)')
     ap.add_argument('--no-fix-refine', dest='fix_refine', action='store_false', default=True,
                     help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
+    ap.add_argument('--sync-bn', dest='sync_bn', action='store_true', default=False,
+                    help='N>1: BatchNorm statistics over the global batch (rod.ddp.SyncBatchNorm; default per rank)')
     ap.add_argument('--probe', default='rod_bn_bwd_reduce,rod_bn_bwd_apply',
                     help='C-ABI entry (or comma list, aggregated as one kernel family) reported in "roofline": '
                          'default the BatchNorm backward (reduce + apply), the family VERDICT r1 names')
@@ -197,7 +199,7 @@ def main():
         from rod.ddp import GradReducer
         reducer = GradReducer(world)  # bucketed RCCL all-reduce, launched during backward
     tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
-                 world_size=world, reducer=reducer, fix_refine=args.fix_refine)
+                 world_size=world, reducer=reducer, fix_refine=args.fix_refine, sync_bn=args.sync_bn)
     batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED + rank)
     source = None
     if args.augment:
@@ -294,7 +296,8 @@ def main():
                        'global_batch': args.batch * world, 'img_hw': [args.height, args.width],
                        'train_range': args.train_range, 'parallelism': f'dp{world}',
                        'augment': bool(args.augment),
-                       **({'dist_backend': 'rccl' if backend == 'nccl' else backend} if world > 1 else {}),
+                       **({'dist_backend': 'rccl' if backend == 'nccl' else backend,
+                           'batchnorm': 'sync (global batch)' if args.sync_bn else 'per rank'} if world > 1 else {}),
                        **({} if args.train_range == 'REFINE' else {'fix_refine': args.fix_refine})},
             'loss': round(loss_val, 5),
             'roofline': rl,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 7
+#define ROD_ABI_VERSION 8
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -138,6 +138,12 @@ size_t rod_bn_finalize_workspace(int nparts, int C);
 int rod_bn_finalize(const float* parts, int nparts, long M, int C, float eps, float decay,
                     float* mean, float* rstd, float* moving_mean, float* moving_var,
                     void* workspace, void* stream);
+/* Partial statistics of x[M, C] (dense rows) as exactly nparts chunks of ceil(M/nparts) rows,
+ * parts [nparts][3][C] in the rod_bn_finalize format (ABI 8).  For a BatchNorm whose
+ * statistics span more rows than this process holds: data-parallel ranks all-gather their
+ * parts and each merges the same array (SyncBN; the reference normalises over its whole
+ * single-device batch, mobilenet.py:417-420). */
+int rod_bn_stat_parts(const void* x, long M, int C, float* parts, int nparts, int dtype, void* stream);
 /* inference: mean = moving_mean, rstd = 1/sqrt(moving_var + eps). */
 int rod_bn_eval_stats(const float* moving_mean, const float* moving_var, float eps,
                       float* mean, float* rstd, int C, void* stream);
@@ -178,6 +184,12 @@ int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const flo
 int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const float* rstd,
                       const float* gamma, const float* beta, float* dgamma, float* dbeta, float* coef,
                       void* workspace, long M, int C, int act, int dtype, void* stream);
+/* The backward partial sums alone (ABI 8): parts [nparts][2][C] = (sum g, sum g*yhat) over
+ * exactly nparts chunks of ceil(M/nparts) rows, for rod_bn_bwd_finalize — after an
+ * all-gather over data-parallel ranks under SyncBN (FusedBatchNormGrad over the global batch). */
+int rod_bn_bwd_parts(const void* dz, const void* y, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, int act, float* parts, int nparts, long M, int C,
+                     int dtype, void* stream);
 
 /* -------------------------------------- dense conv as implicit GEMM (A2 A3 A5)
  * y[m, co] = sum_k A[m, k] * wt[co, k] (+ bias[co]), fp32 accumulation,

@@ -176,7 +176,9 @@ def conv_transpose_2x2(x, w, out_hw):
     return y[:, :, :out_hw[0], :out_hw[1]]
 
 
-def deconv_bone(feats, P, B, training, moving=None):
+def deconv_bone(feats, P, B, training, moving=None, learn_all=False):
+    """catch_net.py:160-230: LEARN_HALF (transpose conv to C/2 ++ 1x1 conv of the bilinear
+    resize) or LEARN_ALL (transpose conv to C), each followed by BN(beta) + leaky."""
     layers = list(reversed(feats))
     out = []
     x = layers[0]
@@ -184,6 +186,9 @@ def deconv_bone(feats, P, B, training, moving=None):
         base = 'deconv/block_%d' % (i + 1)
         if i == 0:
             x = conv(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'])
+        elif learn_all:
+            h, w = layers[i].shape[2], layers[i].shape[3]
+            x = conv_transpose_2x2(x, P[base + '/weight_%d' % i], (h, w))
         else:
             h, w = layers[i].shape[2], layers[i].shape[3]
             up = conv_transpose_2x2(x, P[base + '/weight_%d' % i], (h, w))
@@ -196,16 +201,20 @@ def deconv_bone(feats, P, B, training, moving=None):
     return out
 
 
-def forward(img_nhwc, P, B, training, all_mode=False, moving=None):
-    """Full network on an NHWC fp32 input; returns refine_out (and det_out, clf_out)."""
+def forward(img_nhwc, P, B, training, all_mode=False, moving=None, learn_all=False, concat=False):
+    """Full network on an NHWC fp32 input; returns refine_out (and det_out, clf_out).
+    learn_all: deconv_method LEARN_ALL; concat: merge_method CONCAT (catch_net.py:237-273)."""
     x = img_nhwc.permute(0, 3, 1, 2)
     ep = backbone(x, P, B, training, moving)
     feats = [ep['layer_%d' % t] for t in TAPS]
     refine = head(feats, P, B, 'refine', 4, training, moving)
     if not all_mode:
         return refine
-    dec = deconv_bone(feats, P, B, training, moving)
-    merged = [u + d for u, d in zip(feats, reversed(dec))]
+    dec = deconv_bone(feats, P, B, training, moving, learn_all)
+    if concat:
+        merged = [torch.cat([u, d], 1) for u, d in zip(feats, reversed(dec))]
+    else:
+        merged = [u + d for u, d in zip(feats, reversed(dec))]
     clf = head(merged, P, B, 'clf', 11, training, moving)
     det = head(merged, P, B, 'det', 4, training, moving)
     return refine, det, clf

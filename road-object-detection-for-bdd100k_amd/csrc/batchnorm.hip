@@ -705,6 +705,31 @@ int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const flo
   return check_launch("rod_bn_bwd_apply");
 }
 
+// Partial statistics only (ABI 8), for a BatchNorm whose statistics are merged over more
+// rows than this process holds (SyncBN over data-parallel ranks).
+int rod_bn_stat_parts(const void* x, long M, int C, float* parts, int nparts, int dtype, void* stream) {
+  ROD_CHECK_ARG(x != nullptr && parts != nullptr && M > 0 && C > 0 && nparts > 0 && nparts <= M,
+                "rod_bn_stat_parts: bad arguments M=%ld C=%d nparts=%d", M, C, nparts);
+  stat_parts(dtype, x, M, C, C, parts, nparts, ROD_STREAM(stream));
+  return check_launch("rod_bn_stat_parts");
+}
+
+int rod_bn_bwd_parts(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                     const float* beta, int act, float* parts, int nparts, long M, int C, int dtype, void* stream) {
+  ROD_CHECK_ARG(dz != nullptr && y != nullptr && mean != nullptr && rstd != nullptr && parts != nullptr && M > 0 &&
+                    C > 0 && nparts > 0 && nparts <= M,
+                "rod_bn_bwd_parts: bad arguments M=%ld C=%d nparts=%d", M, C, nparts);
+  ROD_CHECK_ARG(act >= ROD_ACT_NONE && act <= ROD_ACT_LEAKY, "rod_bn_bwd_parts: bad act %d", act);
+  BnPro p;
+  p.mean = mean;
+  p.rstd = rstd;
+  p.gamma = gamma;
+  p.beta = beta;
+  p.act = act;
+  gred_parts(dtype, dz, y, p, M, C, parts, nparts, ROD_STREAM(stream));
+  return check_launch("rod_bn_bwd_parts");
+}
+
 size_t rod_bn_stats_workspace(long M, int C) {
   const int nbx = max_nbx(M, C);
   return (size_t)nbx * 3 * C * sizeof(float) + finalize_ws_bytes(nbx, C);

@@ -7,7 +7,7 @@ each a list of six [B, fh, fw, A, 4 | 11] tensors.
 
 Structure (reference line numbers):
   backbone endpoints layer_11/15/18/20/22/24 (__feats_aug_block NONE, 111-114)
-  ALL: deconv pyramid LEARN_HALF (160-212) + ADD merge (237-273)
+  ALL: deconv pyramid LEARN_HALF (160-212) or LEARN_ALL (214-230) + ADD / CONCAT merge (237-273)
   heads: per level, for ch in [128, k*A]: conv1x1(+bias) -> BN -> leaky(0.2) ->
          conv3x3(+bias) -> BN -> leaky (276-342); head BN is slim's default
          (center, no scale, decay 0.999, eps 1e-3); weights xavier, biases zero.
@@ -52,14 +52,20 @@ class CatchNet:
         self.feat_ch = self._endpoint_channels()
         self.n_anchor = n_anchor_each_layer(backbone_name)
         self._head('refine', self.feat_ch, 4, rng)
+        self.deconv_method = config_dict.get('deconv_method', config.deconv_method.LEARN_HALF)
+        self.merge_method = config_dict.get('merge_method', config.merge_method.ADD)
         if all_mode:
-            if config_dict['deconv_method'] is not config.deconv_method.LEARN_HALF:
-                raise ValueError('Parameter "method(%s)" wrong' % str(config_dict['deconv_method']))
-            if config_dict['merge_method'] is not config.merge_method.ADD:
-                raise ValueError('parameter "method(%s)" wrong...' % str(config_dict['merge_method']))
+            if self.deconv_method not in (config.deconv_method.LEARN_HALF, config.deconv_method.LEARN_ALL):
+                raise ValueError('Parameter "method(%s)" wrong' % str(self.deconv_method))
+            if self.merge_method not in (config.merge_method.ADD, config.merge_method.CONCAT):
+                raise ValueError('parameter "method(%s)" wrong...' % str(self.merge_method))
             self._deconv(rng)
-            self._head('clf', self.feat_ch, config.total_obj_n, rng)
-            self._head('det', self.feat_ch, 4, rng)
+            # the deconv pyramid returns every level at the backbone tap's channel count
+            # (LEARN_HALF: 2 * (C // 2), LEARN_ALL: C), so CONCAT doubles the head input
+            merged_ch = self.feat_ch if self.merge_method is config.merge_method.ADD else \
+                [c + d for c, d in zip(self.feat_ch, self.deconv_ch)]
+            self._head('clf', merged_ch, config.total_obj_n, rng)
+            self._head('det', merged_ch, 4, rng)
         self.store.finalize(device)
 
     # ------------------------------------------------------------------ parameters
@@ -91,18 +97,32 @@ class CatchNet:
                     n += 1
 
     def _deconv(self, rng):
+        """__deconv_bone parameters (catch_net.py:177-230); self.deconv_ch = output channels
+        per level in backbone order."""
         chs = list(reversed(self.feat_ch))
+        out_ch = []
+        i_c = chs[0]
         for i in range(len(chs)):
             base = 'deconv/block_%d' % (i + 1)
             if i == 0:
                 self._conv_params(base + '/Conv', chs[0], 1, chs[0], rng)
                 self._head_bn(base + '/BatchNorm', chs[0])
-            else:
-                f_c, i_c = chs[i] // 2, chs[i - 1]
+                o_c = chs[0]
+            elif self.deconv_method is config.deconv_method.LEARN_HALF:
+                f_c = chs[i] // 2
                 # tf.get_variable('weight_%d', [2, 2, f_c, i_c], trunc-normal 0.02) (catch_net.py:189)
                 self.store.add(base + '/weight_%d' % i, trunc_normal(rng, (2, 2, f_c, i_c), 0.02))
                 self._conv_params(base + '/Conv', f_c, 1, i_c, rng)
                 self._head_bn(base + '/BatchNorm', 2 * f_c)
+                o_c = 2 * f_c
+            else:   # LEARN_ALL (catch_net.py:214-230): [2, 2, f_c = C_target, i_c], BN over f_c
+                f_c = chs[i]
+                self.store.add(base + '/weight_%d' % i, trunc_normal(rng, (2, 2, f_c, i_c), 0.02))
+                self._head_bn(base + '/BatchNorm', f_c)
+                o_c = f_c
+            out_ch.append(o_c)
+            i_c = o_c
+        self.deconv_ch = list(reversed(out_ch))
 
     # ------------------------------------------------------------------ forward
     def _bn(self, x, name, training, act=ops.ROD_ACT_LEAKY, parts=None, pending=False):
@@ -139,8 +159,10 @@ class CatchNet:
         return outs
 
     def deconv_bone(self, feats, training):
-        """LEARN_HALF deconvolution pyramid (catch_net.py:160-212); returns in reversed order."""
+        """Deconvolution pyramid (catch_net.py:160-230), LEARN_HALF or LEARN_ALL; returns the
+        levels in reversed (deepest-first) order."""
         P = self.store.params
+        half = self.deconv_method is config.deconv_method.LEARN_HALF
         layers = list(reversed(feats))
         out = []
         x = layers[0]
@@ -150,7 +172,7 @@ class CatchNet:
             if i == 0:
                 x = ops.materialize(self._conv_bn(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1,
                                                   base + '/BatchNorm', training))
-            else:
+            elif half:
                 B_, h, w, _ = layers[i].shape
                 x_out, x_up, x_rs = xs
                 up = ops.deconv2x2(x_up, P[base + '/weight_%d' % i], (h, w))        # conv2d_transpose
@@ -159,8 +181,15 @@ class CatchNet:
                 out.append(x_out)
                 cat = ops.channel_concat([up, rh])                                   # tf.concat(-1)
                 x = self._bn(cat, base + '/BatchNorm', training)
+            else:
+                B_, h, w, _ = layers[i].shape
+                x_out, x_up = xs
+                up = ops.deconv2x2(x_up, P[base + '/weight_%d' % i], (h, w))        # conv2d_transpose
+                out.append(x_out)
+                x = self._bn(up, base + '/BatchNorm', training)
             if i < n - 1:
-                xs = graph.fork(x, 3)    # output list, transpose conv, resize
+                # output list + transpose conv (+ resize for LEARN_HALF)
+                xs = graph.fork(x, 3 if half else 2)
         out.append(x)
         return out
 
@@ -194,7 +223,10 @@ class CatchNet:
         deconv_in = feats[:-1] + [forks[-1][2]]     # the shallower ones contribute only their shape
         deconv = self.deconv_bone(deconv_in, is_training)
         self.deconv_feats = deconv
-        merged = [ops.add(f[1], d) for f, d in zip(forks, reversed(deconv))]     # ADD merge
+        if self.merge_method is config.merge_method.ADD:
+            merged = [ops.add(f[1], d) for f, d in zip(forks, reversed(deconv))]
+        else:   # CONCAT: tf.concat([backbone, deconv], -1) (catch_net.py:258-263)
+            merged = [ops.channel_concat([f[1], d]) for f, d in zip(forks, reversed(deconv))]
         self.merge_feats = merged
         mf = [graph.fork(m, 2) for m in merged]
         clf_out = self.head_out([m[0] for m in mf], 'clf', config.total_obj_n, is_training)
@@ -206,7 +238,7 @@ _NET_CACHE = {}
 
 
 def get_net(backbone_name, config_dict, device='cuda', seed=0):
-    key = (backbone_name, config_dict['train_range'], config_dict['deconv_method'], config_dict['merge_method'],
+    key = (backbone_name, config_dict['train_range'], config_dict.get('deconv_method'), config_dict.get('merge_method'),
            config_dict['process_backbone_method'], str(device), seed)
     if key not in _NET_CACHE:
         _NET_CACHE[key] = CatchNet(backbone_name, config_dict, device, seed)

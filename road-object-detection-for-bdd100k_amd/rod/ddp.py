@@ -82,5 +82,40 @@ class GradReducer(object):
         for t in tensors:
             dist.all_reduce(t, group=self.group)
 
+    def bn_allgather(self, parts):
+        """[world * nparts, ...] = every rank's BatchNorm partial statistics in rank order
+        (SyncBatchNorm)."""
+        return allgather(parts, self.world, self.group)
+
     def launched(self):
         return sum(1 for b in self.buckets if b['work'] is not None)
+
+
+def allgather(t, world, group=None):
+    """All-gather of a small device tensor into one [world * n, ...] buffer, rank-major, on the
+    compute stream (RCCL all_gather_into_tensor; the list form for gloo)."""
+    t = t.contiguous()
+    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    if dist.get_backend(group) == 'nccl':
+        dist.all_gather_into_tensor(out, t, group=group)
+    else:
+        dist.all_gather(list(out.chunk(world)), t, group=group)
+    return out
+
+
+class SyncBatchNorm(object):
+    """BatchNorm statistics over the global batch of a data-parallel job (rod.ops.SYNC_BN).
+    Forward: each rank's partial statistics [nparts][3][C] (count, mean, M2) are all-gathered
+    and every rank merges the same array (rod_bn_finalize, f64, fixed order), so mean, rstd and
+    the moving averages are identical on all ranks and equal a single process holding the whole
+    batch up to the merge order.  Backward: the partial sums (sum g, sum g*yhat) are gathered the
+    same way for the dx coefficients; dgamma / dbeta stay per-rank sums, which the gradient
+    all-reduce adds up.  One all-gather of 3*C (forward) / 2*C (backward) floats per part and
+    BatchNorm: a few KB to ~1 MB per layer, latency-bound on xGMI."""
+
+    def __init__(self, world, group=None):
+        self.world = world
+        self.group = group
+
+    def gather(self, parts):
+        return allgather(parts, self.world, self.group)

@@ -139,6 +139,19 @@ def copy2d(src, src_ld_bytes, dst, dst_ld_bytes, rows, cols_bytes, src_off=0, ds
               rows, cols_bytes, stream())
 
 
+# ----------------------------------------------------------------------------- SyncBN
+# Data-parallel BatchNorm over the GLOBAL batch (the reference normalises over its
+# whole single-device batch, mobilenet.py:417-420).  None = per-rank statistics (the default);
+# otherwise an object with `.world` and `.gather(parts) -> [world * nparts, ...]` (rank order,
+# rod.ddp.GradReducer.bn_allgather).  Every rank merges the same gathered partial statistics
+# in the same fixed order, so mean / rstd / coefficients are identical on all ranks.
+SYNC_BN = None
+
+
+def _sync_nparts(M):
+    return int(max(1, min(1024, M // 256)))
+
+
 # ----------------------------------------------------------------------------- BatchNorm prologue
 class Pending:
     """act(BatchNorm(y)) whose statistics are known but which is NOT materialised.
@@ -172,6 +185,9 @@ def _pro_args(p):
 def _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
     """rod_bn_bwd: gradient wrt the pre-BatchNorm y from the gradient dz of act(BN(y));
     dgamma / dbeta go to the parameters' flat-buffer slots."""
+    if SYNC_BN is not None:   # reduction over the global batch, then the local apply
+        coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, need_g, need_b)
+        return _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, act, coef)
     N, H, W, C = y.shape
     M = N * H * W
     dz = dz.contiguous()
@@ -198,8 +214,22 @@ def bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
     coef = torch.empty(3 * C, dtype=torch.float32, device=y.device)
     dg = grad_slot(gamma) if need_g else None
     db = grad_slot(beta) if need_b else None
-    ws = workspace(_abi.query("rod_bn_bwd_workspace", M, C), y.device)
-    _abi.call("rod_bn_bwd_reduce", dz, y, mean, rstd, gamma, beta, dg, db, coef, ws, M, C, act, dtcode(y), stream())
+    if SYNC_BN is not None:
+        dz = dz.contiguous()
+        nparts = _sync_nparts(M)
+        parts = torch.empty((nparts, 2, C), dtype=torch.float32, device=y.device)
+        _abi.call("rod_bn_bwd_parts", dz, y, mean, rstd, gamma, beta, act, parts, nparts, M, C, dtcode(y), stream())
+        if dg is not None or db is not None:
+            # parameter gradients from this rank's rows only: the DP reducer sums them
+            _abi.call("rod_bn_bwd_finalize", parts, nparts, M, C, rstd, gamma, dg, db,
+                      torch.empty(3 * C, dtype=torch.float32, device=y.device), stream())
+        gp = SYNC_BN.gather(parts)
+        _abi.call("rod_bn_bwd_finalize", gp, gp.shape[0], M * SYNC_BN.world, C, rstd, gamma, None, None, coef,
+                  stream())
+    else:
+        ws = workspace(_abi.query("rod_bn_bwd_workspace", M, C), y.device)
+        _abi.call("rod_bn_bwd_reduce", dz, y, mean, rstd, gamma, beta, dg, db, coef, ws, M, C, act, dtcode(y),
+                  stream())
     if need_g:
         _mark_written(gamma)
     if need_b:
@@ -297,7 +327,7 @@ class _DW3x3(torch.autograd.Function):
                 raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
             dx = torch.empty_like(x)   # gradient wrt the dw input (the BatchNorm output when pro)
             gred = None
-            if ctx.pro and "gred" in _ENABLE and not ctx.owned:   # BatchNorm-backward sums in the epilogue
+            if ctx.pro and "gred" in _ENABLE and not ctx.owned and SYNC_BN is None:   # sums in the epilogue
                 nparts = _abi.lib().rod_dw3x3_bwd_data_gred_parts(N, H, W, C, s, dtcode(x))
                 parts = torch.empty((nparts, 2, C), dtype=torch.float32, device=x.device)
                 gred = (x, mean, rstd, gamma, beta, ctx.act, parts)
@@ -387,7 +417,7 @@ class _Conv(torch.autograd.Function):
             wt1 = _prep(w, 1, x.dtype, Cout, Cin, ks)
             dx = torch.empty_like(x)   # gradient wrt the conv input (the BatchNorm output when pro)
             gred = None
-            if ctx.pro and "gred" in _ENABLE and not ctx.owned:   # BatchNorm-backward sums in the epilogue
+            if ctx.pro and "gred" in _ENABLE and not ctx.owned and SYNC_BN is None:   # sums in the epilogue
                 parts = torch.empty((-(-(N * H * W) // 128), 2, Cin), dtype=torch.float32, device=x.device)
                 gred = (x, mean, rstd, gamma, beta, ctx.act, parts)
             conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks, gred=gred)
@@ -433,7 +463,17 @@ def bn_statistics(x, mmean, mvar, training, decay, eps=1e-3, parts=None):
     rstd = torch.empty(C, dtype=torch.float32, device=x.device)
     if "epistats" in _DISABLE:
         parts = None
-    if training and parts is not None:  # statistics already reduced by the producer's epilogue
+    if training and SYNC_BN is not None:   # statistics over the global batch (all ranks' parts)
+        if parts is None:
+            nparts = _sync_nparts(M)
+            parts = torch.empty((nparts, 3, C), dtype=torch.float32, device=x.device)
+            _abi.call("rod_bn_stat_parts", x.contiguous(), M, C, parts, nparts, dtcode(x), stream())
+        gp = SYNC_BN.gather(parts)
+        nb = _abi.query("rod_bn_finalize_workspace", gp.shape[0], C)
+        ws = workspace(nb, x.device) if nb else None
+        _abi.call("rod_bn_finalize", gp, gp.shape[0], M * SYNC_BN.world, C, eps, decay, mean, rstd, mmean, mvar, ws,
+                  stream())
+    elif training and parts is not None:  # statistics already reduced by the producer's epilogue
         nb = _abi.query("rod_bn_finalize_workspace", parts.shape[0], C)
         ws = workspace(nb, x.device) if nb else None
         _abi.call("rod_bn_finalize", parts, parts.shape[0], M, C, eps, decay, mean, rstd, mmean, mvar, ws, stream())

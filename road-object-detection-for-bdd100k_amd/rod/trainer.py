@@ -9,7 +9,8 @@ Data-parallel: one process per GPU, the per-image batch sharded across ranks; th
 flat gradient buffer is all-reduced (sum) over RCCL and losses are normalised by the
 GLOBAL batch so the sum equals the single-process gradient (the reference divides by
 bs, net_tools.py:513).  Clipping happens after the reduction (net_tools.py:649).
-BatchNorm statistics are per rank (documented deviation); the hard negatives are
+BatchNorm statistics are per rank by default (documented deviation) or, with
+sync_bn=True, merged over the global batch (rod.ddp.SyncBatchNorm); the hard negatives are
 selected over the global batch (counts + radix histograms all-reduced, ops.hnm_lockstep).
 """
 from __future__ import annotations
@@ -26,7 +27,9 @@ from utils.common_tools import cornerBboxes_2_centerBboxes
 
 class Trainer:
     def __init__(self, img_size, batch_size, dtype=torch.bfloat16, train_range=config.train_range.REFINE,
-                 learning_rate=1e-3, device='cuda', fix_refine=True, seed=0, world_size=1, reducer=None):
+                 learning_rate=1e-3, device='cuda', fix_refine=True, seed=0, world_size=1, reducer=None,
+                 deconv_method=config.deconv_method.LEARN_HALF, merge_method=config.merge_method.ADD,
+                 sync_bn=False):
         self.img_size = tuple(img_size)
         self.batch_size = batch_size          # per-rank batch
         self.world_size = world_size
@@ -35,8 +38,8 @@ class Trainer:
         config.img_size = self.img_size       # init_anchor reads config.img_size (net_tools.py:37-38)
         self.config_dict = {'train_range': train_range,
                             'process_backbone_method': config.process_backbone_method.NONE,
-                            'deconv_method': config.deconv_method.LEARN_HALF,
-                            'merge_method': config.merge_method.ADD}
+                            'deconv_method': deconv_method,     # train.py:131-133 defaults
+                            'merge_method': merge_method}
         self.net = CatchNet('mobilenet_v2', self.config_dict, self.device, seed)
         layer_n = len(config.extract_feat_name['mobilenet_v2'])
         self.anchors = net_tools.anchors_all_layer(self.img_size, config.feat_sizes(self.img_size),
@@ -56,6 +59,13 @@ class Trainer:
             if world_size > 1 and reducer is not None and hasattr(reducer, 'hnm_allreduce') else None
         self.train_range = train_range
         self.fix_refine = fix_refine
+        # BatchNorm over the global batch (opt-in; per-rank statistics otherwise)
+        self.sync_bn = bool(sync_bn and world_size > 1)
+        if self.sync_bn:
+            from rod.ddp import SyncBatchNorm
+            ops.SYNC_BN = SyncBatchNorm(world_size, getattr(reducer, 'group', None))
+        else:
+            ops.SYNC_BN = None
 
     def step(self, img_u8, gt_corner, gt_labels, gt_n):
         losses = self.losses(img_u8, gt_corner, gt_labels, gt_n)

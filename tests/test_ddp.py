@@ -52,6 +52,13 @@ def _worker(rank, world, port, q):
                     launched_midway = red.launched()
             red(st.flat_grad)
             results.append((launched_midway, st.flat_grad.clone()))
+        # SyncBatchNorm gather: every rank gets the same rank-major concatenation
+        from rod.ddp import SyncBatchNorm
+        parts = torch.full((3, 2, 5), float(rank + 1))
+        got = SyncBatchNorm(world).gather(parts)
+        assert got.shape == (3 * world, 2, 5)
+        for r in range(world):
+            assert bool((got[3 * r:3 * r + 3] == r + 1).all())
         # global-batch normalisation: per-rank mean over its shard / world == global mean
         x = torch.arange(8, dtype=torch.float64).reshape(world, -1)[rank]
         local = (x.sum() / (x.numel() * world)).reshape(1)

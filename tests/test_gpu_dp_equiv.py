@@ -1,0 +1,85 @@
+"""Data-parallel step equivalence: one training step of
+2 ranks x (B/2) images — gradient all-reduce, global-batch loss normalisation, global
+hard-negative selection (ALL), and SyncBatchNorm — against ONE process holding all B images.
+
+With sync_bn the losses, the moving averages and the SGD result must match the single
+process within fp32 reordering (1e-5 / normwise 1e-4), the SGD step is bit-exact given the
+reduced gradient, and every parameter gradient within
+max(1e-4, 4x the step's own fp32 sensitivity) normwise — the sensitivity being how far the
+single-process gradient moves under 1e-6 relative noise on its input (two draws): ReLU6 /
+leaky kinks near zero and BatchNorm over the 12-24 rows of the deepest maps at this size make
+single gradient entries move by percents under ANY fp32 reordering (the kernels also pick
+other split-K / slab plans for B/2 rows), as in test_gpu_train.py.  Without sync_bn (the per-rank default) the deviation is
+real and is only reported.  The ranks
+share cuda:0 over gloo (RCCL refuses two ranks on one device); the transport is the only
+difference from an 8-GPU RCCL run."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, 'tests', 'dp_step_worker.py')
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(out, world, train_range, sync, perturb_seed=None):
+    args = [WORKER, '--out', out, '--train_range', train_range] + (['--sync_bn'] if sync else []) + \
+        (['--perturb', '1e-6', '--perturb_seed', str(perturb_seed)] if perturb_seed is not None else [])
+    if world == 1:
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(world),
+               '--master-addr', '127.0.0.1', '--master-port', str(_port())] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, MASTER_ADDR='127.0.0.1'), capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return torch.load(out, weights_only=True)
+
+
+def _nerr(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize('train_range', ['REFINE', 'ALL'])
+def test_two_ranks_equal_one_process(train_range, tmp_path, dev):
+    one = _run(str(tmp_path / 'one.pt'), 1, train_range, False)
+    pert = [_run(str(tmp_path / f'p{s}.pt'), 1, train_range, False, perturb_seed=s) for s in (11, 12)]
+    two = _run(str(tmp_path / 'two.pt'), 2, train_range, True)
+    per = _run(str(tmp_path / 'per.pt'), 2, train_range, False)
+    lo, lt = one['losses'], two['losses']
+    assert torch.allclose(lt, lo, rtol=1e-5, atol=0), (lt, lo)
+    bad, rows = [], []
+    for name in one['trainable']:
+        o, k = one['offsets'][name]
+        g1 = one['grad'][o:o + k]
+        if g1.abs().max() == 0:
+            continue
+        e_sync, e_per = (_nerr(r['grad'][o:o + k], g1) for r in (two, per))
+        e_floor = max(_nerr(r['grad'][o:o + k], g1) for r in pert)
+        rows.append((e_sync, e_floor, e_per))
+        if e_sync > max(1e-4, 4 * e_floor):
+            bad.append((name, e_sync, e_floor, e_per))
+    assert not bad, bad[:10]
+    # clip after the all-reduce, then SGD (net_tools.py:645-651): bit-exact given the reduced gradient
+    ref = (two['flat0'].numpy() - np.float32(1e-2) * np.clip(two['grad'].numpy(), -5, 5)).astype(np.float32)
+    np.testing.assert_array_equal(two['flat'].numpy(), ref)
+    assert torch.equal(two['flat0'], one['flat0'])
+    for k, v in one['buffers'].items():
+        assert _nerr(two['buffers'][k], v) < 1e-4, k
+    t = torch.tensor(rows)
+    print(f'{train_range}: {len(rows)} gradients; normwise error vs one process, median / max: '
+          f'sync {t[:, 0].median():.2g} / {t[:, 0].max():.2g}, input-noise floor {t[:, 1].median():.2g} / '
+          f'{t[:, 1].max():.2g}, per-rank BatchNorm {t[:, 2].median():.2g} / {t[:, 2].max():.2g}')

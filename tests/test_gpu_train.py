@@ -157,29 +157,39 @@ def test_refine_step_matches_oracle(dev, dtype):
     np.testing.assert_array_equal(tr.net.store.flat.detach().cpu().numpy(), ref)
 
 
-def test_all_mode_step_matches_oracle(dev):
+_DM, _MM = config.deconv_method, config.merge_method
+
+
+@pytest.mark.parametrize('dm,mm,hw', [(_DM.LEARN_HALF, _MM.ADD, (320, 576)), (_DM.LEARN_ALL, _MM.ADD, (160, 288)),
+                                      (_DM.LEARN_HALF, _MM.CONCAT, (160, 288)),
+                                      (_DM.LEARN_ALL, _MM.CONCAT, (224, 416))],
+                         ids=['half-add', 'all-add', 'half-concat', 'all-concat'])
+def test_all_mode_step_matches_oracle(dev, dm, mm, hw):
     """train_range=ALL, fix_refine=True (train.py:140-249): outputs, det/clf losses and the
-    gradients of every trainable (deconv / clf / det) parameter."""
+    gradients of every trainable (deconv / clf / det) parameter, for each deconv method
+    (LEARN_HALF / LEARN_ALL, catch_net.py:177-230) and merge method (ADD / CONCAT, 237-273)."""
     from oracle import post as op
     import utils.net_tools as nt
     from nets.catch_net import factory
     from utils.common_tools import cornerBboxes_2_centerBboxes
-    H, W, B = 320, 576, 2
-    tr = Trainer((H, W), B, dtype=torch.float32, device=dev, train_range=config.train_range.ALL, seed=5)
+    (H, W), B = hw, 2
+    tr = Trainer((H, W), B, dtype=torch.float32, device=dev, train_range=config.train_range.ALL, seed=5,
+                 deconv_method=dm, merge_method=mm)
+    kw = dict(all_mode=True, learn_all=dm is _DM.LEARN_ALL, concat=mm is _MM.CONCAT)
     img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=6)
     P32 = {k: v.detach().cpu().clone().requires_grad_(v.requires_grad) for k, v in tr.net.store.params.items()}
     B32 = {k: v.detach().cpu().clone() for k, v in tr.net.store.buffers.items()}
     P64 = {k: v.detach().double().requires_grad_(v.requires_grad) for k, v in P32.items()}
     B64 = {k: v.double() for k, v in B32.items()}
     x = torch.from_numpy(np.float32(2.0 / 255.0) * img.cpu().numpy().astype(np.float32) - np.float32(1.0))
-    o32 = onet.forward(x, P32, B32, True, all_mode=True, moving={})
-    o64 = onet.forward(x.double(), P64, B64, True, all_mode=True, moving={})
+    o32 = onet.forward(x, P32, B32, True, moving={}, **kw)
+    o64 = onet.forward(x.double(), P64, B64, True, moving={}, **kw)
     # a second fp32 evaluation with a different convolution algorithm (oneDNN off): the
     # spread between fp32 implementations bounds what any fp32 implementation can achieve
     P32b = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in P32.items()}
     torch.backends.mkldnn.enabled = False
     try:
-        o32b = onet.forward(x, P32b, {k: v.clone() for k, v in B32.items()}, True, all_mode=True, moving={})
+        o32b = onet.forward(x, P32b, {k: v.clone() for k, v in B32.items()}, True, moving={}, **kw)
     finally:
         torch.backends.mkldnn.enabled = True
 
