@@ -47,9 +47,10 @@ def parse():
                     help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
     ap.add_argument('--sync-bn', dest='sync_bn', action='store_true', default=False,
                     help='N>1: BatchNorm statistics over the global batch (rod.ddp.SyncBatchNorm; default per rank)')
-    ap.add_argument('--probe', default='rod_bn_bwd_reduce,rod_bn_bwd_apply',
+    ap.add_argument('--probe', default='rod_bn_bwd_reduce,rod_bn_bwd_apply,rod_bn_bwd',
                     help='C-ABI entry (or comma list, aggregated as one kernel family) reported in "roofline": '
-                         'default the BatchNorm backward (reduce + apply), the family VERDICT r1 names')
+                         'default the BatchNorm backward (reduce + apply; one-launch rod_bn_bwd on small '
+                         'tensors), the family VERDICT r1 names')
     ap.add_argument('--probe-table', dest='probe_table', default=None,
                     help='time EVERY librod call and write a per-entry table (JSON) here (analysis only)')
     ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'),

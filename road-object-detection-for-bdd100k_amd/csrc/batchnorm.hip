@@ -16,6 +16,7 @@
 
 namespace rod {
 
+
 // Row-chunk reduction plan shared by the statistics and backward-reduce kernels.
 // CV channel vectors are split into cgroups of CVb <= 256 (blockIdx.y); the 256 threads of a
 // block are `lanes` row lanes x CVb channel vectors (no power-of-two padding, so at most
@@ -531,6 +532,180 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
+// Small tensors (M <= SMALL_M rows) in ONE launch: each 1024-thread block owns CVb channel
+// vectors over ALL rows — reduce (fp32 per lane; lanes merged in f64 by wave shuffles, then the
+// 16 wave partials in LDS, fixed order), the coefficients, then (dx != NULL) the apply pass
+// over the same rows, which the block has just read (L2-hot).  The three-launch reduce ->
+// finalize -> apply chain costs 15-45 us on such tensors, mostly launch boundaries and the
+// finalize's dependent loads.
+constexpr int SMALL_T = 1024;
+constexpr long SMALL_M = 4096;
+constexpr int SMALL_CVB = 4;   // channel vectors per block (measured: 4 < 8 < 16 on the step's shapes)
+// the one-launch path needs >= 8 channel groups to spread over CUs (C >= 256 bf16 / 128 fp32);
+// narrower small tensors keep the three-launch chain (measured faster for 4096 x 64)
+static bool small_ok(long M, int CV) { return M <= SMALL_M && CV >= 8 * SMALL_CVB; }
+
+__device__ __forceinline__ double shfl_xor_f64(double v, int o) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __shfl_xor(lo, o, 64);
+  hi = __shfl_xor(hi, o, 64);
+  return __hiloint2double(hi, lo);
+}
+
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(SMALL_T) bn_bwd_small_kernel(const T* __restrict__ dz, const T* __restrict__ y,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, long M, int C,
+                                                               int act, int CVb, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta, float* __restrict__ coef,
+                                                               T* __restrict__ dx) {
+  constexpr int V = VEC ? Vec16<T>::N : 1;
+  constexpr int NW = SMALL_T / 64;
+  __shared__ double red[2][NW][16 * V];
+  __shared__ float cf[3][16 * V];
+  const int tid = threadIdx.x;
+  const int lanes = SMALL_T / CVb;       // CVb a power of two <= 16
+  const int cvl = tid % CVb, pln = tid / CVb;
+  const int CV = C / V;
+  const int cv = blockIdx.x * CVb + cvl;
+  const bool active = cv < CV;
+  const int c = cv * V;
+  float sg[V], sgx[V], mu[V], rs[V], sc[V], sh[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) sg[v] = sgx[v] = 0.f;
+  if (active) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      mu[v] = mean[c + v];
+      rs[v] = rstd[c + v];
+      bn_affine(mean, rstd, gamma, beta, c + v, sc[v], sh[v]);
+    }
+    long r = pln;
+    for (; r + 3L * lanes < M; r += 4L * lanes) {
+      float xa[4][V], ga[4][V];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        load_v<T, VEC>(y + (r + (long)u * lanes) * C + c, xa[u]);
+        load_v<T, VEC>(dz + (r + (long)u * lanes) * C + c, ga[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float g = ga[u][v] * act_grad(fmaf(xa[u][v], sc[v], sh[v]), act);
+          sg[v] += g;
+          sgx[v] = fmaf(g, (xa[u][v] - mu[v]) * rs[v], sgx[v]);
+        }
+    }
+    for (; r < M; r += lanes) {
+      float xv[V], gv[V];
+      load_v<T, VEC>(y + r * C + c, xv);
+      load_v<T, VEC>(dz + r * C + c, gv);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float g = gv[v] * act_grad(fmaf(xv[v], sc[v], sh[v]), act);
+        sg[v] += g;
+        sgx[v] = fmaf(g, (xv[v] - mu[v]) * rs[v], sgx[v]);
+      }
+    }
+  }
+  // the lanes of one channel vector inside a wave sit CVb apart: xor-shuffle tree in f64
+  const int wave = tid >> 6;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    double a = (double)sg[v], b = (double)sgx[v];
+    for (int o = CVb; o < 64; o <<= 1) {
+      a += shfl_xor_f64(a, o);
+      b += shfl_xor_f64(b, o);
+    }
+    if ((tid & 63) < CVb) {
+      red[0][wave][cvl * V + v] = a;
+      red[1][wave][cvl * V + v] = b;
+    }
+  }
+  __syncthreads();
+  if (tid < CVb * V) {
+    const int cb = tid / V, v = tid - cb * V;
+    const int cg = blockIdx.x * CVb + cb;
+    if (cg < CV) {
+      double a = 0.0, b = 0.0;
+      for (int w = 0; w < NW; ++w) {
+        a += red[0][w][cb * V + v];
+        b += red[1][w][cb * V + v];
+      }
+      const int ch = cg * V + v;
+      const float c0 = gamma ? rstd[ch] * gamma[ch] : rstd[ch];
+      const float c1 = (float)(a / (double)M), c2 = (float)(b / (double)M);
+      if (dbeta) dbeta[ch] = (float)a;
+      if (dgamma) dgamma[ch] = (float)b;
+      if (coef) {
+        coef[ch] = c0;
+        coef[C + ch] = c1;
+        coef[2 * C + ch] = c2;
+      }
+      cf[0][cb * V + v] = c0;
+      cf[1][cb * V + v] = c1;
+      cf[2][cb * V + v] = c2;
+    }
+  }
+  if (dx == nullptr) return;
+  __syncthreads();
+  if (!active) return;
+  float a[V], mg[V], mgx[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    a[v] = cf[0][cvl * V + v];
+    mg[v] = cf[1][cvl * V + v];
+    mgx[v] = cf[2][cvl * V + v];
+  }
+  auto row = [&](float (&xv)[V], const float (&gv)[V]) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float g = gv[v] * act_grad(fmaf(xv[v], sc[v], sh[v]), act);
+      xv[v] = a[v] * (g - mg[v] - ((xv[v] - mu[v]) * rs[v]) * mgx[v]);
+    }
+  };
+  long r = pln;
+  for (; r + 3L * lanes < M; r += 4L * lanes) {
+    float xa[4][V], ga[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      load_v<T, VEC>(y + (r + (long)u * lanes) * C + c, xa[u]);
+      load_v<T, VEC>(dz + (r + (long)u * lanes) * C + c, ga[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      row(xa[u], ga[u]);
+      store_v<T, VEC>(dx + (r + (long)u * lanes) * C + c, xa[u]);
+    }
+  }
+  for (; r < M; r += lanes) {
+    float xv[V], gv[V];
+    load_v<T, VEC>(y + r * C + c, xv);
+    load_v<T, VEC>(dz + r * C + c, gv);
+    row(xv, gv);
+    store_v<T, VEC>(dx + r * C + c, xv);
+  }
+}
+
+// Small path launch: SMALL_CVB channel vectors per 1024-thread block (256 row lanes).
+template <typename T>
+static void small_launch(bool vec, const void* dz, const void* y, const float* mean, const float* rstd,
+                         const float* gamma, const float* beta, long M, int C, int act, float* dgamma, float* dbeta,
+                         float* coef, void* dx, hipStream_t s) {
+  const int V = vec ? Vec16<T>::N : 1;
+  const int CV = C / V;
+  const int CVb = SMALL_CVB;
+  if (vec)
+    hipLaunchKernelGGL((bn_bwd_small_kernel<T, true>), dim3(cdiv(CV, CVb)), dim3(SMALL_T), 0, s, (const T*)dz,
+                       (const T*)y, mean, rstd, gamma, beta, M, C, act, CVb, dgamma, dbeta, coef, (T*)dx);
+  else
+    hipLaunchKernelGGL((bn_bwd_small_kernel<T, false>), dim3(cdiv(CV, CVb)), dim3(SMALL_T), 0, s, (const T*)dz,
+                       (const T*)y, mean, rstd, gamma, beta, M, C, act, CVb, dgamma, dbeta, coef, (T*)dx);
+}
+
 template <typename T>
 static bool vec_ok(int C, std::initializer_list<std::pair<const void*, int>> bufs) {
   const int V = Vec16<T>::N;
@@ -546,6 +721,12 @@ static bool vec_ok(int C, std::initializer_list<std::pair<const void*, int>> buf
 // Threads for the row-streaming apply kernels: >= ~8 rows per thread on large tensors (the
 // per-thread coefficient loads amortised), but at least 256 blocks' worth on small ones.
 static long apply_threads(long total) { return std::max(total / 8, std::min(total, 256L * 256)); }
+// grid cap of the apply kernels: ROD_TUNE_APPLY_CAP = 0 -> 2048 blocks, -1 -> one resident wave
+// Grid cap of the apply kernels (68-84 VGPRs: 6-7 blocks of 256 per CU resident): one partial
+// wave of 768 blocks with more rows per thread for mid-size tensors (<= 12M thread-rows:
+// 115200 x 384 147 -> 120 us, 460800 x 192 231 -> 209 us), 1792 (7 per CU) for the large ones
+// (tools/bn_bench.py sweep).
+static int apply_target(long thread_rows) { return thread_rows <= (12L << 20) ? 768 : 1792; }
 
 static int max_nbx(long M, int C) {
   int a = red_plan<float>(M, C, false).nbx;
@@ -559,7 +740,7 @@ static void apply_launch(bool vec, const void* x, const float* mean, const float
                          const float* beta, const void* res, void* y, long M, int C, int ldx, int ldr, int ldy,
                          int act, hipStream_t s) {
   const int V = vec ? Vec16<T>::N : 1;
-  const int blocks = const_channel_blocks(C / V, apply_threads(M * (C / V)));
+  const int blocks = const_channel_blocks(C / V, apply_threads(M * (C / V)), apply_target(M * (C / V)));
 #define LA(VE, RE)                                                                                            \
   hipLaunchKernelGGL((bn_apply_kernel<T, VE, RE>), dim3(blocks), dim3(256), 0, s, (const T*)x, mean, rstd, gamma, \
                      beta, (const T*)res, (T*)y, M, C, ldx, ldr, ldy, act)
@@ -625,7 +806,9 @@ static void bwd_launch(bool vec, const void* dy, const void* x, const float* mea
                      dgamma, dbeta, coef);
   const int V = pl.V;
   // >= ~8 rows per thread so the per-thread coefficient loads (7 x V floats) are amortised
-  const int blocks = const_channel_blocks(C / V, apply_threads(M * (C / V)));
+  const int blocks = const_channel_blocks(
+      C / V, apply_threads(M * (C / V)),
+      apply_target(M * (C / V)));
   if (vec)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dy, (const T*)x, mean,
                        rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
@@ -694,7 +877,9 @@ int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const flo
   ROD_DISPATCH_DTYPE(dtype, {
     const bool vec = vec_ok<T>(C, {{dz, C}, {y, C}, {dy, C}});
     const int V = vec ? Vec16<T>::N : 1;
-    const int blocks = const_channel_blocks(C / V, apply_threads(M * (C / V)));
+    const int blocks = const_channel_blocks(
+        C / V, apply_threads(M * (C / V)),
+        apply_target(M * (C / V)));
     if (vec)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (const T*)dz, (const T*)y,
                          mean, rstd, gamma, beta, coef, (T*)dy, M, C, C, C, C, act);
@@ -798,6 +983,10 @@ int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const fl
   float* slab = (float*)workspace;
   ROD_DISPATCH_DTYPE(dtype, {
     const bool vec = vec_ok<T>(C, {{dz, C}, {y, C}});
+    if (small_ok(M, C / (vec ? Vec16<T>::N : 1))) {
+      small_launch<T>(vec, dz, y, mean, rstd, gamma, beta, M, C, act, dgamma, dbeta, coef, nullptr, s);
+      return check_launch("rod_bn_bwd_reduce");
+    }
     RedPlan pl = red_plan<T>(M, C, vec);
     dim3 grid(pl.nbx, pl.cgroups);
     size_t lds = 2 * 256 * pl.V * sizeof(float);
@@ -825,6 +1014,15 @@ int rod_bn_bwd(const void* dy, const void* x, const float* mean, const float* rs
   hipStream_t s = ROD_STREAM(stream);
   float* slab = (float*)workspace;
   float* coef = slab + (size_t)max_nbx(M, C) * 2 * C;  // after the largest slab
+  if (M <= SMALL_M && lddy == C && ldx == C && lddx == C) {
+    ROD_DISPATCH_DTYPE(dtype, {
+      const bool vec = vec_ok<T>(C, {{dy, C}, {x, C}, {dx, C}});
+      if (small_ok(M, C / (vec ? Vec16<T>::N : 1))) {
+        small_launch<T>(vec, dy, x, mean, rstd, gamma, beta, M, C, act, dgamma, dbeta, coef, dx, s);
+        return check_launch("rod_bn_bwd");
+      }
+    });
+  }
   ROD_DISPATCH_DTYPE(dtype, bwd_launch<T>(vec_ok<T>(C, {{dy, lddy}, {x, ldx}, {dx, lddx}}), dy, x, mean, rstd, gamma,
                                           beta, dx, dgamma, dbeta, slab, coef, M, C, lddy, ldx, lddx, act, s));
   return check_launch("rod_bn_bwd");

@@ -552,6 +552,19 @@ def _needs(p):
     return p is not None and p.requires_grad
 
 
+def bn_bwd_dy(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
+    """d/dy of act(BN(y)) from dz, dgamma / dbeta into their slots.  Small tensors (<= 4096
+    rows: the deep maps and the heads' last levels) take rod_bn_bwd, which runs the reduction,
+    the coefficients and the apply in one launch; larger ones rod_bn_bwd_reduce (reduce +
+    finalize) then rod_bn_bwd_apply."""
+    C = y.shape[-1]
+    M = y.numel() // C
+    if M <= 4096 and SYNC_BN is None:
+        return _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b)
+    coef = bn_bwd_reduce(dz.contiguous(), y, mean, rstd, gamma, beta, act, need_g, need_b)
+    return _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, act, coef)
+
+
 # fused 1x1 backward where it measured faster than the unfused chain (tools/pwbwd_bench.py):
 # the expand-shaped convs (Cout >= 2 Cin) on >= 200k rows
 def _pw_fused_ok(M, Cin, Cout, dtype):
@@ -617,9 +630,9 @@ class _ConvBN(torch.autograd.Function):
         Cout = w.shape[0]
         M = N * H * W
         dz = dz.contiguous()
-        coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
         need_dx = ctx.needs_input_grad[0]
         if ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w) or _needs(b)):
+            coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             gw = grad_slot(w) if _needs(w) else torch.empty((Cout, Cin), dtype=torch.float32, device=y.device)
             gb = grad_slot(b) if _needs(b) else None
             wt1 = _prep(w, 1, x.dtype, Cout, Cin, 1) if need_dx else None
@@ -629,7 +642,7 @@ class _ConvBN(torch.autograd.Function):
             if _needs(b):
                 _mark_written(b)
         else:
-            dy = _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, ctx.act, coef)
+            dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             dx = _conv_bwd_from_dy(x, w, b, ctx.ks, dy, ctx.ipro, need_dx)
         return dx, None, None, None, None, None
 
@@ -668,8 +681,7 @@ class _DWBN(torch.autograd.Function):
         x, w, y, mean, rstd = ctx.saved_tensors
         gamma, beta = ctx.gb
         N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
-        coef = bn_bwd_reduce(dz.contiguous(), y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
-        dy = _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, ctx.act, coef)
+        dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)

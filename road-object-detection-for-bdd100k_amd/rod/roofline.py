@@ -87,7 +87,8 @@ def cost(name, a):
 # substrings of every kernel the entry launches) for attributing rocprofv3 PMC counters
 # (tools/pmc_traffic.py); shared helper kernels (slab_sum, splitk_combine) are not attributed
 ENTRY_KERNELS = {
-    "rod_bn_bwd": (("bn_bwd_apply_kernel",), ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel", "bn_bwd_apply_kernel")),
+    # rod_bn_bwd runs only on small tensors on the training path (ops.bn_bwd_dy): the one-launch kernel
+    "rod_bn_bwd": (("bn_bwd_small_kernel",), ("bn_bwd_small_kernel",)),
     "rod_bn_apply": (("bn_apply_kernel",), ("bn_apply_kernel",)),
     "rod_bn_bwd_reduce": (("bn_bwd_reduce_kernel",), ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel")),
     "rod_bn_bwd_apply": (("bn_bwd_apply_kernel",), ("bn_bwd_apply_kernel",)),

@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--out', required=True)
     ap.add_argument('--batch', type=int, default=4, help='global batch')
-    ap.add_argument('--hw', type=int, nargs=2, default=(160, 288))
+    ap.add_argument('--hw', type=int, nargs=2, default=(320, 576))
     ap.add_argument('--train_range', default='REFINE')
     ap.add_argument('--sync_bn', action='store_true')
     ap.add_argument('--perturb', type=float, default=0.0,
@@ -63,15 +63,24 @@ def main():
     grad = tr.net.store.flat_grad.detach().clone()
     tr.opt.step()
     lv = torch.stack([l.detach().reshape(()).double() for l in losses])
+    # integer decisions of the step (ALL): ODM positives (sum over ranks) and the global
+    # hard-negative k / selected count (rod_softmax_ce_hnm stats [5], [6]; identical on all ranks)
+    dec = torch.zeros(3, dtype=torch.float64, device=dev)
+    if tr_range is config.train_range.ALL:
+        import utils.net_tools as nt
+        dec[0] = tr.last_targets[1].flat[1].sum().double()
+        st = nt.det_clf_loss.last_stats.double()
+        dec[1], dec[2] = st[5], st[6]
     if world > 1:
         torch.distributed.all_reduce(lv)
+        torch.distributed.all_reduce(dec[:1])
     torch.cuda.synchronize()
     if rank == 0:
         store = tr.net.store
         torch.save({'grad': grad.cpu(), 'flat': store.flat.detach().cpu(), 'flat0': flat0.cpu(), 'offsets': dict(store.offsets),
                     'buffers': {k: v.detach().cpu() for k, v in store.buffers.items()},
                     'trainable': [k for k, p in store.params.items() if p.requires_grad],
-                    'losses': lv.cpu()}, a.out)
+                    'losses': lv.cpu(), 'decisions': dec.cpu()}, a.out)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -3,11 +3,11 @@
 hard-negative selection (ALL), and SyncBatchNorm — against ONE process holding all B images.
 
 With sync_bn the losses, the moving averages and the SGD result must match the single
-process within fp32 reordering (1e-5 / normwise 1e-4), the SGD step is bit-exact given the
-reduced gradient, and every parameter gradient within
+process within fp32 reordering (1e-4), the SGD step is bit-exact given the reduced gradient,
+and every parameter gradient and moving average within
 max(1e-4, 4x the step's own fp32 sensitivity) normwise — the sensitivity being how far the
 single-process gradient moves under 1e-6 relative noise on its input (two draws): ReLU6 /
-leaky kinks near zero and BatchNorm over the 12-24 rows of the deepest maps at this size make
+leaky kinks near zero and BatchNorm over the few rows of the deepest maps (3x5 at 320x576) make
 single gradient entries move by percents under ANY fp32 reordering (the kernels also pick
 other split-K / slab plans for B/2 rows), as in test_gpu_train.py.  Without sync_bn (the per-rank default) the deviation is
 real and is only reported.  The ranks
@@ -59,8 +59,10 @@ def test_two_ranks_equal_one_process(train_range, tmp_path, dev):
     pert = [_run(str(tmp_path / f'p{s}.pt'), 1, train_range, False, perturb_seed=s) for s in (11, 12)]
     two = _run(str(tmp_path / 'two.pt'), 2, train_range, True)
     per = _run(str(tmp_path / 'per.pt'), 2, train_range, False)
+    print(f"{train_range}: decisions (ODM positives, k, selected negatives): one {one['decisions'].tolist()} "
+          f"two {two['decisions'].tolist()} noise {[p['decisions'].tolist() for p in pert]}")
     lo, lt = one['losses'], two['losses']
-    assert torch.allclose(lt, lo, rtol=1e-5, atol=0), (lt, lo)
+    assert torch.allclose(lt, lo, rtol=1e-4, atol=0), (lt, lo)
     bad, rows = [], []
     for name in one['trainable']:
         o, k = one['offsets'][name]
@@ -77,8 +79,9 @@ def test_two_ranks_equal_one_process(train_range, tmp_path, dev):
     ref = (two['flat0'].numpy() - np.float32(1e-2) * np.clip(two['grad'].numpy(), -5, 5)).astype(np.float32)
     np.testing.assert_array_equal(two['flat'].numpy(), ref)
     assert torch.equal(two['flat0'], one['flat0'])
-    for k, v in one['buffers'].items():
-        assert _nerr(two['buffers'][k], v) < 1e-4, k
+    for k, v in one['buffers'].items():   # moving averages: same conditioning-aware bound
+        e_floor = max(_nerr(r['buffers'][k], v) for r in pert)
+        assert _nerr(two['buffers'][k], v) <= max(1e-4, 4 * e_floor), (k, _nerr(two['buffers'][k], v), e_floor)
     t = torch.tensor(rows)
     print(f'{train_range}: {len(rows)} gradients; normwise error vs one process, median / max: '
           f'sync {t[:, 0].median():.2g} / {t[:, 0].max():.2g}, input-noise floor {t[:, 1].median():.2g} / '

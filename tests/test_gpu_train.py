@@ -160,9 +160,9 @@ def test_refine_step_matches_oracle(dev, dtype):
 _DM, _MM = config.deconv_method, config.merge_method
 
 
-@pytest.mark.parametrize('dm,mm,hw', [(_DM.LEARN_HALF, _MM.ADD, (320, 576)), (_DM.LEARN_ALL, _MM.ADD, (160, 288)),
-                                      (_DM.LEARN_HALF, _MM.CONCAT, (160, 288)),
-                                      (_DM.LEARN_ALL, _MM.CONCAT, (224, 416))],
+@pytest.mark.parametrize('dm,mm,hw', [(_DM.LEARN_HALF, _MM.ADD, (320, 576)), (_DM.LEARN_ALL, _MM.ADD, (320, 576)),
+                                      (_DM.LEARN_HALF, _MM.CONCAT, (320, 576)),
+                                      (_DM.LEARN_ALL, _MM.CONCAT, (288, 512))],
                          ids=['half-add', 'all-add', 'half-concat', 'all-concat'])
 def test_all_mode_step_matches_oracle(dev, dm, mm, hw):
     """train_range=ALL, fix_refine=True (train.py:140-249): outputs, det/clf losses and the
@@ -244,11 +244,27 @@ def test_all_mode_step_matches_oracle(dev, dm, mm, hw):
             continue
         checked += 1
         g64, g32, g32b = P64[name].grad, P32[name].grad, P32b[name].grad
+        if _bias_before_bn(name, g64, P64):
+            # conv bias followed by a training-mode BatchNorm: its gradient is exactly zero
+            # (the batch mean absorbs it), so only rounding residue is left on both sides
+            wscale = float(P64[name.replace('/biases', '/weights')].grad.abs().max())
+            if float(p._rod_grad.abs().max()) > 1e-4 * wscale:
+                bad.append((name, float(p._rod_grad.abs().max()), wscale))
+            continue
         e = _nerr(p._rod_grad, g64)
         spread = max(_nerr(g32, g64), _nerr(g32b, g64))
         if e > max(2e-3, 4 * spread):
             bad.append((name, e, spread))
     assert checked > 50 and not bad, bad[:10]
+
+
+def _bias_before_bn(name, g64, P64):
+    """A slim.conv2d bias whose conv feeds a training-mode BatchNorm (every head / deconv conv,
+    catch_net.py:301-303): d loss / d bias = sum over rows of d loss / d (BN input) = 0 exactly."""
+    w = name.replace('/biases', '/weights')
+    if not name.endswith('/biases') or w not in P64 or P64[w].grad is None:
+        return False
+    return float(g64.abs().max()) <= 1e-6 * float(P64[w].grad.abs().max())
 
 
 def test_all_mode_train_refine_matches_oracle(dev):
