@@ -28,15 +28,16 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 8
+#define ROD_ABI_VERSION 9
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
 /* activation applied after BatchNorm:
  *   NONE  = identity (project conv, conv_blocks.py:294)
  *   RELU6 = tf.nn.relu6 (mobilenet_v2.py:47)
- *   LEAKY = tf.nn.leaky_relu, alpha 0.2 (catch_net.py:302) */
-enum { ROD_ACT_NONE = 0, ROD_ACT_RELU6 = 1, ROD_ACT_LEAKY = 2 };
+ *   LEAKY = tf.nn.leaky_relu, alpha 0.2 (catch_net.py:302)
+ *   RELU  = tf.nn.relu (vgg_arg_scope activation_fn, nets/backbone/vgg.py:58; ABI 9) */
+enum { ROD_ACT_NONE = 0, ROD_ACT_RELU6 = 1, ROD_ACT_LEAKY = 2, ROD_ACT_RELU = 3 };
 
 /* BatchNorm-apply prologue (ABI 3).  rod_conv_fwd, rod_conv_wgrad, rod_dw3x3_fwd and
  * rod_dw3x3_bwd_filter take, right after their input x, the five arguments
@@ -190,6 +191,33 @@ int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const fl
 int rod_bn_bwd_parts(const void* dz, const void* y, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, int act, float* parts, int nparts, long M, int C,
                      int dtype, void* stream);
+
+/* ------------------------------------------------ VGG-16 backbone (F3, ABI 9)
+ * nets/backbone/vgg.py:67-137 (vgg_16 with the SSD extra blocks 6-10).  C % 8 == 0 (bf16) /
+ * C % 4 == 0 (fp32) for all of these.
+ * slim.max_pool2d([2, 2]) — stride 2, VALID (vgg.py:93-101): Ho = H/2, Wo = W/2 (floor);
+ * argmax [N][Ho][Wo][C] uint8 = window position 0..3 (row-major) of the first maximum. */
+int rod_maxpool2x2(const void* x, void* y, uint8_t* argmax, int N, int H, int W, int C, int dtype, void* stream);
+/* MaxPoolGrad: dx[N][H][W][C] = dy at each window's argmax position, 0 elsewhere. */
+int rod_maxpool2x2_bwd(const void* dy, const uint8_t* argmax, void* dx, int N, int H, int W, int C, int dtype,
+                       void* stream);
+/* tf.layers.dropout(rate, training=True) (vgg.py:106, 111; rate = the reference's
+ * dropout_keep_prob = 0.5): binary = floor(keep_prob + U[0,1)), y = x / keep_prob * binary;
+ * U from a counter-based hash of (seed, element index), mask[n] = binary for the backward. */
+int rod_dropout(const void* x, void* y, uint8_t* mask, long n, float keep_prob, uint64_t seed, int dtype,
+                void* stream);
+int rod_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, long n, float keep_prob, int dtype, void* stream);
+/* 3x3 convolution as an explicit column matrix, for the strides / paddings rod_conv_fwd does
+ * not take: custom_layers.pad2d(1) + VALID stride 2 (vgg.py:116-118, 123-125) and VALID stride 1
+ * (vgg.py:131): col[M = N*Ho*Wo][(i*3 + j)*C + c] = x[n, ho*stride + i - pad_t, wo*stride + j -
+ * pad_l, c] (0 outside), read through the optional BatchNorm / activation prologue (ABI 3).
+ * rod_conv_fwd / rod_conv_wgrad with ksize 1 and Cin = 9*C then run the GEMMs. */
+int rod_im2col3x3(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                  const float* pro_beta, int pro_act, void* col, int N, int H, int W, int C, int stride, int pad_t,
+                  int pad_l, int Ho, int Wo, int dtype, void* stream);
+/* dx[N][H][W][C] = the sum of the column-matrix entries that read each input (col2im). */
+int rod_col2im3x3(const void* col, void* dx, int N, int H, int W, int C, int stride, int pad_t, int pad_l, int Ho,
+                  int Wo, int dtype, void* stream);
 
 /* -------------------------------------- dense conv as implicit GEMM (A2 A3 A5)
  * y[m, co] = sum_k A[m, k] * wt[co, k] (+ bias[co]), fp32 accumulation,

@@ -31,9 +31,14 @@ MOBILENET_V2_STRIDES = [1, 1, 2, 1, 2, 1, 1, 2, 1, 1, 1, 2, 1, 1, 1, 2, 1, 1, 2,
 
 
 def feat_sizes(size, backbone_name='mobilenet_v2'):
-    """{'layer_1': (fh, fw), ...} for an input of size (H, W): TF-SAME ceil chain."""
+    """{'layer_1': (fh, fw), ...} for an input of size (H, W): the TF-SAME ceil chain of the
+    MobileNet-v2 strides, or VGG-16's chain (VALID 2x2 pools, pad2d + VALID 3x3 s2, VALID 3x3)."""
+    if backbone_name == 'vgg_16':
+        from nets.backbone.vgg import feat_sizes as vgg_sizes
+        sizes = vgg_sizes(size)
+        return {'layer_%d' % (j + 1): sizes[name] for j, name in enumerate(extract_feat_name['vgg_16'])}
     if backbone_name != 'mobilenet_v2':
-        raise ValueError('feature sizes are derived for mobilenet_v2 only')
+        raise ValueError('unknown backbone %r' % backbone_name)
     h, w = int(size[0]), int(size[1])
     per_layer = {}
     for i, s in enumerate(MOBILENET_V2_STRIDES):

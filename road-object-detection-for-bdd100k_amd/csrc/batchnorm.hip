@@ -904,7 +904,7 @@ int rod_bn_bwd_parts(const void* dz, const void* y, const float* mean, const flo
   ROD_CHECK_ARG(dz != nullptr && y != nullptr && mean != nullptr && rstd != nullptr && parts != nullptr && M > 0 &&
                     C > 0 && nparts > 0 && nparts <= M,
                 "rod_bn_bwd_parts: bad arguments M=%ld C=%d nparts=%d", M, C, nparts);
-  ROD_CHECK_ARG(act >= ROD_ACT_NONE && act <= ROD_ACT_LEAKY, "rod_bn_bwd_parts: bad act %d", act);
+  ROD_CHECK_ARG(act >= ROD_ACT_NONE && act <= ROD_ACT_RELU, "rod_bn_bwd_parts: bad act %d", act);
   BnPro p;
   p.mean = mean;
   p.rstd = rstd;
@@ -957,7 +957,7 @@ int rod_bn_apply(const void* x, const float* mean, const float* rstd, const floa
                  const void* residual, void* y, long M, int C, int ldx, int ldr, int ldy, int act, int dtype,
                  void* stream) {
   ROD_CHECK_ARG(M > 0 && C > 0, "rod_bn_apply: bad shape");
-  ROD_CHECK_ARG(act >= ROD_ACT_NONE && act <= ROD_ACT_LEAKY, "rod_bn_apply: bad act %d", act);
+  ROD_CHECK_ARG(act >= ROD_ACT_NONE && act <= ROD_ACT_RELU, "rod_bn_apply: bad act %d", act);
   if (ldx == 0) ldx = C;
   if (ldy == 0) ldy = C;
   if (ldr == 0) ldr = C;

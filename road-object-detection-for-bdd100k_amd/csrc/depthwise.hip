@@ -12,6 +12,11 @@
 
 namespace rod {
 
+// template value of the prologue activation meaning "any, chosen at run time" (act_fwd);
+// RELU6 gets its own instantiation, -1 = no prologue
+constexpr int DW_ACT_RT = 99;
+
+
 // V contiguous elements of T held in registers (bf16 x4 = 8-byte, f32 x4 = 16-byte loads).
 template <typename T, int V> struct PackV;
 template <> struct PackV<float, 4> {
@@ -1243,11 +1248,11 @@ static void dw_fwd_launch(const void* x, const BnPro* pro, const float* w, void*
 #define DWF(ST, PA)                                                                                              \
   hipLaunchKernelGGL((dw3x3_fwd_kernel<T, S, V, ST, PA>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, pt, \
                      pl, Ho, Wo, parts, pv)
-  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
+  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : DW_ACT_RT);
   if (parts) {
-    if (pa == ROD_ACT_RELU6) DWF(true, ROD_ACT_RELU6); else if (pa == 3) DWF(true, 3); else DWF(true, -1);
+    if (pa == ROD_ACT_RELU6) DWF(true, ROD_ACT_RELU6); else if (pa == DW_ACT_RT) DWF(true, DW_ACT_RT); else DWF(true, -1);
   } else {
-    if (pa == ROD_ACT_RELU6) DWF(false, ROD_ACT_RELU6); else if (pa == 3) DWF(false, 3); else DWF(false, -1);
+    if (pa == ROD_ACT_RELU6) DWF(false, ROD_ACT_RELU6); else if (pa == DW_ACT_RT) DWF(false, DW_ACT_RT); else DWF(false, -1);
   }
 #undef DWF
 }
@@ -1267,13 +1272,13 @@ static long dw_fwd_lx_launch(const void* x, const BnPro* pro, const float* w, vo
   const DwTile t = dw_tile(N, Ho, Wo, C, S, Vec16<T>::N);
   const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
   const BnPro pv = pro ? *pro : BnPro{};
-  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
+  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : DW_ACT_RT);
 #define DWL(S_, PA, ST)                                                                                       \
   hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, S_, PA, ST>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, \
                      pt, pl, Ho, Wo, t, parts, pv)
 #define DWL_PA(S_, ST)                    \
   if (pa == ROD_ACT_RELU6) DWL(S_, ROD_ACT_RELU6, ST); \
-  else if (pa == 3) DWL(S_, 3, ST);       \
+  else if (pa == DW_ACT_RT) DWL(S_, DW_ACT_RT, ST); \
   else DWL(S_, -1, ST)
   if (S == 1) {
     if (parts) { DWL_PA(1, true); } else { DWL_PA(1, false); }
@@ -1345,8 +1350,8 @@ static void dw_bwd_filter_launch(const void* x, const BnPro* pro, const void* dy
 #define DWW(PA)                                                                                                   \
   hipLaunchKernelGGL((dw3x3_bwd_filter_kernel<T, S, V, PA>), dim3(p.gx, p.gy), dim3(256), 256 * V * sizeof(float), \
                      s, (const T*)x, (const T*)dy, slab, N, H, W, C, pt, pl, Ho, Wo, p.RB, p.spi, pv)
-  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
-  if (pa == ROD_ACT_RELU6) DWW(ROD_ACT_RELU6); else if (pa == 3) DWW(3); else DWW(-1);
+  const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : DW_ACT_RT);
+  if (pa == ROD_ACT_RELU6) DWW(ROD_ACT_RELU6); else if (pa == DW_ACT_RT) DWW(DW_ACT_RT); else DWW(-1);
 #undef DWW
   slab_sum(slab, dw, (int)p.parts(), 9L * C, s);
 }
@@ -1493,14 +1498,14 @@ int rod_dw3x3_bwd_filter(const void* x, const float* pro_mean, const float* pro_
     const DwTile t = dw_tile(N, Ho, Wo, C, stride, Vec16<T>::N);
     const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
     const BnPro pv = pp ? *pp : BnPro{};
-    const int pa = !pp ? -1 : (pp->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : 3);
+    const int pa = !pp ? -1 : (pp->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : DW_ACT_RT);
 #define DWW(S_, PA)                                                                                               \
   hipLaunchKernelGGL((dw3x3_bwdw_lx_kernel<T, S_, PA>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, H, W, \
                      C, pad_t, pad_l, Ho, Wo, t, pv)
     if (stride == 1) {
-      if (pa == ROD_ACT_RELU6) DWW(1, ROD_ACT_RELU6); else if (pa == 3) DWW(1, 3); else DWW(1, -1);
+      if (pa == ROD_ACT_RELU6) DWW(1, ROD_ACT_RELU6); else if (pa == DW_ACT_RT) DWW(1, DW_ACT_RT); else DWW(1, -1);
     } else {
-      if (pa == ROD_ACT_RELU6) DWW(2, ROD_ACT_RELU6); else if (pa == 3) DWW(2, 3); else DWW(2, -1);
+      if (pa == ROD_ACT_RELU6) DWW(2, ROD_ACT_RELU6); else if (pa == DW_ACT_RT) DWW(2, DW_ACT_RT); else DWW(2, -1);
     }
 #undef DWW
     slab_sum(slab, dw, (int)((long)N * t.strips * t.coltiles), 9L * C, s);

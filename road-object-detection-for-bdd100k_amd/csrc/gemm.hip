@@ -55,6 +55,7 @@ template <> struct Chunk8<bf16_t> {
   __device__ __forceinline__ void pro(const float* pt, int c, int act) {
     if (act == ROD_ACT_RELU6) pro_t<ROD_ACT_RELU6>(pt, c);
     else if (act == ROD_ACT_LEAKY) pro_t<ROD_ACT_LEAKY>(pt, c);
+    else if (act == ROD_ACT_RELU) pro_t<ROD_ACT_RELU>(pt, c);
     else pro_t<ROD_ACT_NONE>(pt, c);
   }
 };
@@ -93,6 +94,7 @@ template <> struct Chunk8<float> {
   __device__ __forceinline__ void pro(const float* pt, int c, int act) {
     if (act == ROD_ACT_RELU6) pro_t<ROD_ACT_RELU6>(pt, c);
     else if (act == ROD_ACT_LEAKY) pro_t<ROD_ACT_LEAKY>(pt, c);
+    else if (act == ROD_ACT_RELU) pro_t<ROD_ACT_RELU>(pt, c);
     else pro_t<ROD_ACT_NONE>(pt, c);
   }
 };

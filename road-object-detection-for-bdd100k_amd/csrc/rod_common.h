@@ -109,16 +109,19 @@ template <int ACT>
 __device__ __forceinline__ float act_t(float z) {
   if constexpr (ACT == ROD_ACT_RELU6) return __builtin_amdgcn_fmed3f(z, 0.f, 6.f);  // tf.nn.relu6
   else if constexpr (ACT == ROD_ACT_LEAKY) return fmaxf(z, z * 0.2f);                // leaky_relu(0.2)
+  else if constexpr (ACT == ROD_ACT_RELU) return fmaxf(z, 0.f);                      // tf.nn.relu (VGG)
   else return z;
 }
 __device__ __forceinline__ float act_fwd(float z, int act) {
   if (act == ROD_ACT_RELU6) return act_t<ROD_ACT_RELU6>(z);
   if (act == ROD_ACT_LEAKY) return act_t<ROD_ACT_LEAKY>(z);
+  if (act == ROD_ACT_RELU) return act_t<ROD_ACT_RELU>(z);
   return z;
 }
 __device__ __forceinline__ float act_grad(float z, int act) {
   if (act == ROD_ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;  // Relu6Grad
   if (act == ROD_ACT_LEAKY) return z > 0.f ? 1.f : 0.2f;               // LeakyReluGrad
+  if (act == ROD_ACT_RELU) return z > 0.f ? 1.f : 0.f;                 // ReluGrad
   return 1.f;
 }
 

@@ -78,7 +78,7 @@ def main(argv=None):
     config.img_size = (F.img_height, F.img_width)
     dtype = torch.bfloat16 if F.dtype == 'bf16' else torch.float32
     layer_n = len(config.extract_feat_name[F.backbone_name])
-    anchors_all = net_tools.anchors_all_layer(config.img_size, config.feat_sizes(config.img_size),
+    anchors_all = net_tools.anchors_all_layer(config.img_size, config.feat_sizes(config.img_size, F.backbone_name),
                                               net_tools.init_anchor(layer_n))
     config_dict = {'process_backbone_method': config.process_backbone_method.NONE,
                    'deconv_method': config.deconv_method.LEARN_HALF,

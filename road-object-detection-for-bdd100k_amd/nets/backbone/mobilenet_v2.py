@@ -71,6 +71,10 @@ class MobilenetV2:
             store.add(base + '/project/weights', trunc_normal(rng, (cout, 1, 1, inner), W_STD))
             self._bn(base + '/project/BatchNorm', cout)
 
+    def endpoint_channels(self, names):
+        outs = {'layer_%d' % idx: cout for (idx, _, _, _, _, cout, _, _) in self.plan}
+        return [outs[n] for n in names]
+
     def _bn(self, name, c):
         self.store.add(name + '/gamma', np.ones(c, np.float32))
         self.store.add(name + '/beta', np.zeros(c, np.float32))

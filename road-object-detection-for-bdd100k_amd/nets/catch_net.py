@@ -21,6 +21,7 @@ import torch
 
 import config
 from nets.backbone.mobilenet_v2 import MobilenetV2
+from nets.backbone.vgg import VGG16
 from rod import graph, ops
 from rod.params import ParamStore, trunc_normal, xavier_uniform
 
@@ -37,8 +38,8 @@ class CatchNet:
     """Parameters + forward of the whole detector for one configuration."""
 
     def __init__(self, backbone_name, config_dict, device, seed=0, build_all=None):
-        if backbone_name != 'mobilenet_v2':
-            raise ValueError('backbone %r is not built by this framework (see DESIGN.md)' % backbone_name)
+        if backbone_name not in config.supported_backbone_name:
+            raise ValueError('backbone %r is not supported (config.supported_backbone_name)' % backbone_name)
         if config_dict['process_backbone_method'] is not config.process_backbone_method.NONE:
             raise ValueError('Not support the method(%s) now' % str(config_dict['process_backbone_method']))
         self.backbone_name = backbone_name
@@ -48,7 +49,7 @@ class CatchNet:
         self.all_mode = all_mode
         rng = np.random.default_rng(seed)
         self.store = ParamStore()
-        self.backbone = MobilenetV2(self.store, rng)
+        self.backbone = MobilenetV2(self.store, rng) if backbone_name == 'mobilenet_v2' else VGG16(self.store, rng)
         self.feat_ch = self._endpoint_channels()
         self.n_anchor = n_anchor_each_layer(backbone_name)
         self._head('refine', self.feat_ch, 4, rng)
@@ -70,8 +71,7 @@ class CatchNet:
 
     # ------------------------------------------------------------------ parameters
     def _endpoint_channels(self):
-        outs = {'layer_%d' % idx: cout for (idx, _, _, _, _, cout, _, _) in self.backbone.plan}
-        return [outs[n] for n in config.extract_feat_name[self.backbone_name]]
+        return self.backbone.endpoint_channels(config.extract_feat_name[self.backbone_name])
 
     def _head_bn(self, name, c):
         self.store.add(name + '/beta', np.zeros(c, np.float32))

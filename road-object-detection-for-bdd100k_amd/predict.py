@@ -55,18 +55,19 @@ class Predictor(object):
     """Forward + decode + per-class NMS; reused by bench (inference FPS)."""
 
     def __init__(self, img_size, device, dtype=torch.float32, checkpoint=None, select_threshold=0.1,
-                 nms_threshold=0.4, top_k=400, keep_top_k=200, seed=0):
+                 nms_threshold=0.4, top_k=400, keep_top_k=200, seed=0, backbone_name='mobilenet_v2'):
         from nets.catch_net import CatchNet
         from utils import net_tools
         config.img_size = tuple(img_size)
         self.config_dict = {'process_backbone_method': config.process_backbone_method.NONE,
                             'deconv_method': config.deconv_method.LEARN_HALF,
                             'merge_method': config.merge_method.ADD, 'train_range': config.train_range.ALL}
-        self.net = CatchNet('mobilenet_v2', self.config_dict, device, seed)
+        self.backbone_name = backbone_name
+        self.net = CatchNet(backbone_name, self.config_dict, device, seed)
         if checkpoint is not None:
             from rod.checkpoint import load_variables
             load_variables(self.net.store, checkpoint)
-        self.anchors = net_tools.anchors_all_layer(config.img_size, config.feat_sizes(config.img_size),
+        self.anchors = net_tools.anchors_all_layer(config.img_size, config.feat_sizes(config.img_size, backbone_name),
                                                    net_tools.init_anchor(6))
         self.dtype = dtype
         self.keep_intermediates = False   # tests: keep (logits, probs, boxes) of the last call
@@ -84,7 +85,7 @@ class Predictor(object):
         from rod import ops
         from rod.dataio import network_input
         x = network_input(img_u8, self.dtype)
-        refine_out, det_out, clf_out = factory(x, 'mobilenet_v2', False, self.config_dict, self.dtype,
+        refine_out, det_out, clf_out = factory(x, self.backbone_name, False, self.config_dict, self.dtype,
                                                net=self.net).get_output()
         probs = net_tools.class_probabilities(clf_out)                                     # predict.py:127-128
         boxes = net_tools.decode_all_layers(self.anchors, refine_out, det_out, to_corner=True)  # 130-134
@@ -134,7 +135,7 @@ def main(argv=None):
                                     % F.checkpoint_all)
         logger.warning('--synthetic: checkpoint %r not found, predicting with random weights', F.checkpoint_all)
     pred = Predictor((F.img_height, F.img_width), dev, dtype, ckpt, F.select_threshold, F.nms_threshold, F.top_k,
-                     F.keep_top_k)
+                     F.keep_top_k, backbone_name=F.backbone_name)
     logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
     source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, synthetic=F.synthetic, dtype=dtype,
                          num_readers=F.num_readers)

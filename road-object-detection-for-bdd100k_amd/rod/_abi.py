@@ -33,10 +33,12 @@ ROD_BF16 = 1
 ROD_ACT_NONE = 0
 ROD_ACT_RELU6 = 1
 ROD_ACT_LEAKY = 2
+ROD_ACT_RELU = 3
 
 _CTYPE = {
     "int": ctypes.c_int,
     "long": ctypes.c_long,
+    "uint64_t": ctypes.c_uint64,
     "float": ctypes.c_float,
     "size_t": ctypes.c_size_t,
     "ptr": ctypes.c_void_p,

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import _abi
-from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU6  # noqa: F401
+from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU, ROD_ACT_RELU6  # noqa: F401
 
 _DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
 # debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro
@@ -947,6 +947,11 @@ class _Deconv2x2(torch.autograd.Function):
 
 
 def deconv2x2(x, w, size):
+    # TF's conv2d_transpose (SAME, stride 2) requires in = ceil(out / 2); it raises otherwise
+    # (e.g. VGG-16's VALID chain at 720x1280: 4x8 -> 6x10)
+    if x.shape[1] != -(-int(size[0]) // 2) or x.shape[2] != -(-int(size[1]) // 2):
+        raise ValueError('conv2d_transpose: input %s does not match output %s (stride 2, SAME)' %
+                         (tuple(x.shape[1:3]), tuple(size)))
     return _Deconv2x2.apply(x, w, int(size[0]), int(size[1]))
 
 
@@ -1189,3 +1194,179 @@ def select_topk_nms(probs, boxes, select_threshold, top_k, keep_top_k, nms_thres
     _abi.call("rod_select_topk_nms", probs.contiguous(), boxes.contiguous(), B, A, K, float(select_threshold),
               int(top_k), int(keep_top_k), float(nms_threshold), scores, bxs, ws, stream())
     return scores, bxs
+
+
+# ----------------------------------------------------------------------------- VGG-16 ops (F3)
+# slim.conv2d with activation_fn and no normaliser (vgg_arg_scope: relu, nets/backbone/vgg.py:58):
+# the conv's output y is left as an owned Pending with an identity BatchNorm (mean 0, rstd 1,
+# no gamma / beta) and act = RELU, so consumers apply relu(y*1 + 0) = relu(y) exactly in their
+# load prologue and the node's backward forms dy = dz * relu'(y) itself (rod_bn_bwd_apply with
+# coefficients (1, 0, 0): dy = 1 * (g - 0 - yhat * 0) = g).
+_IDENT = {}
+
+
+def _ident_bn(C, device):
+    key = (int(C), str(device))
+    if key not in _IDENT:
+        zeros = torch.zeros(C, dtype=torch.float32, device=device)
+        ones = torch.ones(C, dtype=torch.float32, device=device)
+        coef = torch.zeros(3 * C, dtype=torch.float32, device=device)
+        coef[:C] = 1.0
+        _IDENT[key] = (zeros, ones, coef)
+    return _IDENT[key]
+
+
+def _prep_flat(w, mode, dtype):
+    """GEMM operand of a [Cout, 3, 3, Cin] weight viewed as a 1x1 conv over 9*Cin columns:
+    mode 0 -> [Cout][9*Cin], mode 1 -> [9*Cin][Cout] (rod_conv_weight_prep, ksize 1)."""
+    Cout, K = w.shape[0], w[0].numel()
+    wt = torch.empty((Cout, K) if mode == 0 else (K, Cout), dtype=dtype, device=w.device)
+    _abi.call("rod_conv_weight_prep", w, wt, Cout, K, 1, mode, dtcode(wt), stream())
+    return wt
+
+
+class _ConvAct(torch.autograd.Function):
+    """slim.conv2d(+bias, activation_fn=act) as one node; geo None = SAME stride 1 (implicit
+    GEMM, ksize 1 / 3), else (stride, pad_t, pad_l, Ho, Wo) for a 3x3 conv through the column
+    matrix (rod_im2col3x3 -> GEMM with ksize 1; vgg.py:116-131)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, ks, ipro, act, geo):
+        N, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        col = None
+        if geo is None:
+            wt = _prep(w, 0, x.dtype, Cout, Cin, ks)
+            y = torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
+            conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ks, None, ipro)
+        else:
+            s, pt, pl, Ho, Wo = geo
+            col = torch.empty((N, Ho, Wo, 9 * Cin), dtype=x.dtype, device=x.device)
+            _abi.call("rod_im2col3x3", x, *_pro_args(ipro), col, N, H, W, Cin, s, pt, pl, Ho, Wo, dtcode(x), stream())
+            y = torch.empty((N, Ho, Wo, Cout), dtype=x.dtype, device=x.device)
+            conv_fwd_raw(col, _prep_flat(w, 0, x.dtype), b, y, N, Ho, Wo, 9 * Cin, Cout, 1)
+        ctx.save_for_backward(x, w, b, y, col)
+        ctx.ks, ctx.ipro, ctx.act, ctx.geo = ks, ipro, act, geo
+        ctx.set_materialize_grads(False)
+        return y
+
+    @staticmethod
+    def backward(ctx, dz):
+        if dz is None:
+            return (None,) * 7
+        x, w, b, y, col = ctx.saved_tensors
+        C = y.shape[-1]
+        zeros, ones, coef = _ident_bn(C, y.device)
+        dy = torch.empty_like(y)
+        _abi.call("rod_bn_bwd_apply", dz.contiguous(), y, zeros, ones, None, None, coef, dy, y.numel() // C, C,
+                  ctx.act, dtcode(y), stream())
+        need_dx = ctx.needs_input_grad[0]
+        if ctx.geo is None:
+            return _conv_bwd_from_dy(x, w, b, ctx.ks, dy, ctx.ipro, need_dx), None, None, None, None, None, None
+        N, H, W, Cin = x.shape
+        s, pt, pl, Ho, Wo = ctx.geo
+        Cout = w.shape[0]
+        dx = None
+        if need_dx:
+            dcol = torch.empty_like(col)
+            conv_fwd_raw(dy, _prep_flat(w, 1, x.dtype), None, dcol, N, Ho, Wo, Cout, 9 * Cin, 1)
+            dx = torch.empty_like(x)
+            _abi.call("rod_col2im3x3", dcol, dx, N, H, W, Cin, s, pt, pl, Ho, Wo, dtcode(x), stream())
+        need_w, need_bias = _needs(w), _needs(b)
+        if need_w or need_bias:
+            gw = grad_slot(w) if need_w else torch.empty(w.shape, dtype=torch.float32, device=x.device)
+            gb = grad_slot(b) if need_bias else None
+            ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, Ho, Wo, 9 * Cin, Cout, 1), x.device)
+            _abi.call("rod_conv_wgrad", col, *_pro_args(None), dy, gw, gb, ws, N, Ho, Wo, 9 * Cin, Cout, 1, 0, 0,
+                      dtcode(x), stream())
+            if need_w:
+                _mark_written(w)
+            if need_bias:
+                _mark_written(b)
+        return dx, None, None, None, None, None, None
+
+
+def conv2d_act(x, w, b, ksize, act=ROD_ACT_RELU, stride=1, padding='SAME', pad=0, training=True):
+    """slim.conv2d(x, Cout, [k, k], stride, padding, activation_fn=act) with no normaliser.
+    padding 'SAME' with stride 1 runs the implicit GEMM; 'VALID' (after an explicit symmetric
+    `pad`, custom_layers.pad2d) or stride 2 runs through the column matrix.  Returns an owned
+    Pending (identity BatchNorm + act) for the consumer's load prologue."""
+    xt, ipro = _in_pro(x)
+    N, H, W, Cin = xt.shape
+    geo = None
+    if not (padding == 'SAME' and stride == 1 and pad == 0):
+        assert ksize == 3, 'strided / VALID convs are 3x3 in the reference (vgg.py:116-131)'
+        if padding == 'SAME':
+            Ho, pt = same_pad(H, stride)
+            Wo, pl = same_pad(W, stride)
+        else:   # explicit pad then VALID
+            Ho, Wo = (H + 2 * pad - 3) // stride + 1, (W + 2 * pad - 3) // stride + 1
+            pt = pl = pad
+        if Ho <= 0 or Wo <= 0:
+            raise ValueError('conv2d_act: input %dx%d too small for a 3x3 VALID conv' % (H, W))
+        geo = (stride, pt, pl, Ho, Wo)
+    y = _ConvAct.apply(xt, w, b, ksize, ipro, act, geo)
+    zeros, ones, _ = _ident_bn(y.shape[-1], y.device)
+    return Pending(y, zeros, ones, None, None, act, training, owned=True)
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        N, H, W, C = x.shape
+        x = x.contiguous()
+        y = torch.empty((N, H // 2, W // 2, C), dtype=x.dtype, device=x.device)
+        am = torch.empty((N, H // 2, W // 2, C), dtype=torch.uint8, device=x.device)
+        _abi.call("rod_maxpool2x2", x, y, am, N, H, W, C, dtcode(x), stream())
+        ctx.save_for_backward(am)
+        ctx.geo = (N, H, W, C)
+        ctx.mark_non_differentiable(am)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (am,) = ctx.saved_tensors
+        N, H, W, C = ctx.geo
+        dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+        _abi.call("rod_maxpool2x2_bwd", dy.contiguous(), am, dx, N, H, W, C, dtcode(dy), stream())
+        return dx
+
+
+def max_pool2x2(x):
+    """slim.max_pool2d(x, [2, 2]) — stride 2, VALID (vgg.py:93-101)."""
+    return _MaxPool.apply(materialize(x))
+
+
+_DROPOUT_CALLS = [0]
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, keep, seed):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+        _abi.call("rod_dropout", x, y, mask, x.numel(), float(keep), int(seed), dtcode(x), stream())
+        ctx.save_for_backward(mask)
+        ctx.keep = keep
+        ctx.mark_non_differentiable(mask)
+        return y, mask
+
+    @staticmethod
+    def backward(ctx, dy, _dmask):
+        (mask,) = ctx.saved_tensors
+        dx = torch.empty_like(dy)
+        _abi.call("rod_dropout_bwd", dy.contiguous(), mask, dx, dy.numel(), float(ctx.keep), dtcode(dy), stream())
+        return dx, None, None
+
+
+def dropout(x, rate, training, seed=None):
+    """tf.layers.dropout(x, rate, training) (vgg.py:106, 111).  Returns (y, mask or None); the
+    seed defaults to a per-process call counter (every call draws a fresh mask)."""
+    x = materialize(x)
+    if not training or rate == 0.0:
+        return x, None
+    if seed is None:
+        _DROPOUT_CALLS[0] += 1
+        seed = 0x5EED0000 + _DROPOUT_CALLS[0]
+    return _Dropout.apply(x, 1.0 - float(rate), seed)

@@ -29,7 +29,7 @@ class Trainer:
     def __init__(self, img_size, batch_size, dtype=torch.bfloat16, train_range=config.train_range.REFINE,
                  learning_rate=1e-3, device='cuda', fix_refine=True, seed=0, world_size=1, reducer=None,
                  deconv_method=config.deconv_method.LEARN_HALF, merge_method=config.merge_method.ADD,
-                 sync_bn=False):
+                 sync_bn=False, backbone_name='mobilenet_v2'):
         self.img_size = tuple(img_size)
         self.batch_size = batch_size          # per-rank batch
         self.world_size = world_size
@@ -40,9 +40,10 @@ class Trainer:
                             'process_backbone_method': config.process_backbone_method.NONE,
                             'deconv_method': deconv_method,     # train.py:131-133 defaults
                             'merge_method': merge_method}
-        self.net = CatchNet('mobilenet_v2', self.config_dict, self.device, seed)
-        layer_n = len(config.extract_feat_name['mobilenet_v2'])
-        self.anchors = net_tools.anchors_all_layer(self.img_size, config.feat_sizes(self.img_size),
+        self.backbone_name = backbone_name
+        self.net = CatchNet(backbone_name, self.config_dict, self.device, seed)
+        layer_n = len(config.extract_feat_name[backbone_name])
+        self.anchors = net_tools.anchors_all_layer(self.img_size, config.feat_sizes(self.img_size, backbone_name),
                                                    net_tools.init_anchor(layer_n))
         self.table = net_tools.anchor_table(self.anchors, self.device)
         store = self.net.store
@@ -84,7 +85,7 @@ class Trainer:
         center = cornerBboxes_2_centerBboxes(gt_corner)              # train.py:109
         tg = net_tools.refine_groundtruth(self.anchors, center, gt_labels, config.refine_method.JACCARD_BIGGER,
                                           n_boxes=gt_n)
-        out = factory(x, 'mobilenet_v2', True, self.config_dict, self.dtype, net=self.net).get_output()
+        out = factory(x, self.backbone_name, True, self.config_dict, self.dtype, net=self.net).get_output()
         scale = float(self.batch_size * self.world_size)
         if self.train_range is config.train_range.REFINE:
             loss = net_tools.refine_loss(out, tg[0], tg[3], targets=tg, scale=scale)

@@ -51,6 +51,9 @@ def parse(argv=None):
     ap.add_argument('--save_every_n_steps', type=int, default=2000)
     ap.add_argument('--fix_refine', type=str2bool, default=True)
     # additions
+    ap.add_argument('--sync_bn', type=str2bool, default=False,
+                    help='data parallel: BatchNorm statistics over the global batch (default per rank; '
+                         'the reference runs on one device)')
     ap.add_argument('--train_range', default='REFINE', choices=['REFINE', 'ALL'])
     ap.add_argument('--img_height', type=int, default=config.img_size[0])
     ap.add_argument('--img_width', type=int, default=config.img_size[1])
@@ -106,7 +109,8 @@ def main(argv=None):
     logger.info('Building model, using backbone---%s' % F.backbone_name)
     trainer = Trainer(config.img_size, F.batch_size, dtype=dtype, train_range=tr_range, learning_rate=F.learning_rate,
                       device=dev, fix_refine=F.fix_refine, seed=F.seed, world_size=world,
-                      reducer=GradReducer(world) if world > 1 else None)
+                      reducer=GradReducer(world) if world > 1 else None, backbone_name=F.backbone_name,
+                      sync_bn=F.sync_bn)
     store = trainer.net.store
     logger.info('Total trainable parameters:%s' % str(store.trainable_count()))
     step0 = 0

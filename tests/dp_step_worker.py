@@ -73,7 +73,8 @@ def main():
         dec[1], dec[2] = st[5], st[6]
     if world > 1:
         torch.distributed.all_reduce(lv)
-        torch.distributed.all_reduce(dec[:1])
+        dec[1] /= world                   # k is global already (identical on every rank)
+        torch.distributed.all_reduce(dec)
     torch.cuda.synchronize()
     if rank == 0:
         store = tr.net.store

@@ -6,7 +6,7 @@ With sync_bn the losses, the moving averages and the SGD result must match the s
 process within fp32 reordering (1e-4), the SGD step is bit-exact given the reduced gradient,
 and every parameter gradient and moving average within
 max(1e-4, 4x the step's own fp32 sensitivity) normwise — the sensitivity being how far the
-single-process gradient moves under 1e-6 relative noise on its input (two draws): ReLU6 /
+single-process gradient moves under 1e-6 / 1e-5 relative noise on its input: ReLU6 /
 leaky kinks near zero and BatchNorm over the few rows of the deepest maps (3x5 at 320x576) make
 single gradient entries move by percents under ANY fp32 reordering (the kernels also pick
 other split-K / slab plans for B/2 rows), as in test_gpu_train.py.  Without sync_bn (the per-rank default) the deviation is
@@ -35,9 +35,9 @@ def _port():
     return p
 
 
-def _run(out, world, train_range, sync, perturb_seed=None):
+def _run(out, world, train_range, sync, perturb_seed=None, amp=1e-6):
     args = [WORKER, '--out', out, '--train_range', train_range] + (['--sync_bn'] if sync else []) + \
-        (['--perturb', '1e-6', '--perturb_seed', str(perturb_seed)] if perturb_seed is not None else [])
+        (['--perturb', str(amp), '--perturb_seed', str(perturb_seed)] if perturb_seed is not None else [])
     if world == 1:
         cmd = [sys.executable] + args
     else:
@@ -56,7 +56,11 @@ def _nerr(a, b):
 @pytest.mark.parametrize('train_range', ['REFINE', 'ALL'])
 def test_two_ranks_equal_one_process(train_range, tmp_path, dev):
     one = _run(str(tmp_path / 'one.pt'), 1, train_range, False)
-    pert = [_run(str(tmp_path / f'p{s}.pt'), 1, train_range, False, perturb_seed=s) for s in (11, 12)]
+    # sensitivity: 1e-6 and 1e-5 relative input noise, two draws each.  In ALL mode the det /
+    # clf head gradients are sums over the few ODM-positive rows, so one leaky-ReLU sign flip
+    # at those rows moves a whole head tensor by percents
+    pert = [_run(str(tmp_path / f'p{s}_{a}.pt'), 1, train_range, False, perturb_seed=s, amp=a)
+            for s in (11, 12) for a in (1e-6, 1e-5)]
     two = _run(str(tmp_path / 'two.pt'), 2, train_range, True)
     per = _run(str(tmp_path / 'per.pt'), 2, train_range, False)
     print(f"{train_range}: decisions (ODM positives, k, selected negatives): one {one['decisions'].tolist()} "

@@ -42,3 +42,27 @@ def test_unknown_methods_raise():
            'deconv_method': 'bogus', 'merge_method': _MM.ADD}
     with pytest.raises(ValueError):
         CatchNet('mobilenet_v2', cfg, 'cpu', 0)
+
+
+def test_vgg_params_and_sizes_match_reference_and_oracle():
+    """VGG-16 (vgg.py:67-137): the tapped sizes at 418x418 equal the reference's own table
+    (config.feat_size_all_layers['vgg_16'], config.py:36-37), and the oracle consumes exactly
+    the product's backbone + refine-head parameters."""
+    from oracle import vgg as ovgg
+    assert config.feat_sizes((418, 418), 'vgg_16') == config.feat_size_all_layers['vgg_16']
+    cfg = {'train_range': config.train_range.REFINE, 'process_backbone_method': config.process_backbone_method.NONE,
+           'deconv_method': _DM.LEARN_HALF, 'merge_method': _MM.ADD}
+    net = CatchNet('vgg_16', cfg, 'cpu', 0)
+    assert net.feat_ch == [512, 512, 1024, 512, 256, 256]
+    P = {k: v.detach().clone().double() for k, v in net.store.params.items()}
+    B = {k: v.detach().clone().double() for k, v in net.store.buffers.items()}
+    used = set()
+
+    class Tracker(dict):
+        def __getitem__(self, k):
+            used.add(k)
+            return dict.__getitem__(self, k)
+    out = ovgg.forward(torch.zeros((1, 288, 512, 3), dtype=torch.float64), Tracker(P), B, False)
+    assert used == set(P)
+    sizes = config.feat_sizes((288, 512), 'vgg_16')
+    assert [tuple(o.shape[1:3]) for o in out] == [sizes['layer_%d' % (i + 1)] for i in range(6)]
