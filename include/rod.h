@@ -325,6 +325,12 @@ int rod_match_anchors(const float* anc_corner, const float* anc_center, const in
                       const float* thr, int L, const float* gt, const int* gt_lbl,
                       const int* gt_n, float* out_off, float* out_cbox, int* out_lbl,
                       int* out_pos, int B, int A, int G, void* stream);
+/* NEAREST_NEIGHBOR (net_tools.py:354-380, ABI 9): the box of least sum of squared encoded
+ * offsets (tf.argmin, first minimum wins) is matched to EVERY anchor (pos_mask = ones);
+ * same arrays as rod_match_anchors without the thresholds. */
+int rod_match_anchors_nn(const float* anc_corner, const float* anc_center, const int* lvl_off, int L, const float* gt,
+                         const int* gt_lbl, const int* gt_n, float* out_off, float* out_cbox, int* out_lbl,
+                         int* out_pos, int B, int A, int G, void* stream);
 /* Masked smooth-L1 (net_tools.py:478-516): per-level sums of
  * smooth_l1((target - pred)*mask) / scale written to loss_lvl[0..L-1] and their
  * sum (accumulated in level order) to loss_lvl[L] (fp32, device, L+1 entries),

@@ -92,6 +92,35 @@ def refine_groundtruth(anchors_all, center_bboxes, labels, thresholds):
     return gt_l, cb_l, lb_l, pm_l
 
 
+def refine_groundtruth_nn(anchors_all, center_bboxes, labels):
+    """NEAREST_NEIGHBOR (net_tools.py:354-380) for ONE image: per anchor, the box with the
+    least sum of squared encoded offsets (argmin, first minimum; the 4-term sum in index order),
+    the masked sum over boxes, pos_mask = ones."""
+    cb = np.asarray(center_bboxes, np.float32)
+    lab = np.asarray(labels)
+    gt_l, cb_l, lb_l, pm_l = [], [], [], []
+    with np.errstate(all='ignore'):
+        for layer in anchors_all:
+            loc = np.stack([encode(layer, cb[i]) for i in range(cb.shape[0])], 0)   # [G, fh, fw, A, 4]
+            sq = loc * loc
+            dist = ((sq[..., 0] + sq[..., 1]) + sq[..., 2]) + sq[..., 3]
+            idx = dist.argmin(0)
+            shp = idx.shape
+            gt = np.zeros(shp + (4,), np.float32)
+            cbox = np.zeros(shp + (4,), np.float32)
+            lbl = np.zeros(shp + (1,), np.int32)
+            for i in range(cb.shape[0]):
+                mask = (idx == i).astype(np.float32)[..., None]
+                cbox = cbox + mask * cb[i]
+                gt = gt + mask * loc[i]
+                lbl = lbl + mask.astype(np.int32) * np.int32(lab[i])
+            gt_l.append(gt)
+            cb_l.append(cbox)
+            lb_l.append(lbl)
+            pm_l.append(np.ones(shp + (1,), np.int32))
+    return gt_l, cb_l, lb_l, pm_l
+
+
 def smooth_l1(x):
     """net_tools.py:478-489."""
     x = np.asarray(x, np.float32)

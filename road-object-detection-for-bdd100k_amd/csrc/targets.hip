@@ -19,6 +19,10 @@ struct LevelInfo {
 
 // One workgroup per (anchor block, image).  The image's centre-form GT boxes are staged
 // in LDS together with their corner form and area.
+// NN = false: JACCARD_BIGGER (net_tools.py:382-421): argmax IoU, positive if >= the level's
+// threshold.  NN = true: NEAREST_NEIGHBOR (net_tools.py:354-380): argmin over the boxes of
+// sum(encode(anchor, box)^2) (tf.argmin, first minimum), every anchor positive.
+template <bool NN>
 __global__ void __launch_bounds__(256) match_anchors_kernel(const float* __restrict__ anc_corner,
                                                             const float* __restrict__ anc_center, LevelInfo li,
                                                             const float* __restrict__ gt, const int* __restrict__ gt_lbl,
@@ -73,6 +77,19 @@ __global__ void __launch_bounds__(256) match_anchors_kernel(const float* __restr
 
   float best = 0.f;
   int idx = 0;
+  if constexpr (NN) {
+    const f32x4 az = *(const f32x4*)(anc_center + (long)a * 4);
+    for (int g = 0; g < n; ++g) {
+      const float o0 = (gz[g * 4 + 0] - az[0]) / az[2], o1 = (gz[g * 4 + 1] - az[1]) / az[3];
+      const float o2 = log_cr(gz[g * 4 + 2] / az[2]), o3 = log_cr(gz[g * 4 + 3] / az[3]);
+      // reduce_sum over the 4 offsets, in index order (parity unpinned vs Eigen's order)
+      const float d = ((o0 * o0 + o1 * o1) + o2 * o2) + o3 * o3;
+      if (g == 0 || d < best) {
+        best = d;
+        idx = g;
+      }
+    }
+  } else {
   for (int g = 0; g < n; ++g) {
     const float iy0 = fmaxf(aymin, gc[g * 4 + 0]);
     const float ix0 = fmaxf(axmin, gc[g * 4 + 1]);
@@ -88,7 +105,9 @@ __global__ void __launch_bounds__(256) match_anchors_kernel(const float* __restr
       idx = g;
     }
   }
-  const bool pos = n > 0 && best >= li.thr[lvl];  // tf.greater_equal (net_tools.py:406)
+  }
+  // tf.greater_equal (net_tools.py:406); NEAREST_NEIGHBOR: pos_mask = ones (net_tools.py:375)
+  const bool pos = n > 0 && (NN || best >= li.thr[lvl]);
 
   const long o = (long)b * A + a;
   float off[4] = {0.f, 0.f, 0.f, 0.f}, cb[4] = {0.f, 0.f, 0.f, 0.f};
@@ -254,9 +273,24 @@ int rod_match_anchors(const float* anc_corner, const float* anc_center, const in
   int e = fill_levels(li, lvl_off, thr, L, A);
   if (e) return e;
   size_t lds = (size_t)G * 10 * sizeof(float);
-  hipLaunchKernelGGL(match_anchors_kernel, dim3(cdiv(A, 256), B), dim3(256), lds, ROD_STREAM(stream), anc_corner,
-                     anc_center, li, gt, gt_lbl, gt_n, out_off, out_cbox, out_lbl, out_pos, A, G);
+  hipLaunchKernelGGL(match_anchors_kernel<false>, dim3(cdiv(A, 256), B), dim3(256), lds, ROD_STREAM(stream),
+                     anc_corner, anc_center, li, gt, gt_lbl, gt_n, out_off, out_cbox, out_lbl, out_pos, A, G);
   return check_launch("rod_match_anchors");
+}
+
+int rod_match_anchors_nn(const float* anc_corner, const float* anc_center, const int* lvl_off, int L, const float* gt,
+                         const int* gt_lbl, const int* gt_n, float* out_off, float* out_cbox, int* out_lbl,
+                         int* out_pos, int B, int A, int G, void* stream) {
+  ROD_CHECK_ARG(B > 0 && A > 0 && G > 0, "rod_match_anchors_nn: bad shape B=%d A=%d G=%d", B, A, G);
+  ROD_CHECK_ARG(G <= 4096, "rod_match_anchors_nn: G=%d exceeds 4096", G);
+  ROD_CHECK_ARG(lvl_off, "rod_match_anchors_nn: lvl_off is a host array and must be given");
+  LevelInfo li;
+  int e = fill_levels(li, lvl_off, nullptr, L, A);
+  if (e) return e;
+  size_t lds = (size_t)G * 10 * sizeof(float);
+  hipLaunchKernelGGL(match_anchors_kernel<true>, dim3(cdiv(A, 256), B), dim3(256), lds, ROD_STREAM(stream),
+                     anc_corner, anc_center, li, gt, gt_lbl, gt_n, out_off, out_cbox, out_lbl, out_pos, A, G);
+  return check_launch("rod_match_anchors_nn");
 }
 
 static int smoothl1_nbx(int B, const LevelInfo& li) {

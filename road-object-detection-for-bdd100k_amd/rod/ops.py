@@ -867,7 +867,9 @@ def boxes_convert(boxes: torch.Tensor, to_center: bool) -> torch.Tensor:
     return out
 
 
-def match_anchors(anc_corner, anc_center, lvl_off, thr, gt_center, gt_lbl, gt_n):
+def match_anchors(anc_corner, anc_center, lvl_off, thr, gt_center, gt_lbl, gt_n, nearest=False):
+    """rod_match_anchors (JACCARD_BIGGER, thresholds thr) or, nearest=True, rod_match_anchors_nn
+    (NEAREST_NEIGHBOR, thr unused)."""
     B, G, _ = gt_center.shape
     A = anc_corner.shape[0]
     dev = gt_center.device
@@ -875,9 +877,14 @@ def match_anchors(anc_corner, anc_center, lvl_off, thr, gt_center, gt_lbl, gt_n)
     cbox = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
     lbl = torch.empty((B, A), dtype=torch.int32, device=dev)
     pos = torch.empty((B, A), dtype=torch.int32, device=dev)
-    _abi.call("rod_match_anchors", anc_corner, anc_center, np.ascontiguousarray(lvl_off, dtype=np.int32),
-              np.ascontiguousarray(thr, dtype=np.float32), len(lvl_off) - 1, gt_center.contiguous(),
-              gt_lbl.contiguous(), gt_n.contiguous(), off, cbox, lbl, pos, B, A, G, stream())
+    lo = np.ascontiguousarray(lvl_off, dtype=np.int32)
+    if nearest:
+        _abi.call("rod_match_anchors_nn", anc_corner, anc_center, lo, len(lvl_off) - 1, gt_center.contiguous(),
+                  gt_lbl.contiguous(), gt_n.contiguous(), off, cbox, lbl, pos, B, A, G, stream())
+    else:
+        _abi.call("rod_match_anchors", anc_corner, anc_center, lo, np.ascontiguousarray(thr, dtype=np.float32),
+                  len(lvl_off) - 1, gt_center.contiguous(), gt_lbl.contiguous(), gt_n.contiguous(), off, cbox, lbl,
+                  pos, B, A, G, stream())
     return off, cbox, lbl, pos
 
 

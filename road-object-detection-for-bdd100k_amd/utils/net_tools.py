@@ -118,17 +118,16 @@ def anchor_table(anchors_all, device) -> AnchorTable:
 
 # ================================================================ targets
 def refine_groundtruth(anchors_all_layer, center_bboxes, labels, method, n_boxes=None, scope="refine_encode"):
-    """JACCARD_BIGGER target assignment (net_tools.py:270-428) on the GPU.
+    """Target assignment (net_tools.py:270-428) on the GPU: JACCARD_BIGGER (382-421) or
+    NEAREST_NEIGHBOR (354-380, every anchor positive).
 
     center_bboxes: [B, G, 4] (or [G, 4]) (yc, xc, h, w); labels [B, G]; n_boxes [B]
     valid boxes per image (default: G).  Returns (gt_list, cbboxes_list, labels_list,
     pos_mask_list) of per-layer views [B, fh, fw, A, 4|1].
     """
-    if method == config.refine_method.NEAREST_NEIGHBOR:
-        raise ValueError('NEAREST_NEIGHBOR matching is not on the hot path (DESIGN.md, out of scope)')
     if method == config.refine_method.JACCARD_TOPK:
         raise ValueError('Not support now')
-    if method != config.refine_method.JACCARD_BIGGER:
+    if method not in (config.refine_method.JACCARD_BIGGER, config.refine_method.NEAREST_NEIGHBOR):
         raise ValueError('Function parameter "method" wrong')
     single = center_bboxes.dim() == 2
     if single:
@@ -141,7 +140,8 @@ def refine_groundtruth(anchors_all_layer, center_bboxes, labels, method, n_boxes
     off, cbox, lbl, pos = ops.match_anchors(tab.corner, tab.center, tab.lvl_off,
                                             config.refine_pos_jac_val_all_layers[:len(tab.shapes)],
                                             center_bboxes.float(), labels.to(torch.int32),
-                                            n_boxes.to(torch.int32))
+                                            n_boxes.to(torch.int32),
+                                            nearest=method == config.refine_method.NEAREST_NEIGHBOR)
     res = (tab.split(off, 4), tab.split(cbox, 4), tab.split(lbl[..., None], 1), tab.split(pos[..., None], 1))
     res = RefineTargets(*res)
     res.flat = (off, cbox, lbl, pos)

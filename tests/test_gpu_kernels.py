@@ -292,6 +292,30 @@ def test_match_anchors_bit_exact(dev, H, W, degenerate):
     assert total_pos > 50
 
 
+@pytest.mark.parametrize('H,W', [(300, 300), (418, 418)])
+@pytest.mark.parametrize('degenerate', [False, True])
+def test_match_anchors_nearest_neighbor_bit_exact(dev, H, W, degenerate):
+    """refine_method.NEAREST_NEIGHBOR (net_tools.py:354-380): every anchor positive, matched to
+    the box of least squared encoded distance; offsets / boxes / labels bit-exact vs the oracle
+    (incl. the NaN poisoning of a zero-size box, as in JACCARD_BIGGER)."""
+    from utils import net_tools as nt
+    rng = np.random.default_rng(17)
+    B, G = 2, 16
+    corner, labels, n = _random_gt(rng, B, G, degenerate)
+    anchors = _anchors(H, W)
+    center_o = ot.corner_to_center(corner)
+    res = nt.refine_groundtruth(anchors, torch.from_numpy(center_o).to(dev), torch.from_numpy(labels).to(dev),
+                                config.refine_method.NEAREST_NEIGHBOR, n_boxes=torch.from_numpy(n).to(dev))
+    gt_l, cb_l, lb_l, pm_l = res
+    for b in range(B):
+        og, oc, ol, op = ot.refine_groundtruth_nn(anchors, center_o[b, :n[b]], labels[b, :n[b]])
+        for l in range(6):
+            np.testing.assert_array_equal(pm_l[l][b].cpu().numpy(), op[l])
+            np.testing.assert_array_equal(lb_l[l][b].cpu().numpy(), ol[l])
+            np.testing.assert_array_equal(cb_l[l][b].cpu().numpy(), oc[l])
+            np.testing.assert_array_equal(gt_l[l][b].cpu().numpy(), og[l])
+
+
 def test_refine_loss(dev):
     from utils import net_tools as nt
     rng = np.random.default_rng(11)
