@@ -219,6 +219,28 @@ int rod_im2col3x3(const void* x, const float* pro_mean, const float* pro_rstd, c
 int rod_col2im3x3(const void* col, void* dx, int N, int H, int W, int C, int stride, int pad_t, int pad_l, int Ho,
                   int Wo, int dtype, void* stream);
 
+/* ------------------------------------- PREORDER_MSF feature augmentation (F4, ABI 9)
+ * process_backbone_method.PREORDER_MSF (nets/catch_net.py:115-152).  rod_se_*: C % 8 (bf16) / 4
+ * (fp32); pad and space_to_depth take any C (16-byte vectors when C allows).
+ * tf.pad(x, [[0,0],[top,0],[left,0],[0,0]]) into y [N][Hp][Wp][C] (zeros elsewhere);
+ * inverse != 0: the gradient, y [N][H][W][C] = x[n, h+top, w+left] of a padded x [N][Hp][Wp][C]. */
+int rod_pad2d(const void* x, void* y, int N, int H, int W, int C, int top, int left, int Hp, int Wp, int inverse,
+              int dtype, void* stream);
+/* tf.space_to_depth(x [N][H][W][C], block): y[n, i, j, (di*block + dj)*C + c] = x[n, i*block + di,
+ * j*block + dj, c]; inverse != 0: depth_to_space (x [N][H/block][W/block][block^2*C] -> y [N][H][W][C]). */
+int rod_space_to_depth(const void* x, void* y, int N, int H, int W, int C, int block, int inverse, int dtype,
+                       void* stream);
+/* se_block (nets/attention_module.py:3-33) on x [N][HW][C]: sq = mean over HW [N][C] fp32,
+ * hid = relu(sq . w1 + b1) [N][C8], e = sigmoid(hid . w2 + b2) [N][C], y = x * e.
+ * w1 [C][C8], w2 [C8][C] (tf.layers.dense kernels), fp32. */
+int rod_se_fwd(const void* x, const float* w1, const float* b1, const float* w2, const float* b2, float* sq,
+               float* hid, float* e, void* y, int N, long HW, int C, int C8, int dtype, void* stream);
+/* Its backward: de = sum_HW dy*x, the dense layers' gradients (dw1 / db1 / dw2 / db2 overwritten,
+ * each may be NULL; summed over the N images), dx = dy*e + dsq/HW.  de, dsq: [N][C] scratch. */
+int rod_se_bwd(const void* dy, const void* x, const float* w1, const float* w2, const float* sq, const float* hid,
+               const float* e, float* de, float* dsq, float* dw1, float* db1, float* dw2, float* db2, void* dx, int N,
+               long HW, int C, int C8, int dtype, void* stream);
+
 /* -------------------------------------- dense conv as implicit GEMM (A2 A3 A5)
  * y[m, co] = sum_k A[m, k] * wt[co, k] (+ bias[co]), fp32 accumulation,
  *   ksize 1: A = x rows [M = N*H*W, Cin] (slim.conv2d [1,1], conv_blocks.py:343)

@@ -201,12 +201,58 @@ def deconv_bone(feats, P, B, training, moving=None, learn_all=False):
     return out
 
 
-def forward(img_nhwc, P, B, training, all_mode=False, moving=None, learn_all=False, concat=False):
+MSF_BLOCKS = [['layer_4', 'layer_7'], ['layer_7', 'layer_11']]
+MSF_COMPRESS = [[4, 16], [3, 12]]
+
+
+def space_to_depth(x, r):
+    """tf.space_to_depth on NCHW: out channel (di*r + dj)*C + c."""
+    Bn, C, H, W = x.shape
+    return x.reshape(Bn, C, H // r, r, W // r, r).permute(0, 3, 5, 1, 2, 4).reshape(Bn, r * r * C, H // r, W // r)
+
+
+def se_block(x, P, name):
+    """attention_module.py:3-33 on NCHW."""
+    sq = x.mean((2, 3))
+    hid = torch.relu(sq @ P[name + '/bottleneck_fc/kernel'] + P[name + '/bottleneck_fc/bias'])
+    e = torch.sigmoid(hid @ P[name + '/recover_fc/kernel'] + P[name + '/recover_fc/bias'])
+    return x * e[:, :, None, None]
+
+
+def feats_aug(ep, P, B, training, moving=None):
+    """__feats_aug_block PREORDER_MSF (catch_net.py:115-152)."""
+    feats, k = [], 0
+    for index, t in enumerate(TAPS):
+        s_feat = ep['layer_%d' % t]
+        if index >= len(MSF_BLOCKS):
+            feats.append(s_feat)
+            continue
+        aug = []
+        for name in MSF_BLOCKS[index]:
+            f = ep[name]
+            h, w = f.shape[2], f.shape[3]
+            rh, rw = round(h / s_feat.shape[2]), round(w / s_feat.shape[3])
+            f = F.pad(f, (abs(w - rw * s_feat.shape[3]), 0, abs(h - rh * s_feat.shape[2]), 0))
+            sfx = '' if k == 0 else '_%d' % k
+            f = conv(f, P['backbone/Conv%s/weights' % sfx], P['backbone/Conv%s/biases' % sfx])
+            bn = 'backbone/BatchNorm' + sfx
+            f = leaky(batch_norm(f, None, P[bn + '/beta'], B[bn + '/moving_mean'], B[bn + '/moving_variance'],
+                                 training, 0.999, 1e-3, moving, bn))
+            if rh > 1:
+                f = space_to_depth(f, rh)
+            aug.append(f)
+            k += 1
+        feats.append(se_block(torch.cat(aug + [s_feat], 1), P, 'backbone/se_aug_layer_%d' % (index + 1)))
+    return feats
+
+
+def forward(img_nhwc, P, B, training, all_mode=False, moving=None, learn_all=False, concat=False, msf=False):
     """Full network on an NHWC fp32 input; returns refine_out (and det_out, clf_out).
-    learn_all: deconv_method LEARN_ALL; concat: merge_method CONCAT (catch_net.py:237-273)."""
+    learn_all: deconv_method LEARN_ALL; concat: merge_method CONCAT (catch_net.py:237-273);
+    msf: process_backbone_method PREORDER_MSF (catch_net.py:115-152)."""
     x = img_nhwc.permute(0, 3, 1, 2)
     ep = backbone(x, P, B, training, moving)
-    feats = [ep['layer_%d' % t] for t in TAPS]
+    feats = feats_aug(ep, P, B, training, moving) if msf else [ep['layer_%d' % t] for t in TAPS]
     refine = head(feats, P, B, 'refine', 4, training, moving)
     if not all_mode:
         return refine

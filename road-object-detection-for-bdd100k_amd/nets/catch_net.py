@@ -40,8 +40,12 @@ class CatchNet:
     def __init__(self, backbone_name, config_dict, device, seed=0, build_all=None):
         if backbone_name not in config.supported_backbone_name:
             raise ValueError('backbone %r is not supported (config.supported_backbone_name)' % backbone_name)
-        if config_dict['process_backbone_method'] is not config.process_backbone_method.NONE:
+        self.msf = config_dict['process_backbone_method'] is config.process_backbone_method.PREORDER_MSF
+        if not self.msf and config_dict['process_backbone_method'] is not config.process_backbone_method.NONE:
             raise ValueError('Not support the method(%s) now' % str(config_dict['process_backbone_method']))
+        if self.msf and backbone_name != 'mobilenet_v2':
+            raise ValueError('Sorry, not support the method(%s) for mobilenet_v2 now ~_~!!' %
+                             str(config_dict['process_backbone_method']))
         self.backbone_name = backbone_name
         self.config_dict = dict(config_dict)
         self.train_range = config_dict['train_range']
@@ -51,6 +55,8 @@ class CatchNet:
         self.store = ParamStore()
         self.backbone = MobilenetV2(self.store, rng) if backbone_name == 'mobilenet_v2' else VGG16(self.store, rng)
         self.feat_ch = self._endpoint_channels()
+        if self.msf:
+            self._msf_params(rng)
         self.n_anchor = n_anchor_each_layer(backbone_name)
         self._head('refine', self.feat_ch, 4, rng)
         self.deconv_method = config_dict.get('deconv_method', config.deconv_method.LEARN_HALF)
@@ -72,6 +78,79 @@ class CatchNet:
     # ------------------------------------------------------------------ parameters
     def _endpoint_channels(self):
         return self.backbone.endpoint_channels(config.extract_feat_name[self.backbone_name])
+
+    # ------------------------------------------------------------------ PREORDER_MSF (catch_net.py:115-152)
+    MSF_BLOCKS = [['layer_4', 'layer_7'], ['layer_7', 'layer_11']]
+    MSF_COMPRESS = [[4, 16], [3, 12]]
+    # space_to_depth blocks round(h / s_h), fixed by the stride chain (layer_4 / layer_7 are 4x / 2x
+    # the size of layer_11, layer_7 / layer_11 4x / 2x that of layer_15); they set the SE widths
+    MSF_RATIOS = [[4, 2], [4, 2]]
+
+    def _msf_params(self, rng):
+        """slim.conv2d 1x1 (+bias; outside the mobilenet arg_scope: xavier, no normaliser) and
+        slim.batch_norm (beta only) per augmented endpoint, named in creation order under the
+        'backbone' scope (Conv, Conv_1, ... / BatchNorm, BatchNorm_1, ...); se_block dense layers
+        'backbone/se_aug_layer_%d/{bottleneck_fc, recover_fc}/{kernel, bias}'."""
+        from nets.backbone.mobilenet_v2 import layer_plan
+        outs = {'layer_%d' % idx: cout for (idx, _, _, _, _, cout, _, _) in layer_plan()}
+        names = config.extract_feat_name['mobilenet_v2']
+        ratios = self.MSF_RATIOS
+        k = 0
+        for index, blocks in enumerate(self.MSF_BLOCKS):
+            ch = outs[names[index]]
+            for (b, cc), r in zip(zip(blocks, self.MSF_COMPRESS[index]), ratios[index]):
+                sfx = '' if k == 0 else '_%d' % k
+                self._conv_params('backbone/Conv' + sfx, cc, 1, outs[b], rng)
+                self._head_bn('backbone/BatchNorm' + sfx, cc)
+                ch += cc * r * r
+                k += 1
+            se = 'backbone/se_aug_layer_%d' % (index + 1)
+            # tf.contrib.layers.variance_scaling_initializer(): truncated normal, 2 / fan_in
+            self.store.add(se + '/bottleneck_fc/kernel', trunc_normal(rng, (ch, ch // 8), float(np.sqrt(2.0 / ch))))
+            self.store.add(se + '/bottleneck_fc/bias', np.zeros(ch // 8, np.float32))
+            self.store.add(se + '/recover_fc/kernel', trunc_normal(rng, (ch // 8, ch), float(np.sqrt(2.0 / (ch // 8)))))
+            self.store.add(se + '/recover_fc/bias', np.zeros(ch, np.float32))
+            self.feat_ch[index] = ch
+
+    def feats_aug(self, endpoints, training):
+        """__feats_aug_block PREORDER_MSF (catch_net.py:115-152) -> the six backbone features."""
+        P = self.store.params
+        names = config.extract_feat_name['mobilenet_v2']
+        uses = {}
+        for index, blocks in enumerate(self.MSF_BLOCKS):
+            for n in blocks + [names[index]]:
+                uses[n] = uses.get(n, 0) + 1
+        pool = {n: list(graph.fork(endpoints[n], k)) if k > 1 else [endpoints[n]] for n, k in uses.items()}
+        feats = []
+        k = 0
+        for index, name in enumerate(names):
+            if index >= len(self.MSF_BLOCKS):
+                feats.append(endpoints[name])
+                continue
+            s_feat = pool[name].pop()
+            s_h, s_w = s_feat.shape[1], s_feat.shape[2]
+            aug = []
+            for b, cc, r in zip(self.MSF_BLOCKS[index], self.MSF_COMPRESS[index], self.MSF_RATIOS[index]):
+                feat = pool[b].pop()
+                h, w = feat.shape[1], feat.shape[2]
+                rh, rw = round(h / s_h), round(w / s_w)
+                if rh != r or rw != r:
+                    raise ValueError('PREORDER_MSF: %s is %dx%d, %s %dx%d: block %d expected' % (b, h, w, name, s_h, s_w, r))
+                feat = ops.pad_top_left(feat, abs(h - rh * s_h), abs(w - rw * s_w))
+                sfx = '' if k == 0 else '_%d' % k
+                x = ops.materialize(self._conv_bn(feat, P['backbone/Conv%s/weights' % sfx],
+                                                  P['backbone/Conv%s/biases' % sfx], 1, 'backbone/BatchNorm' + sfx,
+                                                  training))
+                if rh > 1:
+                    x = ops.space_to_depth(x, rh)
+                aug.append(x)
+                k += 1
+            aug.append(s_feat)
+            se = 'backbone/se_aug_layer_%d' % (index + 1)
+            feats.append(ops.se_block(ops.channel_concat(aug), P[se + '/bottleneck_fc/kernel'],
+                                      P[se + '/bottleneck_fc/bias'], P[se + '/recover_fc/kernel'],
+                                      P[se + '/recover_fc/bias']))
+        return feats
 
     def _head_bn(self, name, c):
         self.store.add(name + '/beta', np.zeros(c, np.float32))
@@ -211,8 +290,12 @@ class CatchNet:
 
     def forward(self, inputs, is_training):
         names = config.extract_feat_name[self.backbone_name]
-        ep = self.backbone(inputs, is_training, taps=names)
-        feats = [ep[n] for n in names]
+        if self.msf:
+            taps = sorted(set(names) | {n for b in self.MSF_BLOCKS for n in b}, key=lambda n: int(n.split('_')[1]))
+            feats = self.feats_aug(self.backbone(inputs, is_training, taps=taps), is_training)
+        else:
+            ep = self.backbone(inputs, is_training, taps=names)
+            feats = [ep[n] for n in names]
         self.backbone_feats = collections.OrderedDict(('layer_%d' % (i + 1), f) for i, f in enumerate(feats))
         if not self.all_mode:
             return self.head_out(feats, 'refine', 4, is_training)

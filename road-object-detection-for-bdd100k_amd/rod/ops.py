@@ -1377,3 +1377,91 @@ def dropout(x, rate, training, seed=None):
         _DROPOUT_CALLS[0] += 1
         seed = 0x5EED0000 + _DROPOUT_CALLS[0]
     return _Dropout.apply(x, 1.0 - float(rate), seed)
+
+
+# ----------------------------------------------------------------------------- PREORDER_MSF ops (F4)
+class _Pad2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, top, left):
+        N, H, W, C = x.shape
+        y = torch.empty((N, H + top, W + left, C), dtype=x.dtype, device=x.device)
+        _abi.call("rod_pad2d", x.contiguous(), y, N, H, W, C, top, left, H + top, W + left, 0, dtcode(x), stream())
+        ctx.geo = (N, H, W, C, top, left)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C, top, left = ctx.geo
+        dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+        _abi.call("rod_pad2d", dy.contiguous(), dx, N, H, W, C, top, left, H + top, W + left, 1, dtcode(dy),
+                  stream())
+        return dx, None, None
+
+
+def pad_top_left(x, top, left):
+    """tf.pad(x, [[0, 0], [top, 0], [left, 0], [0, 0]]) (catch_net.py:135-136)."""
+    x = materialize(x)
+    return x if top == 0 and left == 0 else _Pad2d.apply(x, int(top), int(left))
+
+
+class _SpaceToDepth(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r):
+        N, H, W, C = x.shape
+        y = torch.empty((N, H // r, W // r, r * r * C), dtype=x.dtype, device=x.device)
+        _abi.call("rod_space_to_depth", x.contiguous(), y, N, H, W, C, r, 0, dtcode(x), stream())
+        ctx.geo = (N, H, W, C, r)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C, r = ctx.geo
+        dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+        _abi.call("rod_space_to_depth", dy.contiguous(), dx, N, H, W, C, r, 1, dtcode(dy), stream())
+        return dx, None
+
+
+def space_to_depth(x, block):
+    """tf.space_to_depth(x, block_size) (catch_net.py:142)."""
+    return _SpaceToDepth.apply(materialize(x), int(block))
+
+
+class _SE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        N, H, W, C = x.shape
+        C8 = w1.shape[1]
+        x = x.contiguous()
+        dev = x.device
+        sq = torch.empty((N, C), dtype=torch.float32, device=dev)
+        hid = torch.empty((N, C8), dtype=torch.float32, device=dev)
+        e = torch.empty((N, C), dtype=torch.float32, device=dev)
+        y = torch.empty_like(x)
+        _abi.call("rod_se_fwd", x, w1, b1, w2, b2, sq, hid, e, y, N, H * W, C, C8, dtcode(x), stream())
+        ctx.save_for_backward(x, w1, w2, sq, hid, e)
+        ctx.params = (w1, b1, w2, b2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w1, w2, sq, hid, e = ctx.saved_tensors
+        N, H, W, C = x.shape
+        C8 = w1.shape[1]
+        dev = x.device
+        de = torch.empty((N, C), dtype=torch.float32, device=dev)
+        dsq = torch.empty((N, C), dtype=torch.float32, device=dev)
+        dx = torch.empty_like(x)
+        pw1, pb1, pw2, pb2 = ctx.params
+        slots = [grad_slot(p) if _needs(p) else None for p in (pw1, pb1, pw2, pb2)]
+        _abi.call("rod_se_bwd", dy.contiguous(), x, w1, w2, sq, hid, e, de, dsq, *slots, dx, N, H * W, C, C8,
+                  dtcode(x), stream())
+        for p, s in zip((pw1, pb1, pw2, pb2), slots):
+            if s is not None:
+                _mark_written(p)
+        return dx, None, None, None, None
+
+
+def se_block(x, w1, b1, w2, b2):
+    """attention_module.se_block (attention_module.py:3-33): x * sigmoid(dense(relu(dense(mean_HW x))));
+    w1 [C, C/8], w2 [C/8, C] fp32 (tf.layers.dense kernels)."""
+    return _SE.apply(materialize(x), w1, b1, w2, b2)

@@ -29,7 +29,8 @@ class Trainer:
     def __init__(self, img_size, batch_size, dtype=torch.bfloat16, train_range=config.train_range.REFINE,
                  learning_rate=1e-3, device='cuda', fix_refine=True, seed=0, world_size=1, reducer=None,
                  deconv_method=config.deconv_method.LEARN_HALF, merge_method=config.merge_method.ADD,
-                 sync_bn=False, backbone_name='mobilenet_v2'):
+                 sync_bn=False, backbone_name='mobilenet_v2',
+                 process_backbone_method=config.process_backbone_method.NONE):
         self.img_size = tuple(img_size)
         self.batch_size = batch_size          # per-rank batch
         self.world_size = world_size
@@ -37,7 +38,7 @@ class Trainer:
         self.device = torch.device(device)
         config.img_size = self.img_size       # init_anchor reads config.img_size (net_tools.py:37-38)
         self.config_dict = {'train_range': train_range,
-                            'process_backbone_method': config.process_backbone_method.NONE,
+                            'process_backbone_method': process_backbone_method,
                             'deconv_method': deconv_method,     # train.py:131-133 defaults
                             'merge_method': merge_method}
         self.backbone_name = backbone_name

@@ -441,3 +441,53 @@ def test_dw_bn_prologue(dev, dtype, C, stride, H, W):
         w._rod_grad.zero_()
         return ops.dw3x3(x, w, stride), (lambda: w._rod_grad)
     _fused_vs_materialised(dev, dtype, (2, H, W, C), ops.ROD_ACT_RELU6, True, consumer, 14)
+
+
+@pytest.mark.parametrize('hw,cin', [((2, 3), 256), ((20, 36), 96), ((40, 72), 192), ((40, 72), 64)])
+def test_head_chain_nodes_match_float64(dev, hw, cin):
+    """The refine head exactly as the product runs it (CatchNet._conv_bn: ops.conv2d_bn nodes,
+    BatchNorm + leaky applied in the next conv's load prologue, one materialise at the end)
+    on maps of the step's level sizes, fp32, against float64 — forward and every gradient."""
+    g = torch.Generator().manual_seed(7)
+    H, W = hw
+    x = torch.randn(2, H, W, cin, generator=g)
+    chans = [(cin, 128, 1), (128, 128, 3), (128, 24, 1), (24, 24, 3)]
+    Ws = [torch.randn(co, k, k, ci, generator=g) / np.sqrt(k * k * ci) for ci, co, k in chans]
+    Bs = [torch.randn(co, generator=g) * 0.1 for _, co, _ in chans]
+    Be = [torch.randn(co, generator=g) * 0.1 for _, co, _ in chans]
+
+    def oracle(dt):
+        Wo = [w.to(dt).requires_grad_(True) for w in Ws]
+        Beo = [b.to(dt).requires_grad_(True) for b in Be]
+        h = x.to(dt).permute(0, 3, 1, 2)
+        for i in range(4):
+            h = onet.conv(h, Wo[i], Bs[i].to(dt))
+            h = onet.leaky(onet.batch_norm(h, None, Beo[i], torch.zeros(h.shape[1], dtype=dt),
+                                           torch.ones(h.shape[1], dtype=dt), True, 0.999, 1e-3, {}, 'b%d' % i))
+        return h, Wo, Beo
+    h64, W64, Be64 = oracle(torch.float64)
+    h32, W32, Be32 = oracle(torch.float32)
+    gy = torch.randn(h64.shape, generator=g) * (torch.rand(h64.shape, generator=g) < 0.02)
+    (h64 * gy.double()).sum().backward()
+    (h32 * gy).sum().backward()
+    Wd = [_param(w, dev) for w in Ws]
+    Bd = [_param(b, dev) for b in Bs]
+    Bed = [_param(b, dev) for b in Be]
+    t = x.to(dev)
+    for i, (ci, co, k) in enumerate(chans):
+        t = ops.conv2d_bn(t, Wd[i], Bd[i], k, None, Bed[i], torch.zeros(co, device=dev), torch.ones(co, device=dev),
+                          ops.ROD_ACT_LEAKY, True, 0.999)
+    t = ops.materialize(t)
+    t.backward(gy.permute(0, 2, 3, 1).contiguous().to(dev))
+
+    def ne(a, b):
+        return float((a.detach().double().cpu() - b.detach().double()).abs().max() / b.detach().double().abs().max())
+    rep = []
+    assert ne(t, h64.permute(0, 2, 3, 1)) <= max(1e-5, 4 * ne(h32.permute(0, 2, 3, 1), h64.permute(0, 2, 3, 1)))
+    for i in range(4):
+        for got, r64, r32 in ((Wd[i]._rod_grad, W64[i].grad, W32[i].grad), (Bed[i]._rod_grad, Be64[i].grad,
+                                                                            Be32[i].grad)):
+            rep.append((i, ne(got, r64), ne(r32, r64)))
+    print('head chain', hw, cin, ['%d %.2e/%.2e' % r for r in rep])
+    for i, e, e32 in rep:
+        assert e <= max(1e-4, 4 * e32), rep

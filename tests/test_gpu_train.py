@@ -39,7 +39,7 @@ def _nerr(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-def _oracle_step(tr, img, corner, labels, n, H, W, B, dt, perturb=0.0, seed=0):
+def _oracle_step(tr, img, corner, labels, n, H, W, B, dt, perturb=0.0, seed=0, msf=False):
     P = {k: v.detach().cpu().clone().to(dt).requires_grad_(v.requires_grad) for k, v in tr.net.store.params.items()}
     Bf = {k: v.detach().cpu().clone().to(dt) for k, v in tr.net.store.buffers.items()}
     x = torch.from_numpy(np.float32(2.0 / 255.0) * img.cpu().numpy().astype(np.float32) - np.float32(1.0)).to(dt)
@@ -47,7 +47,7 @@ def _oracle_step(tr, img, corner, labels, n, H, W, B, dt, perturb=0.0, seed=0):
         g = torch.Generator().manual_seed(seed)
         x = x * (1 + perturb * torch.randn(x.shape, generator=g, dtype=dt))
     mov = {}
-    refine = onet.forward(x, P, Bf, True, moving=mov)
+    refine = onet.forward(x, P, Bf, True, moving=mov, msf=msf)
     init = oa.init_anchor(6, (H, W))
     chain = oa.feat_sizes((H, W), [s for (_, s, _, _, _) in onet.SPEC])
     anchors = [oa.anchors_one_layer((H, W), chain[t - 1], init[i]) for i, t in enumerate(onet.TAPS)]

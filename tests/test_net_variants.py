@@ -66,3 +66,22 @@ def test_vgg_params_and_sizes_match_reference_and_oracle():
     assert used == set(P)
     sizes = config.feat_sizes((288, 512), 'vgg_16')
     assert [tuple(o.shape[1:3]) for o in out] == [sizes['layer_%d' % (i + 1)] for i in range(6)]
+
+
+def test_preorder_msf_params_match_oracle():
+    """PREORDER_MSF + SE (catch_net.py:115-152, attention_module.py:3-33): product parameters ==
+    oracle consumption; the augmented levels are 192 channels wide."""
+    cfg = {'train_range': config.train_range.ALL, 'process_backbone_method': config.process_backbone_method.PREORDER_MSF,
+           'deconv_method': _DM.LEARN_HALF, 'merge_method': _MM.ADD}
+    net = CatchNet('mobilenet_v2', cfg, 'cpu', 0)
+    assert net.feat_ch[:2] == [192, 192]
+    P = {k: v.detach().clone().double() for k, v in net.store.params.items()}
+    B = {k: v.detach().clone().double() for k, v in net.store.buffers.items()}
+    used = set()
+
+    class Tracker(dict):
+        def __getitem__(self, k):
+            used.add(k)
+            return dict.__getitem__(self, k)
+    onet.forward(torch.zeros((1, 160, 288, 3), dtype=torch.float64), Tracker(P), B, False, all_mode=True, msf=True)
+    assert used == set(P)
