@@ -14,6 +14,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import config  # noqa: E402
@@ -47,6 +48,9 @@ def parse(argv=None):
     ap.add_argument('--synthetic', type=str2bool, default=False,
                     help='run on synthetic BDD-shaped batches (no dataset needed); results are not real '
                          'metrics.  Without it a missing dataset or checkpoint is an error')
+    ap.add_argument('--vis_dir', default=None,
+                    help='write the first image of every batch with its detections (and ground truth) as PNG '
+                         '(the reference shows them with cv2.imshow)')
     ap.add_argument('--output', default=None, help='write detections of the last batch as JSON')
     return ap.parse_args(argv)
 
@@ -120,6 +124,32 @@ class Predictor(object):
         return ({c: scores[:, c - 1] for c in range(1, K)}, {c: boxes[:, c - 1] for c in range(1, K)})
 
 
+def write_vis(F, bi, img, scores, bboxes, gt_corner, gt_labels, gt_n):
+    """predict.py:151-196 without a display: the first image of the batch resized to
+    vis_height x vis_width with its detections (and ground truth) drawn, written as PNG."""
+    from PIL import Image
+    from utils import net_tools
+    os.makedirs(F.vis_dir, exist_ok=True)
+    im = Image.fromarray(img[0].cpu().numpy()).resize((F.vis_width, F.vis_height), Image.BILINEAR)
+    img_gt = np.asarray(im, np.uint8).copy()
+    img_pred = img_gt.copy()
+    for c in scores:
+        s = scores[c][0].cpu().numpy()
+        if s.any():
+            net_tools.visualize_boxes_and_labels_on_image_array(img_pred, bboxes[c][0].cpu().numpy(),
+                                                                np.full(s.shape, c, np.int32), s,
+                                                                config.category_index)
+    Image.fromarray(img_pred).save(os.path.join(F.vis_dir, 'pred_%04d.png' % bi))
+    if F.vis_groundtruth:
+        n = int(gt_n[0])
+        for box, lab in zip(gt_corner[0, :n].cpu().numpy(), gt_labels[0, :n].cpu().numpy()):
+            if lab > 0:
+                net_tools.visualize_boxes_and_labels_on_image_array(img_gt, box[None], np.array([lab]),
+                                                                    np.array([1.]), config.category_index,
+                                                                    skip_scores=True, skip_labels=True)
+        Image.fromarray(img_gt).save(os.path.join(F.vis_dir, 'gt_%04d.png' % bi))
+
+
 def main(argv=None):
     F = parse(argv)
     logger.info('Asserting parameters')
@@ -140,9 +170,11 @@ def main(argv=None):
     source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, synthetic=F.synthetic, dtype=dtype,
                          num_readers=F.num_readers)
     t0 = time.time()
-    for _ in range(F.num_batches):
-        img, _, _, _ = next(source)
+    for bi in range(F.num_batches):
+        img, gt_corner, gt_labels, gt_n = next(source)
         scores, bboxes = pred(img)
+        if F.vis_dir:
+            write_vis(F, bi, img, scores, bboxes, gt_corner, gt_labels, gt_n)
     torch.cuda.synchronize()
     dt = time.time() - t0
     n_det = {c: int((s > 0).sum().item()) for c, s in scores.items()}

@@ -323,3 +323,10 @@ def detected_bboxes(predictions, localisations, select_threshold=None, nms_thres
         raise NotImplementedError('clipping_bbox is never used by the reference CLIs (predict.py:136)')
     K = predictions.shape[-1]
     return ({c: scores[:, c - 1] for c in range(1, K)}, {c: boxes[:, c - 1] for c in range(1, K)})
+
+
+# ================================================================ visualisation (net_tools.py:761-1106)
+from utils.visualization import (STANDARD_COLORS, draw_bounding_box_on_image,  # noqa: E402,F401
+                                 draw_bounding_box_on_image_array, draw_keypoints_on_image,
+                                 draw_keypoints_on_image_array, draw_mask_on_image_array,
+                                 visualize_boxes_and_labels_on_image_array)

@@ -285,8 +285,13 @@ def test_cli_train_evaluate_predict_on_tfrecords(dev, tmp_path):
     assert ev['num_batches'] == 2 and not ev['synthetic'] and ev['checkpoint'] == ck
     assert np.isfinite(m07) and np.isfinite(m12) and 0 <= m07 <= 1 and 0 <= m12 <= 1
     scores, boxes = _cli('predict', common + ['--batch_size=2', '--checkpoint_all=' + ck,
-                                              '--output=' + str(tmp_path / 'det.json')])
+                                              '--output=' + str(tmp_path / 'det.json'),
+                                              '--vis_dir=' + str(tmp_path / 'vis')])
     assert set(scores) == set(range(1, 11)) and scores[1].shape == (2, 200)
+    from PIL import Image   # predict.py:151-196 drawings, written instead of shown
+    for name in ('pred_0000.png', 'gt_0000.png'):
+        with Image.open(str(tmp_path / 'vis' / name)) as im:
+            assert im.size == (1080, 720)
     # the same weights as a TF-1.x tensor bundle: evaluate restores it and gives the same mAP
     from rod.checkpoint import load_variables, save_variables
     from nets.catch_net import CatchNet

@@ -64,11 +64,12 @@ def test_se_block_matches_float64(dev, shape, sparse):
 
 
 # Gradient floor of this step test: 5e-3 normwise (2e-3 in test_gpu_train.py).  Measured: the
-# level-1 refine head here (BatchNorm over 5760 rows of the 192-channel SE output) carries 3e-3
-# relative fp32 error in its own weight gradient (the fp32 oracle 1e-3), and every tensor
-# upstream of it — the SE, the augmentation convs, layers 8-11 through the residual stream —
-# inherits that 2-3.5e-3 while their own fp32-oracle spread stays at 3-5e-4.  The SE block by
-# itself is exact to 1e-7 (test_se_block_matches_float64); forward outputs and loss keep 1e-4.
+# level-1 refine head here carries 3e-3 relative error in its weight gradient from activation
+# kinks (the same head alone, fed a dense gradient, is within 1e-6 of float64:
+# test_gpu_kernels.py::test_head_chain_nodes_match_float64), and every tensor upstream of it —
+# the SE, the augmentation convs, layers 8-11 through the residual stream — inherits that
+# 2-3.5e-3.  The SE block by itself is exact to 1e-7 (test_se_block_matches_float64); forward
+# outputs and loss keep 1e-4.
 GRAD_FLOOR = 5e-3
 
 
@@ -89,7 +90,11 @@ def test_preorder_msf_refine_step_matches_oracle(dev):
         P32b = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.float32, msf=True)[0]
     finally:
         torch.backends.mkldnn.enabled = True
-    Pp = _oracle_step(tr, img, corner, labels, n, H, W, B, torch.float64, perturb=1e-6, seed=11, msf=True)[0]
+    # ReLU6 / leaky kinks: elements within fp32 rounding of zero flip their branch under ANY
+    # evaluation order; where the REFINE gradient is concentrated on few rows (level 1: BN_1 /
+    # Conv_1 of the refine head) one flip moves a tensor by percents — measured with noise
+    Pp = [_oracle_step(tr, img, corner, labels, n, H, W, B, torch.float64, perturb=a, seed=s_, msf=True)[0]
+          for s_ in (11, 12) for a in (1e-6, 1e-5)]
     from nets.catch_net import factory
     import utils.net_tools as nt
     from utils.common_tools import cornerBboxes_2_centerBboxes
@@ -114,7 +119,7 @@ def test_preorder_msf_refine_step_matches_oracle(dev):
             continue   # conv bias before a training-mode BatchNorm: exactly zero gradient
         checked += 1
         e = _nerr(p._rod_grad, g64)
-        e32 = max(_nerr(g32, g64), _nerr(P32b[name].grad, g64), _nerr(Pp[name].grad, g64))
+        e32 = max([_nerr(g32, g64), _nerr(P32b[name].grad, g64)] + [_nerr(pp[name].grad, g64) for pp in Pp])
         if e > max(GRAD_FLOOR, 4 * e32):
             bad.append((name, e, e32))
     assert checked > 100 and not bad, bad[:10]
