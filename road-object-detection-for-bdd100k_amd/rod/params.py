@@ -124,9 +124,13 @@ class ParamStore:
             self._refresh_prep(dtype)
         return e[0]
 
-    def _refresh_prep(self, dtype):
-        from . import _abi
-        from .ops import dtcode, stream
+    def build_prep_tables(self):
+        """Upload the device tables of rod_conv_weight_prep_batch now (host -> device copies),
+        e.g. before a HIP-graph capture, which may contain the refresh launch but no copy."""
+        for dtype in {d for (_, _, d) in self._prep}:
+            self._prep_table(dtype)
+
+    def _prep_table(self, dtype):
         tab = self._prep_tables.get(dtype)
         if tab is None:
             ents = [e for (n, m, d), e in self._prep.items() if d == dtype]
@@ -140,7 +144,12 @@ class ParamStore:
             dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
             tab = (dev, len(ents), start, ents)
             self._prep_tables[dtype] = tab
-        dev, n, total, ents = tab
+        return tab
+
+    def _refresh_prep(self, dtype):
+        from . import _abi
+        from .ops import dtcode, stream
+        dev, n, total, ents = self._prep_table(dtype)
         _abi.call("rod_conv_weight_prep_batch", dev, n, total, dtcode(ents[0][0]), stream())
         for e in ents:
             e[1] = self.version

@@ -75,7 +75,33 @@ class Trainer:
         if self.reducer is not None:
             self.reducer(self.net.store.flat_grad)
         self.opt.step()
+        self._eager_steps = getattr(self, '_eager_steps', 0) + 1
         return losses
+
+    def step_graphed(self, img_u8, gt_corner, gt_labels, gt_n):
+        """One training step replayed as a HIP graph: the whole forward / backward / SGD launch
+        sequence (~960 kernels) is captured once on the first call after an eager step (which did
+        the lazy set-up: anchor tables, weight-layout cache, workspaces) and replayed from static
+        input buffers, so no per-kernel host dispatch remains.  Every call runs exactly one step;
+        the results are bit-identical to step() (same kernels, same order).  Single process only."""
+        if getattr(self, '_eager_steps', 0) == 0 or self.reducer is not None:
+            return self.step(img_u8, gt_corner, gt_labels, gt_n)
+        new = (img_u8, gt_corner, gt_labels, gt_n)
+        if getattr(self, '_graph', None) is None or any(a.shape != b.shape or a.dtype != b.dtype
+                                                          for a, b in zip(self._graph[1], new)):
+            static = tuple(t.clone() for t in new)
+            self.net.store.build_prep_tables()   # host -> device set-up stays outside the capture
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                out = self.step(*static)
+            self._graph = (g, static, out)
+        g, static, out = self._graph
+        for a, b in zip(static, new):
+            if a.data_ptr() != b.data_ptr():
+                a.copy_(b)
+        g.replay()
+        return out
 
     def losses(self, img_u8, gt_corner, gt_labels, gt_n):
         """Forward of one step: (training loss, [refine, det, clf] in ALL mode)."""

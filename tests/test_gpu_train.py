@@ -376,3 +376,21 @@ def test_trainer_steps_reduce_loss(dev):
     losses = [tr.step(*batch)[0].item() for _ in range(8)]
     assert np.isfinite(losses).all()
     assert losses[-1] < losses[0], losses
+
+
+def test_step_graphed_bit_identical(dev):
+    """Trainer.step_graphed (the step captured once as a HIP graph and replayed) runs exactly
+    the eager step: parameters, moving statistics and losses bit-identical after 4 steps."""
+    H, W, B = 160, 288, 2
+    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=21)
+    ta = Trainer((H, W), B, dtype=torch.bfloat16, device=dev, seed=2)
+    tb = Trainer((H, W), B, dtype=torch.bfloat16, device=dev, seed=2)
+    for _ in range(4):
+        la = ta.step(img, corner, labels, n)
+        lb = tb.step_graphed(img, corner, labels, n)
+    torch.cuda.synchronize()
+    assert tb._graph is not None
+    assert torch.equal(ta.net.store.flat, tb.net.store.flat)
+    for k, v in ta.net.store.buffers.items():
+        assert torch.equal(v, tb.net.store.buffers[k]), k
+    assert torch.equal(la[0], lb[0])
