@@ -214,7 +214,9 @@ def main():
     use_graph = args.graph and world == 1
     step = tr.step_graphed if use_graph else tr.step
 
-    for _ in range(args.warmup):
+    # graphed: the capture happens on the second call (after one eager set-up step), so at
+    # least two untimed calls run before the timed region whatever --warmup says
+    for _ in range(max(args.warmup, 2) if use_graph else args.warmup):
         step(*next_batch())
     torch.cuda.synchronize()
     if world > 1:

@@ -130,7 +130,10 @@ def write_vis(F, bi, img, scores, bboxes, gt_corner, gt_labels, gt_n):
     from PIL import Image
     from utils import net_tools
     os.makedirs(F.vis_dir, exist_ok=True)
-    im = Image.fromarray(img[0].cpu().numpy()).resize((F.vis_width, F.vis_height), Image.BILINEAR)
+    a = img[0].float().cpu().numpy() if img.is_floating_point() else img[0].cpu().numpy()
+    if a.dtype != np.uint8:   # the TFRecord pipeline hands over [-1, 1] images (2/255 x - 1)
+        a = np.uint8(np.clip(np.rint((a + 1.0) * 127.5), 0, 255))
+    im = Image.fromarray(a).resize((F.vis_width, F.vis_height), Image.BILINEAR)
     img_gt = np.asarray(im, np.uint8).copy()
     img_pred = img_gt.copy()
     for c in scores:

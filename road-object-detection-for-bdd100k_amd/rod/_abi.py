@@ -156,6 +156,13 @@ class Probe:
 PROBE = Probe()
 
 
+def _capturing():
+    """True while a HIP graph is being captured: timing events recorded into a capture belong
+    to the graph and cannot be read back, so the probe skips those calls."""
+    import torch
+    return torch.cuda.is_current_stream_capturing()
+
+
 def call(name: str, *args):
     """Call rod_<name>; raise RuntimeError on a non-zero return code."""
     L = lib()
@@ -164,7 +171,7 @@ def call(name: str, *args):
     if len(args) != len(argspec):
         raise TypeError(f"{name} expects {len(argspec)} args, got {len(args)}")
     conv = [(_ptr(a) if t == "ptr" else a) for (t, _), a in zip(argspec, args)]
-    if PROBE.wants(name):
+    if PROBE.wants(name) and not _capturing():
         import torch
         from . import roofline
         s = torch.cuda.current_stream()

@@ -22,6 +22,7 @@ for step in "$@"; do
   case $step in
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
+    clitest) run clitest 400 python -m pytest tests/test_gpu_fullsize.py -m gpu -q -k cli --timeout=300 -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchfast) run benchfast 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
@@ -38,8 +39,8 @@ for step in "$@"; do
     profall) run profall 600 rocprofv3 --kernel-trace --stats -d $OUT/profall_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --train_range ALL ;;
     profpred) run profpred 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 720 --batch 32 --iters 10 ;;
     profpred1080) run profpred1080 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred1080_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 10 ;;
-    pmcfetch) run pmcfetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-inference ;;
-    pmcwrite) run pmcwrite 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-inference ;;
+    pmcfetch) run pmcfetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference ;;
+    pmcwrite) run pmcwrite 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference ;;
     *) echo "unknown step $step" ;;
   esac
 done

@@ -12,6 +12,7 @@ usage: python tools/pmc_traffic.py <fetch csv> <write csv> <out.json> [train_ran
 """
 import collections
 import csv
+import gzip
 import json
 import os
 import sys
@@ -23,7 +24,8 @@ from rod.roofline import ENTRY_KERNELS  # noqa: E402
 
 def per_kernel(path, counter):
     d = collections.defaultdict(lambda: [0, 0.0])
-    for r in csv.DictReader(open(path)):
+    f = gzip.open(path, 'rt') if path.endswith('.gz') else open(path)
+    for r in csv.DictReader(f):
         if r['Counter_Name'] != counter:
             continue
         d[r['Kernel_Name']][0] += 1
