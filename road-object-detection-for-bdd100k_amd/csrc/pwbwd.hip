@@ -15,6 +15,14 @@
 //   3. stages dx in LDS and writes whole 16-byte row segments.
 // dW / db partials per block go to fp32 slabs summed in f64 in fixed order (slab_sum), so the
 // result is deterministic.  Bytes per row: 2*Cout*2 (dz, y) + Cin*2 (x) + Cin*2 (dx).
+//
+// The kernel is latency-bound on its synchronous 64-row steps, so occupancy is what it runs
+// on: the wave index is made scalar (readfirstlane: tile indices and their divisions in
+// SGPRs), per-step offsets are recomputed from an opaque copy of the thread index instead of
+// being hoisted as loop invariants, dz / y are batched two (not four) 16-byte loads deep, and
+// the 7 coefficient fields are read four channels at a time.  The expand shapes went from
+// 1-2 to 3 waves per SIMD: tools/pwbwd_bench.py 4715 -> 3326 us over its eight shapes,
+// outputs bit-identical.
 #include "rod_common.h"
 
 namespace rod {
@@ -57,9 +65,14 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
   bf16_t* Ds = (bf16_t*)(xtab + 2 * Cin);                      // [64][LDD]   dy
   bf16_t* Xs = Ds + PB_BM * LDD;                               // [64][LDX]   a | 1 ; dx staging
   bf16_t* Ws = Xs + PB_BM * LDX;                               // [nxt*16][LDD] wt1
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile indices in SGPRs
   const bool prox = a.xmean != nullptr;
   const bool has_bias = a.partb != nullptr;
+  // act_grad(z, act) as one select chain: z > 0 ? (z < hi ? 1 : 0) : lo — the same {0, 0.2, 1}
+  // factors (NaN -> lo, as the compare-based forms give) without a per-element switch
+  const float ghi = a.act == ROD_ACT_RELU6 ? 6.f : INFINITY;
+  const float glo = a.act == ROD_ACT_LEAKY ? 0.2f : a.act == ROD_ACT_NONE ? 1.f : 0.f;
 
   for (int c = tid; c < Cout; c += 256) {
     float sc, sh;
@@ -105,12 +118,30 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
 
   for (long m0 = mb; m0 < me; m0 += PB_BM) {
     __syncthreads();  // the previous step's readers of Ds / Xs are done
+    // The thread index passes through an opaque copy each step, so the per-thread LDS / global
+    // offsets below are recomputed in the loop (a few VALU ops) instead of being hoisted out of
+    // it as loop invariants — each hoisted offset held a VGPR for the whole kernel and together
+    // they cost two thirds of the occupancy.
+    int tid_l = tid;
+    asm volatile("" : "+v"(tid_l));
+    const int tid = tid_l;
+    const int g = (tid & 63) >> 4, li = tid & 15, q = li >> 2, p = li & 3;
     // ---- 1. dy = BatchNorm backward of (dz, y) -> Ds; a -> Xs ----------------------------
-    const int tot = PB_BM * CCH;
-    for (int base = tid; base < tot; base += 1024) {
-      bf16x8 dv[4], yv[4];
+    // the conv-input rows are loaded first so their latency overlaps the dz / y loads
+    constexpr int XR = NX / 2 > 0 ? NX / 2 : 1;   // 64 * Cin/8 chunks / 256 threads <= NX/2
+    const int xtot = PB_BM * XCH;
+    bf16x8 xr[XR];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+    for (int k = 0; k < XR; ++k) {
+      const int idx = tid + k * 256;
+      const int r = idx / XCH, cc = idx - r * XCH;
+      if (idx < xtot && m0 + r < me) xr[k] = *(const bf16x8*)(a.x + (m0 + r) * Cin + cc * 8);
+    }
+    const int tot = PB_BM * CCH;
+    for (int base = tid; base < tot; base += 512) {
+      bf16x8 dv[2], yv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
         const int idx = base + u * 256;
         const int r = idx / CCH, cc = idx - r * CCH;
         const long m = m0 + r;
@@ -120,31 +151,28 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 2; ++u) {
         const int idx = base + u * 256;
         if (idx >= tot) continue;
         const int r = idx / CCH, cc = idx - r * CCH;
         const long m = m0 + r;
         bf16x8 o;
         if (m < me) {
-          float f[7][8];
+          // two halves of 4 channels: 7 coefficient fields x 4 live at a time
 #pragma unroll
-          for (int k = 0; k < 7; ++k) {
-            const f32x4 lo = *(const f32x4*)(ctab + k * Cout + cc * 8);
-            const f32x4 hi = *(const f32x4*)(ctab + k * Cout + cc * 8 + 4);
+          for (int h = 0; h < 2; ++h) {
+            f32x4 f[7];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              f[k][j] = lo[j];
-              f[k][4 + j] = hi[j];
+            for (int k = 0; k < 7; ++k) f[k] = *(const f32x4*)(ctab + k * Cout + cc * 8 + 4 * h);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int j = 4 * h + jj;
+              const float yj = (float)yv[u][j];
+              const float d = yj - f[0][jj];
+              const float z = fmaf(yj, f[2][jj], f[3][jj]);
+              const float gj = (float)dv[u][j] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
+              o[j] = (bf16_t)(f[4][jj] * (gj - f[5][jj] - (d * f[1][jj]) * f[6][jj]));
             }
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float yj = (float)yv[u][j];
-            const float d = yj - f[0][j];
-            const float z = fmaf(yj, f[2][j], f[3][j]);
-            const float gj = (float)dv[u][j] * act_grad(z, a.act);
-            o[j] = (bf16_t)(f[4][j] * (gj - f[5][j] - (d * f[1][j]) * f[6][j]));
           }
         } else {
 #pragma unroll
@@ -153,12 +181,13 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
         *(bf16x8*)(Ds + r * LDD + cc * 8) = o;
       }
     }
-    for (int idx = tid; idx < PB_BM * XCH; idx += 256) {
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+      const int idx = tid + k * 256;
+      if (idx >= xtot) continue;
       const int r = idx / XCH, cc = idx - r * XCH;
-      const long m = m0 + r;
-      bf16x8 v;
-      if (m < me) {
-        v = *(const bf16x8*)(a.x + m * Cin + cc * 8);
+      bf16x8 v = xr[k];
+      if (m0 + r < me) {
         if (prox) {
           const f32x4 s0 = *(const f32x4*)(xtab + cc * 8), s1 = *(const f32x4*)(xtab + cc * 8 + 4);
           const f32x4 h0 = *(const f32x4*)(xtab + Cin + cc * 8), h1 = *(const f32x4*)(xtab + Cin + cc * 8 + 4);
@@ -263,12 +292,13 @@ static PwBwdPlan pw_bwd_plan(long M, int Cin, int Cout, bool bias) {
   p.nxt = cdiv(Cin, 16);
   p.nx = p.nxt <= 2 ? 2 : p.nxt <= 4 ? 4 : p.nxt <= 8 ? 8 : 12;
   const int per = cdiv(p.nco * p.nci, 4);
-  p.wt = per <= 4 ? 4 : per <= 8 ? 8 : 16;
+  p.wt = per <= 4 ? 4 : per <= 6 ? 6 : per <= 8 ? 8 : 16;
   p.lds = (size_t)Cout * PB_CF * 4 + (size_t)Cin * 2 * 4 +
           ((size_t)PB_BM * (p.kd + 8) + (size_t)PB_BM * (p.nci * 16 + 8) + (size_t)p.nxt * 16 * (p.kd + 8)) * 2;
-  // ~4 blocks per CU worth of row chunks (fewer, longer chunks keep the dW slab small)
+  // two rounds of the 3 resident blocks per CU (measured: 768 / 1024 / 1280 / 1536 / 2048 /
+  // 3072 blocks -> 3471 / 3722 / 3572 / 3326 / 3531 / 3519 us over tools/pwbwd_bench.py)
   const long steps = cdivl(M, PB_BM);
-  p.nblk = (int)std::max<long>(1, std::min<long>(steps, 1024));
+  p.nblk = (int)std::max<long>(1, std::min<long>(steps, 1536));
   p.chunk = cdivl(steps, p.nblk) * PB_BM;
   p.nblk = (int)cdivl(M, p.chunk);
   return p;
@@ -315,6 +345,7 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
   } while (0)
 #define PBW(NX_)                   \
   if (p.wt == 4) PBL(NX_, 4);      \
+  else if (p.wt == 6) PBL(NX_, 6); \
   else if (p.wt == 8) PBL(NX_, 8); \
   else PBL(NX_, 16)
   if (p.nx == 2) PBW(2);

@@ -22,10 +22,14 @@ SHAPES = [(7372800, 16, 96, 1, True), (1843200, 24, 144, 1, True), (1843200, 144
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--pw-only', action='store_true', help='time rod_pw_bwd alone on the shapes it serves')
     a = ap.parse_args()
     dev = torch.device('cuda')
     rows = []
     for (M, Cin, Cout, act, prox) in SHAPES:
+        torch.manual_seed(M + Cin + Cout)
+        if a.pw_only and not ops.pw_bwd_supported(Cin, Cout, bf16):
+            continue
         x = torch.randn(M, Cin, device=dev).to(bf16)
         y = torch.randn(M, Cout, device=dev).to(bf16)
         dz = torch.randn(M, Cout, device=dev).to(bf16)
@@ -49,12 +53,18 @@ def main():
             ops._abi.call('rod_conv_wgrad', x, *ops._pro_args(xpro), dy, dw, None, wws, 1, 1, M, Cin, Cout, 1, 0, 0,
                           ops.dtcode(x), ops.stream())
 
+        coef0 = ops.bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, False, False)
+
+        def pw_only():
+            ops.pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef0, x, xpro, wt1, True, dw, None)
+
         def fused():
             coef = ops.bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, False, False)
             ops.pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, True, dw, None)
 
         res = {}
-        for name, fn in (('unfused', unfused), ('fused', fused)):
+        fns = (('pw', pw_only),) if a.pw_only else (('unfused', unfused), ('fused', fused), ('pw', pw_only))
+        for name, fn in fns:
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -67,12 +77,21 @@ def main():
             res[name] = e0.elapsed_time(e1) / a.iters * 1e3
         # algorithmic bytes of the fused pass + its reduce: dz, y twice, x once, dx once
         alg = 2 * M * (2 * Cout * 2 + 2 * Cin)
-        rows.append({'M': M, 'Cin': Cin, 'Cout': Cout, 'unfused_us': round(res['unfused'], 1),
-                     'fused_us': round(res['fused'], 1), 'speedup': round(res['unfused'] / res['fused'], 3),
-                     'fused_alg_GBps': round(alg / res['fused'] / 1e3, 1)})
+        pw_alg = M * (2 * Cout * 2 + 2 * Cin * 2)
+        pw_only()
+        torch.cuda.synchronize()
+        r = {'M': M, 'Cin': Cin, 'Cout': Cout, 'pw_us': round(res['pw'], 1),
+             'pw_alg_GBps': round(pw_alg / res['pw'] / 1e3, 1),
+             'check': [float(dx.double().nan_to_num().abs().sum()), float(dw.double().abs().sum())]}
+        if not a.pw_only:
+            r.update({'unfused_us': round(res['unfused'], 1), 'fused_us': round(res['fused'], 1),
+                      'speedup': round(res['unfused'] / res['fused'], 3),
+                      'fused_alg_GBps': round(alg / res['fused'] / 1e3, 1)})
+        rows.append(r)
         print(json.dumps(rows[-1]), flush=True)
-    print(json.dumps({'total_unfused_us': round(sum(r['unfused_us'] for r in rows), 1),
-                      'total_fused_us': round(sum(r['fused_us'] for r in rows), 1)}))
+    print(json.dumps({'total_pw_us': round(sum(r['pw_us'] for r in rows), 1),
+                      'total_unfused_us': round(sum(r.get('unfused_us', 0) for r in rows), 1),
+                      'total_fused_us': round(sum(r.get('fused_us', 0) for r in rows), 1)}))
 
 
 if __name__ == '__main__':
