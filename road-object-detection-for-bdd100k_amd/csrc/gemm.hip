@@ -146,6 +146,15 @@ struct RowSrc {
         const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
         if (yy >= 0 && yy < H && xx >= 0 && xx < W) c.load_vec(base + ((long)yy * W + xx) * ldx + ci);
         else c.zero();  // prologue deferred to pro_pending()
+      } else if constexpr (CIN == 0) {
+        // Cin % 8 != 0 (the heads' last 3x3 convs: 4 or num_classes x anchors channels): one
+        // division per chunk, then G-element sub-loads (G = the widest power of two dividing
+        // Cin and ldx, so a sub-load never crosses a tap)
+        const unsigned long al = (unsigned long)base;
+        if (Cin % 4 == 0 && ldx % 4 == 0 && al % (4 * sizeof(T)) == 0) gather<4, PRO>(c, k, K, Cin, H, W, ldx, pt, act);
+        else if (Cin % 2 == 0 && ldx % 2 == 0 && al % (2 * sizeof(T)) == 0)
+          gather<2, PRO>(c, k, K, Cin, H, W, ldx, pt, act);
+        else gather<1, PRO>(c, k, K, Cin, H, W, ldx, pt, act);
       } else {
         const int cin = CIN > 0 ? CIN : Cin;
 #pragma unroll
@@ -165,6 +174,73 @@ struct RowSrc {
         c.ok = false;
       }
     }
+  }
+  // Sequential im2col walk (KS == 3, Cin % 8 == 0) for a k loop that visits k, k + step, ...:
+  // the chunk's tap / channel and the tap's pixel pointer are carried from step to step, so a
+  // step costs a pointer add instead of a division and a 64-bit address rebuild per chunk
+  int wtap, wci;
+  const T* wp;
+  bool wok;
+  __device__ __forceinline__ void walk_set(int H, int W, int ldx) {
+    const int yy = y + wtap / 3 - 1, xx = x + wtap % 3 - 1;
+    wok = valid && wtap < 9 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+    wp = base + ((long)yy * W + xx) * ldx;
+  }
+  __device__ __forceinline__ void walk_init(int k, int Cin, int H, int W, int ldx) {
+    wtap = k / Cin;
+    wci = k - wtap * Cin;
+    walk_set(H, W, ldx);
+  }
+  __device__ __forceinline__ void walk_next(int step, int Cin, int H, int W, int ldx) {
+    wci += step;
+    if (wci >= Cin) {
+      do {
+        wci -= Cin;
+        ++wtap;
+      } while (wci >= Cin);
+      walk_set(H, W, ldx);
+    }
+  }
+  __device__ __forceinline__ void walk_load(Chunk8<T>& c) const {
+    if (wok) c.load_vec(wp + wci);  // prologue deferred (walk_pro)
+    else c.zero();
+  }
+  template <bool PRO>
+  __device__ __forceinline__ void walk_pro(Chunk8<T>& c, const float* pt, int act) const {
+    if constexpr (PRO) {
+      if (c.ok) c.pro(pt, wci, act);
+    }
+  }
+  template <int G, bool PRO>
+  __device__ __forceinline__ void gather(Chunk8<T>& c, int k, int K, int cin, int H, int W, int ldx, const float* pt,
+                                         int act) const {
+    struct alignas(sizeof(T) * G) Sub { T e[G]; };
+    int tap = k / cin, ci = k - tap * cin;
+#pragma unroll
+    for (int j = 0; j < 8; j += G) {
+      Sub v;
+#pragma unroll
+      for (int e = 0; e < G; ++e) v.e[e] = (T)0.f;
+      if (k + j < K) {  // K % G == 0: the sub-load is all in or all out
+        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+          v = *(const Sub*)(base + ((long)yy * W + xx) * ldx + ci);
+          if constexpr (PRO) {
+#pragma unroll
+            for (int e = 0; e < G; ++e)
+              v.e[e] = from_f32<T>(act_fwd(fmaf(to_f32(v.e[e]), pt[2 * (ci + e)], pt[2 * (ci + e) + 1]), act));
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < G; ++e) c.set(j + e, v.e[e]);
+      ci += G;
+      if (ci >= cin) {
+        ci -= cin;
+        ++tap;
+      }
+    }
+    c.ok = false;
   }
   // the deferred prologue of a chunk loaded for k (vector paths), just before it is stored
   template <bool PRO>
@@ -197,8 +273,12 @@ __device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b
 // forward: y[m, co] = sum_k A[m,k] wt[co,k] + bias[co]
 // block 256 threads = 4 waves laid out WM x WN; tile BM x BN; wave tile (BM/WM) x (BN/WN)
 // =====================================================================================
+// BKT: k depth per LDS step.  32: one LDS buffer, two barriers per step (the next step's
+// global loads in flight under the MFMAs).  64 (bf16): two LDS buffers, ONE barrier per step,
+// twice the MFMAs per wave between barriers — the deep-K 3x3 convs (K = 9 x 128), which at 32
+// were load-latency bound (a k step's MFMAs per SIMD shorter than the im2col gather latency).
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool SPLIT = false, bool STATS = false,
-          bool PRO = false, bool GRED = false>
+          bool PRO = false, bool GRED = false, int BKT = BK>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
                                                        const float* __restrict__ bias, T* __restrict__ Y, long M,
                                                        int H, int W, int Cin, int Cout, int ldx, int ldy,
@@ -209,20 +289,23 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   constexpr int WM = 4 / WN;
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
-  constexpr int LD = BK + LdsPad<T>::v;
-  constexpr int ACH = BM * BK / 8 / 256;          // A chunks per thread (=2)
-  constexpr int BCH = (BN * BK / 8 + 255) / 256;  // B chunks per thread
+  static_assert(BKT == BK || (BKT == 64 && sizeof(T) == 2 && !SPLIT), "BKT 64: bf16, no split-K");
+  constexpr bool DB = BKT == 64;                  // double-buffered LDS
+  constexpr int CPR = BKT / 8;                    // 16-byte k chunks per tile row
+  constexpr int RPP = 256 / CPR;                  // tile rows per pass of the block
+  constexpr int LD = BKT + LdsPad<T>::v;
+  constexpr int ACH = BM * BKT / 8 / 256;          // A chunks per thread (2, or 4 at BKT 64)
+  constexpr int BCH = (BN * BKT / 8 + 255) / 256;  // B chunks per thread
   // epilogue staging: one 64-row half of the tile at a time, row pad keeps 16-byte alignment
   constexpr int EV = 16 / sizeof(T);
   constexpr int LDC = BN + EV;
-  constexpr int MAIN_BYTES = (BM + BN) * LD * sizeof(T);
+  constexpr int MAIN_BYTES = (DB ? 2 : 1) * (BM + BN) * LD * sizeof(T);
   constexpr int EPI_BYTES = VY ? 64 * LDC * sizeof(T) : 0;
   constexpr int ST_BYTES = 0;
   constexpr int SM1 = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   constexpr int SMEM = SM1 > ST_BYTES ? SM1 : ST_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  T* As = (T*)smem;
-  T* Bs = As + BM * LD;
+  T* As = (T*)smem;  // LDS buffer b: A tile at As + b(BM+BN)LD, B tile after it
 
   const int K = KS * KS * Cin;
   const int tid = threadIdx.x;
@@ -242,11 +325,11 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   }
   const long m0 = mt * BM;
   const int n0 = nt * BN;
-  const int kc = (tid & 3) * 8;
+  const int kc = (tid % CPR) * 8;
 
   RowSrc<T, KS> rows[ACH];
 #pragma unroll
-  for (int i = 0; i < ACH; ++i) rows[i].init(X, m0 + (tid >> 2) + i * 64, M, H, W, ldx);
+  for (int i = 0; i < ACH; ++i) rows[i].init(X, m0 + tid / CPR + i * RPP, M, H, W, ldx);
   extern __shared__ float pro_lds[];  // PRO: [Cin][2] prologue table (dynamic LDS)
   if constexpr (PRO) {
     stage_pro(pro_lds, pro, Cin);
@@ -254,17 +337,31 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   }
 
   Chunk8<T> ra[ACH], rb[BCH];
+  // 3x3 with 16-byte A chunks: the k loop is sequential (k0 = kb, kb + BKT, ...), so the rows
+  // walk their taps incrementally (RowSrc::walk_*); the state always matches the chunk held in ra
+  constexpr bool WALK = KS == 3 && VA;
+  bool first = true;
   auto load_tiles = [&](int k0) {
+    if constexpr (WALK) {
 #pragma unroll
-    for (int i = 0; i < ACH; ++i)
-      rows[i].template load<VA, PRO>(ra[i], k0 + kc, K, Cin, H, W, ldx, pro_lds, pro.act);
+      for (int i = 0; i < ACH; ++i) {
+        if (first) rows[i].walk_init(k0 + kc, Cin, H, W, ldx);
+        else rows[i].walk_next(BKT, Cin, H, W, ldx);
+        rows[i].walk_load(ra[i]);
+      }
+      first = false;
+    } else {
+#pragma unroll
+      for (int i = 0; i < ACH; ++i)
+        rows[i].template load<VA, PRO>(ra[i], k0 + kc, K, Cin, H, W, ldx, pro_lds, pro.act);
+    }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int cid = tid + i * 256;
-      const int r = cid >> 2;
+      const int r = cid / CPR;
       const int co = n0 + r;
       const int k = k0 + kc;
-      if (cid >= BN * BK / 8) continue;
+      if (cid >= BN * BKT / 8) continue;
       if (co >= Cout || k >= K) {
         rb[i].zero();
       } else if (VB && k + 8 <= K) {
@@ -287,30 +384,59 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   // split-K: this workgroup reduces k in [kb, ke) only
   const int kb = SPLIT ? blockIdx.z * kper : 0;
   const int ke = SPLIT ? (kb + kper < K ? kb + kper : K) : K;
-  load_tiles(kb);
-  for (int k0 = kb; k0 < ke; k0 += BK) {
-    __syncthreads();
+  // stage the registers of the k step at k0 into LDS buffer `buf`
+  auto store_tiles = [&](int k0, int buf) {
+    T* as = As + buf * (BM + BN) * LD;
+    T* bs = as + BM * LD;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      rows[i].template pro_pending<PRO>(ra[i], k0 + kc, Cin, pro_lds, pro.act);
-      ra[i].store_lds(As + ((tid >> 2) + i * 64) * LD + kc);
+      if constexpr (WALK) rows[i].template walk_pro<PRO>(ra[i], pro_lds, pro.act);
+      else rows[i].template pro_pending<PRO>(ra[i], k0 + kc, Cin, pro_lds, pro.act);
+      ra[i].store_lds(as + (tid / CPR + i * RPP) * LD + kc);
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int cid = tid + i * 256;
-      if (cid < BN * BK / 8) rb[i].store_lds(Bs + (cid >> 2) * LD + kc);
+      if (cid < BN * BKT / 8) rb[i].store_lds(bs + (cid / CPR) * LD + kc);
     }
-    __syncthreads();
-    if (k0 + BK < ke) load_tiles(k0 + BK);  // next tile in flight under the MFMAs
+  };
+  auto mma_step = [&](int buf) {
+    const T* as = As + buf * (BM + BN) * LD;
+    const T* bs = as + BM * LD;
     const int fr = lane & 15, fk = (lane >> 4) * 8;
 #pragma unroll
-    for (int a = 0; a < MT; ++a) {
-      const T* pa = As + (wm * (BM / WM) + a * 16 + fr) * LD + fk;
+    for (int kk = 0; kk < BKT; kk += 32)
 #pragma unroll
-      for (int b = 0; b < NT; ++b) {
-        const T* pb = Bs + (wn * (BN / WN) + b * 16 + fr) * LD + fk;
-        mma32(acc[a][b], pa, pb);
+      for (int a = 0; a < MT; ++a) {
+        const T* pa = as + (wm * (BM / WM) + a * 16 + fr) * LD + kk + fk;
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          const T* pb = bs + (wn * (BN / WN) + b * 16 + fr) * LD + kk + fk;
+          mma32(acc[a][b], pa, pb);
+        }
       }
+  };
+  load_tiles(kb);
+  if constexpr (DB) {
+    // buffer b is read in step i and rewritten in step i+1 (after that step's barrier)
+    store_tiles(kb, 0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kb; k0 < ke; k0 += BKT) {
+      const bool more = k0 + BKT < ke;
+      if (more) load_tiles(k0 + BKT);  // next step's global loads in flight under the MFMAs
+      mma_step(buf);
+      if (more) store_tiles(k0 + BKT, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    for (int k0 = kb; k0 < ke; k0 += BKT) {
+      __syncthreads();
+      store_tiles(k0, 0);
+      __syncthreads();
+      if (k0 + BKT < ke) load_tiles(k0 + BKT);  // next tile in flight under the MFMAs
+      mma_step(0);
     }
   }
 
@@ -1173,7 +1299,7 @@ static bool aligned16(const void* p) {
 
 // `pro` (nullable): BatchNorm-apply prologue on the A operand; its table takes 8*Cin bytes of
 // dynamic LDS.
-template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool PRO>
+template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool PRO, int BKT = BK>
 static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
                             int Cout, int ldx, int ldy, float* stats, const BnPro& pro, const BnGred* gr,
                             hipStream_t s) {
@@ -1182,18 +1308,30 @@ static void conv_fwd_launch(const void* x, const void* wt, const float* bias, vo
   const size_t lds = PRO ? 8 * (size_t)Cin : 0;
   if constexpr (VY) {
     if (gr) {
-      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO, true>), grid, dim3(256), lds, s,
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO, true, BKT>), grid, dim3(256), lds, s,
                          (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, nullptr, 0, pro, *gr);
       return;
     }
     if (stats) {
-      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, true, PRO>), grid, dim3(256), lds, s,
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, true, PRO, false, BKT>), grid, dim3(256), lds, s,
                          (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, stats, 0, pro);
       return;
     }
   }
-  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO>), grid, dim3(256), lds, s,
+  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO, false, BKT>), grid, dim3(256), lds, s,
                      (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy, nullptr, 0, pro);
+}
+
+// k depth 64 with double-buffered LDS (bf16) for the 3x3 convs with K % 64 == 0 and a 97..128-wide
+// N tile (the heads' 128 -> 128 3x3), ROD_GEMM_BK64=1 (2: also the 1x1 convs with K >= 256).  Off
+// by default: measured no faster at b = 8 (87.5 vs 87.1 us) and slower at b = 32 (217 vs 185 us per
+// call): 184 VGPRs and 74 KB of LDS drop the kernel from 3 to 2 waves per SIMD.
+static int bk64_mode() {
+  static const int m = [] {
+    const char* e = getenv("ROD_GEMM_BK64");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
 }
 
 // N tile: the whole of Cout in one tile up to 256 (A is read once), else 128-wide tiles.
@@ -1207,6 +1345,15 @@ static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const vo
 #define CF(BN_, VA_, VB_, VY_) \
   conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, gr, s)
   if (va && vb && vy) {
+    if constexpr (sizeof(T) == 2) {
+      const int K = KS * KS * Cin;
+      const int mode = bk64_mode();
+      if (mode > 0 && K % 64 == 0 && Cout > 96 && Cout <= 128 && (KS == 3 || (mode > 1 && K >= 256))) {
+        conv_fwd_launch<T, KS, 128, true, true, true, PRO, 64>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats,
+                                                                pro, gr, s);
+        return;
+      }
+    }
     if (Cout <= 32) CF(32, true, true, true);
     else if (Cout <= 64) CF(64, true, true, true);
     else if (Cout <= 96) CF(96, true, true, true);
@@ -1230,13 +1377,24 @@ static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const vo
 #undef CF
 }
 
-template <typename T, int KS, bool PRO>
-static void conv_fwd_split(const SplitPlan& p, const void* x, const void* wt, float* part, long M, int H, int W,
-                           int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s) {
+template <typename T, int KS, bool PRO, bool VA, bool VB>
+static void conv_fwd_split_t(const SplitPlan& p, const void* x, const void* wt, float* part, long M, int H, int W,
+                             int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, 128), p.splits);
   const size_t lds = PRO ? 8 * (size_t)Cin : 0;
-  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, 128, true, true, false, true, false, PRO>), grid, dim3(256), lds, s,
+  hipLaunchKernelGGL((conv_fwd_kernel<T, KS, 128, VA, VB, false, true, false, PRO>), grid, dim3(256), lds, s,
                      (const T*)x, (const T*)wt, nullptr, nullptr, M, H, W, Cin, Cout, ldx, 0, part, p.kper, pro);
+}
+// split-K over the k-steps (small maps with a deep K).  The non-vector operand paths (the heads'
+// last 3x3 convs, Cin % 8 != 0 on 3x5 .. 23x40 maps) split too: one 128-row tile per image level
+// would otherwise walk all of K in a single workgroup (~50 us of load latency).
+template <typename T, int KS, bool PRO>
+static void conv_fwd_split(bool va, bool vb, const SplitPlan& p, const void* x, const void* wt, float* part, long M,
+                           int H, int W, int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s) {
+  if (va && vb) conv_fwd_split_t<T, KS, PRO, true, true>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
+  else if (va) conv_fwd_split_t<T, KS, PRO, true, false>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
+  else if (vb) conv_fwd_split_t<T, KS, PRO, false, true>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
+  else conv_fwd_split_t<T, KS, PRO, false, false>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
 }
 
 template <typename T>
@@ -1271,14 +1429,14 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
       return;
     }
   }
-  if (ws != nullptr && sp.splits > 1 && va && vb) {
+  if (ws != nullptr && sp.splits > 1 && !(ksize == 3 && Cin == 3)) {
     float* part = (float*)ws;
     if (ksize == 1) {
-      if (pro) conv_fwd_split<T, 1, true>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
-      else conv_fwd_split<T, 1, false>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+      if (pro) conv_fwd_split<T, 1, true>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+      else conv_fwd_split<T, 1, false>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
     } else {
-      if (pro) conv_fwd_split<T, 3, true>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
-      else conv_fwd_split<T, 3, false>(sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+      if (pro) conv_fwd_split<T, 3, true>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+      else conv_fwd_split<T, 3, false>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
     }
     hipLaunchKernelGGL(splitk_combine_kernel<T>, dim3(cdivl(M * Cout, 256)), dim3(256), 0, s, (const float*)part,
                        bias, (T*)y, M, Cout, ldy, sp.splits);

@@ -11,6 +11,8 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
   bn_bwd_reduce        : es*M*C*2 (read dz, read y);  bn_bwd_apply: es*M*C*3
   pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product
   match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
+  ir_block_fwd (fused) : es*(N*H*W*Cin + N*Ho*Wo*Cout) + weights, 2*N*H*W*Cin*inner +
+                         18*N*Ho*Wo*inner + 2*N*Ho*Wo*inner*Cout
 """
 
 _ES = {0: 4, 1: 2}
@@ -77,6 +79,15 @@ def cost(name, a):
         want_dx = a[15] is not None
         byts = es * (2 * M * Cout + M * Cin + (M * Cin if want_dx else 0)) + Cout * Cin * (es + 4)
         return byts, 2 * M * Cin * Cout * (2 if want_dx else 1) + 10 * M * Cout
+    if name == "rod_ir_block_fwd":
+        # fused inverted residual: x read once (the residual re-read is L2-served by design),
+        # out written once, the expanded tensor never in HBM; expand flops over all input
+        # pixels, depthwise + project over the output pixels
+        N, H, W, Cin, inner, Cout, s, dt = a[18], a[19], a[20], a[21], a[22], a[23], a[24], a[25]
+        es = _ES[dt]
+        Ho, Wo = -(-H // s), -(-W // s)
+        byts = es * (N * H * W * Cin + N * Ho * Wo * Cout) + es * inner * (Cin + Cout) + 36 * inner
+        return byts, 2 * N * H * W * Cin * inner + 18 * N * Ho * Wo * inner + 2 * N * Ho * Wo * inner * Cout
     if name == "rod_match_anchors":
         B, A, G = a[12], a[13], a[14]
         return B * A * 56 + A * 32 + B * G * 20, 15 * G * A * B
@@ -99,4 +110,5 @@ ENTRY_KERNELS = {
     "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
     "rod_conv_fwd": (("conv_fwd_kernel", "stem_conv_fwd_kernel"), ("conv_fwd_kernel", "stem_conv_fwd_kernel")),
     "rod_bn_finalize": (("bn_parts_merge_kernel",), ("bn_parts_merge_kernel",)),
+    "rod_ir_block_fwd": (("ir_block_fwd_kernel",), ("ir_block_fwd_kernel",)),
 }

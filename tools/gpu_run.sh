@@ -18,6 +18,13 @@ run() {  # name timeout cmd...
   if fatal $rc; then echo "FATAL rc=$rc in $name; stopping"; exit $rc; fi
   return 0
 }
+# kernel-trace CSVs can be tens of MB (gpurun copies back <= 64 MiB): summarise on the box, keep
+# the per-kernel stats CSV, drop the raw trace
+summ() {  # dir marker iterations title
+  python tools/trace_summary.py $1/run_kernel_trace.csv "$2" $3 "$4" > $1/summary.txt 2>&1
+  rm -f $1/run_kernel_trace.csv $1/run_agent_info.csv
+  head -25 $1/summary.txt | cut -c1-200
+}
 for step in "$@"; do
   case $step in
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
@@ -35,12 +42,25 @@ for step in "$@"; do
          run cli_predict 300 python road-object-detection-for-bdd100k_amd/predict.py --checkpoint_all=gpurun_out/ckpt/mobilenet_v2.model --batch_size=2 --num_batches=2 --output=gpurun_out/pred.json ;;
     probetable) run probetable 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_table.json ;;
     probetableall) run probetableall 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-inference --train_range ALL --probe-table $OUT/${TAG}_probe_table_all.json ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --kernel-steps 0 &&
+         summ $OUT/prof_$TAG normalize_image 5+2 "REFINE train step bf16 b8 720p, graph replays" ;;
     profall) run profall 600 rocprofv3 --kernel-trace --stats -d $OUT/profall_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --train_range ALL ;;
-    profpred) run profpred 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 720 --batch 32 --iters 10 ;;
-    profpred1080) run profpred1080 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred1080_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 10 ;;
+    profpred) run profpred 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 720 --batch 32 --iters 10 &&
+         summ $OUT/profpred_$TAG normalize_image 10 "predict path bf16 b32 720p, graph replays" ;;
+    profpred1080) run profpred1080 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred1080_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 10 &&
+         summ $OUT/profpred1080_$TAG normalize_image 10 "predict path bf16 b8 1080p, graph replays" ;;
     pmcfetch) run pmcfetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference ;;
     pmcwrite) run pmcwrite 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference ;;
+    cbhead) run cbhead 300 python tools/conv_bench.py --shapes 7,13,14,15 ;;
+    cball) run cball 300 python tools/conv_bench.py ;;
+    convtests) run convtests 600 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_stem.py -m gpu -q -x --timeout=300 -p no:cacheprovider ;;
+    c5) run c5probe 300 python tools/c5_report.py probe --res 1080 --batch 8 --out $OUT/${TAG}_c5_probe.json &&
+        run c5f 130 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/c5f_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 3 --no-graph &&
+        run c5w 130 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/c5w_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 3 --no-graph &&
+        run c5m 130 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/c5m_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 3 --no-graph &&
+        f=$(ls $OUT/c5f_$TAG/*counter_collection.csv) && w=$(ls $OUT/c5w_$TAG/*counter_collection.csv) && m=$(ls $OUT/c5m_$TAG/*counter_collection.csv) &&
+        python tools/c5_report.py pmc $OUT/${TAG}_c5_probe.json $f $w $m --out $OUT/${TAG}_c5_report.json &&
+        gzip -f $f $w $m ;;
     *) echo "unknown step $step" ;;
   esac
 done
