@@ -141,6 +141,18 @@ def inference_fps(args, dev, dtype, batch=32, steps=5, warmup=2, hw=None):
             'mAP@0.5': None, 'mAP_note': 'no BDD100K data or trained checkpoint on the box (synthetic inputs)'}
 
 
+def replicated(r, world, dev):
+    """An inference leg run by every rank: whole-job images/s over the slowest rank's time."""
+    if world == 1:
+        return r
+    t = torch.tensor([r['ms_per_batch']], device=dev, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    ms = float(t.item())
+    r = dict(r, ms_per_batch=round(ms, 3), value=round(world * r['batch'] * 1e3 / ms, 2), n_gpus=world,
+             parallelism=f'{world} replicas (one per GPU, no exchange)')
+    return r
+
+
 NORTH_STAR = ('rod_dw3x3_fwd', 'rod_dw3x3_bwd_data', 'rod_dw3x3_bwd_filter', 'rod_conv_fwd', 'rod_conv_wgrad',
               'rod_pw_bwd', 'rod_bn_bwd_reduce', 'rod_bn_bwd_apply', 'rod_bn_bwd')
 
@@ -274,6 +286,14 @@ def main():
                               'alg_TFLOPs': fl / max(t, 1e-9) / 1e9})
             json.dump({'entries': rows, 'top_calls': calls}, f, indent=1)
 
+    # inference legs (configs[3], configs[4]): at N > 1 every rank runs the same predict path on
+    # its own batch (inference does not shard: replicas); the aggregate is all ranks' images over
+    # the slowest rank's time
+    inf = inf1080 = None
+    if args.inference:
+        inf = replicated(inference_fps(args, dev, dtype), world, dev)
+        if args.inference_1080:   # configs[4]: 1920x1080 bf16, fused inverted-residual blocks
+            inf1080 = replicated(inference_fps(args, dev, dtype, batch=8, hw=(1080, 1920)), world, dev)
     if rank == 0:
         per_launch_ms = ms / max(n_launch, 1)
         achieved_gbs = byts / max(ms, 1e-9) / 1e6
@@ -323,10 +343,10 @@ def main():
         }
         if kernels is not None:
             out['kernels'] = kernels
-        if args.inference and world == 1:
-            out['inference'] = inference_fps(args, dev, dtype)
-            if args.inference_1080:   # configs[4]: 1920x1080 bf16, fused inverted-residual blocks
-                out['inference_1080p'] = inference_fps(args, dev, dtype, batch=8, hw=(1080, 1920))
+        if inf is not None:
+            out['inference'] = inf
+        if inf1080 is not None:
+            out['inference_1080p'] = inf1080
         if args.cpu_baseline and world == 1:
             out['cpu_baseline'] = cpu_baseline(args.height, args.width)
         print(json.dumps(out), flush=True)

@@ -251,6 +251,25 @@ struct RowSrc {
   }
 };
 
+// chunk = p[0..7] with elements j >= left zero, in G-element loads (p G-aligned, left % G == 0)
+template <int G, typename T>
+__device__ __forceinline__ void load_sub(Chunk8<T>& c, const T* p, int left) {
+  struct alignas(sizeof(T) * G) Sub { T e[G]; };
+#pragma unroll
+  for (int j = 0; j < 8; j += G) {
+    Sub v;
+    if (j < left) {
+      v = *(const Sub*)(p + j);
+    } else {
+#pragma unroll
+      for (int e = 0; e < G; ++e) v.e[e] = (T)0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < G; ++e) c.set(j + e, v.e[e]);
+  }
+  c.ok = false;
+}
+
 // Stage the prologue table [Cin][2] = (scale, offset) into LDS (caller syncs).
 __device__ __forceinline__ void stage_pro(float* pt, const BnPro& p, int Cin) {
   for (int c = threadIdx.x; c < Cin; c += blockDim.x) bn_pro_affine(p, c, pt[2 * c], pt[2 * c + 1]);
@@ -367,8 +386,12 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
       } else if (VB && k + 8 <= K) {
         rb[i].load_vec(Wt + (long)co * K + k);
       } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) rb[i].set(j, (k + j < K) ? Wt[(long)co * K + k + j] : (T)0.f);
+        // unaligned rows (K % 8 != 0: the heads' last 3x3 convs): G-element sub-loads, G the
+        // widest power of two dividing K (Wt is 16-byte aligned, so the row start is G-aligned)
+        const T* wrow = Wt + (long)co * K + k;
+        if (K % 4 == 0) load_sub<4>(rb[i], wrow, K - k);
+        else if (K % 2 == 0) load_sub<2>(rb[i], wrow, K - k);
+        else load_sub<1>(rb[i], wrow, K - k);
       }
     }
   };
@@ -1364,15 +1387,18 @@ static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const vo
     else CF(128, true, true, true);
     return;
   }
-  if (PRO || Cout > 64) {
-    if (va && vb) CF(128, true, true, false); else if (va) CF(128, true, false, false);
-    else if (vb) CF(128, false, true, false); else CF(128, false, false, false);
-  } else if (Cout <= 32) {
-    if (va && vb) CF(32, true, true, false); else if (va) CF(32, true, false, false);
-    else if (vb) CF(32, false, true, false); else CF(32, false, false, false);
+  // direct-store epilogue (Cout or ldy not a multiple of 8: the heads' last convs, 4 / 11 x
+  // anchors channels): the N tile is the smallest of 32 / 64 / 96 / 128 covering Cout (a 128-wide
+  // tile for 36 or 66 outputs wasted half the MFMAs and B loads); B rows load in G-element
+  // pieces (VB false), which also covers the aligned case at two 8-byte loads per chunk
+  if (Cout <= 32) {
+    if (va) CF(32, true, false, false); else CF(32, false, false, false);
+  } else if (Cout <= 64) {
+    if (va) CF(64, true, false, false); else CF(64, false, false, false);
+  } else if (Cout <= 96) {
+    if (va) CF(96, true, false, false); else CF(96, false, false, false);
   } else {
-    if (va && vb) CF(64, true, true, false); else if (va) CF(64, true, false, false);
-    else if (vb) CF(64, false, true, false); else CF(64, false, false, false);
+    if (va) CF(128, true, false, false); else CF(128, false, false, false);
   }
 #undef CF
 }

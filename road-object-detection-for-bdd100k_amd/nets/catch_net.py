@@ -289,6 +289,16 @@ class CatchNet:
             mb.BN_DECAY, HEAD_BN_DECAY = saved
 
     def forward(self, inputs, is_training):
+        if is_training:
+            return self._forward(inputs, is_training)
+        # inference: every BatchNorm's eval statistics from one launch (ParamStore.eval_refresh)
+        self.store.eval_refresh(HEAD_BN_EPS)
+        try:
+            return self._forward(inputs, is_training)
+        finally:
+            self.store.eval_release()
+
+    def _forward(self, inputs, is_training):
         names = config.extract_feat_name[self.backbone_name]
         if self.msf:
             taps = sorted(set(names) | {n for b in self.MSF_BLOCKS for n in b}, key=lambda n: int(n.split('_')[1]))

@@ -481,6 +481,9 @@ def bn_statistics(x, mmean, mvar, training, decay, eps=1e-3, parts=None):
         ws = workspace(_abi.query("rod_bn_stats_workspace", M, C), x.device)
         _abi.call("rod_bn_stats", x, M, C, 0, eps, decay, mean, rstd, mmean, mvar, ws, dtcode(x), stream())
     else:
+        hit = _eval_cached(mmean, mvar, eps)
+        if hit is not None:
+            return hit
         _abi.call("rod_bn_eval_stats", mmean, mvar, eps, mean, rstd, C, stream())
     return mean, rstd
 
@@ -764,7 +767,17 @@ def ir_block_set_mode(mode):
     return int(_abi.lib().rod_ir_block_set_mode(int(mode)))
 
 
+def _eval_cached(mmean, mvar, eps):
+    st = getattr(mmean, "_rod_store", None)
+    if st is None or getattr(mvar, "_rod_store", None) is not st:
+        return None
+    return st.eval_views(mmean, mvar, eps)
+
+
 def eval_stats(mmean, mvar, eps):
+    hit = _eval_cached(mmean, mvar, eps)
+    if hit is not None:
+        return hit
     C = mmean.numel()
     mean = torch.empty(C, dtype=torch.float32, device=mmean.device)
     rstd = torch.empty(C, dtype=torch.float32, device=mmean.device)

@@ -88,9 +88,44 @@ class ParamStore:
             p._rod_name = name
             p._rod_store = self
             self.params[name] = p
+        # BatchNorm moving statistics: views of ONE flat buffer, so the eval-mode (mean, rstd) of
+        # every BatchNorm comes from a single rod_bn_eval_stats launch per forward (eval_refresh)
+        nb = sum(arr.size for arr in self._buffers.values())
+        hb = np.concatenate([arr.reshape(-1) for arr in self._buffers.values()]) if nb else np.zeros(1, np.float32)
+        self.flat_buf = torch.from_numpy(hb).to(self.device)
+        self._eval_out = torch.empty((2, max(nb, 1)), dtype=torch.float32, device=self.device)
+        self._eval_eps = None
+        o = 0
         for name, arr in self._buffers.items():
-            self.buffers[name] = torch.from_numpy(arr.copy()).to(self.device)
+            b = self.flat_buf[o:o + arr.size].view(arr.shape)
+            b._rod_store = self
+            self.buffers[name] = b
+            o += arr.size
         return self
+
+    # ---- eval-mode BatchNorm statistics -----------------------------------------------
+    def eval_refresh(self, eps):
+        """(mean, rstd) = (moving_mean, 1/sqrt(moving_var + eps)) of EVERY buffer element in one
+        launch (rod_bn_eval_stats over the flat buffer); until eval_release(), eval_views serves
+        each BatchNorm's slices from it instead of a launch per BatchNorm."""
+        from . import _abi
+        from .ops import stream
+        n = self.flat_buf.numel()
+        _abi.call("rod_bn_eval_stats", self.flat_buf, self.flat_buf, eps, self._eval_out[0], self._eval_out[1], n,
+                  stream())
+        self._eval_eps = eps
+
+    def eval_release(self):
+        self._eval_eps = None
+
+    def eval_views(self, mmean, mvar, eps):
+        """The refreshed (mean, rstd) slices of one BatchNorm, or None outside a refresh."""
+        if self._eval_eps is None or eps != self._eval_eps:
+            return None
+        base = self.flat_buf.data_ptr()
+        om, ov = (mmean.data_ptr() - base) // 4, (mvar.data_ptr() - base) // 4
+        C = mmean.numel()
+        return self._eval_out[0, om:om + C], self._eval_out[1, ov:ov + C]
 
     def set_trainable(self, predicate):
         """requires_grad per parameter name (train.py:160-166 trainable-var filtering)."""
