@@ -63,6 +63,17 @@ typedef __bf16 ir_bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float relu6_bf16(float v, float sc, float sh) {
   return (float)(bf16_t)act_t<ROD_ACT_RELU6>(fmaf(v, sc, sh));
 }
+typedef float ir_f32x2 __attribute__((ext_vector_type(2)));
+// two values of relu6_bf16((float)(bf16_t)a, sc, sh), packed as bf16x2 bits: the rounding pair
+// and the BatchNorm fma pair each take one packed instruction (v_cvt_pk_bf16_f32, v_pk_fma_f32);
+// per element the same operations, in the same order, as relu6_bf16
+__device__ __forceinline__ unsigned relu6_pair(float a, float b, ir_f32x2 sc2, ir_f32x2 sh2) {
+  const ir_bf16x2 r = ir_bf16x2{(bf16_t)a, (bf16_t)b};
+  ir_f32x2 v = {(float)r[0], (float)r[1]};
+  v = __builtin_elementwise_fma(v, sc2, sh2);
+  const ir_bf16x2 o = ir_bf16x2{(bf16_t)act_t<ROD_ACT_RELU6>(v.x), (bf16_t)act_t<ROD_ACT_RELU6>(v.y)};
+  return __builtin_bit_cast(unsigned, o);
+}
 
 // LDS layout (elements), all offsets multiples of 8 bf16 (16 bytes)
 template <int S>
@@ -71,7 +82,9 @@ struct IrLayout {
   static constexpr int PI = Tl::IH * Tl::IW;
   static constexpr int PIP = (PI + 15) / 16 * 16;
   static constexpr int PO = Tl::TH * Tl::TW;
-  static constexpr int LDE = PIP + 2;       // E plane stride: odd word count (conflict-free rows)
+  // E plane stride: an odd word count, chosen so the expand epilogue's b32 stores (16 channels
+  // x 4 pixel groups per wave) meet at most 2 lanes per bank (PIP + 2: 4)
+  static constexpr int LDE = PIP + 6;
   static constexpr int LDD = PO + 8;        // D plane stride (16-byte aligned rows)
   int KX, LDX, LDW, xs, we, wp, par, e, d, total;
   // nbuf parameter buffers: 2 (double-buffered chunk stream) or one per chunk (resident)
@@ -350,20 +363,27 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
       for (int nt = 0; nt < 2; ++nt) {
         const int e = nt * 16 + li;
         const float sc = F[9 * IR_CK + e], sh = F[10 * IR_CK + e];   // zero past inner
-        const bool eok = c * IR_CK + e < inner;
+        const ir_f32x2 sc2 = {sc, sc}, sh2 = {sh, sh};
+        const unsigned emask = c * IR_CK + e < inner ? 0xFFFFFFFFu : 0u;
 #pragma unroll
         for (int i = 0; i < MTE; ++i) {
           const int mt = wave + 4 * i;
           if (mt * 16 >= PIP) continue;
           // conv output rounded (rod_conv_fwd), then the depthwise's BatchNorm + ReLU6
-          // prologue (rounded); padding pixels and channels past inner are 0
-          float z[4];
+          // prologue (rounded); padding pixels and channels past inner are 0 (masked bits:
+          // bf16 +0, as the unfused chain's zero padding)
+          const unsigned in4 = (inside >> (i * 4)) & 15u;
+          unsigned o[2];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            z[r] = (eok && ((inside >> (i * 4 + r)) & 1)) ? relu6_bf16((float)(bf16_t)acc[i][nt][r], sc, sh) : 0.f;
-          bf16_t* dst = Es + e * LDE + mt * 16 + 4 * g;
-          *(ir_bf16x2*)dst = ir_bf16x2{(bf16_t)z[0], (bf16_t)z[1]};
-          *(ir_bf16x2*)(dst + 2) = ir_bf16x2{(bf16_t)z[2], (bf16_t)z[3]};
+          for (int h = 0; h < 2; ++h) {
+            unsigned m = emask;
+            if (in4 != 15u)
+              m &= (((in4 >> (2 * h)) & 1u) ? 0x0000FFFFu : 0u) | (((in4 >> (2 * h + 1)) & 1u) ? 0xFFFF0000u : 0u);
+            o[h] = relu6_pair(acc[i][nt][2 * h], acc[i][nt][2 * h + 1], sc2, sh2) & m;
+          }
+          unsigned* dst = (unsigned*)(Es + e * LDE + mt * 16 + 4 * g);
+          dst[0] = o[0];
+          dst[1] = o[1];
         }
       }
     }
@@ -376,12 +396,14 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
 #pragma unroll
       for (int k = 0; k < 9; ++k) w[k] = wdc[k * IR_CK];
       const float dsc = F[11 * IR_CK + ch], dsh = F[12 * IR_CK + ch];
-      const bool eok = c * IR_CK + ch < inner;
-      float acc[TW];
+      const ir_f32x2 dsc2 = {dsc, dsc}, dsh2 = {dsh, dsh};
+      const unsigned emask = c * IR_CK + ch < inner ? 0xFFFFFFFFu : 0u;
+      // output pairs (2p, 2p + 1) accumulate as one packed fma per tap (v_pk_fma_f32)
+      ir_f32x2 acc[TW / 2];
 #pragma unroll
-      for (int ox = 0; ox < TW; ++ox) acc[ox] = 0.f;
+      for (int p = 0; p < TW / 2; ++p) acc[p] = ir_f32x2{0.f, 0.f};
       const bf16_t* ep = Es + ch * LDE;
-      // taps in raster order (i, j): acc = fma(E, w, acc), as rod_dw3x3_fwd
+      // taps in raster order (i, j): acc = fma(E, w, acc) per output, as rod_dw3x3_fwd
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         float rowv[IW];
@@ -393,16 +415,21 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
           rowv[2 * q + 1] = (float)v[1];
         }
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < 3; ++j) {
+          const ir_f32x2 w2 = {w[i * 3 + j], w[i * 3 + j]};
 #pragma unroll
-          for (int ox = 0; ox < TW; ++ox) acc[ox] = fmaf(rowv[ox * S + j], w[i * 3 + j], acc[ox]);
+          for (int p = 0; p < TW / 2; ++p) {
+            const ir_f32x2 v = {rowv[(2 * p) * S + j], rowv[(2 * p + 1) * S + j]};
+            acc[p] = __builtin_elementwise_fma(v, w2, acc[p]);
+          }
+        }
       }
-      bf16x8 o[TW / 8];
+      unsigned o[TW / 2];
 #pragma unroll
-      for (int ox = 0; ox < TW; ++ox)
-        o[ox / 8][ox % 8] = (bf16_t)(eok ? relu6_bf16((float)(bf16_t)acc[ox], dsc, dsh) : 0.f);
+      for (int p = 0; p < TW / 2; ++p) o[p] = relu6_pair(acc[p].x, acc[p].y, dsc2, dsh2) & emask;
 #pragma unroll
-      for (int h = 0; h < TW / 8; ++h) *(bf16x8*)(Dt + ch * LDD + oy * TW + 8 * h) = o[h];
+      for (int h = 0; h < TW / 8; ++h)
+        *(uint4*)(Dt + ch * LDD + oy * TW + 8 * h) = uint4{o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]};
     }
     __syncthreads();
     // ---- C. project: acc[q, co] += D^T[q, 32 chunk channels] . Wp[co, chunk] -------------------

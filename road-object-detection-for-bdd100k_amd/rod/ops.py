@@ -748,10 +748,12 @@ def ir_block_supported(Cin, inner, Cout, stride, residual, dtype):
 
 def ir_block_preferred(Cin, inner, Cout, stride, residual, dtype):
     """Whether the eval backbone should take the fused block: where it measured faster than
-    the unfused chain on MI355X (tools/irblock_bench.py, HIP-graph replay, b8 720p / 1080p;
-    DESIGN.md §N1) — the persistent variant (parameters resident in LDS) at stride 1, or at
-    stride 2 on a 16-channel input.  Elsewhere (the deep blocks' parameters do not fit in LDS,
-    the stride-2 blocks with wider inputs) the unfused chain is faster."""
+    the unfused chain on MI355X (tools/irblock_bench.py, b8 720p / 1080p; DESIGN.md §6,
+    profiles/r2s3_irblock_bench.txt) — the persistent variant (parameters resident in LDS) at
+    stride 1, or at stride 2 on a 16-channel input.  Elsewhere (the deep blocks' parameters do
+    not fit in LDS, the stride-2 blocks with wider inputs) the unfused chain is faster; the
+    stride-2 24- and 32-channel blocks measure 1.03-1.14x fused at b8 but lose at the predict
+    path's b32 (18.76 -> 18.88 ms per batch with them fused)."""
     if not ir_block_supported(Cin, inner, Cout, stride, residual, dtype):
         return False
     if "irblock_all" in _ENABLE:

@@ -61,6 +61,11 @@ for step in "$@"; do
         f=$(ls $OUT/c5f_$TAG/*counter_collection.csv) && w=$(ls $OUT/c5w_$TAG/*counter_collection.csv) && m=$(ls $OUT/c5m_$TAG/*counter_collection.csv) &&
         python tools/c5_report.py pmc $OUT/${TAG}_c5_probe.json $f $w $m --out $OUT/${TAG}_c5_report.json &&
         gzip -f $f $w $m ;;
+    irpmc) run irpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU -d $OUT/irpmc_$TAG -o run --output-format csv -- python3 tools/irblock_bench.py --iters 3 --res 1080 &&
+           python tools/pmc_kernel_summary.py $OUT/irpmc_$TAG/run_counter_collection.csv ir_block_fwd > $OUT/${TAG}_irpmc.txt &&
+           gzip -f $OUT/irpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_irpmc.txt ;;
+    irbench) run irbench 300 python tools/irblock_bench.py --iters 10 --res 720 1080 ;;
+    irtests) run irtests 300 python -m pytest tests/test_gpu_irblock.py -m gpu -q -x --timeout=250 -p no:cacheprovider ;;
     *) echo "unknown step $step" ;;
   esac
 done
