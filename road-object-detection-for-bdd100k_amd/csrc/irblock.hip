@@ -271,7 +271,10 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
     }
   };
   // ---- input window of tile tt: 16-byte pieces (zero outside the image and past Cin) ------
-  const int XCH = KX / 8;
+  // the persistent variants have KX / 8 fixed by XP (ir_persist_pieces: 3 or 5 pieces <=> 4, 6
+  // pieces <=> 8), so the piece -> (pixel, chunk) split is a shift
+  constexpr int XCHC = XP == 6 ? 8 : 4;
+  const int XCH = PERSIST ? XCHC : KX / 8;
   auto xfetch = [&](int tt) {   // -> pf (persistent prefetch); the host checks PIP*XCH <= XP*256
     const int tx = tt % ntx, rest = tt / ntx;
     const int nn = rest / nty, h0 = (rest % nty) * TH * S - a.pt, w0 = tx * TW * S - a.pl;
@@ -303,6 +306,17 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
   // which of this lane's expand-output pixels lie inside the image (TF-SAME zero padding)
   unsigned inside = 0;
   auto set_inside = [&]() {
+    // interior tiles (the window inside the image: all but the border tiles) in one
+    // wave-uniform test
+    if (hi0 >= 0 && hi0 + Tl::IH <= a.H && wi0 >= 0 && wi0 + IW <= a.W) {
+      inside = 0xFFFFFFFFu;
+#pragma unroll
+      for (int i = 0; i < MTE; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if ((wave + 4 * i) * 16 + 4 * g + r >= PI) inside &= ~(1u << (i * 4 + r));
+      return;
+    }
     inside = 0;
 #pragma unroll
     for (int i = 0; i < MTE; ++i)
