@@ -983,6 +983,28 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
       for (int r = 0; r < 4; ++r) acc[a][b][r] = 0.f;
 
   Chunk8<T> rdv[RPT], rxv[RPT];
+  // 3x3 with 16-byte chunks: the thread's im2col column k0 + lc (tap, channel) is fixed for the
+  // whole block and its rows walk forward, so the pixel coordinates are carried from step to
+  // step instead of re-derived by 64-bit divisions per row (RowSrc::init)
+  constexpr bool WALKW = KS == 3 && VA && CIN == 0;
+  int wy[RPT], wx[RPT], wnn[RPT], kdy = 0, kdx = 0, kci = 0;
+  bool kok = false;
+  if constexpr (WALKW) {
+    const int kk = k0 + lc;
+    kok = kk < K;
+    const int tap = kok ? kk / Cin : 0;
+    kci = kk - tap * Cin;
+    kdy = tap / 3 - 1;
+    kdx = tap % 3 - 1;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const long row = mb + lr + u * BK;
+      wx[u] = (int)(row % W);
+      const long t = row / W;
+      wy[u] = (int)(t % H);
+      wnn[u] = (int)(t / H);
+    }
+  }
   auto load_one = [&](long row, Chunk8<T>& rd, Chunk8<T>& rx) {
     // dy[row, co0+lc .. +7]
     if (row >= me || co0 + lc >= Cout) {
@@ -993,13 +1015,34 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
 #pragma unroll
       for (int j = 0; j < 8; ++j) rd.set(j, (co0 + lc + j < Cout) ? DY[row * lddy + co0 + lc + j] : (T)0.f);
     }
-    RowSrc<T, KS, CIN> rs;
-    rs.init(X, row < me ? row : M, M, H, W, ldx);
-    rs.template load<VA, PRO>(rx, k0 + lc, K, Cin, H, W, ldx, pro_lds, pro.act);
+    if constexpr (!WALKW) {
+      RowSrc<T, KS, CIN> rs;
+      rs.init(X, row < me ? row : M, M, H, W, ldx);
+      rs.template load<VA, PRO>(rx, k0 + lc, K, Cin, H, W, ldx, pro_lds, pro.act);
+    }
   };
   auto load_step = [&](long m) {
 #pragma unroll
-    for (int u = 0; u < RPT; ++u) load_one(m + lr + u * BK, rdv[u], rxv[u]);
+    for (int u = 0; u < RPT; ++u) {
+      load_one(m + lr + u * BK, rdv[u], rxv[u]);
+      if constexpr (WALKW) {
+        // the thread's k (tap, channel) is fixed; its rows advance by RPT * BK pixels per step
+        const long row = m + lr + u * BK;
+        const int yy = wy[u] + kdy, xx = wx[u] + kdx;
+        if (kok && row < me && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          rxv[u].load_vec(X + (((long)wnn[u] * H + yy) * W + xx) * ldx + kci);
+        else
+          rxv[u].zero();
+        wx[u] += RPT * BK;
+        while (wx[u] >= W) {
+          wx[u] -= W;
+          if (++wy[u] == H) {
+            wy[u] = 0;
+            ++wnn[u];
+          }
+        }
+      }
+    }
   };
 
   if (mb < me) load_step(mb);
@@ -1008,7 +1051,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const T* __restrict__ X
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
       rdv[u].store_lds(Ds + (lr + u * BK) * WG_LD + lc);
-      if constexpr (PRO) {
+      if constexpr (PRO && WALKW) {
+        if (rxv[u].ok) rxv[u].pro(pro_lds, kci, pro.act);
+      } else if constexpr (PRO) {
         RowSrc<T, KS, CIN> rp;  // (pro_pending only needs KS)
         rp.template pro_pending<PRO>(rxv[u], k0 + lc, Cin, pro_lds, pro.act);
       }
