@@ -65,6 +65,8 @@ for step in "$@"; do
            python tools/pmc_kernel_summary.py $OUT/irpmc_$TAG/run_counter_collection.csv ir_block_fwd > $OUT/${TAG}_irpmc.txt &&
            gzip -f $OUT/irpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_irpmc.txt ;;
     irbench) run irbench 300 python tools/irblock_bench.py --iters 10 --res 720 1080 ;;
+    dwab) run dwa 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_w0.so python tools/dw_bench.py --out /tmp/${TAG}_dw0.pt &&
+          run dwb 300 python tools/dw_bench.py --check /tmp/${TAG}_dw0.pt ;;
     irtests) run irtests 300 python -m pytest tests/test_gpu_irblock.py -m gpu -q -x --timeout=250 -p no:cacheprovider ;;
     *) echo "unknown step $step" ;;
   esac
