@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 9
+#define ROD_ABI_VERSION 10
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -118,6 +118,19 @@ int rod_dw3x3_bwd_filter(const void* x, const float* pro_mean, const float* pro_
                          const float* pro_gamma, const float* pro_beta, int pro_act, const void* dy,
                          float* dw, void* workspace, int N, int H, int W, int C, int stride, int pad_t,
                          int pad_l, int Ho, int Wo, int dtype, void* stream);
+/* The BatchNorm backward of the depthwise's output fused into its filter gradient (ABI 10):
+ * dy = FusedBatchNormGrad-apply of (dz, y) with the coefficients coef[3][C] of
+ * rod_bn_bwd_reduce (exactly rod_bn_bwd_apply's arithmetic; y = this depthwise's output before
+ * its BatchNorm, bn_act its activation) is formed as the kernel streams dz / y, written to dy
+ * (for rod_dw3x3_bwd_data), and contracted with x into dw — the separate apply pass over the
+ * widest backbone tensors is never run (ref conv_blocks.py:238-247 + mobilenet.py:417-420).
+ * Same workspace as rod_dw3x3_bwd_filter. */
+int rod_dw3x3_bwd_filter_bn(const void* x, const float* pro_mean, const float* pro_rstd,
+                            const float* pro_gamma, const float* pro_beta, int pro_act, const void* dz,
+                            const void* y, const float* bn_mean, const float* bn_rstd, const float* bn_gamma,
+                            const float* bn_beta, int bn_act, const float* coef, void* dy, float* dw,
+                            void* workspace, int N, int H, int W, int C, int stride, int pad_t, int pad_l,
+                            int Ho, int Wo, int dtype, void* stream);
 
 /* ------------------------------------------------ BatchNorm (A4)
  * slim.batch_norm, fused, NHWC (mobilenet.py:417-420; catch_net.py:302).

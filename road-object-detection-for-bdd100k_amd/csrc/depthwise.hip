@@ -672,10 +672,22 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_data_lx_kernel(const T* __restr
 // (S=2: five) input rows ahead; the 9 taps accumulate in fp32 registers; per block the
 // computing columns are summed per channel in column order into part (n*strips + strip)*
 // coltiles + ct of the [parts][9][C] slab (channels of cgroup cg).
-template <typename T, int S, int PACT>
+// GP (rod_dw3x3_bwd_filter_bn): `dy` holds dz, the gradient at this depthwise's BatchNorm +
+// activation output; the dy queue loads dz and the pre-BatchNorm y of the same pixel and forms
+// the BatchNorm-backward apply in registers (rod_bn_bwd_apply's arithmetic, rounded to T) when
+// the row enters the queue, contracts that value and stores it once to gd.dy (every output
+// pixel belongs to exactly one thread's computing column / strip / channel group).
+struct DwGrad {
+  const void* y;
+  const float *mean, *rstd, *gamma, *beta, *coef;
+  int act;
+  void* dy;
+};
+template <typename T, int S, int PACT, bool GP = false>
 __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                             float* __restrict__ slab, int H, int W, int C, int pt,
-                                                            int pl, int Ho, int Wo, DwTile tl, BnPro pro) {
+                                                            int pl, int Ho, int Wo, DwTile tl, BnPro pro,
+                                                            DwGrad gd = DwGrad{}) {
   constexpr int V = Vec16<T>::N;
   constexpr int XS = 2 * 256 * 16;
   constexpr int SS = 256 * V * 4;
@@ -732,6 +744,49 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
       for (int v = 0; v < V; ++v) d.set(v, 0.f);
     }
   };
+  // GP: per-channel constants of the BatchNorm-backward apply, and the raw (dz, y) loads of
+  // the rows still in flight (their apply runs when they enter the contraction queue)
+  constexpr int GV = GP ? V : 1;
+  float gmu[GV], grs[GV], gsc[GV], gsh[GV], ga[GV], gmg[GV], gmx[GV];
+  const T* yn = nullptr;
+  T* dyo = nullptr;
+  if constexpr (GP) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      gmu[v] = gd.mean[c + v];
+      grs[v] = gd.rstd[c + v];
+      bn_affine(gd.mean, gd.rstd, gd.gamma, gd.beta, c + v, gsc[v], gsh[v]);
+      ga[v] = gd.coef[c + v];
+      gmg[v] = gd.coef[C + c + v];
+      gmx[v] = gd.coef[2 * C + c + v];
+    }
+    yn = (const T*)gd.y + (long)n * Ho * Wo * C + c;
+    dyo = (T*)gd.dy + (long)n * Ho * Wo * C + c;
+  }
+  auto gload = [&](Vec16<T>& d, Vec16<T>& yv, int m) {
+    if (comp && m >= 0 && m < nout) {
+      const long o = ((long)(ho0 + m) * Wo + wo) * C;
+      d.load(dn + o);
+      yv.load(yn + o);
+    }
+  };
+  // (dz, y) of row m -> the applied gradient in d (zero outside the strip), stored to gd.dy
+  auto gapply = [&](Vec16<T>& d, const Vec16<T>& yv, int m) {
+    if (comp && m >= 0 && m < nout) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float xv = yv.get(v);
+        const float dd = xv - gmu[v];
+        const float z = fmaf(xv, gsc[v], gsh[v]);
+        const float g = d.get(v) * act_grad(z, gd.act);
+        d.set(v, ga[v] * (g - gmg[v] - (dd * grs[v]) * gmx[v]));
+      }
+      d.store(dyo + ((long)(ho0 + m) * Wo + wo) * C);
+    } else {
+#pragma unroll
+      for (int v = 0; v < V; ++v) d.set(v, 0.f);
+    }
+  };
   auto addrow = [&](int i, const Vec16<T>& d, const float (&t0)[V], const float (&t1)[V], const float (&t2)[V]) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -757,11 +812,22 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
     issue(2, 2);
     // dy queue: d0 = output q, d1 = q-1, d2 = q-2 at input row q; f1, f2 = q+1, q+2 in flight
     Vec16<T> d0, d1, d2, f1, f2;
-    dload(d0, 0);
-    dload(d1, -1);
-    dload(d2, -2);
-    dload(f1, 1);
-    dload(f2, 2);
+    Vec16<T> y1, y2;  // GP: y of the rows in flight in f1, f2
+    if constexpr (GP) {
+      Vec16<T> y0;
+      gload(d0, y0, 0);
+      gapply(d0, y0, 0);
+      dload(d1, -1);
+      dload(d2, -2);
+      gload(f1, y1, 1);
+      gload(f2, y2, 2);
+    } else {
+      dload(d0, 0);
+      dload(d1, -1);
+      dload(d2, -2);
+      dload(f1, 1);
+      dload(f2, 2);
+    }
     for (int q0 = 0; q0 < nin; q0 += 3) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -791,7 +857,13 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
         d1 = d0;
         d0 = f1;
         f1 = f2;
-        dload(f2, q + 3);
+        if constexpr (GP) {
+          gapply(d0, y1, q + 1);
+          y1 = y2;
+          gload(f2, y2, q + 3);
+        } else {
+          dload(f2, q + 3);
+        }
       }
     }
   } else {
@@ -811,10 +883,20 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
     for (int k = 0; k < 4; ++k) issue(k, k);
     // dy queue at input row q = 2m (+1): dm1 = output m-1, dm = m; f1, f2 = m+1, m+2 in flight
     Vec16<T> dm1, dm, f1, f2;
-    dload(dm1, -1);
-    dload(dm, 0);
-    dload(f1, 1);
-    dload(f2, 2);
+    Vec16<T> y1, y2;  // GP: y of the rows in flight in f1, f2
+    if constexpr (GP) {
+      Vec16<T> y0;
+      dload(dm1, -1);
+      gload(dm, y0, 0);
+      gapply(dm, y0, 0);
+      gload(f1, y1, 1);
+      gload(f2, y2, 2);
+    } else {
+      dload(dm1, -1);
+      dload(dm, 0);
+      dload(f1, 1);
+      dload(f2, 2);
+    }
     for (int q0 = 0; q0 < nin; q0 += 4) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -843,7 +925,13 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
           dm1 = dm;
           dm = f1;
           f1 = f2;
-          dload(f2, (q >> 1) + 3);
+          if constexpr (GP) {
+            gapply(dm, y1, (q >> 1) + 1);
+            y1 = y2;
+            gload(f2, y2, (q >> 1) + 3);
+          } else {
+            dload(f2, (q >> 1) + 3);
+          }
         }
       }
     }
@@ -1525,6 +1613,57 @@ int rod_dw3x3_bwd_filter(const void* x, const float* pro_mean, const float* pro_
     return ROD_EINVAL;
   }
   return check_launch("rod_dw3x3_bwd_filter");
+}
+
+int rod_bn_bwd_apply(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                     const float* beta, const float* coef, void* dy, long M, int C, int act, int dtype, void* stream);
+
+int rod_dw3x3_bwd_filter_bn(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                            const float* pro_beta, int pro_act, const void* dz, const void* y, const float* bn_mean,
+                            const float* bn_rstd, const float* bn_gamma, const float* bn_beta, int bn_act,
+                            const float* coef, void* dy, float* dw, void* workspace, int N, int H, int W, int C,
+                            int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream) {
+  DW_ARGS_OK("rod_dw3x3_bwd_filter_bn");
+  ROD_CHECK_ARG(workspace != nullptr && dz != nullptr && y != nullptr && dy != nullptr && coef != nullptr &&
+                    bn_mean != nullptr && bn_rstd != nullptr,
+                "rod_dw3x3_bwd_filter_bn: NULL tensor argument");
+  ROD_CHECK_ARG(!pro_mean || pro_rstd, "rod_dw3x3_bwd_filter_bn: BatchNorm prologue needs mean and rstd");
+  ROD_CHECK_ARG(bn_act >= ROD_ACT_NONE && bn_act <= ROD_ACT_RELU, "rod_dw3x3_bwd_filter_bn: bad act %d", bn_act);
+  hipStream_t s = ROD_STREAM(stream);
+  const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  const BnPro* pp = pro_mean ? &pro : nullptr;
+  const DwGrad gd{y, bn_mean, bn_rstd, bn_gamma, bn_beta, coef, bn_act, dy};
+  auto gp = [&](auto tag) {  // the fused kernel (LDS-exchange engine, 16-byte packs)
+    typedef decltype(tag) T;
+    const DwTile t = dw_tile(N, Ho, Wo, C, stride, Vec16<T>::N);
+    const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
+    const BnPro pv = pp ? *pp : BnPro{};
+    const int pa = !pp ? -1 : (pp->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : DW_ACT_RT);
+    float* slab = (float*)workspace;
+#define DWG(S_, PA)                                                                                                \
+  hipLaunchKernelGGL((dw3x3_bwdw_lx_kernel<T, S_, PA, true>), grid, dim3(256), 0, s, (const T*)x, (const T*)dz, slab, \
+                     H, W, C, pad_t, pad_l, Ho, Wo, t, pv, gd)
+    if (stride == 1) {
+      if (pa == ROD_ACT_RELU6) DWG(1, ROD_ACT_RELU6); else if (pa == DW_ACT_RT) DWG(1, DW_ACT_RT); else DWG(1, -1);
+    } else {
+      if (pa == ROD_ACT_RELU6) DWG(2, ROD_ACT_RELU6); else if (pa == DW_ACT_RT) DWG(2, DW_ACT_RT); else DWG(2, -1);
+    }
+#undef DWG
+    slab_sum(slab, dw, (int)((long)N * t.strips * t.coltiles), 9L * C, s);
+  };
+  const bool al = ((((uintptr_t)y) | ((uintptr_t)dy)) & 15) == 0;
+  if (dtype == ROD_BF16 && al && dw_lx_ok<bf16_t>(x, dz, C)) {
+    gp(bf16_t{});
+  } else if (dtype == ROD_F32 && al && dw_lx_ok<float>(x, dz, C)) {
+    gp(float{});
+  } else {  // no fused kernel for this layout: apply pass, then the plain filter gradient
+    int rc = rod_bn_bwd_apply(dz, y, bn_mean, bn_rstd, bn_gamma, bn_beta, coef, dy, (long)N * Ho * Wo, C, bn_act,
+                              dtype, stream);
+    if (rc) return rc;
+    return rod_dw3x3_bwd_filter(x, pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act, dy, dw, workspace, N, H, W, C,
+                                stride, pad_t, pad_l, Ho, Wo, dtype, stream);
+  }
+  return check_launch("rod_dw3x3_bwd_filter_bn");
 }
 
 }  // extern "C"

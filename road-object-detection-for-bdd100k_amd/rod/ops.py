@@ -684,6 +684,25 @@ class _DWBN(torch.autograd.Function):
         x, w, y, mean, rstd = ctx.saved_tensors
         gamma, beta = ctx.gb
         N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
+        if _needs(w) and N * Ho * Wo > 4096 and "dwbn" in _ENABLE:
+            # opt-in (ROD_ENABLE=dwbn): the BatchNorm-backward apply runs inside the filter
+            # gradient, which writes dy for the backward-data pass (rod_dw3x3_bwd_filter_bn).
+            # Bit-identical, but measured no faster per step: the apply pass it
+            # removes (-1.59 ms) comes back as filter-gradient time (+1.22 ms, VALU-bound)
+            dz = dz.contiguous()
+            coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            dy = torch.empty_like(y)
+            ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
+            det = lambda t: None if t is None else t.detach()
+            _abi.call("rod_dw3x3_bwd_filter_bn", x, *_pro_args(ctx.ipro), dz, y, mean, rstd, det(gamma), det(beta),
+                      ctx.act, coef, dy, grad_slot(w), ws, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x), stream())
+            _mark_written(w)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty_like(x)
+                _abi.call("rod_dw3x3_bwd_data", dy, w, dx, *_gred_args(None), N, H, W, C, s, pt, pl, Ho, Wo,
+                          dtcode(x), stream())
+            return dx, None, None, None, None
         dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
         dx = None
         if ctx.needs_input_grad[0]:

@@ -33,6 +33,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchfast) run benchfast 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    benchfp32) run benchfp32 600 python bench.py --dtype fp32 --steps 5 --warmup 2 --no-cpu-baseline --no-inference ;;
     benchall) run benchall 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-cpu-baseline --no-inference ;;
     benchallfr) run benchallfr 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-fix-refine --no-cpu-baseline --no-inference ;;
     benchaug) run benchaug 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_aug.json ;;
@@ -67,6 +68,7 @@ for step in "$@"; do
     irbench) run irbench 300 python tools/irblock_bench.py --iters 10 --res 720 1080 ;;
     dwab) run dwa 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_w0.so python tools/dw_bench.py --out /tmp/${TAG}_dw0.pt &&
           run dwb 300 python tools/dw_bench.py --check /tmp/${TAG}_dw0.pt ;;
+    dwbn) run dwbn 600 python -m pytest tests/test_gpu_dwbn.py tests/test_gpu_train.py tests/test_gpu_kernels.py -m gpu -q -x --timeout=500 -p no:cacheprovider ;;
     irtests) run irtests 300 python -m pytest tests/test_gpu_irblock.py -m gpu -q -x --timeout=250 -p no:cacheprovider ;;
     *) echo "unknown step $step" ;;
   esac
