@@ -42,6 +42,53 @@ def workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+class _Side:
+    """Weight gradients on a side stream (single process): a conv's / depthwise's filter
+    gradient only reads (x, dy) and writes its own slot of the flat gradient buffer, so it can
+    run beside the backward-data chain that the rest of the backward waits on.  The side stream
+    forks from the main stream where dy is ready and is joined once, before the optimizer step
+    (join()); the tensors it reads stay referenced until then, so the caching allocator cannot
+    hand their memory to main-stream work in between.  Works under HIP-graph capture (the fork /
+    join become graph edges).  Opt-in (ROD_ENABLE=side: measured slower, the overlapped kernels
+    contend for the same CUs and HBM — DESIGN.md §6); never under data parallelism (the gradient
+    buckets are reduced from inside backward); outside SIDE.backward (tests, other callers of
+    .backward()) everything stays on the calling stream."""
+
+    def __init__(self):
+        self.on = False
+        self.stream = None
+        self.keep = []
+
+    def backward(self, loss, device):
+        """graph.backward(loss) with the weight gradients on the side stream, joined before
+        returning (so every caller after it sees complete gradients on the main stream)."""
+        from . import graph
+        if "side" in _DISABLE:
+            return graph.backward(loss)
+        if self.stream is None or self.stream.device != torch.device(device):
+            self.stream = torch.cuda.Stream(device=device)
+        self.on = True
+        try:
+            graph.backward(loss)
+        finally:
+            self.on = False
+            torch.cuda.current_stream().wait_stream(self.stream)
+            self.keep.clear()
+
+    def run(self, fn, *keep):
+        if not self.on:
+            return fn()
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            r = fn()
+        self.keep.extend(keep)
+        return r
+
+
+
+SIDE = _Side()
+
+
 def grad_slot(p):
     """The flat-buffer gradient view registered for parameter tensor p (or None)."""
     return getattr(p, "_rod_grad", None)
@@ -575,25 +622,29 @@ def _pw_fused_ok(M, Cin, Cout, dtype):
 
 
 def _conv_bwd_from_dy(x, w, b, ks, dy, pro, need_dx):
-    """rod_conv_fwd (mode-1 weights) for dx and rod_conv_wgrad for dw / db from a dense dy."""
+    """rod_conv_fwd (mode-1 weights) for dx and rod_conv_wgrad for dw / db from a dense dy
+    (the weight gradient on the side stream when SIDE is on)."""
     N, H, W, Cin = x.shape
     Cout = w.shape[0]
+    need_w, need_bias = _needs(w), _needs(b)
+    if need_w or need_bias:
+        gw = grad_slot(w) if need_w else torch.empty(w.shape, dtype=torch.float32, device=x.device)
+        gb = grad_slot(b) if need_bias else None
+
+        def wgrad():
+            ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, H, W, Cin, Cout, ks), x.device)
+            _abi.call("rod_conv_wgrad", x, *_pro_args(pro), dy, gw, gb, ws, N, H, W, Cin, Cout, ks, 0, 0,
+                      dtcode(x), stream())
+        SIDE.run(wgrad, x, dy, gw, pro)
+        if need_w:
+            _mark_written(w)
+        if need_bias:
+            _mark_written(b)
     dx = None
     if need_dx:
         wt1 = _prep(w, 1, x.dtype, Cout, Cin, ks)
         dx = torch.empty_like(x)
         conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks)
-    need_w, need_bias = _needs(w), _needs(b)
-    if need_w or need_bias:
-        gw = grad_slot(w) if need_w else torch.empty(w.shape, dtype=torch.float32, device=x.device)
-        gb = grad_slot(b) if need_bias else None
-        ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, H, W, Cin, Cout, ks), x.device)
-        _abi.call("rod_conv_wgrad", x, *_pro_args(pro), dy, gw, gb, ws, N, H, W, Cin, Cout, ks, 0, 0, dtcode(x),
-                  stream())
-        if need_w:
-            _mark_written(w)
-        if need_bias:
-            _mark_written(b)
     return dx
 
 
@@ -704,16 +755,18 @@ class _DWBN(torch.autograd.Function):
                           dtcode(x), stream())
             return dx, None, None, None, None
         dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+        if _needs(w):
+            def filt():
+                ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
+                _abi.call("rod_dw3x3_bwd_filter", x, *_pro_args(ctx.ipro), dy, grad_slot(w), ws, N, H, W, C, s, pt,
+                          pl, Ho, Wo, dtcode(x), stream())
+            SIDE.run(filt, x, dy, ctx.ipro)
+            _mark_written(w)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             _abi.call("rod_dw3x3_bwd_data", dy, w, dx, *_gred_args(None), N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x),
                       stream())
-        if _needs(w):
-            ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
-            _abi.call("rod_dw3x3_bwd_filter", x, *_pro_args(ctx.ipro), dy, grad_slot(w), ws, N, H, W, C, s, pt, pl,
-                      Ho, Wo, dtcode(x), stream())
-            _mark_written(w)
         return dx, None, None, None, None
 
 

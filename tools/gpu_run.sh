@@ -34,6 +34,9 @@ for step in "$@"; do
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchfast) run benchfast 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchfp32) run benchfp32 600 python bench.py --dtype fp32 --steps 5 --warmup 2 --no-cpu-baseline --no-inference ;;
+    benchgred) run benchgred 400 env ROD_ENABLE=gred python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-inference --kernel-steps 0 &&
+               run benchbase 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-inference --kernel-steps 0 &&
+               run benchgreddw 400 env ROD_ENABLE=gred,dwbn python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-inference --kernel-steps 0 ;;
     benchall) run benchall 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-cpu-baseline --no-inference ;;
     benchallfr) run benchallfr 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-fix-refine --no-cpu-baseline --no-inference ;;
     benchaug) run benchaug 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_aug.json ;;
@@ -69,6 +72,7 @@ for step in "$@"; do
     dwab) run dwa 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_w0.so python tools/dw_bench.py --out /tmp/${TAG}_dw0.pt &&
           run dwb 300 python tools/dw_bench.py --check /tmp/${TAG}_dw0.pt ;;
     dwbn) run dwbn 600 python -m pytest tests/test_gpu_dwbn.py tests/test_gpu_train.py tests/test_gpu_kernels.py -m gpu -q -x --timeout=500 -p no:cacheprovider ;;
+    traintests) run traintests 800 python -m pytest tests/test_gpu_train.py tests/test_gpu_fullsize.py tests/test_gpu_vgg.py tests/test_gpu_msf.py tests/test_gpu_dp_equiv.py -m gpu -q -x --timeout=500 -p no:cacheprovider ;;
     irtests) run irtests 300 python -m pytest tests/test_gpu_irblock.py -m gpu -q -x --timeout=250 -p no:cacheprovider ;;
     *) echo "unknown step $step" ;;
   esac
