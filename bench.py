@@ -157,6 +157,14 @@ NORTH_STAR = ('rod_dw3x3_fwd', 'rod_dw3x3_bwd_data', 'rod_dw3x3_bwd_filter', 'ro
               'rod_pw_bwd', 'rod_bn_bwd_reduce', 'rod_bn_bwd_apply', 'rod_bn_bwd')
 
 
+def gpu_head_start(ms=120):
+    """Park the stream behind a spin kernel (~ms) before the eager probe steps, so the host
+    queues their launches ahead of the GPU: every probe event pair then brackets its kernels
+    back to back, not host dispatch gaps (an eager step issues in ~21 ms against ~25 ms of GPU
+    work, tools/host_time.py, so without this some intervals include waits for the host)."""
+    torch.cuda._sleep(int(ms * 1e-3 * 2.4e9))
+
+
 def kernel_rooflines(tr, batch, steps, dtype):
     """Per-entry rooflines of the north-star kernels (depthwise 3x3, the pointwise / 3x3 GEMMs,
     the BatchNorm backward), timed with HIP events around every call of `steps` extra training
@@ -164,6 +172,7 @@ def kernel_rooflines(tr, batch, steps, dtype):
     Aggregate over all calls of the entry, and its single most expensive call shape."""
     from rod import _abi, roofline
     _abi.PROBE.arm(NORTH_STAR)
+    gpu_head_start()
     for _ in range(steps):
         tr.step(*batch)
     torch.cuda.synchronize()
@@ -256,6 +265,7 @@ def main():
         # a replayed graph makes no host calls to time: the dominant kernel's rooflines come
         # from two eager steps after the timed region (same kernels, same arguments)
         _abi.PROBE.arm(probe_set)
+        gpu_head_start()
         for _ in range(2):
             tr.step(*next_batch())
         torch.cuda.synchronize()
