@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------- backward
-template <typename T, bool VEC, bool PM = false>
+template <typename T, bool VEC, bool PM = false, int U = 4>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
@@ -393,15 +393,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
       }
     };
     long r = r0 + pln;
-    for (; r + 3L * lanes < r1; r += 4L * lanes) {
-      float xa[4][V], ga[4][V];
+    for (; r + (U - 1L) * lanes < r1; r += (long)U * lanes) {
+      float xa[U][V], ga[U][V];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         load_v<T, VEC>(x + (r + (long)u * lanes) * ldx + c, xa[u]);
         load_v<T, VEC>(dy + (r + (long)u * lanes) * lddy + c, ga[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc(xa[u], ga[u]);
+      for (int u = 0; u < U; ++u) acc(xa[u], ga[u]);
     }
     for (; r < r1; r += lanes) {
       float xv[V], gv[V];
@@ -990,7 +990,16 @@ int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const fl
     RedPlan pl = red_plan<T>(M, C, vec);
     dim3 grid(pl.nbx, pl.cgroups);
     size_t lds = 2 * 256 * pl.V * sizeof(float);
-    if (vec)
+    // eight rows (16 loads) in flight per lane instead of four on the large tensors (>= 64 M
+    // elements: 1471 -> 1401 us at 7372800 x 96, 567 -> 541 us at 1843200 x 144 for reduce + apply,
+    // bit-identical; the mid-size ones lose, e.g. 28800 x 576 77 -> 85 us; tools/bn_bench.py).
+    // ROD_BN_RED_U=4 / 8 forces one form
+    static const int red_u = getenv("ROD_BN_RED_U") ? atoi(getenv("ROD_BN_RED_U")) : 0;
+    const bool u8 = red_u == 8 || (red_u == 0 && (long)M * C >= (64L << 20));
+    if (vec && u8)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, false, 8>), grid, dim3(256), lds, s, (const T*)dz,
+                         (const T*)y, mean, rstd, gamma, beta, M, C, C, C, act, pl.CVb, pl.lanes, pl.chunk, slab);
+    else if (vec)
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), grid, dim3(256), lds, s, (const T*)dz, (const T*)y, mean,
                          rstd, gamma, beta, M, C, C, C, act, pl.CVb, pl.lanes, pl.chunk, slab);
     else
