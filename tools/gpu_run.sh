@@ -40,6 +40,7 @@ for step in "$@"; do
     hosttime) run hosttime 300 python tools/host_time.py --steps 10 ;;
     hostprof) run hostprof 300 python -m cProfile -s tottime tools/host_time.py --steps 5 ;;
     bnu) run bnu4 300 python tools/bn_bench.py --out /tmp/${TAG}_bn4.pt && run bnu8 300 env ROD_BN_RED_U=8 python tools/bn_bench.py --check /tmp/${TAG}_bn4.pt ;;
+    bna) run bna4 300 python tools/bn_bench.py --out /tmp/${TAG}_bn4.pt && run bna8 300 env ROD_BN_APPLY_U=8 python tools/bn_bench.py --check /tmp/${TAG}_bn4.pt ;;
     benchall) run benchall 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-cpu-baseline --no-inference ;;
     benchallfr) run benchallfr 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-fix-refine --no-cpu-baseline --no-inference ;;
     benchaug) run benchaug 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_aug.json ;;
