@@ -41,6 +41,15 @@ for step in "$@"; do
     hostprof) run hostprof 300 python -m cProfile -s tottime tools/host_time.py --steps 5 ;;
     bnu) run bnu4 300 python tools/bn_bench.py --out /tmp/${TAG}_bn4.pt && run bnu8 300 env ROD_BN_RED_U=8 python tools/bn_bench.py --check /tmp/${TAG}_bn4.pt ;;
     bna) run bna4 300 python tools/bn_bench.py --out /tmp/${TAG}_bn4.pt && run bna8 300 env ROD_BN_APPLY_U=8 python tools/bn_bench.py --check /tmp/${TAG}_bn4.pt ;;
+    dwplan) run dwp0 300 python tools/dw_bench.py --out /tmp/${TAG}_dw.pt &&
+            run dwp1 300 env ROD_DW_WANT=2048 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt &&
+            run dwp2 300 env ROD_DW_WANT=512 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt &&
+            run dwp3 300 env ROD_DW_RBMIN=4 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt &&
+            run dwp4 300 env ROD_DW_RBMIN=16 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt ;;
+    dwplan2) run dwq0 300 python tools/dw_bench.py --out /tmp/${TAG}_dw.pt &&
+             run dwq1 300 env ROD_DW_RBMIN=16 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt &&
+             run dwq2 300 env ROD_DW_RBMIN=24 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt &&
+             run dwq3 300 env ROD_DW_RBMIN=32 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt ;;
     benchall) run benchall 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-cpu-baseline --no-inference ;;
     benchallfr) run benchallfr 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-fix-refine --no-cpu-baseline --no-inference ;;
     benchaug) run benchaug 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_aug.json ;;
