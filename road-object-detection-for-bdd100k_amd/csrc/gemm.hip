@@ -1349,7 +1349,10 @@ static WgradPlan wgrad_plan(long M, int Cin, int Cout, int ks) {
   p.ctiles = cdiv(Cout, WG_T);
   p.ktiles = cdiv(K, WG_T);
   const int tiles = p.ctiles * p.ktiles;
-  long splits = std::max<long>(1, std::min<long>(cdivl(2048, tiles), cdivl(M, 512)));
+  // measurement switches: ROD_WG_TARGET (blocks, 2048), ROD_WG_MINROWS (rows per split, 512)
+  static const long wg_target = getenv("ROD_WG_TARGET") ? atol(getenv("ROD_WG_TARGET")) : 2048;
+  static const long wg_minrows = getenv("ROD_WG_MINROWS") ? atol(getenv("ROD_WG_MINROWS")) : 512;
+  long splits = std::max<long>(1, std::min<long>(cdivl(wg_target, tiles), cdivl(M, wg_minrows)));
   long chunk = cdivl(M, splits);
   chunk = cdivl(chunk, BK) * BK;
   p.chunk = chunk;

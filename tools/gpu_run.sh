@@ -50,6 +50,11 @@ for step in "$@"; do
              run dwq1 300 env ROD_DW_RBMIN=16 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt &&
              run dwq2 300 env ROD_DW_RBMIN=24 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt &&
              run dwq3 300 env ROD_DW_RBMIN=32 python tools/dw_bench.py --check /tmp/${TAG}_dw.pt ;;
+    wgplan) run wg0 300 python tools/conv_bench.py --ops wgrad --out /tmp/${TAG}_wg.pt &&
+            run wg1 300 env ROD_WG_TARGET=4096 python tools/conv_bench.py --ops wgrad --check /tmp/${TAG}_wg.pt &&
+            run wg2 300 env ROD_WG_TARGET=1024 python tools/conv_bench.py --ops wgrad --check /tmp/${TAG}_wg.pt &&
+            run wg3 300 env ROD_WG_MINROWS=256 python tools/conv_bench.py --ops wgrad --check /tmp/${TAG}_wg.pt &&
+            run wg4 300 env ROD_WG_MINROWS=1024 python tools/conv_bench.py --ops wgrad --check /tmp/${TAG}_wg.pt ;;
     benchall) run benchall 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-cpu-baseline --no-inference ;;
     benchallfr) run benchallfr 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-fix-refine --no-cpu-baseline --no-inference ;;
     benchaug) run benchaug 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_aug.json ;;
