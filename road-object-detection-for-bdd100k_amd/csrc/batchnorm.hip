@@ -28,14 +28,14 @@ struct RedPlan {
 };
 
 template <typename T>
-static RedPlan red_plan(long M, int C, bool vec) {
+static RedPlan red_plan(long M, int C, bool vec, long want_blocks = 1024) {
   RedPlan r;
   r.V = vec ? Vec16<T>::N : 1;
   r.CV = C / r.V;
   r.cgroups = cdiv(r.CV, 256);
   r.CVb = cdiv(r.CV, r.cgroups);
   r.lanes = 256 / r.CVb;
-  const long want = std::max<long>(1, 1024 / r.cgroups);
+  const long want = std::max<long>(1, want_blocks / r.cgroups);
   // >= 16 rows per lane; 4 on small narrow tensors (C <= 256, M*C <= 4M), whose launches are
   // latency-bound (measured, tools/bn_bench.py)
   const long minchunk = (long)r.lanes * (C <= 256 && M * C <= (4L << 20) ? 4 : 16);
@@ -987,7 +987,12 @@ int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const fl
       small_launch<T>(vec, dz, y, mean, rstd, gamma, beta, M, C, act, dgamma, dbeta, coef, nullptr, s);
       return check_launch("rod_bn_bwd_reduce");
     }
-    RedPlan pl = red_plan<T>(M, C, vec);
+    // the backward reduce aims at 512 blocks (fewer, longer row chunks per block than the
+    // statistics' 1024: tools/bn_bench.py total 3558 -> 3455 us, 460800 x 192 208 -> 182 us);
+    // ROD_BN_RED_WANT overrides (A/B switch).  <= the 1024 plan's blocks, so the workspace
+    // bound (max_nbx) holds
+    static const long red_want = getenv("ROD_BN_RED_WANT") ? atol(getenv("ROD_BN_RED_WANT")) : 512;
+    RedPlan pl = red_plan<T>(M, C, vec, std::min<long>(red_want, 1024));
     dim3 grid(pl.nbx, pl.cgroups);
     size_t lds = 2 * 256 * pl.V * sizeof(float);
     // eight rows (16 loads) in flight per lane instead of four on the large tensors (>= 64 M

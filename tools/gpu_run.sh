@@ -55,6 +55,10 @@ for step in "$@"; do
             run wg2 300 env ROD_WG_TARGET=1024 python tools/conv_bench.py --ops wgrad --check /tmp/${TAG}_wg.pt &&
             run wg3 300 env ROD_WG_MINROWS=256 python tools/conv_bench.py --ops wgrad --check /tmp/${TAG}_wg.pt &&
             run wg4 300 env ROD_WG_MINROWS=1024 python tools/conv_bench.py --ops wgrad --check /tmp/${TAG}_wg.pt ;;
+    bnwant) run bw0 300 python tools/bn_bench.py --out /tmp/${TAG}_bn.pt &&
+            run bw1 300 env ROD_BN_RED_WANT=2048 python tools/bn_bench.py --check /tmp/${TAG}_bn.pt &&
+            run bw2 300 env ROD_BN_RED_WANT=512 python tools/bn_bench.py --check /tmp/${TAG}_bn.pt &&
+            run bw3 300 env ROD_BN_RED_WANT=256 python tools/bn_bench.py --check /tmp/${TAG}_bn.pt ;;
     benchall) run benchall 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-cpu-baseline --no-inference ;;
     benchallfr) run benchallfr 600 python bench.py --steps 5 --warmup 2 --train_range ALL --no-fix-refine --no-cpu-baseline --no-inference ;;
     benchaug) run benchaug 600 python bench.py --steps 10 --warmup 3 --augment --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_aug.json ;;
