@@ -46,8 +46,9 @@ def parse():
     ap.add_argument('--no-fix-refine', dest='fix_refine', action='store_false', default=True,
                     help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
     ap.add_argument('--graph', dest='graph', action='store_true', default=True,
-                    help='N=1: replay the training step as a HIP graph (Trainer.step_graphed; bit-identical '
-                         'to the eager step); N>1 runs eager (the bucketed RCCL reducer is launched from host hooks)')
+                    help='replay the training step as a HIP graph (Trainer.step_graphed; bit-identical to the '
+                         'eager step); at N>1 the bucketed RCCL all-reduces are captured into the graph with the '
+                         'kernels (gloo rehearsals run eager)')
     ap.add_argument('--no-graph', dest='graph', action='store_false')
     ap.add_argument('--sync-bn', dest='sync_bn', action='store_true', default=False,
                     help='N>1: BatchNorm statistics over the global batch (rod.ddp.SyncBatchNorm; default per rank)')
@@ -68,6 +69,14 @@ def parse():
     ap.add_argument('--no-inference', dest='inference', action='store_false')
     ap.add_argument('--inference-1080', dest='inference_1080', action='store_true', default=True)
     ap.add_argument('--no-inference-1080', dest='inference_1080', action='store_false')
+    ap.add_argument('--fp32-leg', dest='fp32_leg', action='store_true', default=True,
+                    help='N=1, bf16 run: also time the same step in fp32 (BASELINE configs[1] as stated, C2) '
+                         'and report it under "training_fp32"')
+    ap.add_argument('--no-fp32-leg', dest='fp32_leg', action='store_false')
+    ap.add_argument('--tfrecord-leg', dest='tfrecord_leg', action='store_true', default=True,
+                    help='N=1: feed the step from a TFRecord of synthetic 1280x720 JPEG frames through the '
+                         'host JPEG decode + GPU augmentation (train.py input path) and report it under "tfrecord"')
+    ap.add_argument('--no-tfrecord-leg', dest='tfrecord_leg', action='store_false')
     return ap.parse_args()
 
 
@@ -111,6 +120,147 @@ def cpu_baseline(H, W):
     return {'value': round(1.0 / dt, 5), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
             'sample': f'1 image {H}x{W}, one full REFINE train step (targets+fwd+bwd+SGD), oracle fp32 PyTorch-CPU, '
                       f'{dt:.1f} s'}
+
+
+def cpu_baseline_inference(H, W, rate=0.02):
+    """Oracle predict path (BASELINE configs[3] / [4] on the CPU) on ONE image: ALL network in
+    eval mode (PyTorch-CPU fp32 restatement), softmax, decode of refine + det against the
+    anchors, per-class select / top-k 400 / NMS 0.4 / keep 200 (oracle.post, numpy).  The
+    background logit is shifted so that ~`rate` of the class scores pass select_threshold 0.1,
+    as in the GPU leg (NMS has real work)."""
+    import config
+    from oracle import anchors as oa
+    from oracle import net as onet
+    from oracle import post as op
+    from nets.catch_net import CatchNet
+    threads = min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    cfg = {'train_range': config.train_range.ALL, 'process_backbone_method': config.process_backbone_method.NONE,
+           'deconv_method': config.deconv_method.LEARN_HALF, 'merge_method': config.merge_method.ADD}
+    net = CatchNet('mobilenet_v2', cfg, 'cpu', 0)   # parameters only (host copy)
+    P = {k: v.detach().clone() for k, v in net.store.params.items()}
+    Bf = {k: v.detach().clone() for k, v in net.store.buffers.items()}
+    g = torch.Generator().manual_seed(77)
+    img = torch.randint(0, 256, (1, H, W, 3), dtype=torch.uint8, generator=g)
+    init = oa.init_anchor(6, (H, W))
+    chain = oa.feat_sizes((H, W), [s for (_, s, _, _, _) in onet.SPEC])
+    centers = np.concatenate([np.stack(oa.anchor_centers(oa.anchors_one_layer((H, W), chain[t - 1], init[i])),
+                                       -1).reshape(-1, 4) for i, t in enumerate(onet.TAPS)]).astype(np.float32)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        x = torch.from_numpy(np.float32(2.0 / 255.0) * img.numpy().astype(np.float32) - np.float32(1.0))
+        refine, det, clf = onet.forward(x, P, Bf, False, all_mode=True)
+    t_net = time.perf_counter() - t0
+    logits = np.concatenate([c.reshape(1, -1, 11).numpy() for c in clf], 1)
+    ro = np.concatenate([r.reshape(1, -1, 4).numpy() for r in refine], 1)
+    do = np.concatenate([d.reshape(1, -1, 4).numpy() for d in det], 1)
+    lo, hi = -30.0, 30.0          # calibration of the score distribution: not timed
+    for _ in range(30):
+        mid = 0.5 * (lo + hi)
+        lg = logits.copy()
+        lg[..., 0] += mid
+        e = np.exp(lg - lg.max(-1, keepdims=True))
+        if float(((e / e.sum(-1, keepdims=True))[..., 1:] >= 0.1).mean()) > rate:
+            lo = mid
+        else:
+            hi = mid
+    logits[..., 0] += hi
+    t1 = time.perf_counter()
+    e, s_, _ = op.softmax_rows(logits)
+    probs = (e / s_).astype(np.float32)
+    boxes = op.decode_corner(centers, ro + do)
+    scores, _, kept = op.detected_bboxes_vec(probs, boxes, 0.1, 0.4, 400, 200)
+    dt = t_net + time.perf_counter() - t1
+    return {'value': round(1.0 / dt, 5), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
+            'sample': f'1 image {H}x{W}: ALL network eval forward (oracle fp32 PyTorch-CPU, {t_net:.1f} s) + '
+                      f'softmax / decode / select / top-k / NMS (oracle numpy, {sum(len(v) for v in kept.values())} '
+                      f'boxes kept), {dt:.1f} s'}
+
+
+def synthetic_jpeg_tfrecord(path, n, H=720, W=1280, seed=5):
+    """A TFRecord (dataset/pascalvoc_to_tfrecords.py schema) of n synthetic BDD-shaped frames:
+    smooth low-frequency colour fields with mild noise (natural-image-like JPEG size, ~0.1-0.3
+    MB at quality 90, unlike i.i.d. noise) and 1..40 boxes each (rod.data.synthetic_boxes)."""
+    import io
+    from PIL import Image
+    from rod import tfrecord
+    from rod.data import synthetic_boxes
+    rng = np.random.default_rng(seed)
+    corner, labels, cnt = synthetic_boxes(n, seed=seed)
+    with tfrecord.TFRecordWriter(path) as w:
+        for i in range(n):
+            small = Image.fromarray(rng.integers(0, 256, (9, 16, 3), dtype=np.uint8))
+            img = np.asarray(small.resize((W, H), Image.BICUBIC), np.int16)
+            img = np.clip(img + rng.integers(-6, 7, img.shape), 0, 255).astype(np.uint8)
+            buf = io.BytesIO()
+            Image.fromarray(img).save(buf, format='JPEG', quality=90)
+            k = int(cnt[i])
+            w.write(tfrecord.encode_detection_example(buf.getvalue(), (H, W, 3), corner[i, :k], labels[i, :k]))
+
+
+def tfrecord_leg(args, tr, dev, dtype, steps=8, n_img=48):
+    """The train.py input path (TFRecord scan + CRC, host JPEG decode on the reference's 4
+    reader threads, process_raw_data_train on the GPU) feeding the training step as train.py
+    runs it (eager Trainer.step: the boxes' padded count changes per batch, so there is no
+    fixed graph to replay).  Reports the host decode rate alone and the fed training rate:
+    when decode is slower than the step, the fed rate falls to the decode rate."""
+    step = tr.step
+    import tempfile
+    from rod.dataio import TFRecordSource
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, 'bdd100k_train_000.tfrecord')
+        t0 = time.perf_counter()
+        synthetic_jpeg_tfrecord(path, n_img, args.height, args.width)
+        t_write = time.perf_counter() - t0
+        nbytes = os.path.getsize(path)
+        src = TFRecordSource([path], args.batch, (args.height, args.width), dev, dtype, train=True, seed=SEED_TF,
+                             num_readers=4)
+        for _ in range(2):
+            step(*next(src))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):   # the host half of next(src): record reads + JPEG decode on the pool
+            list(src.pool.map(src._load, src._take()))
+        t_dec = (time.perf_counter() - t0) / steps
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            losses = step(*next(src))
+        torch.cuda.synchronize()
+        t_fed = (time.perf_counter() - t0) / steps
+        src.pool.shutdown()
+    return {'metric': 'training images/sec fed from TFRecord (host JPEG decode, 4 reader threads, GPU augmentation)',
+            'value': round(args.batch / t_fed, 2), 'unit': 'images/s', 'ms_per_step': round(t_fed * 1e3, 2),
+            'host_decode_images_per_s': round(args.batch / t_dec, 2), 'decode_ms_per_batch': round(t_dec * 1e3, 2),
+            'num_readers': 4, 'records': n_img, 'mean_record_kb': round(nbytes / n_img / 1024, 1),
+            'write_s': round(t_write, 1), 'loss': round(float(losses[0].item()), 4),
+            'data': 'synthetic 1280x720 JPEG frames (smooth colour fields + noise), BDD-shaped boxes'}
+
+
+def fp32_leg(args, dev, steps=10, warmup=2):
+    """BASELINE configs[1] as stated: the REFINE step at 720x1280, batch 8, fp32, one GPU,
+    HIP-graph replay."""
+    from rod.data import SEED, synthetic_batch
+    from rod.trainer import Trainer
+    tr = Trainer((args.height, args.width), args.batch, dtype=torch.float32, device=dev)
+    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED)
+    for _ in range(max(warmup, 2)):
+        tr.step_graphed(*batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        losses = tr.step_graphed(*batch)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out = {'metric': 'training images/sec at 1280x720 fp32', 'value': round(args.batch / dt, 3), 'unit': 'images/s',
+           'ms_per_step': round(dt * 1e3, 3), 'steps': steps, 'dtype': 'fp32', 'batch': args.batch,
+           'loss': round(float(losses[0].item()), 5), 'hip_graph': True}
+    del tr
+    torch.cuda.empty_cache()
+    return out
+
+
+SEED_TF = 4242
 
 
 def inference_fps(args, dev, dtype, batch=32, steps=5, warmup=2, hw=None):
@@ -169,16 +319,24 @@ def kernel_rooflines(tr, batch, steps, dtype):
     """Per-entry rooflines of the north-star kernels (depthwise 3x3, the pointwise / 3x3 GEMMs,
     the BatchNorm backward), timed with HIP events around every call of `steps` extra training
     steps run after the timed region (so the headline number carries no probe overhead).
-    Aggregate over all calls of the entry, and its single most expensive call shape."""
+    Aggregate over all calls of the entry, and its single most expensive call shape.  Every
+    other entry is probed too: the step's summed algorithmic bytes / flops (whole-step
+    roofline) come from the same steps.  Returns (kernels, step_totals)."""
     from rod import _abi, roofline
-    _abi.PROBE.arm(NORTH_STAR)
+    _abi.PROBE.arm('*')
     gpu_head_start()
     for _ in range(steps):
         tr.step(*batch)
     torch.cuda.synchronize()
     _abi.PROBE.disarm()
     agg = _abi.PROBE.table()
+    design = _abi.PROBE.design_table()
     by_shape = _abi.PROBE.table(by_shape=True)
+    totals = {'alg_bytes_per_step': sum(v[2] for v in agg.values()) // steps,
+              'alg_flops_per_step': sum(v[3] for v in agg.values()) // steps,
+              'design_bytes_per_step': sum(design.values()) // steps,
+              'launch_entries_per_step': sum(v[0] for v in agg.values()) // steps,
+              'probed_kernel_ms_per_step': round(sum(v[1] for v in agg.values()) / steps, 3)}
     peak_tf = roofline.MI355X_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else roofline.MI355X_F32_PEAK_TFLOPS
     out = {}
     for name in NORTH_STAR:
@@ -194,7 +352,9 @@ def kernel_rooflines(tr, batch, steps, dtype):
                      'top_call': {'args': list(top[0][1]), 'avg_us': round(1e3 * tms / tn, 1),
                                   'alg_GBps': round(tgbs, 1), 'hbm_frac': round(tgbs / roofline.MI355X_HBM_PEAK_GBS, 4),
                                   'alg_TFLOPs': round(tfl / tms / 1e9, 2)}}
-    return out
+        if design.get(name, b) != b:
+            out[name]['design_GBps'] = round(design[name] / ms / 1e6, 1)
+    return out, totals
 
 
 def main():
@@ -232,13 +392,18 @@ def main():
         from rod.dataio import AugmentedSource
         source = AugmentedSource(args.batch, (args.height, args.width), dev, dtype, seed=SEED + rank, n_distinct=2)
     next_batch = (lambda: next(source)) if source is not None else (lambda: batch)
-    use_graph = args.graph and world == 1
+    # the DP step is captured with its RCCL collectives (Trainer.step_graphed); gloo (host-side
+    # collectives, the one-box rehearsal) cannot be captured and runs eager
+    use_graph = args.graph and (world == 1 or backend == 'nccl')
     step = tr.step_graphed if use_graph else tr.step
 
     # graphed: the capture happens on the second call (after one eager set-up step), so at
     # least two untimed calls run before the timed region whatever --warmup says
-    for _ in range(max(args.warmup, 2) if use_graph else args.warmup):
-        step(*next_batch())
+    first_loss = None
+    for i in range(max(args.warmup, 2) if use_graph else args.warmup):
+        lw = step(*next_batch())
+        if i == 0:   # the first step's loss: from the initial weights, pinned against the fp64
+            first_loss = float(lw[0].item())   # oracle by tests/test_gpu_fullsize.py (bf16, 720p, b8)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -259,7 +424,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    table = _abi.PROBE.table()
+    table, design = _abi.PROBE.table(), _abi.PROBE.design_table()
     probe_steps = args.steps
     if use_graph:
         # a replayed graph makes no host calls to time: the dominant kernel's rooflines come
@@ -270,15 +435,22 @@ def main():
             tr.step(*next_batch())
         torch.cuda.synchronize()
         _abi.PROBE.disarm()
-        table, probe_steps = _abi.PROBE.table(), 2
+        table, design, probe_steps = _abi.PROBE.table(), _abi.PROBE.design_table(), 2
     n_launch, ms, byts, flops = 0, 0.0, 0, 0
     for p in probe_set:
         e = table.get(p, (0, 0.0, 0, 0))
         n_launch, ms, byts, flops = n_launch + e[0], ms + e[1], byts + e[2], flops + e[3]
+    dbytes = sum(design.get(p, 0) for p in probe_set)
     loss_val = float(losses[0].item())
-    kernels = None
+    kernels = step_totals = None
     if args.kernel_steps > 0 and world == 1:
-        kernels = kernel_rooflines(tr, batch, args.kernel_steps, dtype)
+        kernels, step_totals = kernel_rooflines(tr, batch, args.kernel_steps, dtype)
+    tf_leg = None
+    if args.tfrecord_leg and world == 1:
+        tf_leg = tfrecord_leg(args, tr, dev, dtype)
+    fp32 = None
+    if args.fp32_leg and world == 1 and dtype == torch.bfloat16:
+        fp32 = fp32_leg(args, dev)
     if args.probe_table and rank == 0:
         # per-entry live timing (every call bracketed by events; the step itself is slower
         # in this mode, so ms_per_step of such a run is not a bench number)
@@ -332,7 +504,22 @@ def main():
                    'alg_bytes_per_launch': byts // max(n_launch, 1), 'kernel': args.probe.replace(',', ' + '),
                    'launches_per_step': n_launch // max(probe_steps, 1),
                    'avg_launch_us': round(per_launch_ms * 1e3, 2), 'alg_bytes_per_step': byts // max(probe_steps, 1),
-                   'alg_flops_per_step': flops // max(probe_steps, 1)})
+                   'alg_flops_per_step': flops // max(probe_steps, 1),
+                   # the bytes the two-kernel design moves (reduce 2 passes + apply 3 against the
+                   # algorithmic 3 of read dz, read y, write dy; rod.roofline.design_bytes)
+                   'design_bytes_per_step': dbytes // max(probe_steps, 1),
+                   'design_GBps': round(dbytes / max(ms, 1e-9) / 1e6, 1),
+                   'traffic_over_alg': round(traffic / max(byts // max(n_launch, 1), 1), 3) if traffic else None,
+                   'traffic_over_design': round(traffic / max(dbytes // max(n_launch, 1), 1), 3) if traffic else None})
+        step_rl = None
+        if step_totals is not None:
+            # whole step: every call's algorithmic bytes over the timed ms per step
+            sgbs = step_totals['alg_bytes_per_step'] / (elapsed / args.steps) / 1e9
+            step_rl = dict(step_totals, achieved_GBps=round(sgbs, 1), peak=roofline.MI355X_HBM_PEAK_GBS,
+                           frac=round(sgbs / roofline.MI355X_HBM_PEAK_GBS, 4),
+                           alg_TFLOPs=round(step_totals['alg_flops_per_step'] / (elapsed / args.steps) / 1e12, 2),
+                           note='sum of algorithmic bytes of every librod call of a step (rod.roofline) / the timed '
+                                'ms_per_step; probed over eager steps after the timed region')
         imgs = args.batch * world * args.steps
         out = {
             'metric': 'training images/sec at 1280x720 bf16' if dtype == torch.bfloat16 else
@@ -348,11 +535,22 @@ def main():
                        **({'dist_backend': 'rccl' if backend == 'nccl' else backend,
                            'batchnorm': 'sync (global batch)' if args.sync_bn else 'per rank'} if world > 1 else {}),
                        **({} if args.train_range == 'REFINE' else {'fix_refine': args.fix_refine})},
-            'loss': round(loss_val, 5),
+            'loss': round(loss_val, 5), 'loss_first_step': round(first_loss, 5) if first_loss is not None else None,
             'roofline': rl,
         }
+        if step_rl is not None:
+            out['step_roofline'] = step_rl
         if kernels is not None:
             out['kernels'] = kernels
+        if fp32 is not None:
+            out['training_fp32'] = fp32
+        if tf_leg is not None:
+            out['tfrecord'] = tf_leg
+        if args.cpu_baseline and world == 1:
+            if inf is not None:
+                inf['cpu_baseline'] = cpu_baseline_inference(args.height, args.width)
+            if inf1080 is not None:
+                inf1080['cpu_baseline'] = cpu_baseline_inference(1080, 1920)
         if inf is not None:
             out['inference'] = inf
         if inf1080 is not None:

@@ -91,6 +91,20 @@ long rodio_tfrecord_scan(const char* path, long* offsets, long* lengths, long ca
     set_err("rodio_tfrecord_scan: cannot open %s (errno %ld)", path, errno);
     return -1;
   }
+  // the file size bounds every record length: a crafted header with a valid length CRC but a
+  // huge length must not reach the allocation or the seek (std::bad_alloc through extern "C"
+  // would abort the host process; (long)len could overflow)
+  if (fseek(f, 0, SEEK_END) != 0) {
+    set_err("rodio_tfrecord_scan: cannot seek in %s (errno %ld)", path, errno);
+    fclose(f);
+    return -1;
+  }
+  const long fsize = ftell(f);
+  if (fsize < 0 || fseek(f, 0, SEEK_SET) != 0) {
+    set_err("rodio_tfrecord_scan: cannot size %s (errno %ld)", path, errno);
+    fclose(f);
+    return -1;
+  }
   long count = 0, pos = 0;
   uint8_t hdr[12];
   std::string buf;
@@ -110,6 +124,11 @@ long rodio_tfrecord_scan(const char* path, long* offsets, long* lengths, long ca
       return -1;
     }
     long data_off = pos + 12;
+    if (len > (uint64_t)(fsize - data_off) || (uint64_t)(fsize - data_off) - len < 4) {
+      set_err("rodio_tfrecord_scan: %s truncated: the record at byte %ld claims a length past the end of the file", path, pos);
+      fclose(f);
+      return -1;
+    }
     uint8_t foot[4];
     if (verify_data) {
       buf.resize(len);

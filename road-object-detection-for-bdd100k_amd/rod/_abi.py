@@ -146,10 +146,18 @@ class Probe:
         """{entry (or (entry, scalar args) when by_shape): (launches, total_ms, alg_bytes,
         alg_flops)} over the recorded calls."""
         out = {}
-        for name, e0, e1, (b, f), shape in self.records:
+        for name, e0, e1, (b, f, _), shape in self.records:
             key = (name, shape) if by_shape else name
             n, ms, bb, ff = out.get(key, (0, 0.0, 0, 0))
             out[key] = (n + 1, ms + e0.elapsed_time(e1), bb + b, ff + f)
+        return out
+
+    def design_table(self):
+        """{entry: design bytes} (rod.roofline.design_bytes: the bytes the kernels are built to
+        move, >= the algorithmic bytes where a design re-reads a tensor)."""
+        out = {}
+        for name, _, _, (_, _, d), _ in self.records:
+            out[name] = out.get(name, 0) + d
         return out
 
 
@@ -180,7 +188,7 @@ def call(name: str, *args):
         rc = fn(*conv)
         e1.record(s)
         shape = tuple(a for a in args if isinstance(a, (int, float)) and not isinstance(a, bool))
-        PROBE.records.append((name, e0, e1, roofline.cost(name, args), shape))
+        PROBE.records.append((name, e0, e1, roofline.cost(name, args) + (roofline.design_bytes(name, args),), shape))
     else:
         rc = fn(*conv)
     if ret == "int" and rc != 0:

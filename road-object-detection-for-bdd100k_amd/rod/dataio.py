@@ -95,7 +95,7 @@ class TFRecordSource(object):
     (dynamic_pad=True, evaluate.py:109-114) with the counts in n."""
 
     def __init__(self, files, batch_size, img_size, device, dtype, train=True, seed=SEED, num_readers=4,
-                 verify=True, max_images=None):
+                 verify=True, max_images=None, rank=0, world=1):
         from rod import tfrecord
         if not files:
             raise FileNotFoundError('no TFRecord files')
@@ -107,21 +107,34 @@ class TFRecordSource(object):
             raise ValueError('the TFRecord files hold no records')
         self.batch_size, self.img_size, self.device, self.dtype = batch_size, tuple(img_size), device, dtype
         self.train = train
+        # data parallel: every rank draws the SAME permutation (same seed) and reads its own
+        # disjoint slice of it, so one global batch holds no image twice and an epoch is one
+        # pass over the data set (the reference reads it on one device); each rank keeps
+        # len // world records per epoch (the remainder is dropped, as DistributedSampler's
+        # drop_last) so the ranks' epochs stay in step
+        self.rank, self.world = int(rank), max(1, int(world))
         self.rng = np.random.default_rng(seed)
-        self.order = self.rng.permutation(len(self.index)) if train else np.arange(len(self.index))
+        self.order = self._shard(self.rng.permutation(len(self.index)) if train else np.arange(len(self.index)))
         self.pos = 0
         self.epoch = 0
         self.pool = ThreadPoolExecutor(max_workers=max(1, int(num_readers)))
         self.aug = None
         if train:
             from utils.data_pileline_tools import TrainAugmenter
-            self.aug = TrainAugmenter(self.img_size, seed=seed)
+            self.aug = TrainAugmenter(self.img_size, seed=seed + 1000 * self.rank)   # per-rank augmentation draws
 
     def __len__(self):
         return len(self.index)
 
     def __iter__(self):
         return self
+
+    def _shard(self, perm):
+        if self.world == 1:
+            return perm
+        if len(perm) < self.world:   # fewer records than ranks: one record each, reused
+            return perm[self.rank % len(perm):self.rank % len(perm) + 1]
+        return perm[self.rank::self.world][:len(perm) // self.world]
 
     def _load(self, k):
         from rod import tfrecord
@@ -137,7 +150,7 @@ class TFRecordSource(object):
                 self.pos = 0
                 self.epoch += 1
                 if self.train:
-                    self.order = self.rng.permutation(len(self.index))
+                    self.order = self._shard(self.rng.permutation(len(self.index)))
             ks.append(int(self.order[self.pos]))
             self.pos += 1
         return ks
@@ -179,11 +192,13 @@ class TFRecordSource(object):
 
 
 def make_source(dataset_dir, batch_size, img_size, device, split='train', seed=SEED, augment_dtype=None,
-                synthetic=False, dtype=torch.float32, num_readers=4, max_images=None):
+                synthetic=False, dtype=torch.float32, num_readers=4, max_images=None, rank=0, world=1):
     """augment_dtype: training batches go through the GPU augmentation pipeline and come out
     normalised in this dtype; None = network-resolution uint8 batches (eval / predict / bench).
     synthetic: run on synthetic BDD-shaped batches (rod.data) — only when asked for explicitly;
-    a missing dataset is an error, as in the reference (its reader fails on an empty pattern)."""
+    a missing dataset is an error, as in the reference (its reader fails on an empty pattern).
+    rank / world: data parallel — TFRecords are read as disjoint per-rank slices of one shared
+    shuffle; synthetic sources draw per-rank batches (seed + 1000 * rank)."""
     if synthetic:
         log.warning('--synthetic: using synthetic BDD-shaped batches (rod.data), not %r', dataset_dir)
     else:
@@ -193,9 +208,10 @@ def make_source(dataset_dir, batch_size, img_size, device, split='train', seed=S
             train = augment_dtype is not None
             return TFRecordSource(files, batch_size, img_size, torch.device(device),
                                   augment_dtype if train else dtype, train=train, seed=seed, num_readers=num_readers,
-                                  max_images=max_images)
+                                  max_images=max_images, rank=rank, world=world)
         raise FileNotFoundError('no bdd100k_%s_*.tfrecord under %r (pass --synthetic to run on synthetic '
                                 'BDD-shaped batches)' % (split, dataset_dir))
+    seed = seed + 1000 * rank
     if augment_dtype is not None:
         return AugmentedSource(batch_size, img_size, device, augment_dtype, seed)
     return SyntheticSource(batch_size, img_size, device, seed)

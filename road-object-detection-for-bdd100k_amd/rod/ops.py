@@ -1432,6 +1432,7 @@ def max_pool2x2(x):
 
 
 _DROPOUT_CALLS = [0]
+DROPOUT_RANK = [0, 1]   # (rank, world) of a data-parallel job (set by rod.trainer.Trainer)
 
 
 class _Dropout(torch.autograd.Function):
@@ -1456,13 +1457,16 @@ class _Dropout(torch.autograd.Function):
 
 def dropout(x, rate, training, seed=None):
     """tf.layers.dropout(x, rate, training) (vgg.py:106, 111).  Returns (y, mask or None); the
-    seed defaults to a per-process call counter (every call draws a fresh mask)."""
+    seed defaults to a per-process call counter (every call draws a fresh mask), interleaved
+    over the ranks of a data-parallel job so that no two ranks draw the same mask pattern for
+    their shards (one device drawing over the global batch would not correlate them)."""
     x = materialize(x)
     if not training or rate == 0.0:
         return x, None
     if seed is None:
         _DROPOUT_CALLS[0] += 1
-        seed = 0x5EED0000 + _DROPOUT_CALLS[0]
+        rank, world = DROPOUT_RANK
+        seed = 0x5EED0000 + _DROPOUT_CALLS[0] * world + rank
     return _Dropout.apply(x, 1.0 - float(rate), seed)
 
 

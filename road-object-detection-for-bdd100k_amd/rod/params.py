@@ -122,9 +122,17 @@ class ParamStore:
         """The refreshed (mean, rstd) slices of one BatchNorm, or None outside a refresh."""
         if self._eval_eps is None or eps != self._eval_eps:
             return None
-        base = self.flat_buf.data_ptr()
-        om, ov = (mmean.data_ptr() - base) // 4, (mvar.data_ptr() - base) // 4
+        base, n = self.flat_buf.data_ptr(), self.flat_buf.numel()
         C = mmean.numel()
+        offs = []
+        for t in (mmean, mvar):
+            d = t.data_ptr() - base
+            # a buffer rebound outside flat_buf (instead of updated in place) would otherwise
+            # read the wrong slice: fall back to the per-BatchNorm path
+            if t.numel() != C or t.dtype != self.flat_buf.dtype or d % 4 or not 0 <= d // 4 <= n - C:
+                return None
+            offs.append(d // 4)
+        om, ov = offs
         return self._eval_out[0, om:om + C], self._eval_out[1, ov:ov + C]
 
     def set_trainable(self, predicate):

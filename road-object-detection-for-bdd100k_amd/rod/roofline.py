@@ -6,9 +6,13 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
   conv fwd (1x1 / 3x3) : es*(M*Cin + M*Cout + Cout*K) (+4*Cout bias), 2*M*K*Cout
   conv wgrad           : es*(M*Cin + M*Cout) + 4*Cout*K, 2*M*K*Cout
   bn_stats             : es*M*C;  bn_apply: es*M*C*(2 + residual)
-  bn_bwd               : es*M*C*3 (read dy, read x, write dx; the reduce+apply split re-reads
-                         dy and x, so achieved/peak also shows that avoidable re-read)
-  bn_bwd_reduce        : es*M*C*2 (read dz, read y);  bn_bwd_apply: es*M*C*3
+  bn_bwd               : es*M*C*3 (read dy, read x, write dx)
+  bn_bwd_reduce        : es*M*C*2 (read dz, read y: the first, algorithmic reads)
+  bn_bwd_apply         : es*M*C*1 (write dy).  Its reads of dz and y are the SECOND pass of the
+                         reduce -> apply split: design traffic, not algorithmic bytes, so the
+                         BatchNorm backward as a whole counts 3 passes (read dz, read y, write
+                         dy) whichever kernels do them; design_bytes() gives the 5 passes the
+                         two-kernel design moves (reduce 2 + apply 3)
   pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product
   match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
   ir_block_fwd (fused) : es*(N*H*W*Cin + N*Ho*Wo*Cout) + weights, 2*N*H*W*Cin*inner +
@@ -69,7 +73,7 @@ def cost(name, a):
         return _ES[dt] * M * C * 3, 16 * M * C  # algorithmic: read dy, read x, write dx
     if name == "rod_bn_bwd_apply":
         M, C, dt = a[8], a[9], a[11]
-        return _ES[dt] * M * C * 3, 8 * M * C   # read dz, read y, write dy
+        return _ES[dt] * M * C * 1, 8 * M * C   # write dy (dz, y re-read: design traffic)
     if name == "rod_bn_bwd_reduce":
         M, C, dt = a[10], a[11], a[13]
         return _ES[dt] * M * C * 2, 6 * M * C   # read dz, read y
@@ -91,7 +95,73 @@ def cost(name, a):
     if name == "rod_match_anchors":
         B, A, G = a[12], a[13], a[14]
         return B * A * 56 + A * 32 + B * G * 20, 15 * G * A * B
+    # --- the remaining entries of a training / inference step (for the whole-step sum) ---
+    if name == "rod_normalize_image":
+        n, dt = a[2], a[3]
+        return (1 + _ES[dt]) * n, 2 * n
+    if name == "rod_cast":
+        n = a[4]
+        return (_ES[a[1]] + _ES[a[3]]) * n, 0
+    if name == "rod_bn_stat_parts":
+        M, C, nparts, dt = a[1], a[2], a[4], a[5]
+        return _ES[dt] * M * C + 12 * nparts * C, 3 * M * C
+    if name == "rod_bn_finalize":
+        nparts, C = a[1], a[3]
+        return 12 * nparts * C + 16 * C, 10 * nparts * C
+    if name == "rod_bn_bwd_parts":
+        M, C, nparts, dt = a[9], a[10], a[8], a[11]
+        return _ES[dt] * M * C * 2 + 8 * nparts * C, 6 * M * C
+    if name == "rod_bn_bwd_finalize":
+        nparts, C = a[1], a[3]
+        return 8 * nparts * C + 24 * C, 4 * nparts * C
+    if name == "rod_bn_eval_stats":
+        C = a[5]
+        return 16 * C, 3 * C
+    if name == "rod_copy2d":
+        return 2 * a[4] * a[5], 0
+    if name == "rod_add":
+        n, dt = a[3], a[4]
+        return 3 * _ES[dt] * n, n
+    if name == "rod_sgd_clip":
+        n = a[2]
+        return 12 * n, 3 * n                 # read param, read grad, write param (fp32)
+    if name == "rod_conv_weight_prep_batch":
+        total, dt = a[2], a[3]
+        return (4 + _ES[dt]) * total, 0
+    if name == "rod_smoothl1_masked":
+        B, A, dt = a[10], a[11], a[12]
+        es = _ES[dt]
+        wgt = a[8] is not None
+        return B * A * (4 * es + 16 + 4 + 4 * es + (16 if wgt else 0)), 12 * B * A * 4
+    if name == "rod_decode":
+        B, A, dt = a[4], a[5], a[7]
+        return B * A * (2 * 4 * _ES[dt] + 16) + 16 * A, 20 * B * A
+    if name == "rod_softmax":
+        rows, K, dt = a[2], a[3], a[4]
+        return rows * K * (_ES[dt] + 4), 4 * rows * K
+    if name == "rod_select_topk_nms":
+        B, A, K = a[2], a[3], a[4]
+        return B * A * (K * 4 + 16), 0
+    if name == "rod_det_targets":
+        B, A, dt = a[13], a[14], a[15]
+        return B * A * (4 * _ES[dt] + 16 + 16 + 4 + 4 + 16 + 4 + 4 + 4), 40 * B * A
+    if name in ("rod_resize_bilinear", "rod_resize_bilinear_bwd"):
+        N, H, W, C, Ho, Wo, dt = a[2], a[3], a[4], a[5], a[6], a[7], a[8]
+        return _ES[dt] * C * N * (H * W + Ho * Wo), 8 * N * Ho * Wo * C
+    if name in ("rod_depth_to_space2", "rod_space_to_depth2"):
+        N, h, w, Fc, dt = a[2], a[3], a[4], a[5], a[9]
+        return 2 * _ES[dt] * N * h * w * 4 * Fc, 0
     return 0, 0
+
+
+def design_bytes(name, a):
+    """Bytes the call's kernels are DESIGNED to move (>= cost()[0]): differs from the
+    algorithmic count only where a design re-reads a tensor — the apply pass of the two-kernel
+    BatchNorm backward re-reads dz and y (reduce 2 passes + apply 3 = 5 against 3)."""
+    if name == "rod_bn_bwd_apply":
+        M, C, dt = a[8], a[9], a[11]
+        return _ES[dt] * M * C * 3
+    return cost(name, a)[0]
 
 
 # C-ABI entry -> (kernel-name substrings of which exactly one launches once per entry call,

@@ -57,12 +57,15 @@ class Trainer:
         if reducer is not None and hasattr(reducer, 'attach'):
             reducer.attach(store)  # buckets over the trainable parameters (rod.ddp)
         # hard negatives over the global batch (net_tools.py:557-587)
+        # (a reducer is only handed in by a data-parallel job; a 1-rank group exercises the same
+        # exchange path, e.g. the graph-capture test)
+        dp = reducer is not None
         net_tools.HNM_EXCHANGE = (reducer.hnm_allreduce, world_size) \
-            if world_size > 1 and reducer is not None and hasattr(reducer, 'hnm_allreduce') else None
+            if dp and hasattr(reducer, 'hnm_allreduce') else None
         self.train_range = train_range
         self.fix_refine = fix_refine
         # BatchNorm over the global batch (opt-in; per-rank statistics otherwise)
-        self.sync_bn = bool(sync_bn and world_size > 1)
+        self.sync_bn = bool(sync_bn and (world_size > 1 or dp))
         if self.sync_bn:
             from rod.ddp import SyncBatchNorm
             ops.SYNC_BN = SyncBatchNorm(world_size, getattr(reducer, 'group', None))
@@ -72,9 +75,15 @@ class Trainer:
         # process only: under DP the gradient buckets are reduced from inside backward).
         # Measured slower: 24.42 -> 24.93 ms per graphed step
         self._side = world_size == 1 and reducer is None and "side" in ops._ENABLE
+        rank = torch.distributed.get_rank() if world_size > 1 and torch.distributed.is_initialized() else 0
+        ops.DROPOUT_RANK[:] = [rank, world_size]
+        self._eager_steps = 0
+        self._dropout_seen = False   # the step draws dropout masks (vgg_16 training): never graphed
 
     def step(self, img_u8, gt_corner, gt_labels, gt_n):
+        calls = ops._DROPOUT_CALLS[0]
         losses = self.losses(img_u8, gt_corner, gt_labels, gt_n)
+        self._dropout_seen |= ops._DROPOUT_CALLS[0] != calls
         if self._side:
             ops.SIDE.backward(losses[0], self.device)
         else:
@@ -82,7 +91,7 @@ class Trainer:
         if self.reducer is not None:
             self.reducer(self.net.store.flat_grad)
         self.opt.step()
-        self._eager_steps = getattr(self, '_eager_steps', 0) + 1
+        self._eager_steps += 1
         return losses
 
     def step_graphed(self, img_u8, gt_corner, gt_labels, gt_n):
@@ -90,8 +99,17 @@ class Trainer:
         sequence (~960 kernels) is captured once on the first call after an eager step (which did
         the lazy set-up: anchor tables, weight-layout cache, workspaces) and replayed from static
         input buffers, so no per-kernel host dispatch remains.  Every call runs exactly one step;
-        the results are bit-identical to step() (same kernels, same order).  Single process only."""
-        if getattr(self, '_eager_steps', 0) == 0 or self.reducer is not None:
+        the results are bit-identical to step() (same kernels, same order).  Host-side step state
+        (opt.global_step) advances once per replay.  A step that draws dropout masks (the vgg_16
+        backbone in training) runs eager: its mask seed is a host counter that a replay would
+        freeze.
+
+        Data parallel (RCCL): the bucketed gradient all-reduces that backward launches, the
+        hard-negative exchange and the SyncBatchNorm all-gathers are captured with the kernels
+        (RCCL collectives are stream-ordered and capturable; each bucket joins the compute
+        stream before SGD, so the capture closes on one stream) and replay with them.  gloo
+        runs on the host and cannot be captured: with it the step stays eager."""
+        if self._eager_steps == 0 or self._dropout_seen or not self._graphable():
             return self.step(img_u8, gt_corner, gt_labels, gt_n)
         new = (img_u8, gt_corner, gt_labels, gt_n)
         if getattr(self, '_graph', None) is None or any(a.shape != b.shape or a.dtype != b.dtype
@@ -100,15 +118,28 @@ class Trainer:
             self.net.store.build_prep_tables()   # host -> device set-up stays outside the capture
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
-            with torch.cuda.graph(g):
+            st = self.net.store
+            gstep, eager, version = self.opt.global_step, self._eager_steps, st.version
+            # thread_local: RCCL's watchdog thread may query its events while this thread captures
+            with torch.cuda.graph(g, capture_error_mode='thread_local' if self.reducer is not None else 'global'):
                 out = self.step(*static)
+            # the capture recorded the step without running it: host counters as before
+            self.opt.global_step, self._eager_steps, st.version = gstep, eager, version
             self._graph = (g, static, out)
         g, static, out = self._graph
         for a, b in zip(static, new):
             if a.data_ptr() != b.data_ptr():
                 a.copy_(b)
         g.replay()
+        self.opt.global_step += 1
+        self.net.store.version += 1   # the replay's SGD changed the parameters (derived layouts stale)
         return out
+
+    def _graphable(self):
+        if self.reducer is None:
+            return True
+        import torch.distributed as dist
+        return dist.is_initialized() and dist.get_backend(getattr(self.reducer, 'group', None)) == 'nccl'
 
     def losses(self, img_u8, gt_corner, gt_labels, gt_n):
         """Forward of one step: (training loss, [refine, det, clf] in ALL mode)."""

@@ -129,9 +129,9 @@ def main(argv=None):
             logger.info('TF variables init success...')
     trainer.opt.global_step = step0
     logger.info('Building data pileline, using dataset---%s' % 'bdd100k_train')
-    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, seed=1000 * rank + F.seed,
+    source = make_source(F.dataset_dir, F.batch_size, config.img_size, dev, seed=F.seed,
                          augment_dtype=dtype if F.augment else None, synthetic=F.synthetic, dtype=dtype,
-                         num_readers=F.num_readers)
+                         num_readers=F.num_readers, rank=rank, world=world)
 
     os.makedirs(F.summary_dir, exist_ok=True)
     summ = open(os.path.join(F.summary_dir, 'train_rank%d.jsonl' % rank), 'a') if rank == 0 else None

@@ -27,6 +27,7 @@ def main():
     ap.add_argument('--perturb', type=float, default=0.0,
                     help='relative noise on the normalised input (sensitivity probe of the step itself)')
     ap.add_argument('--perturb_seed', type=int, default=0)
+    ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
     a = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -44,7 +45,8 @@ def main():
     from rod.trainer import Trainer
     tr_range = getattr(config.train_range, a.train_range)
     bl = a.batch // world
-    tr = Trainer(tuple(a.hw), bl, dtype=torch.float32, train_range=tr_range, learning_rate=1e-2, device=dev,
+    dtype = torch.bfloat16 if a.dtype == 'bf16' else torch.float32
+    tr = Trainer(tuple(a.hw), bl, dtype=dtype, train_range=tr_range, learning_rate=1e-2, device=dev,
                  seed=7, world_size=world, reducer=reducer, sync_bn=a.sync_bn)
     img, corner, labels, n = synthetic_batch(a.batch, a.hw[0], a.hw[1], dev, seed=8)
     # every run feeds the same normalised fp32 input ((2/255)x - 1, train.py:126, on the host)

@@ -35,9 +35,10 @@ def _port():
     return p
 
 
-def _run(out, world, train_range, sync, perturb_seed=None, amp=1e-6):
+def _run(out, world, train_range, sync, perturb_seed=None, amp=1e-6, extra=()):
     args = [WORKER, '--out', out, '--train_range', train_range] + (['--sync_bn'] if sync else []) + \
-        (['--perturb', str(amp), '--perturb_seed', str(perturb_seed)] if perturb_seed is not None else [])
+        (['--perturb', str(amp), '--perturb_seed', str(perturb_seed)] if perturb_seed is not None else []) + \
+        list(extra)
     if world == 1:
         cmd = [sys.executable] + args
     else:
@@ -90,3 +91,53 @@ def test_two_ranks_equal_one_process(train_range, tmp_path, dev):
     print(f'{train_range}: {len(rows)} gradients; normwise error vs one process, median / max: '
           f'sync {t[:, 0].median():.2g} / {t[:, 0].max():.2g}, input-noise floor {t[:, 1].median():.2g} / '
           f'{t[:, 1].max():.2g}, per-rank BatchNorm {t[:, 2].median():.2g} / {t[:, 2].max():.2g}')
+
+
+def _cos_err(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return 1.0 - float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+
+
+def test_c3_per_rank_bf16_720p_two_by_four_equals_one_by_eight(tmp_path, dev):
+    """BASELINE configs[2] (C3: bf16 at 1280x720, 8 images per rank) at the arithmetic one rank
+    does: a REFINE step of 2 ranks x 4 images with SyncBatchNorm against one process holding
+    all 8, both bf16 at 720x1280 (ref train.py:116-127, net_tools.py:557-587; 8 ranks x 8 is
+    the same per-rank work over the same exchange).  Bound: bf16 itself.  Each gradient tensor's
+    angular error (1 - cos) against the one-process step must stay within
+    max(1e-3, 4x) that of the one-process step re-run with bf16-sized input noise (4e-3 relative:
+    most inputs move by one bf16 ulp), and the loss within max(1e-3, 4x the noise floor)
+    relative; the SGD update is bit-exact given the reduced gradient, and every moving statistic
+    is within max(1e-3, 4x the noise floor) normwise."""
+    ex = ['--dtype', 'bf16', '--hw', '720', '1280', '--batch', '8']
+    one = _run(str(tmp_path / 'one.pt'), 1, 'REFINE', False, extra=ex)
+    pert = [_run(str(tmp_path / f'p{s}.pt'), 1, 'REFINE', False, perturb_seed=s, amp=4e-3, extra=ex)
+            for s in (11, 12)]
+    two = _run(str(tmp_path / 'two.pt'), 2, 'REFINE', True, extra=ex)
+    lo, lt = one['losses'], two['losses']
+    lp = max(float((p['losses'] - lo).abs().max() / lo.abs().max()) for p in pert)
+    print('C3 bf16 720p losses: one', lo.tolist(), 'two x four (sync)', lt.tolist(), 'noise floor', lp)
+    assert float((lt - lo).abs().max() / lo.abs().max()) <= max(1e-3, 4 * lp)
+    bad, rows = [], []
+    for name in one['trainable']:
+        o, k = one['offsets'][name]
+        g1 = one['grad'][o:o + k]
+        if g1.abs().max() == 0:
+            continue
+        e_sync = _cos_err(two['grad'][o:o + k], g1)
+        e_floor = max(_cos_err(p['grad'][o:o + k], g1) for p in pert)
+        rows.append((e_sync, e_floor))
+        if e_sync > max(1e-3, 4 * e_floor):
+            bad.append((name, e_sync, e_floor))
+    assert len(rows) > 100 and not bad, bad[:10]
+    ref = (two['flat0'].numpy() - np.float32(1e-2) * np.clip(two['grad'].numpy(), -5, 5)).astype(np.float32)
+    np.testing.assert_array_equal(two['flat'].numpy(), ref)
+    assert torch.equal(two['flat0'], one['flat0'])
+    badm = []
+    for k, v in one['buffers'].items():   # normwise (moving statistics are fp32 accumulations)
+        e_floor = max(_nerr(p['buffers'][k], v) for p in pert)
+        if _nerr(two['buffers'][k], v) > max(1e-3, 4 * e_floor):
+            badm.append((k, _nerr(two['buffers'][k], v), e_floor))
+    assert not badm, badm[:5]
+    t = torch.tensor(rows)
+    print(f'C3: {len(rows)} gradients; 1 - cos vs one process, median / max: sync {t[:, 0].median():.2g} / '
+          f'{t[:, 0].max():.2g}, bf16 input-noise floor {t[:, 1].median():.2g} / {t[:, 1].max():.2g}')

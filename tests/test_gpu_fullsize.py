@@ -215,6 +215,90 @@ def test_refine_step_fp32_720p_b8(dev):
     assert not bad, bad[:10]
 
 
+def _cosd(a, b):
+    a = torch.as_tensor(a).detach().double().cpu().reshape(-1)
+    b = torch.as_tensor(b).detach().double().cpu().reshape(-1)
+    return 1.0 - float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+
+
+def test_refine_step_bf16_720p_b8_bench_config(dev):
+    """The configuration bench.py times (BASELINE metric: bf16, 720x1280, 8 images, REFINE,
+    ref train.py:250-327 / net_tools.py:492-516), from bench.py's own initial state: Trainer
+    seed 0, lr 1e-3, rod.data.synthetic_batch(seed=SEED).  Its loss is bench.py's
+    "loss_first_step".  Truth: the oracle step in float64.  Baseline for what bf16 can reach:
+    the same oracle step evaluated with every tensor in bf16 (PyTorch ops on the GPU, an
+    independent bf16 implementation).  Bars:
+      loss             within max(1e-2, 4x the bf16 baseline's) relative of float64;
+      head outputs /   angular error (1 - cos) vs float64 within max(0.02, 3x) the bf16
+      moving stats /   baseline's, on tensors the bf16 baseline represents at all (its
+      gradients        cos >= 0.95);
+      SGD + clip       bit-exact given the gradient (net_tools.py:645-651)."""
+    import utils.net_tools as nt
+    from nets.catch_net import factory
+    from rod.data import SEED, synthetic_batch
+    from rod.trainer import Trainer
+    from utils.common_tools import cornerBboxes_2_centerBboxes
+    B, bf16 = 8, torch.bfloat16
+    tr = Trainer((H, W), B, dtype=bf16, device=dev)          # as bench.py builds it
+    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=SEED)
+    snap = ({k: v.detach().cpu().clone() for k, v in tr.net.store.params.items()},
+            {k: v.detach().cpu().clone() for k, v in tr.net.store.buffers.items()})
+    p0 = tr.net.store.flat.detach().clone()
+    x = ops.normalize_image(img, bf16)
+    tg = nt.refine_groundtruth(tr.anchors, cornerBboxes_2_centerBboxes(corner), labels,
+                               config.refine_method.JACCARD_BIGGER, n_boxes=n)
+    outs = factory(x, 'mobilenet_v2', True, tr.config_dict, bf16, net=tr.net).get_output()
+    loss = nt.refine_loss(outs, tg[0], tg[3], targets=tg)
+    loss.backward()
+    torch.cuda.synchronize()
+    # the same step through Trainer.step (bench.py's path) gives the same loss bit for bit
+    tr2 = Trainer((H, W), B, dtype=bf16, device=dev)
+    l_bench = tr2.step(img, corner, labels, n)[0]
+    assert torch.equal(l_bench, loss.detach().reshape(l_bench.shape)), (l_bench.item(), loss.item())
+    del tr2
+    Pb, movb, refb, lossb = _oracle_refine_step(tr, snap, img, corner, labels, n, B, bf16, device=dev)
+    Pb = {k: v.grad.float().cpu() if v.grad is not None else None for k, v in Pb.items()}
+    refb = [r.detach().float().cpu() for r in refb]
+    movb = {k: v.float().cpu() for k, v in movb.items()}
+    lossb = float(lossb.item())
+    torch.cuda.empty_cache()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    P64, mov64, ref64, loss64 = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float64)
+    l64 = loss64.item()
+    lrel, lrel_b = abs(loss.item() - l64) / abs(l64), abs(lossb - l64) / abs(l64)
+    print('bf16 720p b8 loss', loss.item(), 'fp64', l64, 'rel', lrel, '| bf16 oracle', lossb, 'rel', lrel_b)
+    assert lrel <= max(1e-2, 4 * lrel_b)
+    rep = [(l, _cosd(a, o), _cosd(b_, o)) for l, (a, b_, o) in enumerate(zip(outs, refb, ref64))]
+    print('per-level 1-cos vs fp64 (hip, bf16 oracle):', rep)
+    for l, e_h, e_b in rep:
+        if e_b <= 0.05:
+            assert e_h <= max(0.02, 3 * e_b), rep
+    bad_mov = []
+    for k, v in mov64.items():
+        if _cosd(movb[k], v) <= 0.05 and _cosd(tr.net.store.buffers[k], v) > max(0.02, 3 * _cosd(movb[k], v)):
+            bad_mov.append((k, _cosd(tr.net.store.buffers[k], v), _cosd(movb[k], v)))
+    assert not bad_mov, bad_mov[:5]
+    bad, checked, rows = [], 0, []
+    for name, p in tr.net.store.params.items():
+        g64, gb = P64[name].grad, Pb[name]
+        if gb is None or float(g64.abs().max()) == 0 or _cosd(gb, g64) > 0.05:
+            continue   # not representable in bf16 at all (or zero by construction)
+        checked += 1
+        e_h, e_b = _cosd(p._rod_grad, g64), _cosd(gb, g64)
+        rows.append((e_h, e_b, name))
+        if e_h > max(0.02, 3 * e_b):
+            bad.append((name, e_h, e_b))
+    rows.sort(reverse=True)
+    for r in rows[:8]:
+        print('grad 1-cos %.3e  bf16 oracle %.3e  %s' % r)
+    print('checked', checked, 'of', len(tr.net.store.params), 'parameter gradients')
+    assert checked > 100 and not bad, bad[:10]
+    flat_g = tr.net.store.flat_grad.detach().clone()
+    tr.opt.step()
+    ref = (p0.cpu().numpy() - np.float32(1e-3) * np.clip(flat_g.cpu().numpy(), -5, 5)).astype(np.float32)
+    np.testing.assert_array_equal(tr.net.store.flat.detach().cpu().numpy(), ref)
+
+
 # ------------------------------------------------------------------------------- (c)
 def test_predict_b32_nms_bit_exact(dev):
     import predict
@@ -259,6 +343,76 @@ def test_predict_b32_nms_bit_exact(dev):
         for c in range(1, 11):
             assert torch.equal(sg[c], scores[c]) and torch.equal(bg[c], bboxes[c])
     assert pr._graph is not None
+
+
+def test_predict_1080p_fused_blocks_match_oracle(dev):
+    """C5 (BASELINE configs[4]): predict.py's inference path at 1920x1080, bf16, batch 2, with
+    the fused inverted-residual blocks (rod_ir_block_fwd, ref conv_blocks.py:163-312) on.
+      * the fused kernel actually runs (probe), on every block it supports here;
+      * head outputs (refine / det offsets, clf logits) against the float64 oracle network in
+        eval mode on the same input (ref predict.py:127-137): normwise error within 1.5x that of
+        the same predictor with the fused blocks off (ROD_DISABLE=irblock: the unfused bf16
+        chain) + 1e-3, and below 0.1;
+      * softmax, decode and the per-class select / top-k / NMS keep lists and outputs bit-exact
+        against oracle.post given the network's logits and offsets (~2 % of the class scores
+        pass select_threshold 0.1)."""
+    import predict
+    import utils.net_tools as nt
+    from rod import _abi
+    from rod.data import detector_like_scores, synthetic_batch
+    Hc, Wc, B = 1080, 1920, 2
+    pr = predict.Predictor((Hc, Wc), dev, torch.bfloat16, seed=51)
+    probe = synthetic_batch(2, Hc, Wc, dev, seed=52)[0]
+    f_probe = detector_like_scores(pr, probe, rate=0.02)
+    img = synthetic_batch(B, Hc, Wc, dev, seed=53)[0]
+    pr.keep_intermediates = True
+    _abi.PROBE.arm('rod_ir_block_fwd')
+    scores, bboxes = pr(img)
+    torch.cuda.synchronize()
+    _abi.PROBE.disarm()
+    n_fused = _abi.PROBE.table().get('rod_ir_block_fwd', (0,))[0]
+    print('fused blocks launched:', n_fused, 'probe pass fraction', f_probe)
+    assert n_fused >= 4
+    logits, probs, boxes, roff, doff = (t.clone() for t in pr.last)
+    ops._DISABLE.add('irblock')
+    try:
+        pr(img)
+        u_logits, _, _, u_roff, u_doff = pr.last
+    finally:
+        ops._DISABLE.discard('irblock')
+    # float64 oracle of the ALL network in eval mode (moving statistics as calibrated)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    P = {k: v.detach().double().cpu() for k, v in pr.net.store.params.items()}
+    Bf = {k: v.detach().double().cpu() for k, v in pr.net.store.buffers.items()}
+    # the product normalises into bf16 first ((2/255)x - 1 in fp32, rounded once; network_input):
+    # the oracle gets that same input
+    x = torch.from_numpy(f32(2.0 / 255.0) * img.cpu().numpy().astype(f32) - f32(1.0)).to(torch.bfloat16).double()
+    with torch.no_grad():
+        r64, d64, c64 = onet.forward(x, P, Bf, False, all_mode=True)
+    cat = lambda ts, k: torch.cat([t.reshape(B, -1, k) for t in ts], 1)
+    rep = []
+    for name, got, unf, want in (('refine', roff, u_roff, cat(r64, 4)), ('det', doff, u_doff, cat(d64, 4)),
+                                 ('clf', logits, u_logits, cat(c64, 11))):
+        ef, eu = _nerr(got.float(), want), _nerr(unf.float(), want)
+        rep.append((name, ef, eu))
+        assert ef <= 1.5 * eu + 1e-3 and ef < 0.1, rep
+    print('1080p head outputs, normwise error vs fp64 (fused, unfused):', rep)
+    lg = logits.float().cpu().numpy()
+    e, s_, _ = op.softmax_rows(lg)
+    P_ = probs.cpu().numpy()
+    np.testing.assert_array_equal(P_, (e / s_).astype(f32))
+    tab = nt.anchor_table(pr.anchors, dev)
+    BX = boxes.cpu().numpy()
+    np.testing.assert_array_equal(BX, op.decode_corner(tab.center_np, roff.float().cpu().numpy() +
+                                                       doff.float().cpu().numpy()))
+    s_ref, b_ref, kept = op.detected_bboxes_vec(P_, BX, 0.1, 0.4, 400, 200)
+    S = np.stack([scores[c].cpu().numpy() for c in range(1, 11)], 1)
+    Bo = np.stack([bboxes[c].cpu().numpy() for c in range(1, 11)], 1)
+    np.testing.assert_array_equal(S, s_ref)
+    np.testing.assert_array_equal(Bo, b_ref)
+    n_kept = sum(len(v) for v in kept.values())
+    print('1080p kept detections over', B, 'images x 10 classes:', n_kept)
+    assert n_kept > 20 * B
 
 
 # ------------------------------------------------------------------------------- (d)

@@ -394,3 +394,6 @@ def test_step_graphed_bit_identical(dev):
     for k, v in ta.net.store.buffers.items():
         assert torch.equal(v, tb.net.store.buffers[k]), k
     assert torch.equal(la[0], lb[0])
+    # host-side step state advances once per replay, as it does per eager step
+    assert ta.opt.global_step == tb.opt.global_step == 4
+    assert tb.net.store.version == ta.net.store.version

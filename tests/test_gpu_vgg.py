@@ -151,3 +151,28 @@ def test_vgg_refine_step_matches_oracle(dev):
         if e > max(2e-3, 4 * e32):
             bad.append((name, e, e32))
     assert not bad, bad[:10]
+
+
+def test_vgg_step_graphed_draws_fresh_dropout_masks(dev):
+    """Trainer.step_graphed with the vgg_16 backbone (dropout in training, vgg.py:106, 111) runs
+    eager: a replayed graph would reuse one dropout seed forever.  Over three calls it matches
+    three eager steps bit for bit (same seed sequence), draws a new mask every step, and
+    advances opt.global_step once per call."""
+    H, W, B = 288, 512, 1
+    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=9)
+    ta = Trainer((H, W), B, dtype=torch.bfloat16, device=dev, seed=3, backbone_name='vgg_16')
+    tb = Trainer((H, W), B, dtype=torch.bfloat16, device=dev, seed=3, backbone_name='vgg_16')
+    ops._DROPOUT_CALLS[0] = 0
+    masks_a = []
+    for _ in range(3):
+        la = ta.step(img, corner, labels, n)
+        masks_a.append(ta.net.backbone.last_dropout_masks[0].clone())
+    ops._DROPOUT_CALLS[0] = 0
+    for _ in range(3):
+        lb = tb.step_graphed(img, corner, labels, n)
+    torch.cuda.synchronize()
+    assert getattr(tb, '_graph', None) is None and tb._dropout_seen
+    assert not torch.equal(masks_a[0], masks_a[1]) and not torch.equal(masks_a[1], masks_a[2])
+    assert torch.equal(tb.net.backbone.last_dropout_masks[0], masks_a[2])
+    assert torch.equal(ta.net.store.flat, tb.net.store.flat) and torch.equal(la[0], lb[0])
+    assert ta.opt.global_step == tb.opt.global_step == 3
