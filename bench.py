@@ -240,11 +240,12 @@ def tfrecord_leg(args, tr, dev, dtype, steps=8, n_img=48):
 def fp32_leg(args, dev, steps=10, warmup=2):
     """BASELINE configs[1] as stated: the REFINE step at 720x1280, batch 8, fp32, one GPU,
     HIP-graph replay."""
-    from rod.data import SEED, synthetic_batch
+    from rod.data import C2_BATCH_SEED, C2_WEIGHT_SEED, synthetic_batch
     from rod.trainer import Trainer
-    tr = Trainer((args.height, args.width), args.batch, dtype=torch.float32, device=dev)
-    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED)
-    for _ in range(max(warmup, 2)):
+    tr = Trainer((args.height, args.width), args.batch, dtype=torch.float32, device=dev, seed=C2_WEIGHT_SEED)
+    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=C2_BATCH_SEED)
+    first = float(tr.step_graphed(*batch)[0].item())   # pinned by tests/test_gpu_fullsize.py (fp32)
+    for _ in range(max(warmup, 2) - 1):
         tr.step_graphed(*batch)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -254,7 +255,7 @@ def fp32_leg(args, dev, steps=10, warmup=2):
     dt = (time.perf_counter() - t0) / steps
     out = {'metric': 'training images/sec at 1280x720 fp32', 'value': round(args.batch / dt, 3), 'unit': 'images/s',
            'ms_per_step': round(dt * 1e3, 3), 'steps': steps, 'dtype': 'fp32', 'batch': args.batch,
-           'loss': round(float(losses[0].item()), 5), 'hip_graph': True}
+           'loss': round(float(losses[0].item()), 5), 'loss_first_step': round(first, 5), 'hip_graph': True}
     del tr
     torch.cuda.empty_cache()
     return out
@@ -375,7 +376,7 @@ def main():
     dev = torch.device('cuda', local)
     import config
     from rod import _abi, roofline
-    from rod.data import SEED, synthetic_batch
+    from rod.data import C2_BATCH_SEED, C2_WEIGHT_SEED, SEED, synthetic_batch
     from rod.trainer import Trainer
 
     dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
@@ -385,8 +386,10 @@ def main():
         from rod.ddp import GradReducer
         reducer = GradReducer(world)  # bucketed RCCL all-reduce, launched during backward
     tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
-                 world_size=world, reducer=reducer, fix_refine=args.fix_refine, sync_bn=args.sync_bn)
-    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=SEED + rank)
+                 world_size=world, reducer=reducer, fix_refine=args.fix_refine, sync_bn=args.sync_bn,
+                 seed=C2_WEIGHT_SEED)
+    # rank 0's batch and the initial weights are the ones tests/test_gpu_fullsize.py pins
+    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=C2_BATCH_SEED + rank)
     source = None
     if args.augment:
         from rod.dataio import AugmentedSource

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 10
+#define ROD_ABI_VERSION 11
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -487,6 +487,20 @@ int rod_select_topk_nms(const float* probs, const float* boxes, int B, int A, in
  * Plain SGD with clip by value (net_tools.py:645-651):
  *   p -= lr * clamp(g, -clip, clip)   over one flat fp32 buffer. */
 int rod_sgd_clip(float* param, const float* grad, long n, float lr, float clip, void* stream);
+
+/* ------------------------------------------------ deferred parameter-gradient sums (ABI 11)
+ * The weight / bias gradients of rod_conv_wgrad, rod_dw3x3_bwd_filter(_bn) and rod_pw_bwd end in
+ * a fixed-order f64 sum of per-workgroup fp32 partial slabs, whose only readers are the
+ * optimizer (ApplyGradientDescent under net_tools.py:645-651) and the data-parallel all-reduce.
+ * rod_slab_defer(1) makes the calling thread queue those sums instead of launching them (the
+ * ONE exception to "no pointer kept past the call": the caller keeps the partial slabs and
+ * the gradient outputs alive, unmodified, until the flush); rod_slab_flush runs every queued
+ * sum on `stream` as one batched launch per 32 sums, bit-identical to the immediate launches;
+ * rod_slab_defer(0) stops queueing (queued sums stay queued until flushed).  rod_slab_defer
+ * returns the previous mode, rod_slab_pending the queue length. */
+int rod_slab_defer(int on);
+int rod_slab_pending(void);
+int rod_slab_flush(void* stream);
 
 #ifdef __cplusplus
 }

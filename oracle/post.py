@@ -5,8 +5,9 @@ mining, per-class NMS and VOC AP — numpy restatements of the reference:
   det_clf_loss           utils/net_tools.py:519-623
   detected_bboxes        utils/net_tools.py:658-758 + tf_extended/bboxes.py:60-232
                          (tf.image.non_max_suppression semantics of TF 1.x CPU kernel)
-  bboxes_matching        tf_extended/bboxes.py:246-334
-  precision / recall/AP  tf_extended/metrics.py:100-258
+  bboxes_matching        tf_extended/bboxes.py:246-334, 452-479 (bboxes_jaccard)
+  streaming_ap           evaluate.py:146-208 + tf_extended/metrics.py:100-258 (TP/FP arrays,
+                         precision / recall, VOC07 / VOC12 AP)
 
 float32 per-op arithmetic; exp/log correctly rounded via float64 (same convention as the
 kernels); sums of losses in float64."""
@@ -166,6 +167,73 @@ def detected_bboxes(probs, boxes, select_threshold, nms_threshold, top_k, keep_t
             out_s[b, c - 1, :len(sel)] = s[sel]
             out_b[b, c - 1, :len(sel)] = bx[sel]
     return out_s, out_b, kept_idx
+
+
+def bboxes_jaccard_one(ref, g):
+    """bboxes_jaccard (tf_extended/bboxes.py:452-479) of ONE detection against each ground
+    truth box, float32 per op in TF's evaluation order; safe_divide -> 0 when union <= 0."""
+    int_ymin = max(g[0], ref[0])
+    int_xmin = max(g[1], ref[1])
+    int_ymax = min(g[2], ref[2])
+    int_xmax = min(g[3], ref[3])
+    h = max(f32(int_ymax - int_ymin), f32(0))
+    w = max(f32(int_xmax - int_xmin), f32(0))
+    inter = f32(h * w)
+    union = f32(f32(-inter + f32(f32(g[2] - g[0]) * f32(g[3] - g[1]))) + f32(f32(ref[2] - ref[0]) * f32(ref[3] - ref[1])))
+    return f32(inter / union) if union > 0 else f32(0)
+
+
+def bboxes_matching(label, scores, bboxes, glabels, gbboxes, gdifficults, thr=0.5):
+    """bboxes_matching (tf_extended/bboxes.py:246-334), one image, a plain loop over the
+    score-sorted detections: best ground truth of the same label by IoU (argmax: first
+    maximum), TP if above `thr` (strict) and not yet matched, FP if matched already or below;
+    difficult ground truth records neither.  Returns (n_gt, tp list, fp list)."""
+    n_gt = sum(1 for lb, d in zip(glabels, gdifficults) if lb == label and not d)
+    gmatch = [False] * len(glabels)
+    tp, fp = [], []
+    for i in range(len(scores)):
+        if len(glabels) == 0:
+            tp.append(False)
+            fp.append(True)
+            continue
+        jac = [bboxes_jaccard_one(bboxes[i], gbboxes[j]) * f32(1.0 if glabels[j] == label else 0.0)
+               for j in range(len(glabels))]
+        idx = max(range(len(jac)), key=lambda j: (jac[j], -j))
+        match = jac[idx] > thr
+        nd = not gdifficults[idx]
+        tp.append(nd and match and not gmatch[idx])
+        fp.append(nd and (gmatch[idx] or not match))
+        if nd and match:
+            gmatch[idx] = True
+    return n_gt, tp, fp
+
+
+def streaming_ap(batches, classes, thr=0.5, counts=False):
+    """evaluate.py:146-208 over a list of batches, each (scores {c: [B, N]}, boxes {c: [B, N, 4]},
+    glabels [B, G], gboxes [B, G, 4], gcount [B]): matching per image and class, the streaming
+    TP/FP arrays (metrics.py:133-206: rows with tp or fp and score > 1e-4 are kept, in batch
+    order), then VOC07 / VOC12 AP per class (voc_ap).  Returns ({c: ap07}, {c: ap12}) (and
+    {c: (n_tp, n_fp, n_gt)} with counts=True)."""
+    acc = {c: ([], [], [], 0) for c in classes}
+    for scores, boxes, glabels, gboxes, gcount in batches:
+        for c in classes:
+            tps, fps, scs, ng = acc[c]
+            for b in range(len(gcount)):
+                g = int(gcount[b])
+                n, tp, fp = bboxes_matching(c, scores[c][b], boxes[c][b], list(glabels[b, :g]), gboxes[b, :g],
+                                            [False] * g, thr)
+                ng += n
+                for t, f_, sc in zip(tp, fp, scores[c][b]):
+                    if (t or f_) and sc > f32(1e-4):
+                        tps.append(t)
+                        fps.append(f_)
+                        scs.append(float(sc))
+            acc[c] = (tps, fps, scs, ng)
+    ap07 = {c: voc_ap(a[0], a[1], a[2], a[3], True) for c, a in acc.items()}
+    ap12 = {c: voc_ap(a[0], a[1], a[2], a[3], False) for c, a in acc.items()}
+    if counts:
+        return ap07, ap12, {c: (sum(a[0]), sum(a[1]), a[3]) for c, a in acc.items()}
+    return ap07, ap12
 
 
 def voc_ap(tp, fp, scores, n_gt, voc07=True):

@@ -2,6 +2,9 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "rod_common.h"
 
 namespace rod {
@@ -55,11 +58,76 @@ __global__ void __launch_bounds__(256) slab_sum_kernel(const float* __restrict__
   }
 }
 
-void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s) {
+// Deferred slab sums (rod_slab_defer / rod_slab_flush).  A training step's parameter-gradient
+// entries (conv / depthwise / fused-pointwise weight gradients, bias column sums) each end in a
+// slab_sum of a few microseconds, ~115 launches per step whose only consumers are the optimizer
+// and the data-parallel reducer.  While deferral is on, those sums are queued on the host and
+// rod_slab_flush runs them as ONE batched launch per SLAB_BATCH jobs, each job with the exact
+// block geometry and summation order of its own launch (bit-identical outputs).  The jobs are
+// passed by value in the kernel arguments, so a flush is capturable in a HIP graph.
+struct SlabJob {
+  const float* slab;
+  float* out;
+  long n;
+  int nslab;
+  int cb;  // columns per block (4, 8 or 32): as slab_sum would have launched it
+};
+constexpr int SLAB_BATCH = 32;
+struct SlabBatch {
+  SlabJob job[SLAB_BATCH];
+  int first[SLAB_BATCH + 1];  // first block of each job; first[cnt] = grid size
+  int cnt;
+};
+
+__global__ void __launch_bounds__(256) slab_sum_batch_kernel(SlabBatch b) {
+  __shared__ double red[320];  // [L][CB + 1] for L = 256 / CB, CB in {4, 8, 32}
+  int e = 0;
+  while (e + 1 < b.cnt && (int)blockIdx.x >= b.first[e + 1]) ++e;
+  const SlabJob j = b.job[e];
+  const int CB = j.cb, L = 256 / CB;
+  const int tx = threadIdx.x % CB, ty = threadIdx.x / CB;
+  const long i = (long)(blockIdx.x - b.first[e]) * CB + tx;
+  const long n = j.n;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (i < n) {
+    int k = ty;
+    for (; k + 3 * L < j.nslab; k += 4 * L) {
+      s0 += (double)j.slab[(long)k * n + i];
+      s1 += (double)j.slab[(long)(k + L) * n + i];
+      s2 += (double)j.slab[(long)(k + 2 * L) * n + i];
+      s3 += (double)j.slab[(long)(k + 3 * L) * n + i];
+    }
+    for (; k < j.nslab; k += L) s0 += (double)j.slab[(long)k * n + i];
+  }
+  red[ty * (CB + 1) + tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ty == 0 && i < n) {
+    double t = 0.0;
+    for (int k = 0; k < L; ++k) t += red[k * (CB + 1) + tx];
+    j.out[i] = (float)t;
+  }
+}
+
+static thread_local bool g_slab_defer = false;
+static thread_local std::vector<SlabJob>* g_slab_jobs = nullptr;
+
+static int slab_cb(int nslab, long n) {
+  if (n >= 256L * 32 || nslab <= 64) return 32;
+  if (n >= 256L * 8) return 8;
+  return 4;
+}
+
+void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s, bool deferrable) {
   if (n <= 0) return;
-  if (n >= 256L * 32 || nslab <= 64)
+  const int cb = slab_cb(nslab, n);
+  if (deferrable && g_slab_defer) {
+    if (!g_slab_jobs) g_slab_jobs = new std::vector<SlabJob>();
+    g_slab_jobs->push_back(SlabJob{slab, out, n, nslab, cb});
+    return;
+  }
+  if (cb == 32)
     hipLaunchKernelGGL(slab_sum_kernel<32>, dim3(cdivl(n, 32)), dim3(256), 0, s, slab, out, nslab, n);
-  else if (n >= 256L * 8)
+  else if (cb == 8)
     hipLaunchKernelGGL(slab_sum_kernel<8>, dim3(cdivl(n, 8)), dim3(256), 0, s, slab, out, nslab, n);
   else
     hipLaunchKernelGGL(slab_sum_kernel<4>, dim3(cdivl(n, 4)), dim3(256), 0, s, slab, out, nslab, n);
@@ -166,6 +234,37 @@ int rod_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, v
     return ROD_EINVAL;
   }
   return check_launch("rod_cast");
+}
+
+int rod_slab_defer(int on) {
+  const int prev = g_slab_defer ? 1 : 0;
+  g_slab_defer = on != 0;
+  return prev;
+}
+
+int rod_slab_pending(void) { return g_slab_jobs ? (int)g_slab_jobs->size() : 0; }
+
+int rod_slab_flush(void* stream) {
+  hipStream_t s = ROD_STREAM(stream);
+  if (!g_slab_jobs || g_slab_jobs->empty()) return 0;
+  std::vector<SlabJob> jobs;
+  jobs.swap(*g_slab_jobs);
+  for (size_t k0 = 0; k0 < jobs.size(); k0 += SLAB_BATCH) {
+    SlabBatch b{};
+    b.cnt = (int)std::min<size_t>(SLAB_BATCH, jobs.size() - k0);
+    long blocks = 0;
+    for (int e = 0; e < b.cnt; ++e) {
+      b.job[e] = jobs[k0 + e];
+      b.first[e] = (int)blocks;
+      blocks += cdivl(b.job[e].n, b.job[e].cb);
+    }
+    b.first[b.cnt] = (int)blocks;
+    ROD_CHECK_ARG(blocks < (1L << 31), "rod_slab_flush: batch too large");
+    hipLaunchKernelGGL(slab_sum_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, s, b);
+    const int rc = check_launch("rod_slab_flush");
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int rod_sgd_clip(float* param, const float* grad, long n, float lr, float clip, void* stream) {

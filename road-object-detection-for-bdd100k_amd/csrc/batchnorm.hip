@@ -865,7 +865,7 @@ int rod_bn_bwd_finalize(const float* parts, int nparts, long M, int C, const flo
   ROD_CHECK_ARG(parts != nullptr && nparts > 0 && M > 0 && C > 0 && coef != nullptr && rstd != nullptr,
                 "rod_bn_bwd_finalize: bad arguments");
   hipStream_t s = ROD_STREAM(stream);
-  slab_sum(parts, coef + C, nparts, 2L * C, s);  // f64, fixed order
+  slab_sum(parts, coef + C, nparts, 2L * C, s, false);  // f64, fixed order (read by the coef kernel)
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, M, C, rstd, gamma, dgamma, dbeta, coef);
   return check_launch("rod_bn_bwd_finalize");
 }

@@ -23,7 +23,9 @@ void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 // out[i] = sum_b slab[b*n + i] (fp32 partials, f64 accumulation, fixed order).
 // Blocks of CB columns x 256/CB slab lanes (CB adapts to n), so long slabs and wide rows both parallelise.
-void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s);
+// deferrable: a parameter-gradient sum that rod_slab_defer(1) may queue for rod_slab_flush (its
+// output is read by no kernel before the flush); false for sums a later kernel of the same call reads.
+void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s, bool deferrable = true);
 // Grid size for a grid-stride loop over rows x CV channel vectors in which every thread
 // keeps ONE channel vector: (blocks * 256) % CV == 0 and blocks ~ target.
 int const_channel_blocks(int CV, long total, int target = 2048);

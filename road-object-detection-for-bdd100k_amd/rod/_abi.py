@@ -171,6 +171,13 @@ def _capturing():
     return torch.cuda.is_current_stream_capturing()
 
 
+# entries whose parameter-gradient sums rod_slab_defer(1) may queue (include/rod.h, ABI 11)
+DEFERRING = frozenset(("rod_conv_wgrad", "rod_dw3x3_bwd_filter", "rod_dw3x3_bwd_filter_bn", "rod_pw_bwd"))
+# while sums are deferred: every tensor handed to such an entry (partial slabs, gradient outputs)
+# is kept referenced until rod_slab_flush has been enqueued (rod.ops.SlabDefer)
+KEEP = None
+
+
 def call(name: str, *args):
     """Call rod_<name>; raise RuntimeError on a non-zero return code."""
     L = lib()
@@ -178,6 +185,8 @@ def call(name: str, *args):
     ret, argspec = _LIB.protos[name]
     if len(args) != len(argspec):
         raise TypeError(f"{name} expects {len(argspec)} args, got {len(args)}")
+    if KEEP is not None and name in DEFERRING:
+        KEEP.extend(a for a in args if hasattr(a, "data_ptr"))
     conv = [(_ptr(a) if t == "ptr" else a) for (t, _), a in zip(argspec, args)]
     if PROBE.wants(name) and not _capturing():
         import torch

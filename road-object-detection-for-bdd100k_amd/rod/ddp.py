@@ -55,6 +55,8 @@ class GradReducer(object):
 
     def _launch(self, b):
         if b['work'] is None:
+            from . import ops
+            ops.SLAB.flush()   # deferred weight-gradient sums land before the bucket is reduced
             view = self.store.flat_grad[b['lo']:b['hi']]
             b['work'] = dist.all_reduce(view, group=self.group, async_op=True)
 

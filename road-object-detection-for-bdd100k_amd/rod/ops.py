@@ -89,6 +89,46 @@ class _Side:
 SIDE = _Side()
 
 
+class SlabDefer(object):
+    """Deferred parameter-gradient sums over one backward (rod_slab_defer / rod_slab_flush,
+    include/rod.h ABI 11): the weight-gradient entries queue their final fixed-order slab sums
+    instead of launching ~115 tiny kernels per step, and flush() runs them as a few batched
+    launches (bit-identical).  The tensors those entries were given stay referenced until the
+    flush is enqueued, so the caching allocator cannot hand their memory to later work.
+    Everything that reads a parameter gradient runs after flush(): the optimizer, and each
+    data-parallel bucket all-reduce (rod.ddp.GradReducer flushes before launching one)."""
+
+    def __init__(self):
+        self.active = False
+
+    def begin(self):
+        if "slabdefer" in _DISABLE:
+            return
+        _abi.lib().rod_slab_defer(1)
+        _abi.KEEP = []
+        self.active = True
+
+    def flush(self):
+        """Enqueue every queued sum on the current stream (deferral stays on)."""
+        if not self.active:
+            return
+        _abi.call("rod_slab_flush", stream())
+        _abi.KEEP = []    # the flush is enqueued: stream order protects the slabs from here on
+
+    def end(self):
+        if not self.active:
+            return
+        try:
+            self.flush()
+        finally:
+            _abi.lib().rod_slab_defer(0)
+            _abi.KEEP = None
+            self.active = False
+
+
+SLAB = SlabDefer()
+
+
 def grad_slot(p):
     """The flat-buffer gradient view registered for parameter tensor p (or None)."""
     return getattr(p, "_rod_grad", None)

@@ -87,7 +87,12 @@ class Trainer:
         if self._side:
             ops.SIDE.backward(losses[0], self.device)
         else:
-            graph.backward(losses[0])
+            # the weight-gradient slab sums are batched into a few launches at the end
+            ops.SLAB.begin()
+            try:
+                graph.backward(losses[0])
+            finally:
+                ops.SLAB.end()
         if self.reducer is not None:
             self.reducer(self.net.store.flat_grad)
         self.opt.step()

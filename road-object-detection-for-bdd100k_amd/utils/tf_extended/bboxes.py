@@ -1,7 +1,9 @@
 """utils/tf_extended/bboxes.py — box algebra and detection <-> ground-truth matching.
 
 Host numpy float32 (the reference evaluates these on the CPU, evaluate.py:146).  The
-sort/NMS entry points (bboxes_sort, bboxes_nms_batch) forward to the GPU kernel.
+sort/NMS entry points (bboxes_sort, bboxes_nms_batch) run on the GPU through
+rod_select_topk_nms (one launch per class; net_tools.detected_bboxes fuses select + sort +
+NMS of all classes into one).
 """
 import numpy as np
 
@@ -76,13 +78,49 @@ def bboxes_flip_left_right(bboxes):
     return np.stack([b[..., 0], 1 - b[..., 3], b[..., 2], 1 - b[..., 1]], -1)
 
 
+def _select_one_class(scores, bboxes, top_k, keep_top_k, nms_threshold):
+    """rod_select_topk_nms on ONE class's [B, N] scores and [B, N, 4] boxes (device tensors):
+    the scores become column 1 of a [B, N, 2] table (column 0, the background, is ignored by
+    the kernel), select threshold 0 keeps every row (scores are probabilities, >= 0), so the
+    kernel runs top-k (descending, ties to the lower index) and greedy NMS only."""
+    import torch
+    from rod import ops
+    s = torch.as_tensor(scores)
+    b = torch.as_tensor(bboxes)
+    if s.device.type != 'cuda':
+        raise ValueError('bboxes_sort / bboxes_nms_batch run on the GPU: pass cuda tensors')
+    B, N = s.shape
+    probs = torch.zeros((B, N, 2), dtype=torch.float32, device=s.device)
+    probs[..., 1] = s.float()
+    out_s, out_b = ops.select_topk_nms(probs, b.float().contiguous(), 0.0, top_k, keep_top_k, nms_threshold,
+                                       compact=False)
+    return out_s[:, 0], out_b[:, 0]
+
+
 def bboxes_sort(scores, bboxes, top_k=400, scope=None):
-    raise NotImplementedError('sorting is fused with NMS: use utils.net_tools.detected_bboxes '
-                              '(rod_select_topk_nms)')
+    """bboxes.py:60-100: the top_k scores of every image in decreasing order (tf.nn.top_k,
+    ties to the lower index) with their boxes gathered — [B, top_k], [B, top_k, 4]; dict
+    inputs (one entry per class) give dicts.  Scores must be >= 0 (class probabilities, as at
+    the reference's only call site, net_tools.py:750) and top_k <= min(N, 1024)."""
+    if isinstance(scores, dict) or isinstance(bboxes, dict):
+        out = {c: bboxes_sort(scores[c], bboxes[c], top_k) for c in scores}
+        return {c: v[0] for c, v in out.items()}, {c: v[1] for c, v in out.items()}
+    if top_k > scores.shape[-1]:
+        raise ValueError('bboxes_sort: top_k %d > %d scores (tf.nn.top_k fails the same way)'
+                         % (top_k, scores.shape[-1]))
+    # no suppression: an IoU is never > +inf
+    return _select_one_class(scores, bboxes, top_k, top_k, float('inf'))
 
 
 def bboxes_nms_batch(scores, bboxes, nms_threshold=0.5, keep_top_k=200, scope=None):
-    raise NotImplementedError('use utils.net_tools.detected_bboxes (rod_select_topk_nms)')
+    """bboxes.py:192-232: tf.image.non_max_suppression per image (greedy in score order, a box
+    is dropped when its IoU with a kept one is > nms_threshold), the kept scores / boxes in
+    score order, zero-padded to keep_top_k — [B, keep_top_k], [B, keep_top_k, 4]; dicts per
+    class as in the reference.  N <= 1024 candidates per image (the output of bboxes_sort)."""
+    if isinstance(scores, dict) or isinstance(bboxes, dict):
+        out = {c: bboxes_nms_batch(scores[c], bboxes[c], nms_threshold, keep_top_k) for c in scores}
+        return {c: v[0] for c, v in out.items()}, {c: v[1] for c, v in out.items()}
+    return _select_one_class(scores, bboxes, scores.shape[-1], keep_top_k, nms_threshold)
 
 
 def bboxes_matching(label, scores, bboxes, glabels, gbboxes, gdifficults, matching_threshold=0.5, scope=None):

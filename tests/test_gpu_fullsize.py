@@ -133,16 +133,40 @@ def _oracle_refine_step(tr, snap, img, corner, labels, n, B, dt, device='cpu'):
     return P, mov, refine, loss
 
 
+_TRUTH = {}
+
+
+def _c2_truth(tr, snap, img, corner, labels, n, B):
+    """The float64 oracle REFINE step from bench.py's initial state (rod.data.C2_WEIGHT_SEED /
+    C2_BATCH_SEED), computed once per module: (parameter gradients, moving statistics, outputs,
+    loss).  ~3 CPU-minutes at 720x1280 b8; shared by the fp32 and the bf16 step tests."""
+    if 'c2' not in _TRUTH:
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        P64, mov64, ref64, loss64 = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float64)
+        _TRUTH['c2'] = ({k: v.grad.detach().clone() if v.grad is not None else None for k, v in P64.items()},
+                        {k: v.detach().clone() for k, v in mov64.items()},
+                        [r.detach().clone() for r in ref64], float(loss64.item()),
+                        {k: v.clone() for k, v in snap[0].items()})
+    g64, mov64, ref64, loss64, snap0 = _TRUTH['c2']
+    assert all(torch.equal(snap0[k], v) for k, v in snap[0].items()), 'not the C2 initial weights'
+    return g64, mov64, ref64, loss64
+
+
+class _Grad(object):   # a parameter-like holder of a cached oracle gradient
+    def __init__(self, g):
+        self.grad = g
+
+
 def test_refine_step_fp32_720p_b8(dev):
     import utils.net_tools as nt
     from nets.catch_net import factory
-    from rod.data import synthetic_batch
+    from rod.data import C2_BATCH_SEED, C2_WEIGHT_SEED, synthetic_batch
     from rod.trainer import Trainer
     from utils.common_tools import cornerBboxes_2_centerBboxes
     B = 8     # C2: BDD100K 1280x720 fp32 batch 8 (at B=2 the 3x5 level's BatchNorms see 30 rows and
     #           float32 itself — PyTorch's CPU evaluation as much as this one — lands at 1.25e-4)
-    tr = Trainer((H, W), B, dtype=torch.float32, device=dev, learning_rate=1e-3, seed=21)
-    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=22)
+    tr = Trainer((H, W), B, dtype=torch.float32, device=dev, learning_rate=1e-3, seed=C2_WEIGHT_SEED)
+    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=C2_BATCH_SEED)
     snap = ({k: v.detach().cpu().clone() for k, v in tr.net.store.params.items()},
             {k: v.detach().cpu().clone() for k, v in tr.net.store.buffers.items()})
     x = ops.normalize_image(img, torch.float32)
@@ -152,12 +176,12 @@ def test_refine_step_fp32_720p_b8(dev):
     loss = nt.refine_loss(outs, tg[0], tg[3], targets=tg)
     loss.backward()
     torch.cuda.synchronize()
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
-    P64, mov64, ref64, loss64 = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float64)
+    g64, mov64, ref64, l64 = _c2_truth(tr, snap, img, corner, labels, n, B)
+    P64 = {k: _Grad(v) for k, v in g64.items()}
     rep = [(l, _nerr(a, o64)) for l, (a, o64) in enumerate(zip(outs, ref64))]
     print('per-level normwise error vs fp64:', rep)
-    lrel = abs(loss.item() - loss64.item()) / abs(loss64.item())
-    print('loss', loss.item(), 'fp64', loss64.item(), 'rel', lrel)
+    lrel = abs(loss.item() - l64) / abs(l64)
+    print('loss', loss.item(), 'fp64', l64, 'rel', lrel)
     # level 6 sits 24 backbone layers + 4 head convs deep; per-level float32 error roughly
     # doubles per level (4e-6 ... 1.2e-4 measured, the fp32 PyTorch oracle alike)
     assert all(e <= (1e-4 if l < 5 else 2e-4) for l, e in rep), rep
@@ -224,10 +248,10 @@ def _cosd(a, b):
 def test_refine_step_bf16_720p_b8_bench_config(dev):
     """The configuration bench.py times (BASELINE metric: bf16, 720x1280, 8 images, REFINE,
     ref train.py:250-327 / net_tools.py:492-516), from bench.py's own initial state: Trainer
-    seed 0, lr 1e-3, rod.data.synthetic_batch(seed=SEED).  Its loss is bench.py's
-    "loss_first_step".  Truth: the oracle step in float64.  Baseline for what bf16 can reach:
-    the same oracle step evaluated with every tensor in bf16 (PyTorch ops on the GPU, an
-    independent bf16 implementation).  Bars:
+    seed C2_WEIGHT_SEED, lr 1e-3, rod.data.synthetic_batch(seed=C2_BATCH_SEED).  Its loss is
+    bench.py's "loss_first_step".  Truth: the oracle step in float64 (shared with the fp32
+    test).  Baseline for what bf16 can reach: the same oracle step evaluated with every tensor
+    in bf16 (PyTorch-CPU, an independent bf16 implementation).  Bars:
       loss             within max(1e-2, 4x the bf16 baseline's) relative of float64;
       head outputs /   angular error (1 - cos) vs float64 within max(0.02, 3x) the bf16
       moving stats /   baseline's, on tensors the bf16 baseline represents at all (its
@@ -235,12 +259,12 @@ def test_refine_step_bf16_720p_b8_bench_config(dev):
       SGD + clip       bit-exact given the gradient (net_tools.py:645-651)."""
     import utils.net_tools as nt
     from nets.catch_net import factory
-    from rod.data import SEED, synthetic_batch
+    from rod.data import C2_BATCH_SEED, C2_WEIGHT_SEED, synthetic_batch
     from rod.trainer import Trainer
     from utils.common_tools import cornerBboxes_2_centerBboxes
     B, bf16 = 8, torch.bfloat16
-    tr = Trainer((H, W), B, dtype=bf16, device=dev)          # as bench.py builds it
-    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=SEED)
+    tr = Trainer((H, W), B, dtype=bf16, device=dev, seed=C2_WEIGHT_SEED)     # as bench.py builds it
+    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=C2_BATCH_SEED)
     snap = ({k: v.detach().cpu().clone() for k, v in tr.net.store.params.items()},
             {k: v.detach().cpu().clone() for k, v in tr.net.store.buffers.items()})
     p0 = tr.net.store.flat.detach().clone()
@@ -252,19 +276,18 @@ def test_refine_step_bf16_720p_b8_bench_config(dev):
     loss.backward()
     torch.cuda.synchronize()
     # the same step through Trainer.step (bench.py's path) gives the same loss bit for bit
-    tr2 = Trainer((H, W), B, dtype=bf16, device=dev)
+    tr2 = Trainer((H, W), B, dtype=bf16, device=dev, seed=C2_WEIGHT_SEED)
     l_bench = tr2.step(img, corner, labels, n)[0]
     assert torch.equal(l_bench, loss.detach().reshape(l_bench.shape)), (l_bench.item(), loss.item())
     del tr2
-    Pb, movb, refb, lossb = _oracle_refine_step(tr, snap, img, corner, labels, n, B, bf16, device=dev)
-    Pb = {k: v.grad.float().cpu() if v.grad is not None else None for k, v in Pb.items()}
-    refb = [r.detach().float().cpu() for r in refb]
-    movb = {k: v.float().cpu() for k, v in movb.items()}
-    lossb = float(lossb.item())
-    torch.cuda.empty_cache()
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    P64, mov64, ref64, loss64 = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float64)
-    l64 = loss64.item()
+    Pb, movb, refb, lossb = _oracle_refine_step(tr, snap, img, corner, labels, n, B, bf16)
+    Pb = {k: v.grad.float() if v.grad is not None else None for k, v in Pb.items()}
+    refb = [r.detach().float() for r in refb]
+    movb = {k: v.float() for k, v in movb.items()}
+    lossb = float(lossb.item())
+    g64, mov64, ref64, l64 = _c2_truth(tr, snap, img, corner, labels, n, B)
+    P64 = {k: _Grad(v) for k, v in g64.items()}
     lrel, lrel_b = abs(loss.item() - l64) / abs(l64), abs(lossb - l64) / abs(l64)
     print('bf16 720p b8 loss', loss.item(), 'fp64', l64, 'rel', lrel, '| bf16 oracle', lossb, 'rel', lrel_b)
     assert lrel <= max(1e-2, 4 * lrel_b)

@@ -397,3 +397,31 @@ def test_step_graphed_bit_identical(dev):
     # host-side step state advances once per replay, as it does per eager step
     assert ta.opt.global_step == tb.opt.global_step == 4
     assert tb.net.store.version == ta.net.store.version
+
+
+@pytest.mark.parametrize('train_range', ['REFINE', 'ALL'])
+def test_deferred_slab_sums_bit_identical(dev, train_range):
+    """Trainer.step batches the weight-gradient slab sums into a few launches (rod_slab_defer /
+    rod_slab_flush, ABI 11): parameters, moving statistics and losses after two steps are
+    bit-identical to the immediate per-entry sums (ROD_DISABLE=slabdefer), and nothing is left
+    queued after a step."""
+    from rod import _abi
+    H, W, B = 160, 288, 2
+    rng = getattr(config.train_range, train_range)
+    img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=23)
+    runs = []
+    for off in (True, False):
+        if off:
+            ops._DISABLE.add('slabdefer')
+        try:
+            tr = Trainer((H, W), B, dtype=torch.bfloat16, device=dev, seed=2, train_range=rng, fix_refine=False)
+            ls = [tr.step(img, corner, labels, n)[0].clone() for _ in range(2)]
+        finally:
+            ops._DISABLE.discard('slabdefer')
+        torch.cuda.synchronize()
+        assert _abi.lib().rod_slab_pending() == 0
+        runs.append((tr.net.store.flat.clone(), {k: v.clone() for k, v in tr.net.store.buffers.items()}, ls))
+    (fa, ba, la), (fb, bb, lb) = runs
+    assert torch.equal(fa, fb)
+    assert all(torch.equal(v, bb[k]) for k, v in ba.items())
+    assert all(torch.equal(x, y) for x, y in zip(la, lb))

@@ -191,3 +191,173 @@ def test_tf_bundle_roundtrip_into_store(tmp_path):
     open(d, 'wb').write(raw)
     with pytest.raises(IOError, match='checksum'):
         ck.read_tf_bundle(prefix)
+
+
+# ---------------------------------------------------------------- F2: tensor-bundle layout vs TF's protos
+
+def _crc32c_py(data, crc=0):
+    """Bitwise CRC32C (Castagnoli, reflected 0x82F63B78): independent of librodio."""
+    crc ^= 0xFFFFFFFF
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 & -(crc & 1))
+    return crc ^ 0xFFFFFFFF
+
+
+def _mask_py(c):   # tensorflow/core/lib/hash/crc32c.h Mask()
+    return ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xa282ead8) & 0xFFFFFFFF
+
+
+def _leveldb_rows(raw):
+    """Minimal reader of the LevelDB table format as published (table_format.md, which TF's
+    tensorflow/core/lib/io/table follows): 48-byte footer (metaindex + index BlockHandles,
+    zero padding, magic 0xdb4775248b80fb57 LE), blocks of prefix-compressed entries with a
+    restart array, each block followed by a type byte and the masked CRC32C of block + type."""
+    def varint(b, p):
+        v = s = 0
+        while True:
+            x = b[p]
+            p += 1
+            v |= (x & 0x7F) << s
+            s += 7
+            if x < 0x80:
+                return v, p
+
+    def block(off, size):
+        blk, typ = raw[off:off + size], raw[off + size]
+        assert typ == 0, 'compressed block'
+        assert struct.unpack_from('<I', raw, off + size + 1)[0] == _mask_py(_crc32c_py(raw[off:off + size + 1]))
+        n = struct.unpack_from('<I', blk, len(blk) - 4)[0]
+        end, p, key, rows = len(blk) - 4 - 4 * n, 0, b'', []
+        while p < end:
+            sh, p = varint(blk, p)
+            ns, p = varint(blk, p)
+            vl, p = varint(blk, p)
+            key = key[:sh] + blk[p:p + ns]
+            p += ns
+            rows.append((key, blk[p:p + vl]))
+            p += vl
+        return rows
+    foot = raw[-48:]
+    assert struct.unpack_from('<Q', foot, 40)[0] == 0xdb4775248b80fb57
+    _, p = varint(foot, 0)
+    _, p = varint(foot, p)
+    io_, p = varint(foot, p)
+    isz, p = varint(foot, p)
+    rows = []
+    for _, h in block(io_, isz):
+        o, q = varint(h, 0)
+        sz, _ = varint(h, q)
+        rows += block(o, sz)
+    return rows
+
+
+def _bundle_classes():
+    """BundleHeaderProto / BundleEntryProto (tensorflow/core/protobuf/tensor_bundle.proto) with
+    VersionDef (framework/versions.proto), TensorShapeProto (tensor_shape.proto),
+    TensorSliceProto (tensor_slice.proto) and DataType (types.proto), from field numbers."""
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+    fd = descriptor_pb2.FileDescriptorProto(name='rod_test_bundle.proto', package='tfb', syntax='proto3')
+    F = descriptor_pb2.FieldDescriptorProto
+    rep, opt = F.LABEL_REPEATED, F.LABEL_OPTIONAL
+    dt = fd.enum_type.add(name='DataType')
+    for n, v in [('DT_INVALID', 0), ('DT_FLOAT', 1), ('DT_DOUBLE', 2), ('DT_INT32', 3), ('DT_UINT8', 4),
+                 ('DT_INT16', 5), ('DT_INT8', 6), ('DT_STRING', 7), ('DT_INT64', 9), ('DT_BOOL', 10),
+                 ('DT_BFLOAT16', 14), ('DT_HALF', 19)]:
+        dt.value.add(name=n, number=v)
+
+    def msg(parent, name, fields):
+        m = parent.add(name=name)
+        for fname, num, typ, label, tname in fields:
+            f = m.field.add(name=fname, number=num, type=typ, label=label)
+            if tname:
+                f.type_name = tname
+        return m
+    msg(fd.message_type, 'VersionDef', [('producer', 1, F.TYPE_INT32, opt, None),
+                                        ('min_consumer', 2, F.TYPE_INT32, opt, None),
+                                        ('bad_consumers', 3, F.TYPE_INT32, rep, None)])
+    shp = msg(fd.message_type, 'TensorShapeProto', [('dim', 2, F.TYPE_MESSAGE, rep, '.tfb.TensorShapeProto.Dim'),
+                                                    ('unknown_rank', 3, F.TYPE_BOOL, opt, None)])
+    msg(shp.nested_type, 'Dim', [('size', 1, F.TYPE_INT64, opt, None), ('name', 2, F.TYPE_STRING, opt, None)])
+    msg(fd.message_type, 'TensorSliceProto', [])
+    hdr = msg(fd.message_type, 'BundleHeaderProto', [('num_shards', 1, F.TYPE_INT32, opt, None),
+                                                     ('endianness', 2, F.TYPE_ENUM, opt,
+                                                      '.tfb.BundleHeaderProto.Endianness'),
+                                                     ('version', 3, F.TYPE_MESSAGE, opt, '.tfb.VersionDef')])
+    en = hdr.enum_type.add(name='Endianness')
+    en.value.add(name='LITTLE', number=0)
+    en.value.add(name='BIG', number=1)
+    msg(fd.message_type, 'BundleEntryProto', [('dtype', 1, F.TYPE_ENUM, opt, '.tfb.DataType'),
+                                              ('shape', 2, F.TYPE_MESSAGE, opt, '.tfb.TensorShapeProto'),
+                                              ('shard_id', 3, F.TYPE_INT32, opt, None),
+                                              ('offset', 4, F.TYPE_INT64, opt, None),
+                                              ('size', 5, F.TYPE_INT64, opt, None),
+                                              ('crc32c', 6, F.TYPE_FIXED32, opt, None),
+                                              ('slices', 7, F.TYPE_MESSAGE, rep, '.tfb.TensorSliceProto')])
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    get = lambda n: message_factory.GetMessageClass(pool.FindMessageTypeByName('tfb.' + n))
+    return get('BundleHeaderProto'), get('BundleEntryProto')
+
+
+_BUNDLE = {'global_step': np.array(77, np.int64),
+           'backbone/MobilenetV2/Conv/weights': np.arange(3 * 3 * 3 * 4, dtype=np.float32).reshape(3, 3, 3, 4) / 7,
+           'refine/block_1/Conv/biases': np.array([-1.5, 0.25, 3e-8], np.float32),
+           'deconv/block_2/weight_1': np.linspace(-1, 1, 2 * 2 * 5 * 6).astype(np.float32).reshape(2, 2, 5, 6),
+           'counts': np.array([[1, -2], [3, 2 ** 40]], np.int64), 'flags': np.array([True, False, True])}
+
+
+def test_tf_bundle_layout_against_tf_protos(tmp_path):
+    """F2 (ref train.py:155-158, 191-193, 278-283 — tf.train.Saver bundles).  What
+    rod.checkpoint writes is read back with an independent LevelDB-table reader and TF's own
+    message layouts (protobuf from descriptors): header (1 shard, little endian, version
+    producer 1), one BundleEntryProto per variable in key order (dtype enum, shape dims,
+    shard 0, back-to-back offsets / sizes into .data-00000-of-00001, masked CRC32C of the
+    bytes); and a bundle whose index values protobuf itself serialised reads back through
+    rod.checkpoint.read_tf_bundle."""
+    from rod import checkpoint as ck
+    Header, Entry = _bundle_classes()
+    prefix = str(tmp_path / 'a' / 'model')
+    ck.write_tf_bundle(prefix, _BUNDLE)
+    rows = _leveldb_rows(open(prefix + '.index', 'rb').read())
+    assert [k for k, _ in rows] == [b''] + sorted(k.encode() for k in _BUNDLE)
+    h = Header()
+    h.ParseFromString(rows[0][1])
+    assert h.num_shards == 1 and h.endianness == 0 and h.version.producer == 1
+    data = open(prefix + '.data-00000-of-00001', 'rb').read()
+    dtnum = {np.dtype(np.float32): 1, np.dtype(np.int64): 9, np.dtype(np.bool_): 10}
+    pos = 0
+    for k, v in rows[1:]:
+        e = Entry()
+        e.ParseFromString(v)
+        a = _BUNDLE[k.decode()]
+        assert e.dtype == dtnum[a.dtype] and [d.size for d in e.shape.dim] == list(a.shape)
+        assert e.shard_id == 0 and e.offset == pos and e.size == a.nbytes and not e.slices
+        raw = data[e.offset:e.offset + e.size]
+        assert raw == a.astype(a.dtype.newbyteorder('<')).tobytes()
+        assert e.crc32c == _mask_py(_crc32c_py(raw))
+        pos += e.size
+    assert pos == len(data)
+    # the other direction: index values serialised by protobuf (field order, defaults and
+    # encodings of its choosing) in a table, read by rod.checkpoint
+    q = str(tmp_path / 'b' / 'model')
+    os.makedirs(os.path.dirname(q))
+    h2 = Header(num_shards=1)
+    h2.version.producer = 1
+    rows2, blob = [(b'', h2.SerializeToString())], bytearray()
+    for name in sorted(_BUNDLE):
+        a = _BUNDLE[name]
+        raw = a.astype(a.dtype.newbyteorder('<')).tobytes()
+        e = Entry(dtype=dtnum[a.dtype], offset=len(blob), size=len(raw), crc32c=_mask_py(_crc32c_py(raw)))
+        for d in a.shape:
+            e.shape.dim.add(size=d)
+        rows2.append((name.encode(), e.SerializeToString()))
+        blob += raw
+    open(q + '.data-00000-of-00001', 'wb').write(bytes(blob))
+    ck.write_sstable(q + '.index', rows2)
+    got = ck.read_tf_bundle(q)
+    assert set(got) == set(_BUNDLE)
+    for k, a in _BUNDLE.items():
+        np.testing.assert_array_equal(got[k], a)
+        assert got[k].shape == a.shape

@@ -117,3 +117,49 @@ def test_vectorised_nms_oracle_equals_scalar():
         np.testing.assert_array_equal(a[0], b[0])
         np.testing.assert_array_equal(a[1], b[1])
         assert a[2] == b[2]
+
+
+def test_product_matching_and_streaming_ap_match_oracle():
+    """utils.tf_extended matching + streaming TP/FP + VOC AP (the host half of evaluate.py:
+    146-208) against oracle.post.bboxes_matching / streaming_ap (a plain-loop restatement of
+    tf_extended/bboxes.py:246-334 and metrics.py:100-258) on random batches with shared labels,
+    duplicate detections, ties and padded (zero-score) rows."""
+    import utils.tf_extended as tfe
+    from oracle import post as op
+    rng = np.random.default_rng(11)
+    classes = [1, 2, 3]
+    batches, state = [], None
+    for _ in range(4):
+        B, N, G = 3, 12, 6
+        gcount = rng.integers(0, G + 1, B)
+        gl = rng.integers(1, 4, (B, G)).astype(np.int64)
+        c0 = rng.uniform(0.1, 0.9, (B, G, 2))
+        hw = rng.uniform(0.05, 0.4, (B, G, 2))
+        gb = np.concatenate([c0 - hw / 2, c0 + hw / 2], -1).astype(f32)
+        scores, boxes = {}, {}
+        for c in classes:
+            s = np.sort(rng.random((B, N)).astype(f32), 1)[:, ::-1].copy()
+            s[:, -3:] = 0                                   # padded rows of the NMS output
+            s[:, 2] = s[:, 1]                               # a tie
+            jit = rng.normal(0, 0.03, (B, N, 4)).astype(f32)
+            pick = rng.integers(0, G, (B, N))
+            bx = np.take_along_axis(gb, pick[..., None], 1) + jit   # near (some) ground truth
+            bx[:, 3] = bx[:, 1]                                       # a duplicate detection
+            scores[c], boxes[c] = s, bx.astype(f32)
+        batches.append((scores, boxes, gl, gb, gcount))
+        n_g, tp, fp, _ = tfe.bboxes_matching_batch(classes, scores, boxes, gl, gb, np.zeros_like(gl),
+                                                   matching_threshold=0.5, gt_counts=gcount)
+        for c in classes:
+            for b in range(B):
+                g = int(gcount[b])
+                n, t, f_ = op.bboxes_matching(c, scores[c][b], boxes[c][b], list(gl[b, :g]), gb[b, :g], [False] * g)
+                assert n == n_g[c][b] and list(tp[c][b]) == t and list(fp[c][b]) == f_
+        state = tfe.streaming_tp_fp_arrays(n_g, tp, fp, scores, state=state)
+    ap07, ap12 = op.streaming_ap(batches, classes)
+    hits = 0
+    for c in classes:
+        p, r = tfe.precision_recall(*state[c].value())
+        hits += int(state[c].value()[2].sum())
+        assert tfe.average_precision_voc07(p, r) == pytest.approx(ap07[c], abs=1e-12)
+        assert tfe.average_precision_voc12(p, r) == pytest.approx(ap12[c], abs=1e-12)
+    assert hits > 10 and 0 < min(ap12.values()) < 1

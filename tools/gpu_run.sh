@@ -91,6 +91,15 @@ for step in "$@"; do
            python tools/pmc_kernel_summary.py $OUT/irpmc_$TAG/run_counter_collection.csv ir_block_fwd > $OUT/${TAG}_irpmc.txt &&
            gzip -f $OUT/irpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_irpmc.txt ;;
     irbench) run irbench 300 python tools/irblock_bench.py --iters 10 --res 720 1080 ;;
+    dwpmc) run dwpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM SQ_INSTS_VALU SQ_BUSY_CYCLES -d $OUT/dwpmc_$TAG -o run --output-format csv -- python3 tools/dw_bench.py --iters 3 &&
+           python tools/pmc_kernel_summary.py $OUT/dwpmc_$TAG/run_counter_collection.csv dw3x3 > $OUT/${TAG}_dwpmc.txt &&
+           gzip -f $OUT/dwpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_dwpmc.txt ;;
+    bnpmc) run bnpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES -d $OUT/bnpmc_$TAG -o run --output-format csv -- python3 tools/bn_bench.py --iters 3 &&
+           python tools/pmc_kernel_summary.py $OUT/bnpmc_$TAG/run_counter_collection.csv bn_ > $OUT/${TAG}_bnpmc.txt &&
+           gzip -f $OUT/bnpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_bnpmc.txt ;;
+    dwbench) run dwbench 300 python tools/dw_bench.py ;;
+    bnbench) run bnbench 300 python tools/bn_bench.py ;;
+    cbench) run cbench 300 python tools/conv_bench.py ;;
     dwab) run dwa 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_w0.so python tools/dw_bench.py --out /tmp/${TAG}_dw0.pt &&
           run dwb 300 python tools/dw_bench.py --check /tmp/${TAG}_dw0.pt ;;
     dwbn) run dwbn 600 python -m pytest tests/test_gpu_dwbn.py tests/test_gpu_train.py tests/test_gpu_kernels.py -m gpu -q -x --timeout=500 -p no:cacheprovider ;;
