@@ -370,6 +370,9 @@ def main():
         local = local % torch.cuda.device_count() if backend != 'nccl' else local
         torch.cuda.set_device(local)
         if backend == 'nccl':
+            # the step is captured with its RCCL collectives (Trainer.step_graphed): no event of an eager
+            # collective may be recycled into the capture while the watchdog still polls it
+            os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
             torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             torch.distributed.init_process_group(backend)

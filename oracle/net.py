@@ -24,6 +24,35 @@ TAPS = [11, 15, 18, 20, 22, 24]  # config.py:30-31
 N_ANCHOR = [6, 9, 9, 9, 9, 9]
 
 
+# Storage-rounding emulation (test baseline only): with set_storage(torch.bfloat16) every tensor
+# the product keeps in HBM — conv / depthwise outputs, BatchNorm + activation outputs, residual
+# sums — is rounded to bf16 after fp32 arithmetic, and so is the gradient w.r.t. each of them in
+# backward: "bf16 storage, fp32 arithmetic", the product's bf16 mode, as an independent
+# PyTorch-CPU evaluation (the plain bf16 evaluation rounds every intermediate op as well).
+_STORE = [None]
+
+
+class _RoundST(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t, dt):
+        return t.to(dt).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(_STORE[0]).to(g.dtype), None
+
+
+def set_storage(dtype):
+    """dtype (e.g. torch.bfloat16) or None (no rounding); returns the previous setting."""
+    prev = _STORE[0]
+    _STORE[0] = dtype
+    return prev
+
+
+def _st(t):
+    return t if _STORE[0] is None else _RoundST.apply(t, _STORE[0])
+
+
 def make_divisible(v, d, min_value=None):
     """conv_blocks.py:50-57."""
     min_value = d if min_value is None else min_value
@@ -43,7 +72,7 @@ def conv(x, w, b=None, stride=1):
     pt, pb = same_pad(x.shape[2], stride, k)
     pl, pr = same_pad(x.shape[3], stride, k)
     x = F.pad(x, (pl, pr, pt, pb))
-    return F.conv2d(x, w.permute(0, 3, 1, 2), b, stride)
+    return _st(F.conv2d(x, w.permute(0, 3, 1, 2), b, stride))
 
 
 def dwconv(x, w, stride):
@@ -52,7 +81,7 @@ def dwconv(x, w, stride):
     pt, pb = same_pad(x.shape[2], stride, 3)
     pl, pr = same_pad(x.shape[3], stride, 3)
     x = F.pad(x, (pl, pr, pt, pb))
-    return F.conv2d(x, w.permute(2, 0, 1)[:, None], None, stride, groups=C)
+    return _st(F.conv2d(x, w.permute(2, 0, 1)[:, None], None, stride, groups=C))
 
 
 def batch_norm(x, gamma, beta, mm, mv, training, decay, eps=1e-3, moving=None, name=None):
@@ -104,7 +133,7 @@ def backbone(x, P, B, training, moving=None, scope='backbone/MobilenetV2'):
     def bn(t, name, act):
         y = batch_norm(t, P[name + '/gamma'], P[name + '/beta'], B[name + '/moving_mean'],
                        B[name + '/moving_variance'], training, 0.997, 1e-3, moving, name)
-        return relu6(y) if act else y
+        return _st(relu6(y) if act else y)
 
     for (idx, kind, s, cin, inner, cout, res, sc) in layer_plan():
         base = scope + '/' + sc
@@ -117,7 +146,7 @@ def backbone(x, P, B, training, moving=None, scope='backbone/MobilenetV2'):
             x = bn(dwconv(x, P[base + '/depthwise/depthwise_weights'], s), base + '/depthwise/BatchNorm', True)
             x = bn(conv(x, P[base + '/project/weights']), base + '/project/BatchNorm', False)
             if res:
-                x = x + inp
+                x = _st(x + inp)
         eps['layer_%d' % idx] = x
     return eps
 
@@ -133,8 +162,8 @@ def head(feats, P, B, scope, k, training, moving=None):
                 cn = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
                 bn_ = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
                 x = conv(x, P[cn + '/weights'], P[cn + '/biases'])
-                x = leaky(batch_norm(x, None, P[bn_ + '/beta'], B[bn_ + '/moving_mean'],
-                                     B[bn_ + '/moving_variance'], training, 0.999, 1e-3, moving, bn_))
+                x = _st(leaky(batch_norm(x, None, P[bn_ + '/beta'], B[bn_ + '/moving_mean'],
+                                         B[bn_ + '/moving_variance'], training, 0.999, 1e-3, moving, bn_)))
                 n += 1
         Bn, C, fh, fw = x.shape
         outs.append(x.permute(0, 2, 3, 1).reshape(Bn, fh, fw, N_ANCHOR[i], k))

@@ -3,6 +3,8 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <vector>
 
 #include "rod_common.h"
@@ -108,8 +110,11 @@ __global__ void __launch_bounds__(256) slab_sum_batch_kernel(SlabBatch b) {
   }
 }
 
-static thread_local bool g_slab_defer = false;
-static thread_local std::vector<SlabJob>* g_slab_jobs = nullptr;
+// process-wide, not thread-local: PyTorch runs the backward of custom autograd Functions on its
+// per-device worker thread, not on the thread that calls rod_slab_defer / rod_slab_flush
+static std::atomic<bool> g_slab_defer{false};
+static std::mutex g_slab_mu;
+static std::vector<SlabJob>* g_slab_jobs = nullptr;
 
 static int slab_cb(int nslab, long n) {
   if (n >= 256L * 32 || nslab <= 64) return 32;
@@ -120,7 +125,8 @@ static int slab_cb(int nslab, long n) {
 void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s, bool deferrable) {
   if (n <= 0) return;
   const int cb = slab_cb(nslab, n);
-  if (deferrable && g_slab_defer) {
+  if (deferrable && g_slab_defer.load()) {
+    std::lock_guard<std::mutex> lk(g_slab_mu);
     if (!g_slab_jobs) g_slab_jobs = new std::vector<SlabJob>();
     g_slab_jobs->push_back(SlabJob{slab, out, n, nslab, cb});
     return;
@@ -236,19 +242,21 @@ int rod_cast(const void* src, int src_dtype, void* dst, int dst_dtype, long n, v
   return check_launch("rod_cast");
 }
 
-int rod_slab_defer(int on) {
-  const int prev = g_slab_defer ? 1 : 0;
-  g_slab_defer = on != 0;
-  return prev;
-}
+int rod_slab_defer(int on) { return g_slab_defer.exchange(on != 0) ? 1 : 0; }
 
-int rod_slab_pending(void) { return g_slab_jobs ? (int)g_slab_jobs->size() : 0; }
+int rod_slab_pending(void) {
+  std::lock_guard<std::mutex> lk(g_slab_mu);
+  return g_slab_jobs ? (int)g_slab_jobs->size() : 0;
+}
 
 int rod_slab_flush(void* stream) {
   hipStream_t s = ROD_STREAM(stream);
-  if (!g_slab_jobs || g_slab_jobs->empty()) return 0;
   std::vector<SlabJob> jobs;
-  jobs.swap(*g_slab_jobs);
+  {
+    std::lock_guard<std::mutex> lk(g_slab_mu);
+    if (!g_slab_jobs || g_slab_jobs->empty()) return 0;
+    jobs.swap(*g_slab_jobs);
+  }
   for (size_t k0 = 0; k0 < jobs.size(); k0 += SLAB_BATCH) {
     SlabBatch b{};
     b.cnt = (int)std::min<size_t>(SLAB_BATCH, jobs.size() - k0);

@@ -1676,3 +1676,298 @@ int rod_dw3x3_bwd_filter_bn(const void* x, const float* pro_mean, const float* p
 }
 
 }  // extern "C"
+
+// =====================================================================================
+// Fused stride-1 depthwise backward (ABI 12): the backward of
+//   x = act_e(BN_e(ye))  ->  yd = dw3x3(x, w) (stride 1, TF-SAME)  ->  act_d(BN_d(yd))
+// from dz (the gradient at act_d(BN_d(yd))) in ONE pass over the rows, for a depthwise whose
+// input is the BatchNorm-prologue form of its producer (the expand conv, or the stem):
+//   dy  = the BatchNorm-backward apply of BN_d (rod_bn_bwd_apply's arithmetic, rounded to T;
+//         coef from rod_bn_bwd_reduce over (dz, yd));
+//   dx  = DepthwiseConv2dNativeBackpropInput(dy, w)        (rounded to T: dz of BN_e)
+//   dw  = DepthwiseConv2dNativeBackpropFilter(x, dy)       (fp32 partials, fixed-order sum)
+//   and, with gparts, the BatchNorm-backward sums of BN_e over (dx, ye): per part and channel
+//   (sum g, sum g*yhat), g = dx*act_e'(BN_e(ye)), yhat = (ye - mean_e)*rstd_e — what
+//   rod_bn_bwd_reduce would compute next, in rod_bn_bwd_finalize's [parts][2][C] format.
+// Unfused, these are rod_bn_bwd_apply (read dz, yd; write dy), rod_dw3x3_bwd_data (read dy;
+// write dx), rod_dw3x3_bwd_filter (read ye, dy) and the producer's rod_bn_bwd_reduce (read
+// dx, ye): 9 passes over C-wide tensors.  Fused: read ye, dz, yd, write dx — 4 passes; dy never
+// exists in memory.
+//
+// Engine: the LDS neighbour exchange of dw_lx_body (stride 1), 4 channels per thread (bf16:
+// 8-byte packs) to hold the weights, both BatchNorms' constants and the nine filter
+// accumulators in registers.  Step q handles x row rho = ho0 - 2 + q and dy row rho + 1: each
+// thread converts its column's ye (prologue) and (dz, yd) (apply), publishes both, and takes
+// its left / right neighbours from LDS.  dy row rho + 1 is the last dy row dx row rho needs
+// (taps (0, *)), so dx row rho is emitted at step q; the filter pairs x row rho with the dy rows
+// rho + 1, rho, rho - 1 of the thread's own column (a two-row queue).  dx accumulates in the
+// order of the stride-1 rod_dw3x3_bwd_data kernel (dy rows ascending, taps L, C, R), so dx is
+// bit-identical to the unfused chain; dw and the BN_e sums are reassociated (column tiles).
+// =====================================================================================
+struct DwBwdBn {
+  const float *mean, *rstd, *gamma, *beta, *coef;  // BN_d and its backward coefficients [3][C]
+  int act;
+};
+
+template <typename T, int PACT, bool RED>
+__global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
+                                                              const T* __restrict__ yd, const float* __restrict__ w,
+                                                              T* __restrict__ dx, float* __restrict__ slab,
+                                                              float* __restrict__ gparts, int H, int W, int C,
+                                                              DwTile tl, BnPro pro, DwBwdBn bd) {
+  constexpr int V = 4;
+  typedef PackV<T, V> PK;
+  constexpr int XS = 2 * 2 * 256 * (int)sizeof(PK);  // x and dy slots, double buffered
+  constexpr int SS = 256 * V * 4;                     // per-tap column reduction
+  __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
+  PK* xs = (PK*)smem;              // [2][256]
+  PK* dsl = xs + 2 * 256;          // [2][256]
+  const int tid = threadIdx.x;
+  const int CVb = tl.CVb, P = tl.P;
+  const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
+  int bx, strip, n;
+  xcd_block(bx, strip, n);
+  const int cg = bx % tl.cgroups, ct = bx / tl.cgroups;
+  const int c = (cg * CVb + cvb) * V;
+  const int col = ct * tl.TWo + p - 1;                  // pads (1, 1): input column = output column
+  const bool comp = p >= 1 && p <= P - 2 && col < W;
+  const bool cok = p < P && col >= 0 && col < W;
+  const int ho0 = strip * tl.RB;
+  const int ho1 = ho0 + tl.RB < H ? ho0 + tl.RB : H;
+  const int xlo = ho0 - 1 > 0 ? ho0 - 1 : 0, xhi = ho1 < H - 1 ? ho1 : H - 1;  // rows of x / dy needed
+
+  float wr[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+  DwIn<T, V, PACT> in;
+  in.init(pro, c);
+  float dmu[V], drs[V], dsc[V], dsh[V], da[V], dmg[V], dmx[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    dmu[v] = bd.mean[c + v];
+    drs[v] = bd.rstd[c + v];
+    bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c + v, dsc[v], dsh[v]);
+    da[v] = bd.coef[c + v];
+    dmg[v] = bd.coef[C + c + v];
+    dmx[v] = bd.coef[2 * C + c + v];
+  }
+  constexpr int RV = RED ? V : 1;
+  float emu[RV], ers[RV], sg[RV], sgx[RV];
+  if constexpr (RED) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      emu[v] = pro.mean[c + v];
+      ers[v] = pro.rstd[c + v];
+      sg[v] = sgx[v] = 0.f;
+    }
+  }
+  const long nb = (long)n * H * W * C + c;
+  const T* yen = ye + nb;
+  const T* dzn = dz + nb;
+  const T* ydn = yd + nb;
+  T* dxn = dx + nb;
+
+  // prefetch ring: step q loads x row ho0-2+q and (dz, yd) of row ho0-1+q
+  PK rx[3], rz[3], ry[3];
+  bool okx[3], okd[3];
+  auto issue = [&](int k, int q) {
+    const int rho = ho0 - 2 + q;
+    okx[k] = cok && rho >= xlo && rho <= xhi;
+    okd[k] = cok && rho + 1 >= xlo && rho + 1 <= xhi;
+    if (okx[k]) rx[k].load(yen + ((long)rho * W + col) * C);
+    if (okd[k]) {
+      rz[k].load(dzn + ((long)(rho + 1) * W + col) * C);
+      ry[k].load(ydn + ((long)(rho + 1) * W + col) * C);
+    }
+  };
+  const int nst = ho1 - ho0 + 3;
+  issue(0, 0);
+  issue(1, 1);
+  issue(2, 2);
+  float acc[3][V], fa[9][V], q1[V], q2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    acc[0][v] = acc[1][v] = acc[2][v] = 0.f;
+    q1[v] = q2[v] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) fa[k][v] = 0.f;
+  }
+  for (int q0 = 0; q0 < nst; q0 += 3) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int q = q0 + k;
+      const int rho = ho0 - 2 + q;
+      const int buf = q & 1;
+      // x row rho: the forward's input (prologue, rounded to T), 0 outside the rows needed
+      float xv[V], yraw[V];
+      {
+        in.cvt(rx[k], okx[k], xv);
+        if constexpr (PACT < 0) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) xv[v] = okx[k] ? xv[v] : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) yraw[v] = rx[k].get(v);
+      }
+      // dy row rho + 1: the BatchNorm-backward apply of BN_d, rounded to T
+      float dv[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float yv = ry[k].get(v);
+        const float d = yv - dmu[v];
+        const float z = fmaf(yv, dsc[v], dsh[v]);
+        const float g = rz[k].get(v) * act_grad(z, bd.act);
+        const float o = da[v] * (g - dmg[v] - (d * drs[v]) * dmx[v]);
+        dv[v] = okd[k] ? to_f32(from_f32<T>(o)) : 0.f;
+      }
+      PK px, pd;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        px.set(v, xv[v]);
+        pd.set(v, dv[v]);
+      }
+      issue(k, q + 3);
+      xs[buf * 256 + tid] = px;
+      dsl[buf * 256 + tid] = pd;
+      __syncthreads();
+      if (comp) {
+        const PK xl = xs[buf * 256 + tid - CVb], xr = xs[buf * 256 + tid + CVb];
+        const PK dl = dsl[buf * 256 + tid - CVb], dr = dsl[buf * 256 + tid + CVb];
+        // backward-data: dy row rho+1 is tap row 0 of dx row rho, 1 of rho+1, 2 of rho+2
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int sl = (k + i) % 3;
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            float a = acc[sl][v];
+            a = fmaf(dl.get(v), wr[i * 3 + 2][v], a);
+            a = fmaf(dv[v], wr[i * 3 + 1][v], a);
+            a = fmaf(dr.get(v), wr[i * 3][v], a);
+            acc[sl][v] = a;
+          }
+        }
+        // filter: x row rho with the strip's dy rows rho+1 (tap row 0), rho (1), rho-1 (2)
+        const bool own = rho + 1 >= ho0 && rho + 1 < ho1;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float f0 = own ? dv[v] : 0.f;
+          const float t0 = xl.get(v), t2 = xr.get(v);
+          fa[0][v] = fmaf(f0, t0, fa[0][v]);
+          fa[1][v] = fmaf(f0, xv[v], fa[1][v]);
+          fa[2][v] = fmaf(f0, t2, fa[2][v]);
+          fa[3][v] = fmaf(q1[v], t0, fa[3][v]);
+          fa[4][v] = fmaf(q1[v], xv[v], fa[4][v]);
+          fa[5][v] = fmaf(q1[v], t2, fa[5][v]);
+          fa[6][v] = fmaf(q2[v], t0, fa[6][v]);
+          fa[7][v] = fmaf(q2[v], xv[v], fa[7][v]);
+          fa[8][v] = fmaf(q2[v], t2, fa[8][v]);
+          q2[v] = q1[v];
+          q1[v] = f0;
+        }
+        // dx row rho is complete
+        if (rho >= ho0 && rho < ho1) {
+          PK o;
+#pragma unroll
+          for (int v = 0; v < V; ++v) o.set(v, acc[k][v]);
+          o.store_out(dxn + ((long)rho * W + col) * C);
+          if constexpr (RED) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+              const float z = fmaf(yraw[v], in.sc[v], in.sh[v]);
+              const float g = o.get(v) * act_grad(z, pro.act);
+              sg[v] += g;
+              sgx[v] = fmaf(g, (yraw[v] - emu[v]) * ers[v], sgx[v]);
+            }
+          }
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
+      }
+    }
+  }
+
+  // per channel: sum over the computing columns (column order), tap by tap, then the BN_e sums
+  __syncthreads();
+  float* red = (float*)smem;
+  const int Cc = CVb * V;
+  const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+  auto colsum = [&](const float (&a)[V], float* dst) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) red[tid * V + v] = comp ? a[v] : 0.f;
+    __syncthreads();
+    for (int e = tid; e < Cc; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      float s = 0.f;
+      for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
+      dst[cg * Cc + e] = s;
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int k = 0; k < 9; ++k) colsum(fa[k], slab + (part * 9 + k) * C);
+  if constexpr (RED) {
+    colsum(sg, gparts + part * 2 * C);
+    colsum(sgx, gparts + part * 2 * C + C);
+  }
+}
+
+static DwTile dw_fused_tile(int N, int H, int W, int C) { return dw_tile(N, H, W, C, 1, 4); }
+
+extern "C" {
+
+int rod_dw3x3_bwd_fused_parts(int N, int H, int W, int C) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4) return 0;
+  const DwTile t = dw_fused_tile(N, H, W, C);
+  return (int)((long)N * t.strips * t.coltiles);
+}
+
+size_t rod_dw3x3_bwd_fused_workspace(int N, int H, int W, int C) {
+  return (size_t)rod_dw3x3_bwd_fused_parts(N, H, W, C) * 9 * C * sizeof(float);
+}
+
+int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                        const float* pro_beta, int pro_act, const void* dz, const void* yd, const float* bn_mean,
+                        const float* bn_rstd, const float* bn_gamma, const float* bn_beta, int bn_act,
+                        const float* coef, const float* w, void* dx, float* dw, float* gparts, void* workspace, int N,
+                        int H, int W, int C, int dtype, void* stream) {
+  ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0, "rod_dw3x3_bwd_fused: bad shape (C %% 4 != 0?)");
+  ROD_CHECK_ARG(ye && dz && yd && bn_mean && bn_rstd && coef && w && dx && dw && workspace,
+                "rod_dw3x3_bwd_fused: NULL tensor argument");
+  ROD_CHECK_ARG(!pro_mean || pro_rstd, "rod_dw3x3_bwd_fused: BatchNorm prologue needs mean and rstd");
+  ROD_CHECK_ARG(!gparts || pro_mean, "rod_dw3x3_bwd_fused: the BN_e sums need the input's BatchNorm prologue");
+  ROD_CHECK_ARG(bn_act >= ROD_ACT_NONE && bn_act <= ROD_ACT_RELU, "rod_dw3x3_bwd_fused: bad act %d", bn_act);
+  ROD_CHECK_ARG(dtype == ROD_F32 || dtype == ROD_BF16, "rod_dw3x3_bwd_fused: bad dtype %d", dtype);
+  const int al = dtype == ROD_BF16 ? 7 : 15;
+  ROD_CHECK_ARG(((((uintptr_t)ye) | ((uintptr_t)dz) | ((uintptr_t)yd) | ((uintptr_t)dx)) & al) == 0,
+                "rod_dw3x3_bwd_fused: tensors must be %d-byte aligned", al + 1);
+  hipStream_t s = ROD_STREAM(stream);
+  const DwTile t = dw_fused_tile(N, H, W, C);
+  const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
+  const BnPro pv{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  const DwBwdBn bd{bn_mean, bn_rstd, bn_gamma, bn_beta, coef, bn_act};
+  const int pa = !pro_mean ? -1 : (pro_act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : DW_ACT_RT);
+  float* slab = (float*)workspace;
+  auto go = [&](auto tag) {
+    typedef decltype(tag) T;
+#define DWF2(PA, R)                                                                                                  \
+  hipLaunchKernelGGL((dw3x3_bwd_fused_kernel<T, PA, R>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,         \
+                     (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)
+    if (pa == ROD_ACT_RELU6) {
+      if (gparts) DWF2(ROD_ACT_RELU6, true); else DWF2(ROD_ACT_RELU6, false);
+    } else if (pa == DW_ACT_RT) {
+      if (gparts) DWF2(DW_ACT_RT, true); else DWF2(DW_ACT_RT, false);
+    } else {
+      DWF2(-1, false);
+    }
+#undef DWF2
+  };
+  if (dtype == ROD_BF16) go(bf16_t{}); else go(float{});
+  const int rc = check_launch("rod_dw3x3_bwd_fused");
+  if (rc) return rc;
+  slab_sum(slab, dw, rod_dw3x3_bwd_fused_parts(N, H, W, C), 9L * C, s);
+  return check_launch("rod_dw3x3_bwd_fused");
+}
+
+}  // extern "C"

@@ -66,4 +66,8 @@ def backward(loss):
     key = (loss.device, loss.dtype, tuple(loss.shape))
     if key not in _ONES:
         _ONES[key] = torch.ones_like(loss)
-    torch.autograd.backward(loss, grad_tensors=_ONES[key])
+    try:
+        torch.autograd.backward(loss, grad_tensors=_ONES[key])
+    finally:
+        from .ops import clear_bn_parts
+        clear_bn_parts()   # BatchNorm sums handed between nodes live for one backward

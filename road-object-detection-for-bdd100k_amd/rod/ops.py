@@ -293,6 +293,54 @@ def _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
     return dy
 
 
+# BatchNorm-backward sums handed from a consumer's backward to the producer's: the fused
+# stride-1 depthwise backward (rod_dw3x3_bwd_fused) computes, beside the gradient dx it returns
+# for its input act(BN(y)), that BatchNorm's backward sums over (dx, y).  The producer node
+# (_ConvBN) receives exactly that dx as its dz when the depthwise is the only consumer, and then
+# finalizes the sums instead of running rod_bn_bwd_reduce over (dz, y).  Entries hold their dx
+# (so its memory cannot be reused while listed) and are dropped when the backward ends.
+_BN_PARTS = {}
+
+
+def _put_bn_parts(dx, parts):
+    _BN_PARTS[dx.data_ptr()] = (dx, parts)
+
+
+def _take_bn_parts(dz):
+    e = _BN_PARTS.pop(dz.data_ptr(), None) if dz is not None else None
+    if e is None or e[0] is not dz and (e[0].shape != dz.shape or e[0].dtype != dz.dtype):
+        return None
+    return e[1]
+
+
+def clear_bn_parts():
+    _BN_PARTS.clear()
+
+
+def bn_bwd_coef_from_parts(parts, M, C, rstd, gamma, need_g, need_b):
+    """rod_bn_bwd_finalize of [nparts][2][C] backward sums (a consumer kernel's epilogue) ->
+    coef [3, C]; dgamma / dbeta to the parameters' slots.  Under SyncBatchNorm the parts are
+    all-gathered first (the parameter gradients stay this rank's own sums, as bn_bwd_reduce)."""
+    coef = torch.empty(3 * C, dtype=torch.float32, device=parts.device)
+    dg = grad_slot(gamma) if need_g else None
+    db = grad_slot(beta) if need_b else None
+    nparts = parts.shape[0]
+    if SYNC_BN is not None:
+        if dg is not None or db is not None:
+            _abi.call("rod_bn_bwd_finalize", parts, nparts, M, C, rstd, gamma, dg, db,
+                      torch.empty(3 * C, dtype=torch.float32, device=parts.device), stream())
+        gp = SYNC_BN.gather(parts)
+        _abi.call("rod_bn_bwd_finalize", gp, gp.shape[0], M * SYNC_BN.world, C, rstd, gamma, None, None, coef,
+                  stream())
+    else:
+        _abi.call("rod_bn_bwd_finalize", parts, nparts, M, C, rstd, gamma, dg, db, coef, stream())
+    if need_g:
+        _mark_written(gamma)
+    if need_b:
+        _mark_written(beta)
+    return coef
+
+
 def bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
     """rod_bn_bwd_reduce: the BatchNorm-backward sums of (dz, y) -> coef [3, C] for a consumer
     that applies dy itself; dgamma / dbeta go to the parameters' flat-buffer slots."""
@@ -725,8 +773,12 @@ class _ConvBN(torch.autograd.Function):
         M = N * H * W
         dz = dz.contiguous()
         need_dx = ctx.needs_input_grad[0]
+        parts = _take_bn_parts(dz)   # the BN sums a fused depthwise backward already formed
         if ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w) or _needs(b)):
-            coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            if parts is not None:
+                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, _needs(gamma), _needs(beta))
+            else:
+                coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             gw = grad_slot(w) if _needs(w) else torch.empty((Cout, Cin), dtype=torch.float32, device=y.device)
             gb = grad_slot(b) if _needs(b) else None
             wt1 = _prep(w, 1, x.dtype, Cout, Cin, 1) if need_dx else None
@@ -736,7 +788,11 @@ class _ConvBN(torch.autograd.Function):
             if _needs(b):
                 _mark_written(b)
         else:
-            dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            if parts is not None:
+                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, _needs(gamma), _needs(beta))
+                dy = _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, ctx.act, coef)
+            else:
+                dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             dx = _conv_bwd_from_dy(x, w, b, ctx.ks, dy, ctx.ipro, need_dx)
         return dx, None, None, None, None, None
 
@@ -775,6 +831,24 @@ class _DWBN(torch.autograd.Function):
         x, w, y, mean, rstd = ctx.saved_tensors
         gamma, beta = ctx.gb
         N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
+        if s == 1 and _needs(w) and ctx.needs_input_grad[0] and _dw_fused_ok(N, Ho, Wo, C, x.dtype):
+            # one pass: BN_d backward apply + backward-data + filter gradient (+ the input
+            # BatchNorm's backward sums, handed to the producer) — rod_dw3x3_bwd_fused, ABI 12
+            dz = dz.contiguous()
+            coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            dx = torch.empty_like(x)
+            gparts = None
+            if ctx.ipro is not None:
+                gparts = torch.empty((_abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C), 2, C), dtype=torch.float32,
+                                     device=x.device)
+            ws = workspace(_abi.query("rod_dw3x3_bwd_fused_workspace", N, H, W, C), x.device)
+            det = lambda t: None if t is None else t.detach()
+            _abi.call("rod_dw3x3_bwd_fused", x, *_pro_args(ctx.ipro), dz, y, mean, rstd, det(gamma), det(beta),
+                      ctx.act, coef, w, dx, grad_slot(w), gparts, ws, N, H, W, C, dtcode(x), stream())
+            _mark_written(w)
+            if gparts is not None:
+                _put_bn_parts(dx, gparts)
+            return dx, None, None, None, None
         if _needs(w) and N * Ho * Wo > 4096 and "dwbn" in _ENABLE:
             # opt-in (ROD_ENABLE=dwbn): the BatchNorm-backward apply runs inside the filter
             # gradient, which writes dy for the backward-data pass (rod_dw3x3_bwd_filter_bn).
@@ -808,6 +882,16 @@ class _DWBN(torch.autograd.Function):
             _abi.call("rod_dw3x3_bwd_data", dy, w, dx, *_gred_args(None), N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x),
                       stream())
         return dx, None, None, None, None
+
+
+def _dw_fused_ok(N, H, W, C, dtype):
+    """rod_dw3x3_bwd_fused for a stride-1 depthwise backward (ROD_DISABLE=dwfused: the unfused
+    chain); maps of <= DW_FUSED_MIN rows keep the one-launch small-tensor BatchNorm backward."""
+    return "dwfused" not in _DISABLE and C % 4 == 0 and N * H * W > DW_FUSED_MIN and \
+        dtype in (torch.float32, torch.bfloat16)
+
+
+DW_FUSED_MIN = int(os.environ.get("ROD_DW_FUSED_MIN", "4096"))
 
 
 def _in_pro(x):

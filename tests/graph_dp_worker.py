@@ -24,6 +24,9 @@ def main():
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     import torch.distributed as dist
+    # the step is captured with its RCCL collectives (Trainer.step_graphed): no event of an eager
+    # collective may be recycled into the capture while the watchdog still polls it
+    os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
     dist.init_process_group('nccl', device_id=dev)
     import config
     from rod.data import synthetic_batch

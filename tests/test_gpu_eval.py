@@ -104,6 +104,7 @@ def test_tfe_bboxes_sort_and_nms_batch_match_oracle(dev):
         s_ref, b_ref, kept = op.detected_bboxes_vec(probs, want_b, 0.0, 0.45, top_k, keep)
         np.testing.assert_array_equal(ns[c].cpu().numpy(), s_ref[:, 0])
         np.testing.assert_array_equal(nb[c].cpu().numpy(), b_ref[:, 0])
-        assert all(10 < len(kept[(b, 1)]) < keep for b in range(B))
+        print('kept per image (class %d):' % c, [len(kept[(b, 1)]) for b in range(B)])
+        assert all(10 < len(kept[(b, 1)]) <= keep for b in range(B))
     with pytest.raises(ValueError):
         tfe.bboxes_sort(torch.from_numpy(sc[1]).to(dev), torch.from_numpy(bx[1]).to(dev), top_k=N + 1)

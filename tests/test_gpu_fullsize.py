@@ -112,6 +112,7 @@ def _oracle_refine_step(tr, snap, img, corner, labels, n, B, dt, device='cpu'):
     P = {k: v.clone().to(device, dt).requires_grad_(True) for k, v in snap[0].items()}
     Bf = {k: v.clone().to(device, dt) for k, v in snap[1].items()}
     x = torch.from_numpy(f32(2.0 / 255.0) * img.cpu().numpy().astype(f32) - f32(1.0)).to(device, dt)
+    x = onet._st(x)          # the normalised input is stored too (bf16-storage emulation only)
     mov = {}
     refine = onet.forward(x, P, Bf, True, moving=mov)
     center = ot.corner_to_center(corner.cpu().numpy())
@@ -250,12 +251,15 @@ def test_refine_step_bf16_720p_b8_bench_config(dev):
     ref train.py:250-327 / net_tools.py:492-516), from bench.py's own initial state: Trainer
     seed C2_WEIGHT_SEED, lr 1e-3, rod.data.synthetic_batch(seed=C2_BATCH_SEED).  Its loss is
     bench.py's "loss_first_step".  Truth: the oracle step in float64 (shared with the fp32
-    test).  Baseline for what bf16 can reach: the same oracle step evaluated with every tensor
-    in bf16 (PyTorch-CPU, an independent bf16 implementation).  Bars:
+    test).  Baseline for what bf16 storage can reach: the same oracle step in fp32 arithmetic
+    with every tensor the product stores (conv / depthwise outputs, BatchNorm + activation
+    outputs, residual sums, and the gradients w.r.t. them) rounded to bf16 (oracle.net
+    set_storage; PyTorch-CPU, an independent implementation of bf16 storage).  Bars:
       loss             within max(1e-2, 4x the bf16 baseline's) relative of float64;
       head outputs /   angular error (1 - cos) vs float64 within max(0.02, 3x) the bf16
-      moving stats /   baseline's, on tensors the bf16 baseline represents at all (its
-      gradients        cos >= 0.95);
+      moving stats     baseline's, where that baseline keeps cos >= 0.95;
+      gradients        within max(0.02, 3x) where the baseline keeps cos >= 0.7, and the
+                       median over all tensors within 1.25x the baseline's;
       SGD + clip       bit-exact given the gradient (net_tools.py:645-651)."""
     import utils.net_tools as nt
     from nets.catch_net import factory
@@ -281,7 +285,11 @@ def test_refine_step_bf16_720p_b8_bench_config(dev):
     assert torch.equal(l_bench, loss.detach().reshape(l_bench.shape)), (l_bench.item(), loss.item())
     del tr2
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    Pb, movb, refb, lossb = _oracle_refine_step(tr, snap, img, corner, labels, n, B, bf16)
+    prev = onet.set_storage(bf16)            # fp32 arithmetic, every stored tensor rounded to bf16
+    try:
+        Pb, movb, refb, lossb = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float32)
+    finally:
+        onet.set_storage(prev)
     Pb = {k: v.grad.float() if v.grad is not None else None for k, v in Pb.items()}
     refb = [r.detach().float() for r in refb]
     movb = {k: v.float() for k, v in movb.items()}
@@ -289,10 +297,10 @@ def test_refine_step_bf16_720p_b8_bench_config(dev):
     g64, mov64, ref64, l64 = _c2_truth(tr, snap, img, corner, labels, n, B)
     P64 = {k: _Grad(v) for k, v in g64.items()}
     lrel, lrel_b = abs(loss.item() - l64) / abs(l64), abs(lossb - l64) / abs(l64)
-    print('bf16 720p b8 loss', loss.item(), 'fp64', l64, 'rel', lrel, '| bf16 oracle', lossb, 'rel', lrel_b)
+    print('bf16 720p b8 loss', loss.item(), 'fp64', l64, 'rel', lrel, '| bf16-storage oracle', lossb, 'rel', lrel_b)
     assert lrel <= max(1e-2, 4 * lrel_b)
     rep = [(l, _cosd(a, o), _cosd(b_, o)) for l, (a, b_, o) in enumerate(zip(outs, refb, ref64))]
-    print('per-level 1-cos vs fp64 (hip, bf16 oracle):', rep)
+    print('per-level 1-cos vs fp64 (hip, bf16-storage oracle):', rep)
     for l, e_h, e_b in rep:
         if e_b <= 0.05:
             assert e_h <= max(0.02, 3 * e_b), rep
@@ -301,21 +309,32 @@ def test_refine_step_bf16_720p_b8_bench_config(dev):
         if _cosd(movb[k], v) <= 0.05 and _cosd(tr.net.store.buffers[k], v) > max(0.02, 3 * _cosd(movb[k], v)):
             bad_mov.append((k, _cosd(tr.net.store.buffers[k], v), _cosd(movb[k], v)))
     assert not bad_mov, bad_mov[:5]
-    bad, checked, rows = [], 0, []
+    # gradients: the random-init network is chaotic in depth (a bf16-sized perturbation grows
+    # layer by layer: the forward outputs above decorrelate from float64 level by level, for the
+    # bf16-storage oracle as much as for this path), so the deep tensors' gradients of ANY bf16
+    # evaluation keep little correlation with the truth.  Bar: on every tensor where the
+    # bf16-storage oracle keeps cos >= 0.7, within max(0.02, 3x) its angular error; and over all
+    # tensors the median angular error within 1.25x the oracle's
+    bad, rows, allrows = [], [], []
     for name, p in tr.net.store.params.items():
         g64, gb = P64[name].grad, Pb[name]
-        if gb is None or float(g64.abs().max()) == 0 or _cosd(gb, g64) > 0.05:
-            continue   # not representable in bf16 at all (or zero by construction)
-        checked += 1
+        if gb is None or float(g64.abs().max()) == 0:
+            continue   # zero by construction
         e_h, e_b = _cosd(p._rod_grad, g64), _cosd(gb, g64)
+        allrows.append((e_h, e_b))
+        if e_b > 0.3:
+            continue
         rows.append((e_h, e_b, name))
         if e_h > max(0.02, 3 * e_b):
             bad.append((name, e_h, e_b))
     rows.sort(reverse=True)
     for r in rows[:8]:
-        print('grad 1-cos %.3e  bf16 oracle %.3e  %s' % r)
-    print('checked', checked, 'of', len(tr.net.store.params), 'parameter gradients')
-    assert checked > 100 and not bad, bad[:10]
+        print('grad 1-cos %.3e  bf16-storage oracle %.3e  %s' % r)
+    med_h = float(np.median([r[0] for r in allrows]))
+    med_b = float(np.median([r[1] for r in allrows]))
+    print('checked', len(rows), 'of', len(allrows), 'parameter gradients; median 1-cos hip', med_h, 'oracle', med_b)
+    assert len(rows) >= 20 and not bad, bad[:10]
+    assert med_h <= 1.25 * med_b + 1e-3, (med_h, med_b)
     flat_g = tr.net.store.flat_grad.detach().clone()
     tr.opt.step()
     ref = (p0.cpu().numpy() - np.float32(1e-3) * np.clip(flat_g.cpu().numpy(), -5, 5)).astype(np.float32)

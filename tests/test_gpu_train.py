@@ -409,15 +409,24 @@ def test_deferred_slab_sums_bit_identical(dev, train_range):
     H, W, B = 160, 288, 2
     rng = getattr(config.train_range, train_range)
     img, corner, labels, n = synthetic_batch(B, H, W, dev, seed=23)
-    runs = []
+    runs, queued = [], []
+    real_flush = ops.SLAB.flush
+
+    def counting_flush():   # how many sums were queued when the flush ran
+        queued.append(_abi.lib().rod_slab_pending())
+        real_flush()
     for off in (True, False):
         if off:
             ops._DISABLE.add('slabdefer')
+        ops.SLAB.flush = counting_flush
         try:
             tr = Trainer((H, W), B, dtype=torch.bfloat16, device=dev, seed=2, train_range=rng, fix_refine=False)
             ls = [tr.step(img, corner, labels, n)[0].clone() for _ in range(2)]
         finally:
             ops._DISABLE.discard('slabdefer')
+            ops.SLAB.flush = real_flush
+        if not off:
+            assert max(queued) > 50, queued   # the step's weight-gradient sums were batched
         torch.cuda.synchronize()
         assert _abi.lib().rod_slab_pending() == 0
         runs.append((tr.net.store.flat.clone(), {k: v.clone() for k, v in tr.net.store.buffers.items()}, ls))
