@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 12
+#define ROD_ABI_VERSION 13
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -118,25 +118,28 @@ int rod_dw3x3_bwd_filter(const void* x, const float* pro_mean, const float* pro_
                          const float* pro_gamma, const float* pro_beta, int pro_act, const void* dy,
                          float* dw, void* workspace, int N, int H, int W, int C, int stride, int pad_t,
                          int pad_l, int Ho, int Wo, int dtype, void* stream);
-/* Fused stride-1 depthwise backward (ABI 12): for x = act_e(BN_e(ye)) (the input's
- * BatchNorm-prologue form, pro_*) -> yd = DepthwiseConv2dNative(x, w, stride 1, SAME) ->
- * act_d(BN_d(yd)) (bn_*, with coef [3][C] from rod_bn_bwd_reduce over (dz, yd)), ONE pass over
- * ye, dz, yd (conv_blocks.py:238-247 backward, FusedBatchNormGrad under mobilenet.py:417-420):
+/* Fused depthwise backward (ABI 12 stride 1; ABI 13 adds stride 2): for x = act_e(BN_e(ye))
+ * (the input's BatchNorm-prologue form, pro_*) -> yd = DepthwiseConv2dNative(x, w, stride,
+ * padding pad_t / pad_l) -> act_d(BN_d(yd)) (bn_*, with coef [3][C] from rod_bn_bwd_reduce over
+ * (dz, yd)), ONE pass over ye, dz, yd (conv_blocks.py:238-247 backward, FusedBatchNormGrad
+ * under mobilenet.py:417-420):
  *   dx = DepthwiseConv2dNativeBackpropInput(dy, w)  (T, [N,H,W,C]; bit-identical to
  *        rod_bn_bwd_apply -> rod_dw3x3_bwd_data),
  *   dw = DepthwiseConv2dNativeBackpropFilter(x, dy) (fp32 [3][3][C]),
- * with dy = rod_bn_bwd_apply(dz, yd, ...) formed in registers and never stored; gparts
- * (nullable; needs pro_*) receives BN_e's backward sums over (dx, ye) as
+ * with dy = rod_bn_bwd_apply(dz, yd, ...) ([N,Ho,Wo,C]) formed in registers and never stored;
+ * gparts (nullable; needs pro_*) receives BN_e's backward sums over (dx, ye) as
  * [rod_dw3x3_bwd_fused_parts()][2][C] for rod_bn_bwd_finalize (the producer's
- * rod_bn_bwd_reduce pass disappears).  C % 4 == 0; bf16 tensors 8-byte, fp32 16-byte aligned;
- * workspace = rod_dw3x3_bwd_fused_workspace bytes. */
-int rod_dw3x3_bwd_fused_parts(int N, int H, int W, int C);
-size_t rod_dw3x3_bwd_fused_workspace(int N, int H, int W, int C);
+ * rod_bn_bwd_reduce pass disappears).  stride 1: pad 1, Ho = H, Wo = W; stride 2: pad 0 | 1.
+ * C % 4 == 0; bf16 tensors 8-byte, fp32 16-byte aligned; workspace =
+ * rod_dw3x3_bwd_fused_workspace bytes (both 0 for an unsupported geometry). */
+int rod_dw3x3_bwd_fused_parts(int N, int H, int W, int C, int stride, int pad_t, int pad_l);
+size_t rod_dw3x3_bwd_fused_workspace(int N, int H, int W, int C, int stride, int pad_t, int pad_l);
 int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
                         const float* pro_beta, int pro_act, const void* dz, const void* yd, const float* bn_mean,
                         const float* bn_rstd, const float* bn_gamma, const float* bn_beta, int bn_act,
                         const float* coef, const float* w, void* dx, float* dw, float* gparts, void* workspace, int N,
-                        int H, int W, int C, int dtype, void* stream);
+                        int H, int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype,
+                        void* stream);
 
 /* The BatchNorm backward of the depthwise's output fused into its filter gradient (ABI 10):
  * dy = FusedBatchNormGrad-apply of (dz, y) with the coefficients coef[3][C] of

@@ -1709,7 +1709,7 @@ struct DwBwdBn {
   int act;
 };
 
-template <typename T, int PACT, bool RED>
+template <typename T, int PACT, bool RED, int D = 3>
 __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
                                                               const T* __restrict__ yd, const float* __restrict__ w,
                                                               T* __restrict__ dx, float* __restrict__ slab,
@@ -1769,9 +1769,9 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
   const T* ydn = yd + nb;
   T* dxn = dx + nb;
 
-  // prefetch ring: step q loads x row ho0-2+q and (dz, yd) of row ho0-1+q
-  PK rx[3], rz[3], ry[3];
-  bool okx[3], okd[3];
+  // prefetch ring of D steps: step q loads x row ho0-2+q and (dz, yd) of row ho0-1+q
+  PK rx[D], rz[D], ry[D];
+  bool okx[D], okd[D];
   auto issue = [&](int k, int q) {
     const int rho = ho0 - 2 + q;
     okx[k] = cok && rho >= xlo && rho <= xhi;
@@ -1783,9 +1783,8 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
     }
   };
   const int nst = ho1 - ho0 + 3;
-  issue(0, 0);
-  issue(1, 1);
-  issue(2, 2);
+#pragma unroll
+  for (int k = 0; k < D; ++k) issue(k, k);
   float acc[3][V], fa[9][V], q1[V], q2[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
@@ -1794,12 +1793,16 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
 #pragma unroll
     for (int k = 0; k < 9; ++k) fa[k][v] = 0.f;
   }
-  for (int q0 = 0; q0 < nst; q0 += 3) {
+  // D is a multiple of 3: the ring slot (q mod D) and the dx accumulator slot (q mod 3) are
+  // both compile-time under the unroll
+  static_assert(D % 3 == 0, "ring depth must be a multiple of 3");
+  for (int q0 = 0; q0 < nst; q0 += D) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < D; ++k) {
       const int q = q0 + k;
       const int rho = ho0 - 2 + q;
       const int buf = q & 1;
+      const int k3 = k % 3;
       // x row rho: the forward's input (prologue, rounded to T), 0 outside the rows needed
       float xv[V], yraw[V];
       {
@@ -1828,7 +1831,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
         px.set(v, xv[v]);
         pd.set(v, dv[v]);
       }
-      issue(k, q + 3);
+      issue(k, q + D);
       xs[buf * 256 + tid] = px;
       dsl[buf * 256 + tid] = pd;
       __syncthreads();
@@ -1838,7 +1841,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
         // backward-data: dy row rho+1 is tap row 0 of dx row rho, 1 of rho+1, 2 of rho+2
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-          const int sl = (k + i) % 3;
+          const int sl = (k3 + i) % 3;
 #pragma unroll
           for (int v = 0; v < V; ++v) {
             float a = acc[sl][v];
@@ -1870,7 +1873,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
         if (rho >= ho0 && rho < ho1) {
           PK o;
 #pragma unroll
-          for (int v = 0; v < V; ++v) o.set(v, acc[k][v]);
+          for (int v = 0; v < V; ++v) o.set(v, acc[k3][v]);
           o.store_out(dxn + ((long)rho * W + col) * C);
           if constexpr (RED) {
 #pragma unroll
@@ -1883,7 +1886,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
           }
         }
 #pragma unroll
-        for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
+        for (int v = 0; v < V; ++v) acc[k3][v] = 0.f;
       }
     }
   }
@@ -1913,26 +1916,267 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
   }
 }
 
-static DwTile dw_fused_tile(int N, int H, int W, int C) { return dw_tile(N, H, W, C, 1, 4); }
+// Stride-2 form.  Thread (p, cvb) owns output column b = wo0 + p - 1 (one halo column each
+// side) and the dx / x column pair (2b - pl, 2b - pl + 1); step q handles dy row a = a0 - 1 + q
+// and the x / dx rows 2a - pt, 2a + 1 - pt.  dx's 2x2 block (rows 2a-pt, 2a+1-pt x its column
+// pair) takes dy[a][b], dy[a][b-1] (left neighbour, LDS) and the previous step's dy[a-1][b],
+// dy[a-1][b-1], in the order of dw3x3_bwd_data_s2_kernel (bit-identical dx); the filter pairs
+// dy[a] with x rows 2a-pt (tap row 0), 2a+1-pt (1) and dy[a-1] with 2a-pt (2), the third tap
+// column coming from the right neighbour's first column (LDS).
+template <typename T, int PACT, bool RED, int D = 3>
+__global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
+                                                                 const T* __restrict__ yd, const float* __restrict__ w,
+                                                                 T* __restrict__ dx, float* __restrict__ slab,
+                                                                 float* __restrict__ gparts, int H, int W, int C,
+                                                                 int pt, int pl, int Ho, int Wo, DwTile tl, BnPro pro,
+                                                                 DwBwdBn bd) {
+  constexpr int V = 4;
+  typedef PackV<T, V> PK;
+  constexpr int XS = 3 * 2 * 256 * (int)sizeof(PK);  // dy, x row 0, x row 1 slots, double buffered
+  constexpr int SS = 256 * V * 4;
+  __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
+  PK* dsl = (PK*)smem;         // [2][256]
+  PK* x0s = dsl + 2 * 256;     // [2][256]
+  PK* x1s = x0s + 2 * 256;     // [2][256]
+  const int tid = threadIdx.x;
+  const int CVb = tl.CVb, P = tl.P;
+  const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
+  int bx, strip, n;
+  xcd_block(bx, strip, n);
+  const int cg = bx % tl.cgroups, ct = bx / tl.cgroups;
+  const int c = (cg * CVb + cvb) * V;
+  const int b = ct * tl.TWo + p - 1;
+  const int ci0 = 2 * b - pl;
+  // the tiled map is (A, B): every a / b with a dx row / column (dy rows >= Ho read as zero)
+  const int A = ((H - 1 + pt) >> 1) + 1, B = ((W - 1 + pl) >> 1) + 1;
+  const bool comp = p >= 1 && p <= P - 2 && b < B;
+  const bool cokd = p < P && b >= 0 && b < Wo;
+  const bool cok0 = p < P && ci0 >= 0 && ci0 < W;
+  const bool cok1 = p < P && ci0 + 1 >= 0 && ci0 + 1 < W;
+  const int a0 = strip * tl.RB;
+  const int a1 = a0 + tl.RB < A ? a0 + tl.RB : A;
+
+  float wr[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
+  DwIn<T, V, PACT> in;
+  in.init(pro, c);
+  float dmu[V], drs[V], dsc[V], dsh[V], da[V], dmg[V], dmx[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    dmu[v] = bd.mean[c + v];
+    drs[v] = bd.rstd[c + v];
+    bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c + v, dsc[v], dsh[v]);
+    da[v] = bd.coef[c + v];
+    dmg[v] = bd.coef[C + c + v];
+    dmx[v] = bd.coef[2 * C + c + v];
+  }
+  constexpr int RV = RED ? V : 1;
+  float enb[RV], ers[RV], sg[RV], sgx[RV];  // xhat_e = fma(y_e, rstd, -mean * rstd)
+  if constexpr (RED) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      ers[v] = pro.rstd[c + v];
+      enb[v] = -pro.mean[c + v] * ers[v];
+      sg[v] = sgx[v] = 0.f;
+    }
+  }
+  const T* yen = ye + (long)n * H * W * C + c;
+  T* dxn = dx + (long)n * H * W * C + c;
+  const long ob = (long)n * Ho * Wo * C + c;
+  const T* dzn = dz + ob;
+  const T* ydn = yd + ob;
+
+  // ring slot: dy (dz, yd) of row a, x (ye) at rows 2a-pt, 2a+1-pt x columns ci0, ci0+1
+  PK rz[D], ry[D], rx[D][4];
+  bool okd[D], okx[D][4];
+  const int dlo = a0 - 1 > 0 ? a0 - 1 : 0;
+  const int dhi = a1 - 1 < Ho - 1 ? a1 - 1 : Ho - 1;
+  auto issue = [&](int k, int q) {
+    const int a = a0 - 1 + q;
+    okd[k] = cokd && a >= dlo && a <= dhi;
+    if (okd[k]) {
+      rz[k].load(dzn + ((long)a * Wo + b) * C);
+      ry[k].load(ydn + ((long)a * Wo + b) * C);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = 2 * a - pt + (i >> 1);
+      const bool rowok = a >= a0 && (i < 2 ? a <= a1 : a < a1) && h >= 0 && h < H;
+      okx[k][i] = rowok && ((i & 1) ? cok1 : cok0);
+      if (okx[k][i]) rx[k][i].load(yen + ((long)h * W + ci0 + (i & 1)) * C);
+    }
+  };
+  const int nst = a1 - a0 + 2;
+#pragma unroll
+  for (int k = 0; k < D; ++k) issue(k, k);
+  float fa[9][V], pv[V], pL[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    pv[v] = pL[v] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) fa[k][v] = 0.f;
+  }
+  for (int q0 = 0; q0 < nst; q0 += D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int q = q0 + k;
+      const int a = a0 - 1 + q;
+      const int buf = q & 1;
+      float dv[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float yv = ry[k].get(v);
+        const float d = yv - dmu[v];
+        const float z = fmaf(yv, dsc[v], dsh[v]);
+        const float g = rz[k].get(v) * act_grad(z, bd.act);
+        const float o = da[v] * (g - dmg[v] - (d * drs[v]) * dmx[v]);
+        dv[v] = okd[k] ? to_f32(from_f32<T>(o)) : 0.f;
+      }
+      float xv[4][V], yr[4][V];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        in.cvt(rx[k][i], okx[k][i], xv[i]);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          if constexpr (PACT < 0) xv[i][v] = okx[k][i] ? xv[i][v] : 0.f;
+          yr[i][v] = rx[k][i].get(v);
+        }
+      }
+      PK pd, p0, p1;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        pd.set(v, dv[v]);
+        p0.set(v, xv[0][v]);
+        p1.set(v, xv[2][v]);
+      }
+      issue(k, q + D);
+      dsl[buf * 256 + tid] = pd;
+      x0s[buf * 256 + tid] = p0;
+      x1s[buf * 256 + tid] = p1;
+      __syncthreads();
+      if (comp) {
+        const PK dlp = dsl[buf * 256 + tid - CVb];
+        const PK r0 = x0s[buf * 256 + tid + CVb], r1 = x1s[buf * 256 + tid + CVb];
+        float dL[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) dL[v] = dlp.get(v);
+        if (a >= a0 && a < a1) {
+          // dx block: taps as dw3x3_bwd_data_s2_kernel (c1 = dy[a][b], c0 = dy[a][b-1], p1, p0 = row a-1)
+          float o[4][V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            const float c1 = dv[v], c0 = dL[v], p1v = pv[v], p0v = pL[v];
+            o[0][v] = fmaf(p0v, wr[8][v], fmaf(p1v, wr[6][v], fmaf(c0, wr[2][v], c1 * wr[0][v])));
+            o[1][v] = fmaf(p1v, wr[7][v], c1 * wr[1][v]);
+            o[2][v] = fmaf(c0, wr[5][v], c1 * wr[3][v]);
+            o[3][v] = c1 * wr[4][v];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int h = 2 * a - pt + (i >> 1), ww = ci0 + (i & 1);
+            if (h < 0 || h >= H || ww < 0 || ww >= W) continue;
+            PK pk;
+#pragma unroll
+            for (int v = 0; v < V; ++v) pk.set(v, o[i][v]);
+            pk.store_out(dxn + ((long)h * W + ww) * C);
+            if constexpr (RED) {
+#pragma unroll
+              for (int v = 0; v < V; ++v) {
+                const float z = fmaf(yr[i][v], in.sc[v], in.sh[v]);
+                const float g = pk.get(v) * act_grad(z, pro.act);
+                sg[v] += g;
+                sgx[v] = fmaf(g, fmaf(yr[i][v], ers[v], enb[v]), sgx[v]);
+              }
+            }
+          }
+        }
+        // filter: dy[a] with x rows 2a-pt (tap row 0) and 2a+1-pt (1), dy[a-1] with 2a-pt (2)
+        const bool own = a >= a0 && a < a1, ownp = a - 1 >= a0 && a - 1 < a1;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float f0 = own ? dv[v] : 0.f, f2 = ownp ? pv[v] : 0.f;
+          const float t02 = r0.get(v), t12 = r1.get(v);
+          fa[0][v] = fmaf(f0, xv[0][v], fa[0][v]);
+          fa[1][v] = fmaf(f0, xv[1][v], fa[1][v]);
+          fa[2][v] = fmaf(f0, t02, fa[2][v]);
+          fa[3][v] = fmaf(f0, xv[2][v], fa[3][v]);
+          fa[4][v] = fmaf(f0, xv[3][v], fa[4][v]);
+          fa[5][v] = fmaf(f0, t12, fa[5][v]);
+          fa[6][v] = fmaf(f2, xv[0][v], fa[6][v]);
+          fa[7][v] = fmaf(f2, xv[1][v], fa[7][v]);
+          fa[8][v] = fmaf(f2, t02, fa[8][v]);
+          pv[v] = dv[v];
+          pL[v] = dL[v];
+        }
+      }
+    }
+  }
+
+  __syncthreads();
+  float* red = (float*)smem;
+  const int Cc = CVb * V;
+  const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+  auto colsum = [&](const float (&acc)[V], float* dst) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) red[tid * V + v] = comp ? acc[v] : 0.f;
+    __syncthreads();
+    for (int e = tid; e < Cc; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      float s = 0.f;
+      for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
+      dst[cg * Cc + e] = s;
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int k = 0; k < 9; ++k) colsum(fa[k], slab + (part * 9 + k) * C);
+  if constexpr (RED) {
+    colsum(sg, gparts + part * 2 * C);
+    colsum(sgx, gparts + part * 2 * C + C);
+  }
+}
+
+// Both strides tile a map with one halo column each side (the S=1 plan geometry): stride 1
+// the output (= input) map, stride 2 the (A, B) map of dy positions that own a dx row / column.
+static bool dw_fused_geom(int N, int H, int W, int C, int S, int pt, int pl, int& A, int& B) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4) return false;
+  if (S == 1) {
+    if (pt != 1 || pl != 1) return false;
+    A = H, B = W;
+    return true;
+  }
+  if (S != 2 || pt < 0 || pt > 1 || pl < 0 || pl > 1) return false;
+  A = ((H - 1 + pt) >> 1) + 1, B = ((W - 1 + pl) >> 1) + 1;
+  return true;
+}
 
 extern "C" {
 
-int rod_dw3x3_bwd_fused_parts(int N, int H, int W, int C) {
-  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4) return 0;
-  const DwTile t = dw_fused_tile(N, H, W, C);
+int rod_dw3x3_bwd_fused_parts(int N, int H, int W, int C, int stride, int pad_t, int pad_l) {
+  int A, B;
+  if (!dw_fused_geom(N, H, W, C, stride, pad_t, pad_l, A, B)) return 0;
+  const DwTile t = dw_tile(N, A, B, C, 1, 4);
   return (int)((long)N * t.strips * t.coltiles);
 }
 
-size_t rod_dw3x3_bwd_fused_workspace(int N, int H, int W, int C) {
-  return (size_t)rod_dw3x3_bwd_fused_parts(N, H, W, C) * 9 * C * sizeof(float);
+size_t rod_dw3x3_bwd_fused_workspace(int N, int H, int W, int C, int stride, int pad_t, int pad_l) {
+  return (size_t)rod_dw3x3_bwd_fused_parts(N, H, W, C, stride, pad_t, pad_l) * 9 * C * sizeof(float);
 }
 
 int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
                         const float* pro_beta, int pro_act, const void* dz, const void* yd, const float* bn_mean,
                         const float* bn_rstd, const float* bn_gamma, const float* bn_beta, int bn_act,
                         const float* coef, const float* w, void* dx, float* dw, float* gparts, void* workspace, int N,
-                        int H, int W, int C, int dtype, void* stream) {
-  ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0, "rod_dw3x3_bwd_fused: bad shape (C %% 4 != 0?)");
+                        int H, int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype,
+                        void* stream) {
+  int A = 0, B = 0;
+  ROD_CHECK_ARG(dw_fused_geom(N, H, W, C, stride, pad_t, pad_l, A, B),
+                "rod_dw3x3_bwd_fused: bad shape / stride / padding (C %% 4 != 0? stride 1 needs pad 1, stride 2 pad 0|1)");
+  ROD_CHECK_ARG(Ho > 0 && Wo > 0 && (stride == 1 ? Ho == H && Wo == W : Ho <= A + 1 && Wo <= B + 1),
+                "rod_dw3x3_bwd_fused: output map %dx%d does not match the input", Ho, Wo);
   ROD_CHECK_ARG(ye && dz && yd && bn_mean && bn_rstd && coef && w && dx && dw && workspace,
                 "rod_dw3x3_bwd_fused: NULL tensor argument");
   ROD_CHECK_ARG(!pro_mean || pro_rstd, "rod_dw3x3_bwd_fused: BatchNorm prologue needs mean and rstd");
@@ -1943,7 +2187,7 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
   ROD_CHECK_ARG(((((uintptr_t)ye) | ((uintptr_t)dz) | ((uintptr_t)yd) | ((uintptr_t)dx)) & al) == 0,
                 "rod_dw3x3_bwd_fused: tensors must be %d-byte aligned", al + 1);
   hipStream_t s = ROD_STREAM(stream);
-  const DwTile t = dw_fused_tile(N, H, W, C);
+  const DwTile t = dw_tile(N, A, B, C, 1, 4);
   const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
   const BnPro pv{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
   const DwBwdBn bd{bn_mean, bn_rstd, bn_gamma, bn_beta, coef, bn_act};
@@ -1951,9 +2195,24 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
   float* slab = (float*)workspace;
   auto go = [&](auto tag) {
     typedef decltype(tag) T;
-#define DWF2(PA, R)                                                                                                  \
-  hipLaunchKernelGGL((dw3x3_bwd_fused_kernel<T, PA, R>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,         \
+    // stride-1 prefetch ring depth (steps in flight): 3; ROD_DWF_RING=6 (measurement switch)
+    // measured 3.27 ms (3) vs 3.34 ms (6) over the step's bf16 shapes (tools/dwfused_bench.py)
+    static const int ring_env = getenv("ROD_DWF_RING") ? atoi(getenv("ROD_DWF_RING")) : 0;
+    const int ring = ring_env == 6 ? 6 : 3;
+#define DWF1(PA, R, D)                                                                                               \
+  hipLaunchKernelGGL((dw3x3_bwd_fused_kernel<T, PA, R, D>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,      \
                      (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)
+    // stride 2 ring: 3 steps (bf16), 2 (fp32: 16-byte slots; 3 spills to scratch)
+    constexpr int D2 = sizeof(T) == 2 ? 3 : 2;
+#define DWS2(PA, R)                                                                                                  \
+  hipLaunchKernelGGL((dw3x3_bwd_fused_s2_kernel<T, PA, R, D2>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,   \
+                     (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, pad_t, pad_l, Ho, Wo, t, pv, bd)
+#define DWF2(PA, R)                                                                                                  \
+  do {                                                                                                              \
+    if (stride == 2) DWS2(PA, R);                                                                                   \
+    else if (ring == 3) DWF1(PA, R, 3);                                                                             \
+    else DWF1(PA, R, 6);                                                                                            \
+  } while (0)
     if (pa == ROD_ACT_RELU6) {
       if (gparts) DWF2(ROD_ACT_RELU6, true); else DWF2(ROD_ACT_RELU6, false);
     } else if (pa == DW_ACT_RT) {
@@ -1962,11 +2221,13 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
       DWF2(-1, false);
     }
 #undef DWF2
+#undef DWS2
+#undef DWF1
   };
   if (dtype == ROD_BF16) go(bf16_t{}); else go(float{});
   const int rc = check_launch("rod_dw3x3_bwd_fused");
   if (rc) return rc;
-  slab_sum(slab, dw, rod_dw3x3_bwd_fused_parts(N, H, W, C), 9L * C, s);
+  slab_sum(slab, dw, (int)((long)N * t.strips * t.coltiles), 9L * C, s);
   return check_launch("rod_dw3x3_bwd_fused");
 }
 

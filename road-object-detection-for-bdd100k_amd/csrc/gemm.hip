@@ -1561,6 +1561,17 @@ static void wgrad_va_vd(bool va, bool vd, const WgradPlan& p, const void* x, con
   else wgrad_launch<T, KS, false, false, PRO>(p, x, dy, part, M, H, W, Cin, Cout, ldx, lddy, pro, s);
 }
 
+// workspace layout: [weight-gradient partials][bias column-sum partials].  Separate regions:
+// while rod_slab_defer is on, the weight partials are summed only at rod_slab_flush, after the
+// bias partials have been written.
+static long wgrad_part_floats(int N, int H, int W, int Cin, int Cout, int ksize) {
+  const long M = (long)N * H * W;
+  WgradPlan p = wgrad_plan(M, Cin, Cout, ksize);
+  const long K = (long)ksize * ksize * Cin;
+  if (ksize == 3 && Cin == 3 && Cout == 32) p.splits = std::max(p.splits, stem_wgrad_plan(N, H, W).nblk);
+  return ((long)p.splits * Cout * K + 3) / 4 * 4;
+}
+
 template <typename T>
 static void wgrad_typed(const void* x, const BnPro* pro, const void* dy, float* dw, float* db, float* part, int N,
                         int H, int W, int Cin, int Cout, int ksize, int ldx, int lddy, hipStream_t s) {
@@ -1599,9 +1610,10 @@ static void wgrad_typed(const void* x, const BnPro* pro, const void* dy, float* 
   if (db) {
     long cchunk = std::max<long>(64, cdivl(M, 512));
     int nb = (int)cdivl(M, cchunk);
+    float* partb = part + wgrad_part_floats(N, H, W, Cin, Cout, ksize);
     hipLaunchKernelGGL(colsum_kernel<T>, dim3(nb, cdiv(Cout, 256)), dim3(256), 0, s, (const T*)dy, M, Cout, lddy,
-                       cchunk, part);
-    slab_sum(part, db, nb, (long)Cout, s);
+                       cchunk, partb);
+    slab_sum(partb, db, nb, (long)Cout, s);
   }
 }
 
@@ -1658,13 +1670,9 @@ int rod_conv_weight_prep_batch(const void* table, int n, long total, int dtype, 
 
 size_t rod_conv_wgrad_workspace(int N, int H, int W, int Cin, int Cout, int ksize) {
   const long M = (long)N * H * W;
-  WgradPlan p = wgrad_plan(M, Cin, Cout, ksize);
-  const long K = (long)ksize * ksize * Cin;
-  if (ksize == 3 && Cin == 3 && Cout == 32) p.splits = std::max(p.splits, stem_wgrad_plan(N, H, W).nblk);
-  size_t part = (size_t)p.splits * Cout * K * sizeof(float);
   long cchunk = std::max<long>(64, cdivl(M, 512));
   size_t cs = (size_t)cdivl(M, cchunk) * Cout * sizeof(float);
-  return std::max(part, cs);
+  return (size_t)wgrad_part_floats(N, H, W, Cin, Cout, ksize) * sizeof(float) + cs;
 }
 
 int rod_conv_wgrad(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,

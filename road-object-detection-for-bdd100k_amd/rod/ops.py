@@ -294,7 +294,7 @@ def _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
 
 
 # BatchNorm-backward sums handed from a consumer's backward to the producer's: the fused
-# stride-1 depthwise backward (rod_dw3x3_bwd_fused) computes, beside the gradient dx it returns
+# depthwise backward (rod_dw3x3_bwd_fused) computes, beside the gradient dx it returns
 # for its input act(BN(y)), that BatchNorm's backward sums over (dx, y).  The producer node
 # (_ConvBN) receives exactly that dx as its dz when the depthwise is the only consumer, and then
 # finalizes the sums instead of running rod_bn_bwd_reduce over (dz, y).  Entries hold their dx
@@ -317,7 +317,7 @@ def clear_bn_parts():
     _BN_PARTS.clear()
 
 
-def bn_bwd_coef_from_parts(parts, M, C, rstd, gamma, need_g, need_b):
+def bn_bwd_coef_from_parts(parts, M, C, rstd, gamma, beta, need_g, need_b):
     """rod_bn_bwd_finalize of [nparts][2][C] backward sums (a consumer kernel's epilogue) ->
     coef [3, C]; dgamma / dbeta to the parameters' slots.  Under SyncBatchNorm the parts are
     all-gathered first (the parameter gradients stay this rank's own sums, as bn_bwd_reduce)."""
@@ -776,7 +776,7 @@ class _ConvBN(torch.autograd.Function):
         parts = _take_bn_parts(dz)   # the BN sums a fused depthwise backward already formed
         if ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w) or _needs(b)):
             if parts is not None:
-                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, _needs(gamma), _needs(beta))
+                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))
             else:
                 coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             gw = grad_slot(w) if _needs(w) else torch.empty((Cout, Cin), dtype=torch.float32, device=y.device)
@@ -789,7 +789,7 @@ class _ConvBN(torch.autograd.Function):
                 _mark_written(b)
         else:
             if parts is not None:
-                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, _needs(gamma), _needs(beta))
+                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))
                 dy = _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, ctx.act, coef)
             else:
                 dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
@@ -831,20 +831,22 @@ class _DWBN(torch.autograd.Function):
         x, w, y, mean, rstd = ctx.saved_tensors
         gamma, beta = ctx.gb
         N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
-        if s == 1 and _needs(w) and ctx.needs_input_grad[0] and _dw_fused_ok(N, Ho, Wo, C, x.dtype):
+        if _needs(w) and ctx.needs_input_grad[0] and _dw_fused_ok(N, Ho, Wo, C, x.dtype, s):
             # one pass: BN_d backward apply + backward-data + filter gradient (+ the input
-            # BatchNorm's backward sums, handed to the producer) — rod_dw3x3_bwd_fused, ABI 12
+            # BatchNorm's backward sums, handed to the producer) — rod_dw3x3_bwd_fused
+            # (ABI 12 stride 1, ABI 13 stride 2)
             dz = dz.contiguous()
             coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             dx = torch.empty_like(x)
             gparts = None
             if ctx.ipro is not None:
-                gparts = torch.empty((_abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C), 2, C), dtype=torch.float32,
-                                     device=x.device)
-            ws = workspace(_abi.query("rod_dw3x3_bwd_fused_workspace", N, H, W, C), x.device)
+                gparts = torch.empty((_abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C, s, pt, pl), 2, C),
+                                     dtype=torch.float32, device=x.device)
+            ws = workspace(_abi.query("rod_dw3x3_bwd_fused_workspace", N, H, W, C, s, pt, pl), x.device)
             det = lambda t: None if t is None else t.detach()
             _abi.call("rod_dw3x3_bwd_fused", x, *_pro_args(ctx.ipro), dz, y, mean, rstd, det(gamma), det(beta),
-                      ctx.act, coef, w, dx, grad_slot(w), gparts, ws, N, H, W, C, dtcode(x), stream())
+                      ctx.act, coef, w, dx, grad_slot(w), gparts, ws, N, H, W, C, s, pt, pl, Ho, Wo, dtcode(x),
+                      stream())
             _mark_written(w)
             if gparts is not None:
                 _put_bn_parts(dx, gparts)
@@ -884,10 +886,13 @@ class _DWBN(torch.autograd.Function):
         return dx, None, None, None, None
 
 
-def _dw_fused_ok(N, H, W, C, dtype):
-    """rod_dw3x3_bwd_fused for a stride-1 depthwise backward (ROD_DISABLE=dwfused: the unfused
-    chain); maps of <= DW_FUSED_MIN rows keep the one-launch small-tensor BatchNorm backward."""
-    return "dwfused" not in _DISABLE and C % 4 == 0 and N * H * W > DW_FUSED_MIN and \
+def _dw_fused_ok(N, Ho, Wo, C, dtype, stride=1):
+    """rod_dw3x3_bwd_fused for a depthwise backward (ROD_DISABLE=dwfused: the unfused chain;
+    ROD_DISABLE=dwfused2: stride 1 only); output maps of <= DW_FUSED_MIN rows keep the
+    one-launch small-tensor BatchNorm backward."""
+    if stride == 2 and "dwfused2" in _DISABLE:
+        return False
+    return "dwfused" not in _DISABLE and C % 4 == 0 and N * Ho * Wo > DW_FUSED_MIN and \
         dtype in (torch.float32, torch.bfloat16)
 
 

@@ -13,6 +13,10 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
                          BatchNorm backward as a whole counts 3 passes (read dz, read y, write
                          dy) whichever kernels do them; design_bytes() gives the 5 passes the
                          two-kernel design moves (reduce 2 + apply 3)
+  dw3x3_bwd_fused      : es*(x + dx) + 2*9*C*4, 36*N*Ho*Wo*C + 8*N*Ho*Wo*C (+ 6*N*H*W*C with the
+                         input BatchNorm's sums).  Its reads of dz and y are the BatchNorm
+                         backward's SECOND pass (as for bn_bwd_apply): design traffic; dy is
+                         never stored
   pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product
   match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
   ir_block_fwd (fused) : es*(N*H*W*Cin + N*Ho*Wo*Cout) + weights, 2*N*H*W*Cin*inner +
@@ -48,6 +52,11 @@ def cost(name, a):
         N, H, W, C, Ho, Wo, dt = a[9], a[10], a[11], a[12], a[16], a[17], a[18]
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
+    if name == "rod_dw3x3_bwd_fused":
+        N, H, W, C, Ho, Wo, dt = a[19], a[20], a[21], a[22], a[26], a[27], a[28]
+        es = _ES[dt]
+        red = 6 * N * H * W * C if a[17] is not None else 0
+        return es * 2 * N * H * W * C + 72 * C, 44 * N * Ho * Wo * C + red
     if name == "rod_conv_fwd":
         N, H, W, Cin, Cout, ks, dt = a[18], a[19], a[20], a[21], a[22], a[23], a[26]
         es = _ES[dt]
@@ -161,6 +170,9 @@ def design_bytes(name, a):
     if name == "rod_bn_bwd_apply":
         M, C, dt = a[8], a[9], a[11]
         return _ES[dt] * M * C * 3
+    if name == "rod_dw3x3_bwd_fused":     # + the re-read of dz and y (BatchNorm backward pass 2)
+        N, C, Ho, Wo, dt = a[19], a[22], a[26], a[27], a[28]
+        return cost(name, a)[0] + _ES[dt] * 2 * N * Ho * Wo * C
     return cost(name, a)[0]
 
 
@@ -177,6 +189,7 @@ ENTRY_KERNELS = {
     "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),
+    "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused",), ("dw3x3_bwd_fused",)),
     "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
     "rod_conv_fwd": (("conv_fwd_kernel", "stem_conv_fwd_kernel"), ("conv_fwd_kernel", "stem_conv_fwd_kernel")),
     "rod_bn_finalize": (("bn_parts_merge_kernel",), ("bn_parts_merge_kernel",)),

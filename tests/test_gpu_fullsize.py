@@ -388,20 +388,27 @@ def test_predict_b32_nms_bit_exact(dev):
 
 
 def test_predict_1080p_fused_blocks_match_oracle(dev):
-    """C5 (BASELINE configs[4]): predict.py's inference path at 1920x1080, bf16, batch 2, with
-    the fused inverted-residual blocks (rod_ir_block_fwd, ref conv_blocks.py:163-312) on.
-      * the fused kernel actually runs (probe), on every block it supports here;
-      * head outputs (refine / det offsets, clf logits) against the float64 oracle network in
-        eval mode on the same input (ref predict.py:127-137): normwise error within 1.5x that of
-        the same predictor with the fused blocks off (ROD_DISABLE=irblock: the unfused bf16
-        chain) + 1e-3, and below 0.1;
+    """C5 (BASELINE configs[4]): predict.py's inference path at 1920x1080, batch 2, with the
+    fused inverted-residual blocks (rod_ir_block_fwd, ref conv_blocks.py:163-312) on, BatchNorm
+    calibrated so the heads give a detector-like score distribution.
+      * the fused kernel actually runs (probe);
+      * fp32 (the unfused path): head outputs (refine / det offsets, clf logits) within 1e-3
+        normwise of the float64 oracle network in eval mode (ref predict.py:127-137);
+      * bf16 with the fused blocks: no less accurate than the unfused bf16 chain (1.5x + 1e-3),
+        and within 3x + 1e-2 of what bf16 storage allows — the oracle in fp32 arithmetic with
+        every stored tensor rounded to bf16 (oracle.net.set_storage).  (The calibrated random
+        network amplifies a bf16-sized perturbation layer by layer, so bf16 outputs of ANY
+        implementation sit far from float64 on the deep levels: the storage-rounded oracle
+        measures that conditioning);
       * softmax, decode and the per-class select / top-k / NMS keep lists and outputs bit-exact
         against oracle.post given the network's logits and offsets (~2 % of the class scores
         pass select_threshold 0.1)."""
     import predict
     import utils.net_tools as nt
+    from nets.catch_net import factory
     from rod import _abi
     from rod.data import detector_like_scores, synthetic_batch
+    from rod.dataio import network_input
     Hc, Wc, B = 1080, 1920, 2
     pr = predict.Predictor((Hc, Wc), dev, torch.bfloat16, seed=51)
     probe = synthetic_batch(2, Hc, Wc, dev, seed=52)[0]
@@ -422,23 +429,34 @@ def test_predict_1080p_fused_blocks_match_oracle(dev):
         u_logits, _, _, u_roff, u_doff = pr.last
     finally:
         ops._DISABLE.discard('irblock')
-    # float64 oracle of the ALL network in eval mode (moving statistics as calibrated)
+    # the same calibrated network in fp32 (the unfused fp32 kernels)
+    with torch.no_grad():
+        f_out = factory(network_input(img, torch.float32), 'mobilenet_v2', False, pr.config_dict, torch.float32,
+                        net=pr.net).get_output()
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     P = {k: v.detach().double().cpu() for k, v in pr.net.store.params.items()}
     Bf = {k: v.detach().double().cpu() for k, v in pr.net.store.buffers.items()}
-    # the product normalises into bf16 first ((2/255)x - 1 in fp32, rounded once; network_input):
-    # the oracle gets that same input
-    x = torch.from_numpy(f32(2.0 / 255.0) * img.cpu().numpy().astype(f32) - f32(1.0)).to(torch.bfloat16).double()
+    x32 = torch.from_numpy(f32(2.0 / 255.0) * img.cpu().numpy().astype(f32) - f32(1.0))
     with torch.no_grad():
-        r64, d64, c64 = onet.forward(x, P, Bf, False, all_mode=True)
+        r64, d64, c64 = onet.forward(x32.double(), P, Bf, False, all_mode=True)
+        prev = onet.set_storage(torch.bfloat16)
+        try:
+            rq, dq, cq = onet.forward(onet._st(x32), {k: v.float() for k, v in P.items()},
+                                      {k: v.float() for k, v in Bf.items()}, False, all_mode=True)
+        finally:
+            onet.set_storage(prev)
     cat = lambda ts, k: torch.cat([t.reshape(B, -1, k) for t in ts], 1)
     rep = []
-    for name, got, unf, want in (('refine', roff, u_roff, cat(r64, 4)), ('det', doff, u_doff, cat(d64, 4)),
-                                 ('clf', logits, u_logits, cat(c64, 11))):
-        ef, eu = _nerr(got.float(), want), _nerr(unf.float(), want)
-        rep.append((name, ef, eu))
-        assert ef <= 1.5 * eu + 1e-3 and ef < 0.1, rep
-    print('1080p head outputs, normwise error vs fp64 (fused, unfused):', rep)
+    for name, got, unf, f32o, q, want, k in (('refine', roff, u_roff, f_out[0], rq, r64, 4),
+                                            ('det', doff, u_doff, f_out[1], dq, d64, 4),
+                                            ('clf', logits, u_logits, f_out[2], cq, c64, 11)):
+        want = cat(want, k)
+        ef, eu, e32, eq = _nerr(got.float(), want), _nerr(unf.float(), want), _nerr(cat(f32o, k), want), \
+            _nerr(cat(q, k), want)
+        rep.append((name, ef, eu, e32, eq))
+        assert e32 <= 1e-3, rep
+        assert ef <= 1.5 * eu + 1e-3 and ef <= 3 * eq + 1e-2, rep
+    print('1080p head outputs, normwise error vs fp64 (bf16 fused, bf16 unfused, fp32, bf16-storage oracle):', rep)
     lg = logits.float().cpu().numpy()
     e, s_, _ = op.softmax_rows(lg)
     P_ = probs.cpu().numpy()

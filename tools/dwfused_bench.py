@@ -1,4 +1,4 @@
-"""Stride-1 depthwise backward at the 720x1280 b8 step's shapes: the unfused chain
+"""Depthwise backward (stride 1 and 2) at the 720x1280 b8 step's shapes: the unfused chain
 (rod_bn_bwd_apply -> rod_dw3x3_bwd_data -> rod_dw3x3_bwd_filter -> the input BatchNorm's
 rod_bn_bwd_reduce) against rod_dw3x3_bwd_fused (+ rod_bn_bwd_finalize of its sums).  HIP-event
 timed on the launching stream; GB/s = the fused kernel's algorithmic bytes (read ye, dz, yd;
@@ -13,8 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'road-object-detection-for-bdd100k_amd'))
 from rod import _abi, ops  # noqa: E402
 
-SHAPES = [(8, 720, 1280, 32), (8, 360, 640, 144), (8, 180, 320, 192), (8, 90, 160, 384), (8, 90, 160, 576),
-          (8, 45, 80, 960), (8, 23, 40, 960)]
+SHAPES = [(8, 720, 1280, 32, 1), (8, 360, 640, 144, 1), (8, 180, 320, 192, 1), (8, 90, 160, 384, 1),
+          (8, 90, 160, 576, 1), (8, 45, 80, 960, 1), (8, 23, 40, 960, 1),
+          # the stride-2 blocks (input maps)
+          (8, 720, 1280, 96, 2), (8, 360, 640, 144, 2), (8, 180, 320, 192, 2), (8, 90, 160, 576, 2)]
+
+
+def _same(n, s):
+    o = -(-n // s)
+    return o, max((o - 1) * s + 3 - n, 0) // 2
 
 
 def main():
@@ -28,10 +35,11 @@ def main():
     st = ops.stream()
     act = ops.ROD_ACT_RELU6
     tu = tf = 0.0
-    for (N, H, W, C) in SHAPES:
-        M = N * H * W
-        mk = lambda s=1.0, o=0.0: (torch.randn((N, H, W, C), device=dev, generator=g) * s + o).to(dt)
-        ye, yd, dz = mk(1.3, 0.2), mk(2, 0.4), mk()
+    for (N, H, W, C, S) in SHAPES:
+        (Ho, pt), (Wo, pl) = _same(H, S), _same(W, S)
+        M, Mo = N * H * W, N * Ho * Wo
+        mk = lambda shp, s=1.0, o=0.0: (torch.randn(shp, device=dev, generator=g) * s + o).to(dt)
+        ye, yd, dz = mk((N, H, W, C), 1.3, 0.2), mk((N, Ho, Wo, C), 2, 0.4), mk((N, Ho, Wo, C))
         w = torch.randn((3, 3, C), device=dev, generator=g) * 0.4
         vec = lambda lo=0.5: torch.rand(C, device=dev, generator=g) + lo
         dmean, drstd, dgam, dbet = torch.randn(C, device=dev, generator=g) * 0.3, vec(), vec(), torch.randn(C, device=dev, generator=g)
@@ -39,26 +47,26 @@ def main():
         code = ops.dtcode(ye)
         coef = torch.empty(3 * C, device=dev)
         rws = ops.workspace(_abi.query('rod_bn_bwd_workspace', M, C), dev)
-        _abi.call('rod_bn_bwd_reduce', dz, yd, dmean, drstd, dgam, dbet, None, None, coef, rws, M, C, act, code, st)
+        _abi.call('rod_bn_bwd_reduce', dz, yd, dmean, drstd, dgam, dbet, None, None, coef, rws, Mo, C, act, code, st)
         dy, dx = torch.empty_like(yd), torch.empty_like(ye)
         dw = torch.empty(3, 3, C, device=dev)
-        fws = ops.workspace(_abi.query('rod_dw3x3_bwd_filter_workspace', N, H, W, C), dev)
+        fws = ops.workspace(_abi.query('rod_dw3x3_bwd_filter_workspace', N, Ho, Wo, C), dev)
         ce, dg, db = torch.empty(3 * C, device=dev), torch.empty(C, device=dev), torch.empty(C, device=dev)
-        nparts = _abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C)
+        nparts = _abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C, S, pt, pl)
         gparts = torch.empty((nparts, 2, C), device=dev)
-        ws = ops.workspace(_abi.query('rod_dw3x3_bwd_fused_workspace', N, H, W, C), dev)
+        ws = ops.workspace(_abi.query('rod_dw3x3_bwd_fused_workspace', N, H, W, C, S, pt, pl), dev)
 
         def unfused():
-            _abi.call('rod_bn_bwd_apply', dz, yd, dmean, drstd, dgam, dbet, coef, dy, M, C, act, code, st)
-            _abi.call('rod_dw3x3_bwd_data', dy, w, dx, None, None, None, None, None, 0, None, N, H, W, C, 1, 1, 1, H,
-                      W, code, st)
-            _abi.call('rod_dw3x3_bwd_filter', ye, emean, erstd, egam, ebet, act, dy, dw, fws, N, H, W, C, 1, 1, 1, H,
-                      W, code, st)
+            _abi.call('rod_bn_bwd_apply', dz, yd, dmean, drstd, dgam, dbet, coef, dy, Mo, C, act, code, st)
+            _abi.call('rod_dw3x3_bwd_data', dy, w, dx, None, None, None, None, None, 0, None, N, H, W, C, S, pt, pl,
+                      Ho, Wo, code, st)
+            _abi.call('rod_dw3x3_bwd_filter', ye, emean, erstd, egam, ebet, act, dy, dw, fws, N, H, W, C, S, pt, pl,
+                      Ho, Wo, code, st)
             _abi.call('rod_bn_bwd_reduce', dx, ye, emean, erstd, egam, ebet, dg, db, ce, rws, M, C, act, code, st)
 
         def fused():
             _abi.call('rod_dw3x3_bwd_fused', ye, emean, erstd, egam, ebet, act, dz, yd, dmean, drstd, dgam, dbet, act,
-                      coef, w, dx, dw, gparts, ws, N, H, W, C, code, st)
+                      coef, w, dx, dw, gparts, ws, N, H, W, C, S, pt, pl, Ho, Wo, code, st)
             _abi.call('rod_bn_bwd_finalize', gparts, nparts, M, C, erstd, egam, dg, db, ce, st)
 
         res = []
@@ -72,10 +80,10 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             res.append(e0.elapsed_time(e1) / a.iters * 1e3)
-        byts = 4 * M * C * ye.element_size()
+        byts = 2 * (M + Mo) * C * ye.element_size()
         tu += res[0]
         tf += res[1]
-        print(f'{N}x{H}x{W}x{C:<5d} unfused {res[0]:8.1f} us  fused {res[1]:8.1f} us  x{res[0] / res[1]:5.2f}  '
+        print(f'{N}x{H}x{W}x{C:<5d} s{S} unfused {res[0]:8.1f} us  fused {res[1]:8.1f} us  x{res[0] / res[1]:5.2f}  '
               f'fused-bytes GB/s: unfused {byts / res[0] / 1e3:7.0f} fused {byts / res[1] / 1e3:7.0f}', flush=True)
     print(f'TOTAL unfused {tu:.1f} us fused {tf:.1f} us')
 
