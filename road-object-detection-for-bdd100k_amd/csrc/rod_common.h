@@ -120,11 +120,15 @@ __device__ __forceinline__ float act_fwd(float z, int act) {
   if (act == ROD_ACT_RELU) return act_t<ROD_ACT_RELU>(z);
   return z;
 }
+// Relu6Grad (0 < z < 6), LeakyReluGrad (z > 0 ? 1 : 0.2), ReluGrad (z > 0), none (1) as ONE
+// branch-free select chain: z > 0 ? (!(z >= hi) ? 1 : 0) : lo with (lo, hi) from the
+// activation (hi = NaN: no upper bound; the unordered compare keeps +inf at 1).  Same value
+// as the per-activation forms for every z, NaN and inf included.  The (lo, hi) selects depend
+// only on the wave-uniform act, so they hoist out of the loops: no per-element branches.
 __device__ __forceinline__ float act_grad(float z, int act) {
-  if (act == ROD_ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;  // Relu6Grad
-  if (act == ROD_ACT_LEAKY) return z > 0.f ? 1.f : 0.2f;               // LeakyReluGrad
-  if (act == ROD_ACT_RELU) return z > 0.f ? 1.f : 0.f;                 // ReluGrad
-  return 1.f;
+  const float lo = act == ROD_ACT_LEAKY ? 0.2f : ((act == ROD_ACT_RELU6 || act == ROD_ACT_RELU) ? 0.f : 1.f);
+  const float hi = act == ROD_ACT_RELU6 ? 6.f : __builtin_nanf("");
+  return z > 0.f ? (!(z >= hi) ? 1.f : 0.f) : lo;
 }
 
 // ---- BatchNorm affine -------------------------------------------------------------
