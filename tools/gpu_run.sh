@@ -66,17 +66,17 @@ for step in "$@"; do
     cli) run cli_train 300 python road-object-detection-for-bdd100k_amd/train.py --train_range=ALL --batch_size=2 --max_number_of_steps=4 --log_every_n_steps=2 --save_every_n_steps=4 --checkpoint_refine=None --train_dir=gpurun_out/ckpt --summary_dir=gpurun_out/summ &&
          run cli_eval 300 python road-object-detection-for-bdd100k_amd/evaluate.py --checkpoint_path=gpurun_out/ckpt --batch_size=2 --num_images=6 --eval_dir=gpurun_out/eval &&
          run cli_predict 300 python road-object-detection-for-bdd100k_amd/predict.py --checkpoint_all=gpurun_out/ckpt/mobilenet_v2.model --batch_size=2 --num_batches=2 --output=gpurun_out/pred.json ;;
-    probetable) run probetable 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-inference --probe-table $OUT/${TAG}_probe_table.json ;;
+    probetable) run probetable 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --probe-table $OUT/${TAG}_probe_table.json ;;
     probetableall) run probetableall 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-inference --train_range ALL --probe-table $OUT/${TAG}_probe_table_all.json ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --kernel-steps 0 &&
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --kernel-steps 0 &&
          summ $OUT/prof_$TAG normalize_image 5+2 "REFINE train step bf16 b8 720p, graph replays" ;;
     profall) run profall 600 rocprofv3 --kernel-trace --stats -d $OUT/profall_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --train_range ALL ;;
     profpred) run profpred 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 720 --batch 32 --iters 10 &&
          summ $OUT/profpred_$TAG normalize_image 10 "predict path bf16 b32 720p, graph replays" ;;
     profpred1080) run profpred1080 400 rocprofv3 --kernel-trace --stats -d $OUT/profpred1080_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 10 &&
          summ $OUT/profpred1080_$TAG normalize_image 10 "predict path bf16 b8 1080p, graph replays" ;;
-    pmcfetch) run pmcfetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference ;;
-    pmcwrite) run pmcwrite 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference ;;
+    pmcfetch) run pmcfetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --kernel-steps 0 ;;
+    pmcwrite) run pmcwrite 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$TAG -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --kernel-steps 0 ;;
     cbhead) run cbhead 300 python tools/conv_bench.py --shapes 7,13,14,15 ;;
     cball) run cball 300 python tools/conv_bench.py ;;
     convtests) run convtests 600 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_stem.py -m gpu -q -x --timeout=300 -p no:cacheprovider ;;
@@ -94,6 +94,10 @@ for step in "$@"; do
     dwpmc) run dwpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM SQ_INSTS_VALU SQ_BUSY_CYCLES -d $OUT/dwpmc_$TAG -o run --output-format csv -- python3 tools/dw_bench.py --iters 3 &&
            python tools/pmc_kernel_summary.py $OUT/dwpmc_$TAG/run_counter_collection.csv dw3x3 > $OUT/${TAG}_dwpmc.txt &&
            gzip -f $OUT/dwpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_dwpmc.txt ;;
+    dwfpmc) run dwfpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/dwfpmc_$TAG -o run --output-format csv -- python3 tools/dwfused_bench.py --iters 3 &&
+           python tools/pmc_kernel_summary.py $OUT/dwfpmc_$TAG/run_counter_collection.csv dw3x3_bwd_fused > $OUT/${TAG}_dwfpmc.txt &&
+           gzip -f $OUT/dwfpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_dwfpmc.txt ;;
+    dwfb) run dwfb 300 python tools/dwfused_bench.py ;;
     bnpmc) run bnpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES -d $OUT/bnpmc_$TAG -o run --output-format csv -- python3 tools/bn_bench.py --iters 3 &&
            python tools/pmc_kernel_summary.py $OUT/bnpmc_$TAG/run_counter_collection.csv bn_ > $OUT/${TAG}_bnpmc.txt &&
            gzip -f $OUT/bnpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_bnpmc.txt ;;
