@@ -52,10 +52,11 @@ def parse():
     ap.add_argument('--no-graph', dest='graph', action='store_false')
     ap.add_argument('--sync-bn', dest='sync_bn', action='store_true', default=False,
                     help='N>1: BatchNorm statistics over the global batch (rod.ddp.SyncBatchNorm; default per rank)')
-    ap.add_argument('--probe', default='rod_bn_bwd_reduce,rod_bn_bwd_apply,rod_bn_bwd',
+    ap.add_argument('--probe', default='rod_dw3x3_bwd_fused',
                     help='C-ABI entry (or comma list, aggregated as one kernel family) reported in "roofline": '
-                         'default the BatchNorm backward (reduce + apply; one-launch rod_bn_bwd on small '
-                         'tensors), the family VERDICT r1 names')
+                         'default the fused depthwise backward, the largest entry of the graphed step '
+                         '(profiles/r3_refine_bf16_b8_720p_graph_stats.txt); rounds 1-2 reported the '
+                         'BatchNorm backward (rod_bn_bwd_reduce,rod_bn_bwd_apply,rod_bn_bwd)')
     ap.add_argument('--probe-table', dest='probe_table', default=None,
                     help='time EVERY librod call and write a per-entry table (JSON) here (analysis only)')
     ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'),
@@ -511,8 +512,9 @@ def main():
                    'launches_per_step': n_launch // max(probe_steps, 1),
                    'avg_launch_us': round(per_launch_ms * 1e3, 2), 'alg_bytes_per_step': byts // max(probe_steps, 1),
                    'alg_flops_per_step': flops // max(probe_steps, 1),
-                   # the bytes the two-kernel design moves (reduce 2 passes + apply 3 against the
-                   # algorithmic 3 of read dz, read y, write dy; rod.roofline.design_bytes)
+                   # the bytes the design moves (rod.roofline.design_bytes): for the fused depthwise
+                   # backward + the re-read of (dz, y) of its output BatchNorm (the reduce pass
+                   # read them first); for the BatchNorm family reduce 2 + apply 3 passes
                    'design_bytes_per_step': dbytes // max(probe_steps, 1),
                    'design_GBps': round(dbytes / max(ms, 1e-9) / 1e6, 1),
                    'traffic_over_alg': round(traffic / max(byts // max(n_launch, 1), 1), 3) if traffic else None,

@@ -1916,6 +1916,272 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
   }
 }
 
+// Issue-lean form of dw3x3_bwd_fused_kernel (the default; ROD_DWF_V1=1 selects the one above).
+// Same engine, same per-element arithmetic and accumulation order (dx bit-identical), cut for
+// the instruction stream (tools/dwfused_bench.py PMC: the step was ~230 VALU + ~90 SALU per
+// barrier interval, 2 waves / SIMD, VALU-issue and latency bound):
+//   * per-lane conditions leave the loop body: every thread (halo columns included) loads a
+//     clamped, always-valid column, computes dx / filter / BN_e sums, and only the dx store is
+//     predicated on `comp`; halo sums are dropped by the column reduction as before.  Row
+//     conditions are block-uniform (scalar branches);
+//   * channel pairs run as packed f32 ops (v_pk_fma / v_pk_mul / v_pk_add, per element the same
+//     operation in the same order);
+//   * the activation gradients are specialised (ReLU6: one compare pair + select), and the
+//     BN_e gradient mask comes from the prologue's own z (the x element of the same row);
+//   * yhat_e = fma(ye, rstd, -mean * rstd) (the stride-2 kernel's form).
+typedef float dw_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ dw_f2 f2fma(dw_f2 a, dw_f2 b, dw_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+template <int ACT>
+__device__ __forceinline__ float agrad(float z, int act) {
+  if constexpr (ACT == ROD_ACT_RELU6) return (z > 0.f && !(z >= 6.f)) ? 1.f : 0.f;  // == act_grad(z, RELU6)
+  else return act_grad(z, act);
+}
+template <typename T>
+__device__ __forceinline__ void unpack4(const PackV<T, 4>& p, dw_f2& a, dw_f2& b) {
+  a = dw_f2{p.get(0), p.get(1)};
+  b = dw_f2{p.get(2), p.get(3)};
+}
+__device__ __forceinline__ dw_f2 round2(dw_f2 v, bf16_t) {
+  return dw_f2{(float)(bf16_t)v.x, (float)(bf16_t)v.y};
+}
+__device__ __forceinline__ dw_f2 round2(dw_f2 v, float) { return v; }
+
+template <typename T, int PACT, bool RED, int BACT>
+__global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
+                                                               const T* __restrict__ yd, const float* __restrict__ w,
+                                                               T* __restrict__ dx, float* __restrict__ slab,
+                                                               float* __restrict__ gparts, int H, int W, int C,
+                                                               DwTile tl, BnPro pro, DwBwdBn bd) {
+  constexpr int V = 4, D = 3;
+  typedef PackV<T, V> PK;
+  constexpr int XS = 2 * 2 * 256 * (int)sizeof(PK);
+  constexpr int SS = 256 * V * 4;
+  __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
+  PK* xs = (PK*)smem;
+  PK* dsl = xs + 2 * 256;
+  const int tid = threadIdx.x;
+  const int CVb = tl.CVb, P = tl.P;
+  const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
+  int bx, strip, n;
+  xcd_block(bx, strip, n);
+  const int cg = bx % tl.cgroups, ct = bx / tl.cgroups;
+  const int c = (cg * CVb + cvb) * V;
+  const int col = ct * tl.TWo + p - 1;
+  const bool comp = p >= 1 && p <= P - 2 && col < W;
+  const bool cok = p < P && col >= 0 && col < W;
+  const int colc = col < 0 ? 0 : (col >= W ? W - 1 : col);         // always a valid address
+  const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < 256 ? tid + CVb : tid;
+  const int ho0 = strip * tl.RB;
+  const int ho1 = ho0 + tl.RB < H ? ho0 + tl.RB : H;
+  const int xlo = ho0 - 1 > 0 ? ho0 - 1 : 0, xhi = ho1 < H - 1 ? ho1 : H - 1;
+
+  dw_f2 wr[9][2];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) wr[k][h] = dw_f2{w[k * C + c + 2 * h], w[k * C + c + 2 * h + 1]};
+  dw_f2 psc[2], psh[2], ers[2], enb[2];
+  int pact = 0;
+  if constexpr (PACT >= 0) {
+    pact = pro.act;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float a0, b0, a1, b1;
+      bn_pro_affine(pro, c + 2 * h, a0, b0);
+      bn_pro_affine(pro, c + 2 * h + 1, a1, b1);
+      psc[h] = dw_f2{a0, a1};
+      psh[h] = dw_f2{b0, b1};
+      if constexpr (RED) {
+        ers[h] = dw_f2{pro.rstd[c + 2 * h], pro.rstd[c + 2 * h + 1]};
+        enb[h] = dw_f2{-pro.mean[c + 2 * h] * ers[h].x, -pro.mean[c + 2 * h + 1] * ers[h].y};
+      }
+    }
+  }
+  dw_f2 dmu[2], drs[2], dsc[2], dsh[2], da[2], dmg[2], dmx[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c0 = c + 2 * h;
+    dmu[h] = dw_f2{bd.mean[c0], bd.mean[c0 + 1]};
+    drs[h] = dw_f2{bd.rstd[c0], bd.rstd[c0 + 1]};
+    float s0, t0, s1, t1;
+    bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0, s0, t0);
+    bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0 + 1, s1, t1);
+    dsc[h] = dw_f2{s0, s1};
+    dsh[h] = dw_f2{t0, t1};
+    da[h] = dw_f2{bd.coef[c0], bd.coef[c0 + 1]};
+    dmg[h] = dw_f2{bd.coef[C + c0], bd.coef[C + c0 + 1]};
+    dmx[h] = dw_f2{bd.coef[2 * C + c0], bd.coef[2 * C + c0 + 1]};
+  }
+  dw_f2 sg[2], sgx[2];
+  sg[0] = sg[1] = sgx[0] = sgx[1] = dw_f2{0.f, 0.f};
+  const long nb = (long)n * H * W * C + c;
+  const T* yen = ye + nb + (long)colc * C;
+  const T* dzn = dz + nb + (long)colc * C;
+  const T* ydn = yd + nb + (long)colc * C;
+  T* dxn = dx + nb + (long)colc * C;
+  const long rstr = (long)W * C;
+
+  PK rx[D], rz[D], ry[D];
+  auto issue = [&](int k, int q) {  // row conditions are block-uniform
+    const int rho = ho0 - 2 + q;
+    if (rho >= xlo && rho <= xhi) rx[k].load(yen + rho * rstr);
+    if (rho + 1 >= xlo && rho + 1 <= xhi) {
+      rz[k].load(dzn + (rho + 1) * rstr);
+      ry[k].load(ydn + (rho + 1) * rstr);
+    }
+  };
+  const int nst = ho1 - ho0 + 3;
+#pragma unroll
+  for (int k = 0; k < D; ++k) issue(k, k);
+  dw_f2 acc[3][2], fa[9][2], q1[2], q2[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    acc[0][h] = acc[1][h] = acc[2][h] = q1[h] = q2[h] = dw_f2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) fa[k][h] = dw_f2{0.f, 0.f};
+  }
+  for (int q0 = 0; q0 < nst; q0 += D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int q = q0 + k;
+      const int rho = ho0 - 2 + q;
+      const int buf = q & 1;
+      const int k3 = k % 3;
+      const bool xok = cok && rho >= xlo && rho <= xhi;
+      const bool dok = cok && rho + 1 >= xlo && rho + 1 <= xhi;
+      // x row rho (prologue, rounded to T) and, with RED, BN_e's gradient mask at the same element
+      dw_f2 xv[2], yr[2], em[2];
+      unpack4(rx[k], yr[0], yr[1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        dw_f2 a = yr[h];
+        if constexpr (PACT >= 0) {
+          const dw_f2 z = f2fma(a, psc[h], psh[h]);
+          dw_f2 t;
+          if constexpr (PACT == ROD_ACT_RELU6) {
+            t = dw_f2{act_t<ROD_ACT_RELU6>(z.x), act_t<ROD_ACT_RELU6>(z.y)};
+          } else {
+            t = dw_f2{act_fwd(z.x, pact), act_fwd(z.y, pact)};
+          }
+          a = round2(t, T{});
+          if constexpr (RED) em[h] = dw_f2{agrad<PACT>(z.x, pact), agrad<PACT>(z.y, pact)};
+        }
+        xv[h] = xok ? a : dw_f2{0.f, 0.f};
+      }
+      // dy row rho + 1: BN_d backward apply (rod_bn_bwd_apply's arithmetic), rounded to T
+      dw_f2 dv[2];
+      {
+        dw_f2 yv[2], zv[2];
+        unpack4(ry[k], yv[0], yv[1]);
+        unpack4(rz[k], zv[0], zv[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const dw_f2 d = yv[h] - dmu[h];
+          const dw_f2 z = f2fma(yv[h], dsc[h], dsh[h]);
+          const dw_f2 m = dw_f2{agrad<BACT>(z.x, bd.act), agrad<BACT>(z.y, bd.act)};
+          const dw_f2 g = zv[h] * m;
+          const dw_f2 o = da[h] * ((g - dmg[h]) - (d * drs[h]) * dmx[h]);
+          dv[h] = dok ? round2(o, T{}) : dw_f2{0.f, 0.f};
+        }
+      }
+      PK px, pd;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        px.set(2 * h, xv[h].x);
+        px.set(2 * h + 1, xv[h].y);
+        pd.set(2 * h, dv[h].x);
+        pd.set(2 * h + 1, dv[h].y);
+      }
+      issue(k, q + D);
+      xs[buf * 256 + tid] = px;
+      dsl[buf * 256 + tid] = pd;
+      __syncthreads();
+      dw_f2 xl[2], xr[2], dl[2], dr[2];
+      unpack4(xs[buf * 256 + li], xl[0], xl[1]);
+      unpack4(xs[buf * 256 + ri], xr[0], xr[1]);
+      unpack4(dsl[buf * 256 + li], dl[0], dl[1]);
+      unpack4(dsl[buf * 256 + ri], dr[0], dr[1]);
+      // backward-data: dy row rho+1 is tap row 0 of dx row rho, 1 of rho+1, 2 of rho+2
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int sl = (k3 + i) % 3;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          dw_f2 a = acc[sl][h];
+          a = f2fma(dl[h], wr[i * 3 + 2][h], a);
+          a = f2fma(dv[h], wr[i * 3 + 1][h], a);
+          a = f2fma(dr[h], wr[i * 3][h], a);
+          acc[sl][h] = a;
+        }
+      }
+      // filter: x row rho with the strip's dy rows rho+1 (tap row 0), rho (1), rho-1 (2)
+      const bool own = rho + 1 >= ho0 && rho + 1 < ho1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const dw_f2 f0 = own ? dv[h] : dw_f2{0.f, 0.f};
+        fa[0][h] = f2fma(f0, xl[h], fa[0][h]);
+        fa[1][h] = f2fma(f0, xv[h], fa[1][h]);
+        fa[2][h] = f2fma(f0, xr[h], fa[2][h]);
+        fa[3][h] = f2fma(q1[h], xl[h], fa[3][h]);
+        fa[4][h] = f2fma(q1[h], xv[h], fa[4][h]);
+        fa[5][h] = f2fma(q1[h], xr[h], fa[5][h]);
+        fa[6][h] = f2fma(q2[h], xl[h], fa[6][h]);
+        fa[7][h] = f2fma(q2[h], xv[h], fa[7][h]);
+        fa[8][h] = f2fma(q2[h], xr[h], fa[8][h]);
+        q2[h] = q1[h];
+        q1[h] = f0;
+      }
+      // dx row rho is complete
+      if (rho >= ho0 && rho < ho1) {
+        PK o;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          o.set(2 * h, acc[k3][h].x);
+          o.set(2 * h + 1, acc[k3][h].y);
+        }
+        if (comp) o.store_out(dxn + rho * rstr);
+        if constexpr (RED) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const dw_f2 ov = dw_f2{o.get(2 * h), o.get(2 * h + 1)};
+            const dw_f2 g = ov * em[h];
+            sg[h] += g;
+            sgx[h] = f2fma(g, f2fma(yr[h], ers[h], enb[h]), sgx[h]);
+          }
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) acc[k3][h] = dw_f2{0.f, 0.f};
+    }
+  }
+
+  __syncthreads();
+  float* red = (float*)smem;
+  const int Cc = CVb * V;
+  const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+  auto colsum = [&](const dw_f2 (&a)[2], float* dst) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      red[tid * V + 2 * h] = comp ? a[h].x : 0.f;
+      red[tid * V + 2 * h + 1] = comp ? a[h].y : 0.f;
+    }
+    __syncthreads();
+    for (int e = tid; e < Cc; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      float s = 0.f;
+      for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
+      dst[cg * Cc + e] = s;
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int k = 0; k < 9; ++k) colsum(fa[k], slab + (part * 9 + k) * C);
+  if constexpr (RED) {
+    colsum(sg, gparts + part * 2 * C);
+    colsum(sgx, gparts + part * 2 * C + C);
+  }
+}
+
 // Stride-2 form.  Thread (p, cvb) owns output column b = wo0 + p - 1 (one halo column each
 // side) and the dx / x column pair (2b - pl, 2b - pl + 1); step q handles dy row a = a0 - 1 + q
 // and the x / dx rows 2a - pt, 2a + 1 - pt.  dx's 2x2 block (rows 2a-pt, 2a+1-pt x its column
@@ -2199,6 +2465,8 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
     // measured 3.27 ms (3) vs 3.34 ms (6) over the step's bf16 shapes (tools/dwfused_bench.py)
     static const int ring_env = getenv("ROD_DWF_RING") ? atoi(getenv("ROD_DWF_RING")) : 0;
     const int ring = ring_env == 6 ? 6 : 3;
+    // stride 1: the issue-lean kernel; ROD_DWF_V1=1 (A/B switch) the first form
+    static const bool v1 = getenv("ROD_DWF_V1") && atoi(getenv("ROD_DWF_V1")) == 1;
 #define DWF1(PA, R, D)                                                                                               \
   hipLaunchKernelGGL((dw3x3_bwd_fused_kernel<T, PA, R, D>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,      \
                      (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)
@@ -2207,9 +2475,14 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
 #define DWS2(PA, R)                                                                                                  \
   hipLaunchKernelGGL((dw3x3_bwd_fused_s2_kernel<T, PA, R, D2>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,   \
                      (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, pad_t, pad_l, Ho, Wo, t, pv, bd)
+#define DWV2(PA, R, BA)                                                                                              \
+  hipLaunchKernelGGL((dw3x3_bwd_fused2_kernel<T, PA, R, BA>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,     \
+                     (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)
 #define DWF2(PA, R)                                                                                                  \
   do {                                                                                                              \
     if (stride == 2) DWS2(PA, R);                                                                                   \
+    else if (!v1 && bn_act == ROD_ACT_RELU6) DWV2(PA, R, ROD_ACT_RELU6);                                            \
+    else if (!v1) DWV2(PA, R, DW_ACT_RT);                                                                           \
     else if (ring == 3) DWF1(PA, R, 3);                                                                             \
     else DWF1(PA, R, 6);                                                                                            \
   } while (0)
@@ -2221,6 +2494,7 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
       DWF2(-1, false);
     }
 #undef DWF2
+#undef DWV2
 #undef DWS2
 #undef DWF1
   };

@@ -699,6 +699,218 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   }
 }
 
+// =====================================================================================
+// Streaming 1x1 forward for the expand convs (bf16, K <= 64, Cout = 16*NT <= 192, no bias, no
+// prologue): y[m, :] = x[m, :K] * wt^T, optionally with the BatchNorm statistics parts.
+//
+// The tiled kernel above spends a whole 256-thread block (two barriers, a 128x160 LDS tile, a
+// block-wide epilogue) on one 128-row tile whose single k step is a handful of MFMAs: at K = 24
+// it is latency-bound (24->144 at 360x640: 2.8 TB/s).  Here every wave streams on its own:
+//   * the weights [Cout][K] are staged in LDS once per block (zero-padded to KT*32);
+//   * a wave owns whole 128-row tiles (the statistics part unit) and walks each in 16-row
+//     sub-steps (one MFMA row tile: fewest VGPRs, most waves in flight); the A
+//     fragments (lane l: row l & 15, k 8(l >> 4) .. +7 — exactly the MFMA operand layout) load
+//     straight from global into registers, the next sub-step's while the current one computes
+//     and stores;
+//   * the sub-tile's output rows are rounded once, staged in a wave-private LDS slot and
+//     written back as contiguous 16-byte row segments (the sub-tile is one contiguous run of y);
+//   * statistics: each lane owns one column per 16-wide N tile (rows 4(l>>4) + r of the MFMA
+//     tile), sums (v - pivot) and (v - pivot)^2 over the tile's rows in registers (pivot = mean
+//     of the tile's first 8 rows, values rounded to bf16), and the four lane groups combine by
+//     two xor-shuffles -> (n, mean, M2) of the tile: the [parts][3][C] contract, one part per
+//     128 rows.  No block barrier after the weight staging.
+// =====================================================================================
+constexpr int PWS_WAVES = 4;
+#ifndef PWS_MS
+#define PWS_MS 0
+#endif
+template <int NT, int KT, bool STATS>
+__global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                                                        bf16_t* __restrict__ Y, long M, int K, int ldx, int ldy,
+                                                        float* __restrict__ part) {
+  constexpr int NP = NT * 16;      // Cout
+  constexpr int LDB = KT * 32 + 8;  // weight row stride in LDS (elements)
+  constexpr int LDC = NP + 8;       // staging row stride (elements; 16-byte multiple)
+  // 16-row sub-steps: measured faster than 32-row ones with statistics (24->144 at 360x640: 195 vs
+  // 218 us) and equal without (fewer VGPRs, more waves in flight)
+  constexpr int MS = PWS_MS > 0 ? PWS_MS : 1;
+  constexpr int SUB = 128 / (16 * MS);
+  constexpr int CPR = NP / 8;       // 16-byte chunks per output row
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[NP * LDB];
+  __shared__ __attribute__((aligned(16))) bf16_t Cs[PWS_WAVES][MS * 16 * LDC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, lg = lane >> 4;
+
+  for (int idx = tid; idx < NP * KT * 4; idx += 256) {  // weights -> LDS, k >= K zero
+    const int r = idx / (KT * 4), k = (idx - r * (KT * 4)) * 8;
+    bf16x8 v;
+    if (k < K) v = *(const bf16x8*)(Wt + (long)r * K + k);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16_t)0.f;
+    }
+    *(bf16x8*)(Bs + r * LDB + k) = v;
+  }
+  __syncthreads();
+
+  const long ntiles = (M + 127) >> 7;
+  const long tstride = (long)gridDim.x * PWS_WAVES;
+  long t = (long)blockIdx.x * PWS_WAVES + wave;
+  bf16_t* cs = Cs[wave];
+
+  // A fragments of sub-step (tile, s): rows tile*128 + s*16*MS + 16i + fr, k 32kt + 8lg
+  auto load_a = [&](bf16x8 (&a)[MS][KT], long tile, int s) {
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      const long row = tile * 128 + s * (MS * 16) + i * 16 + fr;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int k = kt * 32 + lg * 8;
+        if (row < M && k < K) a[i][kt] = *(const bf16x8*)(X + row * ldx + k);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[i][kt][e] = (bf16_t)0.f;
+        }
+      }
+    }
+  };
+  bf16x8 ab[MS][KT], an[MS][KT];
+  if (t < ntiles) load_a(ab, t, 0);
+  for (; t < ntiles; t += tstride) {
+    const long row0 = t * 128;
+    const int left = M - row0 < 128 ? (int)(M - row0) : 128;  // valid rows of this tile
+    const bool full = left == 128;
+    float piv[NT], s1[NT], s2[NT];
+#pragma unroll
+    for (int b = 0; b < NT; ++b) piv[b] = s1[b] = s2[b] = 0.f;
+#pragma unroll 1
+    for (int s = 0; s < SUB; ++s) {
+      {  // prefetch the next sub-step (the next tile's first one after the last)
+        const long tn = s + 1 < SUB ? t : t + tstride;
+        if (tn < ntiles) load_a(an, tn, s + 1 < SUB ? s + 1 : 0);
+      }
+      // the weight fragments are re-read from LDS every sub-step (kept out of registers)
+      asm volatile("" ::: "memory");
+      f32x4 acc[MS][NT];
+#pragma unroll
+      for (int i = 0; i < MS; ++i)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[i][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          const bf16x8 bf = *(const bf16x8*)(Bs + (b * 16 + fr) * LDB + kt * 32 + lg * 8);
+#pragma unroll
+          for (int i = 0; i < MS; ++i)
+            acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab[i][kt], bf, acc[i][b], 0, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < MS; ++i)
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) ab[i][kt] = an[i][kt];
+      // epilogue, one 16-wide N tile at a time: round once (the statistics and the staged value
+      // are the stored one), statistics, stage into this wave's LDS slot
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        float v[MS][4];
+#pragma unroll
+        for (int i = 0; i < MS; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[i][r] = (float)(bf16_t)acc[i][b][r];
+        if constexpr (STATS) {
+          if (s == 0) {  // pivot: mean of the tile's first (up to) 8 valid rows, this column
+            float p = 0.f;
+            if (lg < 2) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (full || lg * 4 + r < left) p += v[0][r];
+            }
+            p += __shfl_xor(p, 16, 64);
+            p = __shfl(p, fr, 64);
+            const int pc = left < 8 ? left : 8;
+            piv[b] = full ? p * 0.125f : p / (float)pc;
+          }
+#pragma unroll
+          for (int i = 0; i < MS; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (full || s * (MS * 16) + i * 16 + lg * 4 + r < left) {
+                const float d = v[i][r] - piv[b];
+                s1[b] += d;
+                s2[b] = fmaf(d, d, s2[b]);
+              }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MS; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs[(i * 16 + lg * 4 + r) * LDC + b * 16 + fr] = (bf16_t)v[i][r];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const long rs = row0 + s * (MS * 16);
+#pragma unroll
+      for (int it = 0; it < (MS * 16 * CPR + 63) / 64; ++it) {
+        const int idx = it * 64 + lane;
+        if ((MS * 16 * CPR) % 64 != 0 && idx >= MS * 16 * CPR) break;
+        const int rr = idx / CPR, cc = idx - rr * CPR;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = *(const u32x4*)(cs + rr * LDC + cc * 8);
+        if (rs + rr < M) ROD_ST_OUT((u32x4*)(Y + (rs + rr) * ldy + cc * 8), v);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (STATS) {
+      const float n = (float)left;
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        float a = s1[b], q = s2[b];
+        a += __shfl_xor(a, 16, 64);
+        q += __shfl_xor(q, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (lane < 16) {
+          const float dm = full ? a * (1.0f / 128.0f) : a / n;
+          store_stat_part(part, NP, t, b * 16 + lane, n, piv[b] + dm, fmaxf(q - a * dm, 0.f));
+        }
+      }
+    }
+  }
+}
+
+// rod_conv_fwd's streaming path (pw_stream_kernel): bf16 1x1, no bias / prologue / gred, K <= 64
+// (K % 8 == 0), Cout = 16 * NT for NT in {6, 9, 12}, 16-byte aligned rows.  ROD_PW_STREAM=0 turns
+// it off (A/B measurement switch).
+static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long M, int K, int Cout, int ldx, int ldy,
+                             float* stats, hipStream_t s) {
+  static const bool off = getenv("ROD_PW_STREAM") && atoi(getenv("ROD_PW_STREAM")) == 0;
+  if (off || K > 64 || K % 8 || Cout % 16 || M < 4096) return false;
+  const int nt = Cout / 16, kt = K > 32 ? 2 : 1;
+  const long ntiles = cdivl(M, 128);
+  // waves: <= 3 blocks of 4 waves per CU, every wave the same number of tiles (+-1)
+  const long maxw = 256L * 3 * PWS_WAVES;
+  const long per = cdivl(ntiles, maxw);
+  const int blocks = (int)cdivl(cdivl(ntiles, per), PWS_WAVES);
+#define PWS(NT_, KT_)                                                                                            \
+  do {                                                                                                           \
+    if (stats)                                                                                                   \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, true>), dim3(blocks), dim3(256), 0, s, x, wt, y, M, K, ldx, \
+                         ldy, stats);                                                                            \
+    else                                                                                                         \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, false>), dim3(blocks), dim3(256), 0, s, x, wt, y, M, K,     \
+                         ldx, ldy, nullptr);                                                                     \
+    return true;                                                                                                 \
+  } while (0)
+  if (nt == 6 && kt == 1) PWS(6, 1);
+  if (nt == 9 && kt == 1) PWS(9, 1);
+  if (nt == 12 && kt == 1) PWS(12, 1);
+  if (nt == 6 && kt == 2) PWS(6, 2);
+  if (nt == 9 && kt == 2) PWS(9, 2);
+  if (nt == 12 && kt == 2) PWS(12, 2);
+#undef PWS
+  return false;
+}
+
 // split-K combine: y[m, co] = round(sum_s part[s][m][co] + bias[co]), fixed split order
 template <typename T>
 __global__ void splitk_combine_kernel(const float* __restrict__ part, const float* __restrict__ bias,
@@ -1533,6 +1745,11 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
       hipLaunchKernelGGL((stem_conv_fwd_kernel<T, 64>), dim3(cdiv(W, 64), H, N), dim3(256), 0, s, (const T*)x,
                          (const T*)wt, bias, (T*)y, H, W, ldx, ldy);
     return;
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (ksize == 1 && !pro && !gr && !bias && va && vb && vy &&
+        pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, s))
+      return;
   }
   if (ksize == 1) {
     if (pro) conv_fwd_dispatch<T, 1, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);

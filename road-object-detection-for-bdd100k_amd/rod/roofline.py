@@ -191,7 +191,8 @@ ENTRY_KERNELS = {
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),
     "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused",), ("dw3x3_bwd_fused",)),
     "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
-    "rod_conv_fwd": (("conv_fwd_kernel", "stem_conv_fwd_kernel"), ("conv_fwd_kernel", "stem_conv_fwd_kernel")),
+    "rod_conv_fwd": (("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel"),
+                     ("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel")),
     "rod_bn_finalize": (("bn_parts_merge_kernel",), ("bn_parts_merge_kernel",)),
     "rod_ir_block_fwd": (("ir_block_fwd_kernel",), ("ir_block_fwd_kernel",)),
 }

@@ -183,6 +183,35 @@ def test_conv_epilogue_bn_stats(dev, dtype, ks, Cin, Cout, NHW):
     torch.testing.assert_close(z1.float(), z2.float(), **tol)
 
 
+@pytest.mark.parametrize('Cin,Cout,NHW', [(24, 144, (2, 45, 81)), (16, 96, (1, 37, 131)), (32, 192, (2, 23, 97)),
+                                           (64, 96, (3, 17, 83)), (40, 144, (1, 64, 65)), (8, 192, (1, 33, 129))])
+def test_pw_stream_expand(dev, Cin, Cout, NHW):
+    """The streaming 1x1 forward (pw_stream_kernel: bf16, no bias, K <= 64, Cout % 16 == 0,
+    M >= 4096; M here not a multiple of the 128-row part tile) against the oracle conv, and its
+    statistics parts against the separate statistics pass (ref conv_blocks.py:264-271 expand +
+    BatchNorm).  ROD_PW_STREAM=0 would route these shapes to the tiled kernel."""
+    g = torch.Generator().manual_seed(14)
+    N, H, W = NHW
+    x = (torch.randn(N, H, W, Cin, generator=g) + 0.5).to(torch.bfloat16).float()
+    w = (torch.randn(Cout, 1, 1, Cin, generator=g) / np.sqrt(Cin)).to(torch.bfloat16).float()
+    yo = onet.conv(x.permute(0, 3, 1, 2).double(), w.double(), None).permute(0, 2, 3, 1)
+    xd = x.to(dev, torch.bfloat16)
+    y1, parts = ops.conv2d(xd, w.to(dev), None, 1, want_stats=True)
+    y2 = ops.conv2d(xd, w.to(dev), None, 1)
+    assert torch.equal(y1, y2)
+    # fp32 accumulation of exact bf16 products, rounded once to bf16
+    err = (y1.double().cpu() - yo).abs().max() / yo.abs().max()
+    assert err <= 2 ** -8, float(err)
+    be = torch.zeros(Cout, device=dev)
+    mm1, mv1 = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    mm2, mv2 = mm1.clone(), mv1.clone()
+    z1 = ops.bn_act(y1, None, be, mm1, mv1, ops.ROD_ACT_NONE, True, 0.9, 1e-3, parts=parts)
+    z2 = ops.bn_act(y2, None, be, mm2, mv2, ops.ROD_ACT_NONE, True, 0.9, 1e-3)
+    torch.testing.assert_close(mm1, mm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mv1, mv2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(z1.float(), z2.float(), rtol=1e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('C,stride,H,W', [(144, 1, 45, 80), (96, 2, 90, 161), (6, 1, 13, 17), (960, 1, 3, 5),
                                           (32, 1, 33, 70)])

@@ -98,6 +98,8 @@ for step in "$@"; do
            python tools/pmc_kernel_summary.py $OUT/dwfpmc_$TAG/run_counter_collection.csv dw3x3_bwd_fused > $OUT/${TAG}_dwfpmc.txt &&
            gzip -f $OUT/dwfpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_dwfpmc.txt ;;
     dwfb) run dwfb 300 python tools/dwfused_bench.py ;;
+    pws) run pws0 300 env ROD_PW_STREAM=0 python tools/conv_bench.py --ops fwd_plain,fwd_stats --out /tmp/${TAG}_pws.pt &&
+         run pws1 300 python tools/conv_bench.py --ops fwd_plain,fwd_stats --check /tmp/${TAG}_pws.pt ;;
     bnpmc) run bnpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES -d $OUT/bnpmc_$TAG -o run --output-format csv -- python3 tools/bn_bench.py --iters 3 &&
            python tools/pmc_kernel_summary.py $OUT/bnpmc_$TAG/run_counter_collection.csv bn_ > $OUT/${TAG}_bnpmc.txt &&
            gzip -f $OUT/bnpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_bnpmc.txt ;;
