@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 13
+#define ROD_ABI_VERSION 14
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -304,6 +304,12 @@ int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, co
                  const float* gred_rstd, const float* gred_gamma, const float* gred_beta, int gred_act,
                  float* gred_parts, int N, int H, int W, int Cin, int Cout, int ksize, int ldx, int ldy,
                  int dtype, void* stream);
+/* ABI 14: 1 when rod_conv_fwd of this 1x1 shape (no bias, no prologue, 16-byte aligned dense
+ * rows) takes the streaming kernel, whose gred epilogue costs about one extra read of gred_y —
+ * the caller then asks for the gred sums instead of running rod_bn_bwd_reduce over (dz, y)
+ * afterwards (the project conv's backward-data and the depthwise BatchNorm it feeds,
+ * conv_blocks.py:287-294 -> 238-247); 0 otherwise.  M = N*H*W rows, K = Cin. */
+int rod_conv_fwd_stream_ok(long M, int K, int Cout, int dtype);
 /* Weight layouts derived from the fp32 master weight w[Cout][ksize][ksize][Cin]:
  *   mode 0: forward operand      wt[co][i][j][ci]           (cast to dtype)
  *   mode 1: backward-data operand wt[ci][2-i][2-j][co]       (transposed, flipped)

@@ -700,51 +700,60 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 }
 
 // =====================================================================================
-// Streaming 1x1 forward for the expand convs (bf16, K <= 64, Cout = 16*NT <= 192, no bias, no
-// prologue): y[m, :] = x[m, :K] * wt^T, optionally with the BatchNorm statistics parts.
+// Streaming 1x1 GEMM (bf16, K <= 96, no bias / prologue): y[m, n0 .. n0 + 16*NT) = x[m, :K] *
+// wt[n0 .., :K]^T over N groups of 16*NT columns (blockIdx.y), with an optional epilogue:
+//   MODE 1: the BatchNorm statistics parts of y ([ceil(M/128)][3][Cout], the forward expand);
+//   MODE 2: "gred" — the BatchNorm-backward sums of y taken as dz against the pre-BatchNorm
+//           tensor gr.y at the same positions ([ceil(M/128)][2][Cout]: sum g, sum g*yhat,
+//           g = dz * act'(BN(gr.y))), for a backward-data whose output is the gradient of a
+//           BatchNorm's output (the project conv's dx = the depthwise BatchNorm's dz): the
+//           separate rod_bn_bwd_reduce pass over (dz, y) is not needed.
 //
 // The tiled kernel above spends a whole 256-thread block (two barriers, a 128x160 LDS tile, a
 // block-wide epilogue) on one 128-row tile whose single k step is a handful of MFMAs: at K = 24
 // it is latency-bound (24->144 at 360x640: 2.8 TB/s).  Here every wave streams on its own:
-//   * the weights [Cout][K] are staged in LDS once per block (zero-padded to KT*32);
-//   * a wave owns whole 128-row tiles (the statistics part unit) and walks each in 16-row
-//     sub-steps (one MFMA row tile: fewest VGPRs, most waves in flight); the A
-//     fragments (lane l: row l & 15, k 8(l >> 4) .. +7 — exactly the MFMA operand layout) load
-//     straight from global into registers, the next sub-step's while the current one computes
-//     and stores;
+//   * the weights of the N group [16*NT][K] are staged in LDS once per block (zero-padded to
+//     KT*32);
+//   * a wave owns whole 128-row tiles (the statistics / sums part unit) and walks each in 16-row
+//     sub-steps (one MFMA row tile: fewest VGPRs, most waves in flight; measured faster than
+//     32-row ones: 24->144 at 360x640 with statistics 195 vs 218 us); the A fragments (lane l:
+//     row l & 15, k 8(l >> 4) .. +7 — exactly the MFMA operand layout) load straight from global
+//     into registers, the next sub-step's while the current one computes and stores;
 //   * the sub-tile's output rows are rounded once, staged in a wave-private LDS slot and
-//     written back as contiguous 16-byte row segments (the sub-tile is one contiguous run of y);
+//     written back as 16-byte row segments;
 //   * statistics: each lane owns one column per 16-wide N tile (rows 4(l>>4) + r of the MFMA
 //     tile), sums (v - pivot) and (v - pivot)^2 over the tile's rows in registers (pivot = mean
 //     of the tile's first 8 rows, values rounded to bf16), and the four lane groups combine by
-//     two xor-shuffles -> (n, mean, M2) of the tile: the [parts][3][C] contract, one part per
-//     128 rows.  No block barrier after the weight staging.
+//     two xor-shuffles -> (n, mean, M2) of the tile;
+//   * gred: the write-back gives every lane a FIXED 8-channel chunk (lane = row group rg x
+//     chunk cc, rows rg, rg + RG, ...), so the lane's BatchNorm constants stay in registers and
+//     its sums run over its rows in order; gr.y's rows are loaded (16-byte chunks) before the
+//     sub-step's MFMAs; at the tile's end the RG row groups are added in order (shuffles).
+// No block barrier after the weight staging.
 // =====================================================================================
 constexpr int PWS_WAVES = 4;
-#ifndef PWS_MS
-#define PWS_MS 0
-#endif
-template <int NT, int KT, bool STATS>
+template <int NT, int KT, int MODE>
 __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
-                                                        bf16_t* __restrict__ Y, long M, int K, int ldx, int ldy,
-                                                        float* __restrict__ part) {
-  constexpr int NP = NT * 16;      // Cout
+                                                        bf16_t* __restrict__ Y, long M, int K, int Cout, int ldx,
+                                                        int ldy, float* __restrict__ part, BnGred gr) {
+  constexpr int NP = NT * 16;       // columns of the N group
   constexpr int LDB = KT * 32 + 8;  // weight row stride in LDS (elements)
   constexpr int LDC = NP + 8;       // staging row stride (elements; 16-byte multiple)
-  // 16-row sub-steps: measured faster than 32-row ones with statistics (24->144 at 360x640: 195 vs
-  // 218 us) and equal without (fewer VGPRs, more waves in flight)
-  constexpr int MS = PWS_MS > 0 ? PWS_MS : 1;
-  constexpr int SUB = 128 / (16 * MS);
-  constexpr int CPR = NP / 8;       // 16-byte chunks per output row
+  constexpr int SUB = 8;            // 16-row sub-steps per 128-row tile
+  constexpr int CPR = NP / 8;       // 16-byte chunks per output row of the group
+  constexpr int RG = 64 / CPR;      // gred: row groups of lanes (lanes >= RG*CPR idle)
+  constexpr int JN = (16 + RG - 1) / RG;
+  constexpr bool STATS = MODE == 1, GRED = MODE == 2;
   __shared__ __attribute__((aligned(16))) bf16_t Bs[NP * LDB];
-  __shared__ __attribute__((aligned(16))) bf16_t Cs[PWS_WAVES][MS * 16 * LDC];
+  __shared__ __attribute__((aligned(16))) bf16_t Cs[PWS_WAVES][16 * LDC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, lg = lane >> 4;
+  const int n0 = blockIdx.y * NP;
 
   for (int idx = tid; idx < NP * KT * 4; idx += 256) {  // weights -> LDS, k >= K zero
     const int r = idx / (KT * 4), k = (idx - r * (KT * 4)) * 8;
     bf16x8 v;
-    if (k < K) v = *(const bf16x8*)(Wt + (long)r * K + k);
+    if (k < K) v = *(const bf16x8*)(Wt + (long)(n0 + r) * K + k);
     else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (bf16_t)0.f;
@@ -757,25 +766,49 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
   const long tstride = (long)gridDim.x * PWS_WAVES;
   long t = (long)blockIdx.x * PWS_WAVES + wave;
   bf16_t* cs = Cs[wave];
+  // gred: this lane's fixed chunk (row group rg, channels gc .. gc+7) and its BatchNorm constants
+  const int rg = lane / CPR, cc = lane - (lane / CPR) * CPR;
+  const bool gact = GRED && rg < RG;
+  const int gc = n0 + cc * 8;
+  constexpr int GV = GRED ? 8 : 1;
+  float gsc[GV], gsh[GV], gmu[GV], grs[GV], sg[GV], sgx[GV];
+  if constexpr (GRED) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gred_coef(gr.p, gc + e, gsc[e], gsh[e], gmu[e], grs[e]);
+      sg[e] = sgx[e] = 0.f;
+    }
+  }
 
-  // A fragments of sub-step (tile, s): rows tile*128 + s*16*MS + 16i + fr, k 32kt + 8lg
-  auto load_a = [&](bf16x8 (&a)[MS][KT], long tile, int s) {
+  // A fragments of sub-step (tile, s): rows tile*128 + 16s + fr, k 32kt + 8lg
+  auto load_a = [&](bf16x8 (&a)[KT], long tile, int s) {
+    const long row = tile * 128 + s * 16 + fr;
 #pragma unroll
-    for (int i = 0; i < MS; ++i) {
-      const long row = tile * 128 + s * (MS * 16) + i * 16 + fr;
+    for (int kt = 0; kt < KT; ++kt) {
+      const int k = kt * 32 + lg * 8;
+      if (row < M && k < K) a[kt] = *(const bf16x8*)(X + row * ldx + k);
+      else {
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
-        const int k = kt * 32 + lg * 8;
-        if (row < M && k < K) a[i][kt] = *(const bf16x8*)(X + row * ldx + k);
-        else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) a[i][kt][e] = (bf16_t)0.f;
-        }
+        for (int e = 0; e < 8; ++e) a[kt][e] = (bf16_t)0.f;
       }
     }
   };
-  bf16x8 ab[MS][KT], an[MS][KT];
-  if (t < ntiles) load_a(ab, t, 0);
+  // gred: this lane's rows of gr.y for the sub-step starting at row rs (one sub-step ahead)
+  auto load_y = [&](bf16x8 (&yv)[GRED ? JN : 1], long rs) {
+    if constexpr (GRED) {
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        const int rr = rg + RG * j;
+        if (gact && rr < 16 && rs + rr < M) yv[j] = *(const bf16x8*)((const bf16_t*)gr.y + (rs + rr) * ldy + gc);
+      }
+    }
+  };
+  bf16x8 ab[KT], an[KT];
+  bf16x8 yb[GRED ? JN : 1], yn[GRED ? JN : 1];
+  if (t < ntiles) {
+    load_a(ab, t, 0);
+    load_y(yb, t * 128);
+  }
   for (; t < ntiles; t += tstride) {
     const long row0 = t * 128;
     const int left = M - row0 < 128 ? (int)(M - row0) : 128;  // valid rows of this tile
@@ -785,46 +818,42 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
     for (int b = 0; b < NT; ++b) piv[b] = s1[b] = s2[b] = 0.f;
 #pragma unroll 1
     for (int s = 0; s < SUB; ++s) {
-      {  // prefetch the next sub-step (the next tile's first one after the last)
+      const long rs = row0 + s * 16;
+      {  // prefetch the next sub-step (the next tile's first one after the last): A and gr.y
         const long tn = s + 1 < SUB ? t : t + tstride;
-        if (tn < ntiles) load_a(an, tn, s + 1 < SUB ? s + 1 : 0);
+        if (tn < ntiles) {
+          load_a(an, tn, s + 1 < SUB ? s + 1 : 0);
+          if constexpr (GRED) load_y(yn, tn * 128 + (s + 1 < SUB ? s + 1 : 0) * 16);
+        }
       }
       // the weight fragments are re-read from LDS every sub-step (kept out of registers)
       asm volatile("" ::: "memory");
-      f32x4 acc[MS][NT];
+      f32x4 acc[NT];
 #pragma unroll
-      for (int i = 0; i < MS; ++i)
-#pragma unroll
-        for (int b = 0; b < NT; ++b) acc[i][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < NT; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int b = 0; b < NT; ++b) {
           const bf16x8 bf = *(const bf16x8*)(Bs + (b * 16 + fr) * LDB + kt * 32 + lg * 8);
-#pragma unroll
-          for (int i = 0; i < MS; ++i)
-            acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab[i][kt], bf, acc[i][b], 0, 0, 0);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab[kt], bf, acc[b], 0, 0, 0);
         }
 #pragma unroll
-      for (int i = 0; i < MS; ++i)
-#pragma unroll
-        for (int kt = 0; kt < KT; ++kt) ab[i][kt] = an[i][kt];
+      for (int kt = 0; kt < KT; ++kt) ab[kt] = an[kt];
       // epilogue, one 16-wide N tile at a time: round once (the statistics and the staged value
       // are the stored one), statistics, stage into this wave's LDS slot
 #pragma unroll
       for (int b = 0; b < NT; ++b) {
-        float v[MS][4];
+        float v[4];
 #pragma unroll
-        for (int i = 0; i < MS; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[i][r] = (float)(bf16_t)acc[i][b][r];
+        for (int r = 0; r < 4; ++r) v[r] = (float)(bf16_t)acc[b][r];
         if constexpr (STATS) {
           if (s == 0) {  // pivot: mean of the tile's first (up to) 8 valid rows, this column
             float p = 0.f;
             if (lg < 2) {
 #pragma unroll
               for (int r = 0; r < 4; ++r)
-                if (full || lg * 4 + r < left) p += v[0][r];
+                if (full || lg * 4 + r < left) p += v[r];
             }
             p += __shfl_xor(p, 16, 64);
             p = __shfl(p, fr, 64);
@@ -832,33 +861,48 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
             piv[b] = full ? p * 0.125f : p / (float)pc;
           }
 #pragma unroll
-          for (int i = 0; i < MS; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              if (full || s * (MS * 16) + i * 16 + lg * 4 + r < left) {
-                const float d = v[i][r] - piv[b];
-                s1[b] += d;
-                s2[b] = fmaf(d, d, s2[b]);
-              }
+          for (int r = 0; r < 4; ++r) {
+            if (full || s * 16 + lg * 4 + r < left) {
+              const float d = v[r] - piv[b];
+              s1[b] += d;
+              s2[b] = fmaf(d, d, s2[b]);
             }
+          }
         }
 #pragma unroll
-        for (int i = 0; i < MS; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) cs[(i * 16 + lg * 4 + r) * LDC + b * 16 + fr] = (bf16_t)v[i][r];
+        for (int r = 0; r < 4; ++r) cs[(lg * 4 + r) * LDC + b * 16 + fr] = (bf16_t)v[r];
       }
       __builtin_amdgcn_wave_barrier();
-      const long rs = row0 + s * (MS * 16);
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      if constexpr (GRED) {
+        // fixed-chunk write-back + the BatchNorm-backward sums of the stored values
+        if (gact) {
 #pragma unroll
-      for (int it = 0; it < (MS * 16 * CPR + 63) / 64; ++it) {
-        const int idx = it * 64 + lane;
-        if ((MS * 16 * CPR) % 64 != 0 && idx >= MS * 16 * CPR) break;
-        const int rr = idx / CPR, cc = idx - rr * CPR;
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 v = *(const u32x4*)(cs + rr * LDC + cc * 8);
-        if (rs + rr < M) ROD_ST_OUT((u32x4*)(Y + (rs + rr) * ldy + cc * 8), v);
+          for (int j = 0; j < JN; ++j) {
+            const int rr = rg + RG * j;
+            if (rr >= 16 || rs + rr >= M) continue;
+            const bf16x8 dv = *(const bf16x8*)(cs + rr * LDC + cc * 8);
+            ROD_ST_OUT((u32x4*)(Y + (rs + rr) * ldy + gc), __builtin_bit_cast(u32x4, dv));
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              gred_acc((float)dv[e], (float)yb[j][e], gsc[e], gsh[e], gmu[e], grs[e], gr.p.act, sg[e], sgx[e]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < (16 * CPR + 63) / 64; ++it) {
+          const int idx = it * 64 + lane;
+          if ((16 * CPR) % 64 != 0 && idx >= 16 * CPR) break;
+          const int rr = idx / CPR, c8 = idx - rr * CPR;
+          const u32x4 v = *(const u32x4*)(cs + rr * LDC + c8 * 8);
+          if (rs + rr < M) ROD_ST_OUT((u32x4*)(Y + (rs + rr) * ldy + n0 + c8 * 8), v);
+        }
       }
       __builtin_amdgcn_wave_barrier();
+      if constexpr (GRED) {
+#pragma unroll
+        for (int j = 0; j < JN; ++j) yb[j] = yn[j];
+      }
     }
     if constexpr (STATS) {
       const float n = (float)left;
@@ -871,42 +915,83 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
         q += __shfl_xor(q, 32, 64);
         if (lane < 16) {
           const float dm = full ? a * (1.0f / 128.0f) : a / n;
-          store_stat_part(part, NP, t, b * 16 + lane, n, piv[b] + dm, fmaxf(q - a * dm, 0.f));
+          store_stat_part(part, Cout, t, n0 + b * 16 + lane, n, piv[b] + dm, fmaxf(q - a * dm, 0.f));
         }
+      }
+    }
+    if constexpr (GRED) {
+      // the tile's part: row groups added in order (lane rg*CPR + cc holds group rg of chunk cc)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float a = sg[e], q = sgx[e];
+#pragma unroll
+        for (int k = 1; k < RG; ++k) {
+          a += __shfl(sg[e], cc + k * CPR, 64);
+          q += __shfl(sgx[e], cc + k * CPR, 64);
+        }
+        if (gact && rg == 0) {
+          gr.parts[t * 2 * Cout + gc + e] = a;
+          gr.parts[t * 2 * Cout + Cout + gc + e] = q;
+        }
+        sg[e] = sgx[e] = 0.f;
       }
     }
   }
 }
 
-// rod_conv_fwd's streaming path (pw_stream_kernel): bf16 1x1, no bias / prologue / gred, K <= 64
-// (K % 8 == 0), Cout = 16 * NT for NT in {6, 9, 12}, 16-byte aligned rows.  ROD_PW_STREAM=0 turns
-// it off (A/B measurement switch).
-static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long M, int K, int Cout, int ldx, int ldy,
-                             float* stats, hipStream_t s) {
+// rod_conv_fwd's streaming path (pw_stream_kernel): bf16 1x1, no bias / prologue, K <= 96
+// (K % 8 == 0), Cout a multiple of 96, 144 or 192 (N groups of 6, 9 or 12 MFMA tiles),
+// 16-byte aligned rows, M >= 4096; statistics parts or the gred sums (dense y) or neither.
+// ROD_PW_STREAM=0 turns it off (A/B measurement switch).
+static int pw_stream_groups(long M, int K, int Cout, int& nt, bool gred = false) {
   static const bool off = getenv("ROD_PW_STREAM") && atoi(getenv("ROD_PW_STREAM")) == 0;
-  if (off || K > 64 || K % 8 || Cout % 16 || M < 4096) return false;
-  const int nt = Cout / 16, kt = K > 32 ? 2 : 1;
+  if (off || K > 96 || K % 8 || Cout % 16 || M < 4096) return 0;
+  // gred: narrow groups (3 MFMA tiles: the lane's fixed chunks span more rows, fewer VGPRs for
+  // its BatchNorm constants, row sums and prefetched gr.y); otherwise the widest that divides Cout
+  static const int gred_first[] = {3, 2, 4, 6, 9, 12, 8};
+  static const int wide_first[] = {12, 9, 6, 8, 4, 3, 2};
+  for (int c : gred ? gred_first : wide_first) {
+    if (Cout % (16 * c) == 0) {
+      nt = c;
+      return Cout / (16 * c);
+    }
+  }
+  return 0;
+}
+static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long M, int K, int Cout, int ldx, int ldy,
+                             float* stats, const BnGred* gr, hipStream_t s) {
+  int nt = 0;
+  const int ng = pw_stream_groups(M, K, Cout, nt, gr != nullptr);
+  if (ng == 0 || (gr && (stats || ldy != Cout))) return false;
+  const int kt = K > 64 ? 3 : K > 32 ? 2 : 1;
   const long ntiles = cdivl(M, 128);
-  // waves: <= 3 blocks of 4 waves per CU, every wave the same number of tiles (+-1)
-  const long maxw = 256L * 3 * PWS_WAVES;
+  // waves: <= 3 blocks of 4 waves per CU (over all N groups), every wave the same number of
+  // tiles (+-1)
+  const long maxw = cdivl(256L * 3 * PWS_WAVES, ng);
   const long per = cdivl(ntiles, maxw);
-  const int blocks = (int)cdivl(cdivl(ntiles, per), PWS_WAVES);
-#define PWS(NT_, KT_)                                                                                            \
-  do {                                                                                                           \
-    if (stats)                                                                                                   \
-      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, true>), dim3(blocks), dim3(256), 0, s, x, wt, y, M, K, ldx, \
-                         ldy, stats);                                                                            \
-    else                                                                                                         \
-      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, false>), dim3(blocks), dim3(256), 0, s, x, wt, y, M, K,     \
-                         ldx, ldy, nullptr);                                                                     \
-    return true;                                                                                                 \
+  const dim3 grid((unsigned)cdivl(cdivl(ntiles, per), PWS_WAVES), ng);
+  const BnGred g = gr ? *gr : BnGred{};
+#define PWS(NT_, KT_)                                                                                           \
+  do {                                                                                                          \
+    if (gr)                                                                                                     \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, 2>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, ldy, \
+                         nullptr, g);                                                                           \
+    else if (stats)                                                                                             \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, 1>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, ldy, \
+                         stats, g);                                                                             \
+    else                                                                                                        \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, 0>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, ldy, \
+                         nullptr, g);                                                                           \
+    return true;                                                                                                \
   } while (0)
-  if (nt == 6 && kt == 1) PWS(6, 1);
-  if (nt == 9 && kt == 1) PWS(9, 1);
-  if (nt == 12 && kt == 1) PWS(12, 1);
-  if (nt == 6 && kt == 2) PWS(6, 2);
-  if (nt == 9 && kt == 2) PWS(9, 2);
-  if (nt == 12 && kt == 2) PWS(12, 2);
+#define PWK(NT_)                  \
+  if (nt == NT_) {                \
+    if (kt == 1) PWS(NT_, 1);     \
+    else if (kt == 2) PWS(NT_, 2); \
+    else PWS(NT_, 3);             \
+  }
+  PWK(2) PWK(3) PWK(4) PWK(6) PWK(8) PWK(9) PWK(12)
+#undef PWK
 #undef PWS
   return false;
 }
@@ -1747,8 +1832,8 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
     return;
   }
   if constexpr (sizeof(T) == 2) {
-    if (ksize == 1 && !pro && !gr && !bias && va && vb && vy &&
-        pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, s))
+    if (ksize == 1 && !pro && !bias && va && vb && vy &&
+        pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, gr, s))
       return;
   }
   if (ksize == 1) {
@@ -1839,6 +1924,11 @@ static void wgrad_typed(const void* x, const BnPro* pro, const void* dy, float* 
 using namespace rod;
 
 extern "C" {
+
+int rod_conv_fwd_stream_ok(long M, int K, int Cout, int dtype) {
+  int nt = 0;
+  return dtype == ROD_BF16 && pw_stream_groups(M, K, Cout, nt) > 0 ? 1 : 0;
+}
 
 size_t rod_conv_fwd_workspace(int N, int H, int W, int Cin, int Cout, int ksize) {
   const long M = (long)N * H * W;

@@ -23,7 +23,9 @@ _DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
 # debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro
 _DISABLE = set(os.environ.get("ROD_DISABLE", "").split(","))
 # opt-in paths (comma list): gred = BatchNorm-backward reduction fused into the backward-data
-# epilogues (measured slower than the separate streaming reduce on MI355X: DESIGN.md §6)
+# epilogues (measured slower than the separate streaming reduce on MI355X: DESIGN.md §6);
+# gredpw = the same for the 1x1 convs that take the streaming kernel (measured neutral); dwbn,
+# side: DESIGN.md §6
 _ENABLE = set(os.environ.get("ROD_ENABLE", "").split(","))
 
 
@@ -732,7 +734,21 @@ def _conv_bwd_from_dy(x, w, b, ks, dy, pro, need_dx):
     if need_dx:
         wt1 = _prep(w, 1, x.dtype, Cout, Cin, ks)
         dx = torch.empty_like(x)
-        conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks)
+        gred = None
+        if pro is not None and ks == 1 and "gredpw" in _ENABLE and \
+                _abi.lib().rod_conv_fwd_stream_ok(N * H * W, Cout, Cin, dtcode(x)):
+            # opt-in (ROD_ENABLE=gredpw): dx is the gradient of the input's BatchNorm output (an
+            # owned Pending: the depthwise BatchNorm of the block, conv_blocks.py:238-247); the
+            # streaming backward-data also forms that BatchNorm's backward sums over (dx, x),
+            # handed to its producer (_DWBN), which then skips its rod_bn_bwd_reduce pass.
+            # Correct (tests/test_gpu_gred.py, the step tests) but measured no faster: the
+            # reduce passes it removes (-0.8 ms) come back as backward-data time (+0.6-0.8 ms:
+            # the extra read of x at ~3 TB/s, narrow N groups re-reading dy), DESIGN.md §6
+            parts = torch.empty((-(-(N * H * W) // 128), 2, Cin), dtype=torch.float32, device=x.device)
+            gred = (x,) + tuple(pro) + (parts,)
+        conv_fwd_raw(dy, wt1, None, dx, N, H, W, Cout, Cin, ks, gred=gred)
+        if gred is not None:
+            _put_bn_parts(dx, gred[-1])
     return dx
 
 
@@ -831,12 +847,20 @@ class _DWBN(torch.autograd.Function):
         x, w, y, mean, rstd = ctx.saved_tensors
         gamma, beta = ctx.gb
         N, H, W, C, s, pt, pl, Ho, Wo = ctx.geo
+        # the BatchNorm-backward sums of (dz, y) when the consumer's backward-data formed them
+        # (the project conv's streaming kernel, _conv_bwd_from_dy)
+        parts = _take_bn_parts(dz)
+
+        def coef_d():
+            if parts is not None:
+                return bn_bwd_coef_from_parts(parts, N * Ho * Wo, C, rstd, gamma, beta, _needs(gamma), _needs(beta))
+            return bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
         if _needs(w) and ctx.needs_input_grad[0] and _dw_fused_ok(N, Ho, Wo, C, x.dtype, s):
             # one pass: BN_d backward apply + backward-data + filter gradient (+ the input
             # BatchNorm's backward sums, handed to the producer) — rod_dw3x3_bwd_fused
             # (ABI 12 stride 1, ABI 13 stride 2)
             dz = dz.contiguous()
-            coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            coef = coef_d()
             dx = torch.empty_like(x)
             gparts = None
             if ctx.ipro is not None:
@@ -857,7 +881,7 @@ class _DWBN(torch.autograd.Function):
             # Bit-identical, but measured no faster per step: the apply pass it
             # removes (-1.59 ms) comes back as filter-gradient time (+1.22 ms, VALU-bound)
             dz = dz.contiguous()
-            coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            coef = coef_d()
             dy = torch.empty_like(y)
             ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)
             det = lambda t: None if t is None else t.detach()
@@ -870,7 +894,10 @@ class _DWBN(torch.autograd.Function):
                 _abi.call("rod_dw3x3_bwd_data", dy, w, dx, *_gred_args(None), N, H, W, C, s, pt, pl, Ho, Wo,
                           dtcode(x), stream())
             return dx, None, None, None, None
-        dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+        if parts is not None:
+            dy = _bn_bwd_apply(dz, y, mean, rstd, gamma, beta, ctx.act, coef_d())
+        else:
+            dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
         if _needs(w):
             def filt():
                 ws = workspace(_abi.query("rod_dw3x3_bwd_filter_workspace", N, Ho, Wo, C), x.device)

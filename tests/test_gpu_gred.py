@@ -83,7 +83,14 @@ def test_dw_bwd_data_gred(dev, dtype, C, stride, H, W):
                                               (1, 160, 960, (2, 3, 5), ops.ROD_ACT_RELU6),
                                               (3, 128, 128, (2, 10, 18), ops.ROD_ACT_LEAKY),
                                               (3, 36, 36, (2, 10, 18), ops.ROD_ACT_LEAKY),
-                                              (1, 36, 128, (2, 7, 9), ops.ROD_ACT_LEAKY)])
+                                              (1, 36, 128, (2, 7, 9), ops.ROD_ACT_LEAKY),
+                                              # streaming kernel (pw_stream_kernel, ABI 14): M >= 4096, not a
+                                              # multiple of the 128-row part; N groups of 192 / 144 / 96
+                                              (1, 24, 144, (2, 45, 81), ops.ROD_ACT_RELU6),
+                                              (1, 16, 32, (1, 64, 70), ops.ROD_ACT_RELU6),
+                                              (1, 32, 192, (2, 23, 97), ops.ROD_ACT_RELU6),
+                                              (1, 64, 384, (1, 45, 93), ops.ROD_ACT_RELU6),
+                                              (1, 96, 576, (1, 45, 91), ops.ROD_ACT_LEAKY)])
 def test_conv_bwd_data_gred(dev, dtype, ks, Cdz, Cy, NHW, act):
     """rod_conv_fwd(dz_out, wt mode 1) as the backward-data of a conv Cy -> Cdz."""
     g = torch.Generator().manual_seed(23)
