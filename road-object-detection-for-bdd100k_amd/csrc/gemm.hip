@@ -941,11 +941,13 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
 
 // rod_conv_fwd's streaming path (pw_stream_kernel): bf16 1x1, no bias / prologue, K <= 96
 // (K % 8 == 0), Cout a multiple of 96, 144 or 192 (N groups of 6, 9 or 12 MFMA tiles),
-// 16-byte aligned rows, M >= 4096; statistics parts or the gred sums (dense y) or neither.
+// 16-byte aligned rows, M >= 65536; statistics parts or the gred sums (dense y) or neither.
 // ROD_PW_STREAM=0 turns it off (A/B measurement switch).
 static int pw_stream_groups(long M, int K, int Cout, int& nt, bool gred = false) {
   static const bool off = getenv("ROD_PW_STREAM") && atoi(getenv("ROD_PW_STREAM")) == 0;
-  if (off || K > 96 || K % 8 || Cout % 16 || M < 4096) return 0;
+  // >= 512 row tiles: on the 45x80 maps (225 tiles) the tiled kernel measured faster
+  // (tools/conv_bench.py: 96->576 18.2 vs 23.1 us)
+  if (off || K > 96 || K % 8 || Cout % 16 || M < 65536) return 0;
   // gred: narrow groups (3 MFMA tiles: the lane's fixed chunks span more rows, fewer VGPRs for
   // its BatchNorm constants, row sums and prefetched gr.y); otherwise the widest that divides Cout
   static const int gred_first[] = {3, 2, 4, 6, 9, 12, 8};

@@ -84,13 +84,13 @@ def test_dw_bwd_data_gred(dev, dtype, C, stride, H, W):
                                               (3, 128, 128, (2, 10, 18), ops.ROD_ACT_LEAKY),
                                               (3, 36, 36, (2, 10, 18), ops.ROD_ACT_LEAKY),
                                               (1, 36, 128, (2, 7, 9), ops.ROD_ACT_LEAKY),
-                                              # streaming kernel (pw_stream_kernel, ABI 14): M >= 4096, not a
-                                              # multiple of the 128-row part; N groups of 192 / 144 / 96
-                                              (1, 24, 144, (2, 45, 81), ops.ROD_ACT_RELU6),
-                                              (1, 16, 32, (1, 64, 70), ops.ROD_ACT_RELU6),
-                                              (1, 32, 192, (2, 23, 97), ops.ROD_ACT_RELU6),
-                                              (1, 64, 384, (1, 45, 93), ops.ROD_ACT_RELU6),
-                                              (1, 96, 576, (1, 45, 91), ops.ROD_ACT_LEAKY)])
+                                              # streaming kernel (pw_stream_kernel, ABI 14): M >= 65536, not a
+                                              # multiple of the 128-row part; N groups of 48 / 32 / 64
+                                              (1, 24, 144, (2, 181, 321), ops.ROD_ACT_RELU6),
+                                              (1, 16, 32, (1, 257, 259), ops.ROD_ACT_RELU6),
+                                              (1, 32, 192, (2, 181, 183), ops.ROD_ACT_RELU6),
+                                              (1, 64, 384, (1, 257, 257), ops.ROD_ACT_RELU6),
+                                              (1, 96, 576, (1, 256, 257), ops.ROD_ACT_LEAKY)])
 def test_conv_bwd_data_gred(dev, dtype, ks, Cdz, Cy, NHW, act):
     """rod_conv_fwd(dz_out, wt mode 1) as the backward-data of a conv Cy -> Cdz."""
     g = torch.Generator().manual_seed(23)

@@ -183,11 +183,12 @@ def test_conv_epilogue_bn_stats(dev, dtype, ks, Cin, Cout, NHW):
     torch.testing.assert_close(z1.float(), z2.float(), **tol)
 
 
-@pytest.mark.parametrize('Cin,Cout,NHW', [(24, 144, (2, 45, 81)), (16, 96, (1, 37, 131)), (32, 192, (2, 23, 97)),
-                                           (64, 96, (3, 17, 83)), (40, 144, (1, 64, 65)), (8, 192, (1, 33, 129))])
+@pytest.mark.parametrize('Cin,Cout,NHW', [(24, 144, (2, 181, 321)), (16, 96, (1, 257, 259)), (32, 192, (2, 181, 183)),
+                                           (64, 96, (3, 97, 227)), (40, 144, (1, 256, 263)), (8, 192, (1, 259, 255)),
+                                           (64, 384, (1, 257, 257)), (96, 576, (1, 256, 257))])
 def test_pw_stream_expand(dev, Cin, Cout, NHW):
     """The streaming 1x1 forward (pw_stream_kernel: bf16, no bias, K <= 64, Cout % 16 == 0,
-    M >= 4096; M here not a multiple of the 128-row part tile) against the oracle conv, and its
+    M >= 65536; M here not a multiple of the 128-row part tile) against the oracle conv, and its
     statistics parts against the separate statistics pass (ref conv_blocks.py:264-271 expand +
     BatchNorm).  ROD_PW_STREAM=0 would route these shapes to the tiled kernel."""
     g = torch.Generator().manual_seed(14)
