@@ -370,12 +370,12 @@ __device__ __forceinline__ void lds_barrier() {
 // backward-data (DepthwiseConv2dNativeBackpropInput) is this kernel on dy with pads
 // (2-pt, 2-pl).  GRED: the BatchNorm-backward partial sums of the rounded outputs against the
 // pre-BatchNorm y of the layer below (rod_common.h), y prefetched two rows ahead.
-template <typename T, int S, int PACT, bool STATS, bool FLIP, bool GRED>
+template <typename T, int S, int PACT, bool STATS, bool FLIP, bool GRED, int V = Vec16<T>::N>
 __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float* __restrict__ w, T* __restrict__ y,
                                            int H, int W, int C, int pt, int pl, int Ho, int Wo, const DwTile& tl,
                                            float* __restrict__ parts, const BnPro& pro, const BnGred& gr) {
   static_assert(S == 1 || !(FLIP || GRED), "the backward-data form is stride 1");
-  constexpr int V = Vec16<T>::N;
+  typedef PackV<T, V> PK;  // 16-byte packs, or 8-byte (bf16 x 4: half the per-thread state)
   // LDS: prefetch ring of D input rows (S=2: column pairs) + the double-buffered exchange
   // slot; the statistics merge reuses the front after the row loop
   constexpr int XS = 2 * 256 * 16;            // double-buffered exchange slot
@@ -418,23 +418,21 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
   const T* gyn = GRED ? (const T*)gr.y + (long)n * Ho * Wo * C + c : nullptr;
   PackV<T, V> gring[GRED ? 3 : 1];
 
-  auto cvt = [&](const Vec16<T>& r, bool ok, float (&o)[V]) {
-    PackV<T, V> pk;
-    pk.v = r.v;
-    in.cvt(pk, ok, o);
+  auto cvt = [&](const PK& r, bool ok, float (&o)[V]) {
+    in.cvt(r, ok, o);
     if constexpr (PACT < 0) {
 #pragma unroll
       for (int v = 0; v < V; ++v) o[v] = ok ? o[v] : 0.f;
     }
   };
   auto publish = [&](const float (&o)[V], int buf) {
-    Vec16<T> st;
+    PK st;
 #pragma unroll
     for (int v = 0; v < V; ++v) st.set(v, o[v]);
     st.store(xs + (buf * 256 + tid) * V);
   };
   auto emit = [&](const float (&a)[V], int ho, bool first) {
-    Vec16<T> o;
+    PK o;
 #pragma unroll
     for (int v = 0; v < V; ++v) o.set(v, a[v]);
     o.store_out(yn + ((long)ho * Wo + wo) * C);
@@ -464,7 +462,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
   if constexpr (S == 1) {
     const int hi0 = ho0 - pt;
     const int nin = ho1 - ho0 + 2;
-    Vec16<T> ring[3];
+    PK ring[3];
     bool rok[3];
     auto issue = [&](int k, int q) {
       const int hi = hi0 + q;
@@ -497,7 +495,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
         publish(cen, buf);
         __syncthreads();
         if (comp) {
-          Vec16<T> L, R;
+          PK L, R;
           L.load(xs + (buf * 256 + tid - CVb) * V);
           R.load(xs + (buf * 256 + tid + CVb) * V);
           // row q feeds output m = q - i with weight row i: slot (k - i) mod 3
@@ -528,7 +526,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
   } else {
     const int hi0 = 2 * ho0 - pt;
     const int nin = 2 * (ho1 - ho0) + 1;
-    Vec16<T> ring[4][2];
+    PK ring[4][2];
     bool rok[4][2];
     auto issue = [&](int k, int q) {
       const int hi = hi0 + q;
@@ -557,7 +555,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
         publish(c0, buf);
         __syncthreads();
         if (comp) {
-          Vec16<T> R;
+          PK R;
           R.load(xs + (buf * 256 + tid + CVb) * V);
           // q = q0 + k, q0 % 4 == 0: k even -> weight row 0 into output q/2 (slot k/2) and
           // row 2 into output q/2 - 1 (slot 1 - k/2, then complete); k odd -> row 1 into
@@ -659,12 +657,12 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
   }
 }
 
-template <typename T, int S, int PACT, bool STATS>
+template <typename T, int S, int PACT, bool STATS, int V = Vec16<T>::N>
 __global__ void __launch_bounds__(256) dw3x3_fwd_lx_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                            T* __restrict__ y, int H, int W, int C, int pt, int pl,
                                                            int Ho, int Wo, DwTile tl, float* __restrict__ parts,
                                                            BnPro pro) {
-  dw_lx_body<T, S, PACT, STATS, false, false>(x, w, y, H, W, C, pt, pl, Ho, Wo, tl, parts, pro, BnGred{});
+  dw_lx_body<T, S, PACT, STATS, false, false, V>(x, w, y, H, W, C, pt, pl, Ho, Wo, tl, parts, pro, BnGred{});
 }
 // stride-1 backward-data (DepthwiseConv2dNativeBackpropInput): the body with flipped taps
 template <typename T, bool GRED>
@@ -1363,16 +1361,35 @@ static long dw_lx_parts(int N, int Ho, int Wo, int C, int S, int V) {
   const DwTile t = dw_tile(N, Ho, Wo, C, S, V);
   return (long)N * t.strips * t.coltiles;
 }
+// channel pack of the forward LX kernel: 16-byte packs, or (bf16, output maps of <= 512K pixels)
+// 8-byte packs with half the per-thread weights / accumulators / statistics in registers (106
+// instead of 192 VGPRs with the prologue and statistics: 4 waves / SIMD instead of 2).  Measured
+// (tools/dw_bench.py fwdpro): 180x320x192 126 -> 109 us, 90x160x384 68 -> 60, 45x80x576 41 -> 33,
+// 23x40x960 26 -> 23; slower on the 720p / 360p maps (360x640x144 s2 188 -> 206), which keep 16.
+// ROD_DW_FWD_V=4 / 8 forces one width (A/B switch).
+static int dw_fwd_v(int dtype, long pixels) {
+  static const int env = getenv("ROD_DW_FWD_V") ? atoi(getenv("ROD_DW_FWD_V")) : 0;
+  if (dtype == ROD_F32) return 4;
+  if (env == 4 || env == 8) return env;
+  return pixels <= 512L * 1024 ? 4 : 8;
+}
 template <typename T>
 static long dw_fwd_lx_launch(const void* x, const BnPro* pro, const float* w, void* y, float* parts, int N, int H,
                              int W, int C, int S, int pt, int pl, int Ho, int Wo, hipStream_t s) {
-  const DwTile t = dw_tile(N, Ho, Wo, C, S, Vec16<T>::N);
+  const int V = dw_fwd_v(sizeof(T) == 2 ? ROD_BF16 : ROD_F32, (long)N * Ho * Wo);
+  const DwTile t = dw_tile(N, Ho, Wo, C, S, V);
   const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
   const BnPro pv = pro ? *pro : BnPro{};
   const int pa = !pro ? -1 : (pro->act == ROD_ACT_RELU6 ? ROD_ACT_RELU6 : DW_ACT_RT);
-#define DWL(S_, PA, ST)                                                                                       \
-  hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, S_, PA, ST>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, C, \
-                     pt, pl, Ho, Wo, t, parts, pv)
+#define DWL(S_, PA, ST)                                                                                           \
+  do {                                                                                                            \
+    if (sizeof(T) == 2 && V == 4)                                                                                 \
+      hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, S_, PA, ST, 4>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W, \
+                         C, pt, pl, Ho, Wo, t, parts, pv);                                                        \
+    else                                                                                                          \
+      hipLaunchKernelGGL((dw3x3_fwd_lx_kernel<T, S_, PA, ST>), grid, dim3(256), 0, s, (const T*)x, w, (T*)y, H, W,  \
+                         C, pt, pl, Ho, Wo, t, parts, pv);                                                        \
+  } while (0)
 #define DWL_PA(S_, ST)                    \
   if (pa == ROD_ACT_RELU6) DWL(S_, ROD_ACT_RELU6, ST); \
   else if (pa == DW_ACT_RT) DWL(S_, DW_ACT_RT, ST); \
@@ -1477,7 +1494,7 @@ int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C, int stride, int dtype
   // exactly the parts the launch for 16-byte-aligned x / y writes: the LDS-exchange kernel
   // when C fills 16-byte packs, else the register-strip kernel's grid
   const int V16 = dtype == ROD_F32 ? 4 : 8;
-  if (C % V16 == 0) return (int)dw_lx_parts(N, Ho, Wo, C, stride == 2 ? 2 : 1, V16);
+  if (C % V16 == 0) return (int)dw_lx_parts(N, Ho, Wo, C, stride == 2 ? 2 : 1, dw_fwd_v(dtype, (long)N * Ho * Wo));
   const int V = dtype == ROD_F32 ? (C % 4 == 0 ? 4 : 1) : (C % 4 == 0 ? 4 : 1);
   const dim3 g = dw_fwd_grid(N, Ho, Wo, C, V);
   return (int)(g.x * g.y * g.z);
