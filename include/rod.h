@@ -347,10 +347,13 @@ int rod_ir_block_fwd(const void* x, const void* we, const float* e_mean, const f
                      const float* p_mean, const float* p_rstd, const float* p_gamma, const float* p_beta,
                      int residual, void* y, int N, int H, int W, int Cin, int inner, int Cout, int stride,
                      int dtype, void* stream);
-/* Variant switch (process-wide; returns the previous value): 1 (default) runs a persistent
- * launch — every chunk's parameters resident in LDS, each workgroup walking tiles with the
- * next tile's input window in flight — wherever those parameters fit in LDS; 0 always runs
- * one tile per workgroup.  Both give identical output. */
+/* Variant switch (process-wide; returns the previous value).  Bit 0 (set by default): a
+ * persistent launch — every chunk's parameters resident in LDS, each workgroup walking tiles
+ * with the next tile's input window in flight — wherever those parameters fit in LDS; clear:
+ * one tile per workgroup (identical output).  Bit 1 (ABI 14, clear by default): the exact
+ * rounding of the unfused eval chain (each conv output rounded to bf16 before its BatchNorm),
+ * bit-identical to it; clear: the accumulators go through BatchNorm (+ ReLU6) in fp32 and are
+ * rounded once. */
 int rod_ir_block_set_mode(int mode);
 /* 1 when the block runs the persistent variant (all of its parameters fit in LDS). */
 int rod_ir_block_persistent(int Cin, int inner, int Cout, int stride, int residual, int dtype);

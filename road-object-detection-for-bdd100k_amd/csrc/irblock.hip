@@ -20,12 +20,16 @@
 // double-buffered LDS parameter block, so no phase waits on an L2 round trip.
 // HBM traffic per block: the input window and the output tile (plus L2-resident weights).
 //
-// Rounding follows the unfused librod eval path exactly — each conv output rounded to bf16,
-// the BatchNorm prologue form act(fma(y, scale, offset)) rounded to bf16, the same MFMA
-// k-step order for both GEMMs (32-deep steps in ascending k) and the depthwise taps in raster
-// order — so the output is bit-identical to rod_conv_fwd -> rod_dw3x3_fwd -> rod_conv_fwd ->
-// rod_bn_apply on the same weights wherever those run without split-K
-// (tests/test_gpu_irblock.py).
+// Rounding (default): the expand / depthwise / project accumulators go through their BatchNorm
+// (+ ReLU6) in fp32 and are rounded to bf16 once — the unfused chain rounds each conv output
+// first, then the BatchNorm result again; skipping the first rounding is closer to the fp32
+// reference and saves three packed instructions per pair of expanded values (the kernel is
+// VALU-issue bound).  Exact mode (rod_ir_block_set_mode bit 1) follows the unfused librod eval
+// path exactly — each conv output rounded to bf16, the BatchNorm prologue form
+// act(fma(y, scale, offset)) rounded to bf16, the same MFMA k-step order for both GEMMs (32-deep
+// steps in ascending k) and the depthwise taps in raster order — bit-identical to rod_conv_fwd
+// -> rod_dw3x3_fwd -> rod_conv_fwd -> rod_bn_apply wherever those run without split-K
+// (tests/test_gpu_irblock.py checks both modes).
 #include "rod_common.h"
 
 namespace rod {
@@ -75,6 +79,21 @@ __device__ __forceinline__ unsigned relu6_pair(float a, float b, ir_f32x2 sc2, i
   return __builtin_bit_cast(unsigned, o);
 }
 
+// the single-rounding form (the default, EX = false): the BatchNorm fma on the fp32 accumulators
+// themselves — no bf16 rounding of the conv / depthwise output before its BatchNorm, one rounding
+// after the ReLU6 — three packed-pair instructions fewer per pair of expanded values
+__device__ __forceinline__ unsigned relu6_pair_nr(float a, float b, ir_f32x2 sc2, ir_f32x2 sh2) {
+  ir_f32x2 v = {a, b};
+  v = __builtin_elementwise_fma(v, sc2, sh2);
+  const ir_bf16x2 o = ir_bf16x2{(bf16_t)act_t<ROD_ACT_RELU6>(v.x), (bf16_t)act_t<ROD_ACT_RELU6>(v.y)};
+  return __builtin_bit_cast(unsigned, o);
+}
+template <bool EX>
+__device__ __forceinline__ unsigned relu6_pair_t(float a, float b, ir_f32x2 sc2, ir_f32x2 sh2) {
+  if constexpr (EX) return relu6_pair(a, b, sc2, sh2);
+  else return relu6_pair_nr(a, b, sc2, sh2);
+}
+
 // LDS layout (elements), all offsets multiples of 8 bf16 (16 bytes)
 template <int S>
 struct IrLayout {
@@ -114,7 +133,7 @@ struct IrLayout {
 // XP == 0: one tile per workgroup, chunk parameters streamed through a double buffer.
 // XP > 0 (persistent): every chunk's parameters resident in LDS, the workgroup walks tiles and
 // holds the next tile's input window (XP 16-byte pieces per thread) in registers meanwhile.
-template <int S, int NT, int XP>
+template <int S, int NT, int XP, bool EX>
 __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles) {
   constexpr bool PERSIST = XP > 0;
   using Tl = IrTile<S>;
@@ -393,7 +412,7 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
             unsigned m = emask;
             if (in4 != 15u)
               m &= (((in4 >> (2 * h)) & 1u) ? 0x0000FFFFu : 0u) | (((in4 >> (2 * h + 1)) & 1u) ? 0xFFFF0000u : 0u);
-            o[h] = relu6_pair(acc[i][nt][2 * h], acc[i][nt][2 * h + 1], sc2, sh2) & m;
+            o[h] = relu6_pair_t<EX>(acc[i][nt][2 * h], acc[i][nt][2 * h + 1], sc2, sh2) & m;
           }
           unsigned* dst = (unsigned*)(Es + e * LDE + mt * 16 + 4 * g);
           dst[0] = o[0];
@@ -440,7 +459,7 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
       }
       unsigned o[TW / 2];
 #pragma unroll
-      for (int p = 0; p < TW / 2; ++p) o[p] = relu6_pair(acc[p].x, acc[p].y, dsc2, dsh2) & emask;
+      for (int p = 0; p < TW / 2; ++p) o[p] = relu6_pair_t<EX>(acc[p].x, acc[p].y, dsc2, dsh2) & emask;
 #pragma unroll
       for (int h = 0; h < TW / 8; ++h)
         *(uint4*)(Dt + ch * LDD + oy * TW + 8 * h) = uint4{o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]};
@@ -479,7 +498,8 @@ __global__ void __launch_bounds__(256) ir_block_fwd_kernel(IrArgs a, int ntiles)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = mt * 16 + 4 * g + r;
-        float z = fmaf((float)(bf16_t)accp[i][nt][r], sc, sh);   // project rounded, linear BN
+        // linear BN of the project output (EX: rounded to bf16 first, as the unfused chain)
+        float z = fmaf(EX ? (float)(bf16_t)accp[i][nt][r] : accp[i][nt][r], sc, sh);
         if (a.residual && co < Cout) {
           const int oy = q / TW, ox = q - oy * TW;   // S == 1: the input pixel under q
           z = z + (float)Xs[((oy + 1) * IW + ox + 1) * LDX + co];
@@ -559,12 +579,12 @@ static int ir_num_cus() {
   return cus;
 }
 
-template <int S, int NT, int XP>
+template <int S, int NT, int XP, bool EX>
 static void ir_launch(const IrArgs& a, int N, hipStream_t s) {
   using Tl = IrTile<S>;
   const int nchunk = cdiv(a.inner, IR_CK);
   const size_t lds = ir_lds<S>(a.Cin, a.Cout, XP ? nchunk : 2);
-  const void* fn = (const void*)ir_block_fwd_kernel<S, NT, XP>;
+  const void* fn = (const void*)ir_block_fwd_kernel<S, NT, XP, EX>;
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int ntx = cdiv(a.Wo, Tl::TW), nty = cdiv(a.Ho, Tl::TH);
   const int ntiles = ntx * nty * N;
@@ -572,23 +592,28 @@ static void ir_launch(const IrArgs& a, int N, hipStream_t s) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
     const int grid = std::min(ntiles, per_cu * ir_num_cus());
-    hipLaunchKernelGGL((ir_block_fwd_kernel<S, NT, XP>), dim3(grid), dim3(256), lds, s, a, ntiles);
+    hipLaunchKernelGGL((ir_block_fwd_kernel<S, NT, XP, EX>), dim3(grid), dim3(256), lds, s, a, ntiles);
   } else {
     dim3 grid(ntx, nty, N);
-    hipLaunchKernelGGL((ir_block_fwd_kernel<S, NT, XP>), grid, dim3(256), lds, s, a, ntiles);
+    hipLaunchKernelGGL((ir_block_fwd_kernel<S, NT, XP, EX>), grid, dim3(256), lds, s, a, ntiles);
   }
 }
 
+template <int S, int NT, bool EX>
+static void ir_launch_xp2(const IrArgs& a, int N, hipStream_t s) {
+  const int xp = (ir_persist_mode & 1) ? ir_persist_pieces(a.Cin, a.inner, a.Cout, S) : 0;
+  if constexpr (S == 1) {
+    if (xp == 3) return ir_launch<S, NT, 3, EX>(a, N, s);
+    if (xp == 6) return ir_launch<S, NT, 6, EX>(a, N, s);
+  } else {
+    if (xp == 5) return ir_launch<S, NT, 5, EX>(a, N, s);
+  }
+  ir_launch<S, NT, 0, EX>(a, N, s);
+}
 template <int S, int NT>
 static void ir_launch_xp(const IrArgs& a, int N, hipStream_t s) {
-  const int xp = ir_persist_mode ? ir_persist_pieces(a.Cin, a.inner, a.Cout, S) : 0;
-  if constexpr (S == 1) {
-    if (xp == 3) return ir_launch<S, NT, 3>(a, N, s);
-    if (xp == 6) return ir_launch<S, NT, 6>(a, N, s);
-  } else {
-    if (xp == 5) return ir_launch<S, NT, 5>(a, N, s);
-  }
-  ir_launch<S, NT, 0>(a, N, s);
+  if (ir_persist_mode & 2) ir_launch_xp2<S, NT, true>(a, N, s);
+  else ir_launch_xp2<S, NT, false>(a, N, s);
 }
 
 }  // namespace rod
@@ -597,10 +622,12 @@ using namespace rod;
 
 extern "C" {
 
-// 1 (default): persistent resident-parameter variant where it fits; 0: never (A/B timing)
+// bit 0 (default set): persistent resident-parameter variant where it fits (clear: never, A/B
+// timing); bit 1: the exact-rounding form, bit-identical to the unfused librod eval chain (clear,
+// the default: one rounding per expanded value, tests/test_gpu_irblock.py holds it to the oracle)
 int rod_ir_block_set_mode(int mode) {
   const int old = ir_persist_mode;
-  ir_persist_mode = mode ? 1 : 0;
+  ir_persist_mode = mode & 3;
   return old;
 }
 

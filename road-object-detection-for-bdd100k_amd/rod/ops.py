@@ -991,9 +991,13 @@ def ir_block_preferred(Cin, inner, Cout, stride, residual, dtype):
     return pers and (stride == 1 or Cin <= 16)
 
 
+IR_PERSIST, IR_EXACT = 1, 2
+
+
 def ir_block_set_mode(mode):
-    """rod_ir_block_set_mode: 1 = persistent resident-parameter launch where it fits (default),
-    0 = one tile per workgroup.  Returns the previous mode."""
+    """rod_ir_block_set_mode: bit IR_PERSIST = persistent resident-parameter launch where it fits
+    (default on), bit IR_EXACT = the unfused chain's rounding, bit for bit (default off: one
+    rounding per expanded value).  Returns the previous mode."""
     return int(_abi.lib().rod_ir_block_set_mode(int(mode)))
 
 

@@ -57,6 +57,11 @@ def main():
                 ops.ir_block_fwd(x, we, ev[0], wd, ev[1], wp, ev[2], s, res)
                 ops.ir_block_set_mode(old)
 
+            def fused_exact():  # the unfused chain's rounding, bit for bit
+                old = ops.ir_block_set_mode(ops.IR_PERSIST | ops.IR_EXACT)
+                ops.ir_block_fwd(x, we, ev[0], wd, ev[1], wp, ev[2], s, res)
+                ops.ir_block_set_mode(old)
+
             def unfused():
                 pe = ops.conv2d_bn(x, we, None, 1, ones(inner), zeros(inner), zeros(inner), ones(inner),
                                    ops.ROD_ACT_RELU6, False, 0.997, 1e-3)
@@ -67,7 +72,7 @@ def main():
                 ops.materialize(pp, x if res else None)
             t = {}
             with torch.no_grad():
-                for name, fn in (('fused', fused), ('fused_tile', fused_tile), ('unfused', unfused)):
+                for name, fn in (('fused', fused), ('fused_exact', fused_exact), ('fused_tile', fused_tile), ('unfused', unfused)):
                     # replayed as a HIP graph: GPU time, not the Python dispatch of the unfused chain
                     for _ in range(3):
                         fn()
@@ -93,7 +98,8 @@ def main():
             flops = 2.0 * ntile * (ih * iw * cin * inner + th * tw * inner * cout)
             alg_flops = 2.0 * N * (h * w * cin * inner + ho * wo * inner * cout) + 18.0 * N * ho * wo * inner
             r = {'layer': idx, 'shape': [N, h, w, cin, inner, cout, s, int(res)],
-                 'fused_us': round(t['fused'], 1), 'tile_us': round(t['fused_tile'], 1),
+                 'fused_us': round(t['fused'], 1), 'exact_us': round(t['fused_exact'], 1),
+                 'tile_us': round(t['fused_tile'], 1),
                  'unfused_us': round(t['unfused'], 1),
                  'speedup': round(t['unfused'] / t['fused'], 2),
                  'fused_GBps': round(byts / t['fused'] / 1e3, 1),
@@ -102,6 +108,7 @@ def main():
             rows.append(r)
             print(R, json.dumps(r), flush=True)
         tot = {'fused_us': round(sum(r['fused_us'] for r in rows), 1),
+               'exact_us': round(sum(r['exact_us'] for r in rows), 1),
                'tile_us': round(sum(r['tile_us'] for r in rows), 1),
                'unfused_us': round(sum(r['unfused_us'] for r in rows), 1)}
         print(R, 'total', json.dumps(tot), flush=True)
