@@ -49,6 +49,16 @@ template <> struct PackV<bf16_t, 8> {
   __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x8*)p = v; }
   __device__ __forceinline__ void store_out(bf16_t* p) const { ROD_ST_OUT((bf16x8*)p, v); }
 };
+template <> struct PackV<bf16_t, 2> {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  bf16x2_t v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x2_t*)p; }
+  __device__ __forceinline__ void zero() { v = bf16x2_t{(bf16_t)0.f, (bf16_t)0.f}; }
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+  __device__ __forceinline__ void set(int i, float a) { v[i] = (bf16_t)a; }
+  __device__ __forceinline__ void store(bf16_t* p) const { *(bf16x2_t*)p = v; }
+  __device__ __forceinline__ void store_out(bf16_t* p) const { ROD_ST_OUT((bf16x2_t*)p, v); }
+};
 template <typename T> struct PackV<T, 1> {
   T v;
   __device__ __forceinline__ void load(const T* p) { v = *p; }
@@ -1958,26 +1968,35 @@ __device__ __forceinline__ void unpack4(const PackV<T, 4>& p, dw_f2& a, dw_f2& b
   a = dw_f2{p.get(0), p.get(1)};
   b = dw_f2{p.get(2), p.get(3)};
 }
+template <typename T, int V>
+__device__ __forceinline__ void unpackv(const PackV<T, V>& p, dw_f2 (&o)[V / 2]) {
+#pragma unroll
+  for (int h = 0; h < V / 2; ++h) o[h] = dw_f2{p.get(2 * h), p.get(2 * h + 1)};
+}
 __device__ __forceinline__ dw_f2 round2(dw_f2 v, bf16_t) {
   return dw_f2{(float)(bf16_t)v.x, (float)(bf16_t)v.y};
 }
 __device__ __forceinline__ dw_f2 round2(dw_f2 v, float) { return v; }
 
-template <typename T, int PACT, bool RED, int BACT>
-__global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
+// V = 2: the same tile with twice the threads (512 per block), each holding 2 channels — half the
+// per-thread weights, accumulators and BatchNorm constants, twice the waves in flight
+template <typename T, int PACT, bool RED, int BACT, int V = 4, int D = 3>
+__global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
                                                                const T* __restrict__ yd, const float* __restrict__ w,
                                                                T* __restrict__ dx, float* __restrict__ slab,
                                                                float* __restrict__ gparts, int H, int W, int C,
                                                                DwTile tl, BnPro pro, DwBwdBn bd) {
-  constexpr int V = 4, D = 3;
+  static_assert(D % 3 == 0, "the ring steps a multiple of the 3 accumulator rows");
+  constexpr int VP = V / 2;  // V channels per thread = VP packed pairs
+  constexpr int TB = 1024 / V;      // threads per block (the tile of the 4-channel plan)
   typedef PackV<T, V> PK;
-  constexpr int XS = 2 * 2 * 256 * (int)sizeof(PK);
-  constexpr int SS = 256 * V * 4;
+  constexpr int XS = 2 * 2 * TB * (int)sizeof(PK);
+  constexpr int SS = TB * V * 4;
   __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
   PK* xs = (PK*)smem;
-  PK* dsl = xs + 2 * 256;
+  PK* dsl = xs + 2 * TB;
   const int tid = threadIdx.x;
-  const int CVb = tl.CVb, P = tl.P;
+  const int CVb = tl.CVb * (4 / V), P = tl.P;
   const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
   int bx, strip, n;
   xcd_block(bx, strip, n);
@@ -1987,22 +2006,22 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
   const bool comp = p >= 1 && p <= P - 2 && col < W;
   const bool cok = p < P && col >= 0 && col < W;
   const int colc = col < 0 ? 0 : (col >= W ? W - 1 : col);         // always a valid address
-  const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < 256 ? tid + CVb : tid;
+  const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < TB ? tid + CVb : tid;
   const int ho0 = strip * tl.RB;
   const int ho1 = ho0 + tl.RB < H ? ho0 + tl.RB : H;
   const int xlo = ho0 - 1 > 0 ? ho0 - 1 : 0, xhi = ho1 < H - 1 ? ho1 : H - 1;
 
-  dw_f2 wr[9][2];
+  dw_f2 wr[9][VP];
 #pragma unroll
   for (int k = 0; k < 9; ++k)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) wr[k][h] = dw_f2{w[k * C + c + 2 * h], w[k * C + c + 2 * h + 1]};
-  dw_f2 psc[2], psh[2], ers[2], enb[2];
+    for (int h = 0; h < VP; ++h) wr[k][h] = dw_f2{w[k * C + c + 2 * h], w[k * C + c + 2 * h + 1]};
+  dw_f2 psc[VP], psh[VP], ers[VP], enb[VP];
   int pact = 0;
   if constexpr (PACT >= 0) {
     pact = pro.act;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < VP; ++h) {
       float a0, b0, a1, b1;
       bn_pro_affine(pro, c + 2 * h, a0, b0);
       bn_pro_affine(pro, c + 2 * h + 1, a1, b1);
@@ -2014,9 +2033,9 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
       }
     }
   }
-  dw_f2 dmu[2], drs[2], dsc[2], dsh[2], da[2], dmg[2], dmx[2];
+  dw_f2 dmu[VP], drs[VP], dsc[VP], dsh[VP], da[VP], dmg[VP], dmx[VP];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < VP; ++h) {
     const int c0 = c + 2 * h;
     dmu[h] = dw_f2{bd.mean[c0], bd.mean[c0 + 1]};
     drs[h] = dw_f2{bd.rstd[c0], bd.rstd[c0 + 1]};
@@ -2029,8 +2048,9 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
     dmg[h] = dw_f2{bd.coef[C + c0], bd.coef[C + c0 + 1]};
     dmx[h] = dw_f2{bd.coef[2 * C + c0], bd.coef[2 * C + c0 + 1]};
   }
-  dw_f2 sg[2], sgx[2];
-  sg[0] = sg[1] = sgx[0] = sgx[1] = dw_f2{0.f, 0.f};
+  dw_f2 sg[VP], sgx[VP];
+#pragma unroll
+  for (int h = 0; h < VP; ++h) sg[h] = sgx[h] = dw_f2{0.f, 0.f};
   const long nb = (long)n * H * W * C + c;
   const T* yen = ye + nb + (long)colc * C;
   const T* dzn = dz + nb + (long)colc * C;
@@ -2050,9 +2070,9 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
   const int nst = ho1 - ho0 + 3;
 #pragma unroll
   for (int k = 0; k < D; ++k) issue(k, k);
-  dw_f2 acc[3][2], fa[9][2], q1[2], q2[2];
+  dw_f2 acc[3][VP], fa[9][VP], q1[VP], q2[VP];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < VP; ++h) {
     acc[0][h] = acc[1][h] = acc[2][h] = q1[h] = q2[h] = dw_f2{0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 9; ++k) fa[k][h] = dw_f2{0.f, 0.f};
@@ -2061,16 +2081,19 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       const int q = q0 + k;
+      if constexpr (D > 3) {  // the deep ring's tail steps are empty (block-uniform)
+        if (q >= nst) break;
+      }
       const int rho = ho0 - 2 + q;
       const int buf = q & 1;
       const int k3 = k % 3;
       const bool xok = cok && rho >= xlo && rho <= xhi;
       const bool dok = cok && rho + 1 >= xlo && rho + 1 <= xhi;
       // x row rho (prologue, rounded to T) and, with RED, BN_e's gradient mask at the same element
-      dw_f2 xv[2], yr[2], em[2];
-      unpack4(rx[k], yr[0], yr[1]);
+      dw_f2 xv[VP], yr[VP], em[VP];
+      unpackv(rx[k], yr);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < VP; ++h) {
         dw_f2 a = yr[h];
         if constexpr (PACT >= 0) {
           const dw_f2 z = f2fma(a, psc[h], psh[h]);
@@ -2086,13 +2109,13 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
         xv[h] = xok ? a : dw_f2{0.f, 0.f};
       }
       // dy row rho + 1: BN_d backward apply (rod_bn_bwd_apply's arithmetic), rounded to T
-      dw_f2 dv[2];
+      dw_f2 dv[VP];
       {
-        dw_f2 yv[2], zv[2];
-        unpack4(ry[k], yv[0], yv[1]);
-        unpack4(rz[k], zv[0], zv[1]);
+        dw_f2 yv[VP], zv[VP];
+        unpackv(ry[k], yv);
+        unpackv(rz[k], zv);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < VP; ++h) {
           const dw_f2 d = yv[h] - dmu[h];
           const dw_f2 z = f2fma(yv[h], dsc[h], dsh[h]);
           const dw_f2 m = dw_f2{agrad<BACT>(z.x, bd.act), agrad<BACT>(z.y, bd.act)};
@@ -2103,27 +2126,27 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
       }
       PK px, pd;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < VP; ++h) {
         px.set(2 * h, xv[h].x);
         px.set(2 * h + 1, xv[h].y);
         pd.set(2 * h, dv[h].x);
         pd.set(2 * h + 1, dv[h].y);
       }
       issue(k, q + D);
-      xs[buf * 256 + tid] = px;
-      dsl[buf * 256 + tid] = pd;
+      xs[buf * TB + tid] = px;
+      dsl[buf * TB + tid] = pd;
       __syncthreads();
-      dw_f2 xl[2], xr[2], dl[2], dr[2];
-      unpack4(xs[buf * 256 + li], xl[0], xl[1]);
-      unpack4(xs[buf * 256 + ri], xr[0], xr[1]);
-      unpack4(dsl[buf * 256 + li], dl[0], dl[1]);
-      unpack4(dsl[buf * 256 + ri], dr[0], dr[1]);
+      dw_f2 xl[VP], xr[VP], dl[VP], dr[VP];
+      unpackv(xs[buf * TB + li], xl);
+      unpackv(xs[buf * TB + ri], xr);
+      unpackv(dsl[buf * TB + li], dl);
+      unpackv(dsl[buf * TB + ri], dr);
       // backward-data: dy row rho+1 is tap row 0 of dx row rho, 1 of rho+1, 2 of rho+2
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int sl = (k3 + i) % 3;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < VP; ++h) {
           dw_f2 a = acc[sl][h];
           a = f2fma(dl[h], wr[i * 3 + 2][h], a);
           a = f2fma(dv[h], wr[i * 3 + 1][h], a);
@@ -2134,7 +2157,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
       // filter: x row rho with the strip's dy rows rho+1 (tap row 0), rho (1), rho-1 (2)
       const bool own = rho + 1 >= ho0 && rho + 1 < ho1;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < VP; ++h) {
         const dw_f2 f0 = own ? dv[h] : dw_f2{0.f, 0.f};
         fa[0][h] = f2fma(f0, xl[h], fa[0][h]);
         fa[1][h] = f2fma(f0, xv[h], fa[1][h]);
@@ -2152,14 +2175,14 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
       if (rho >= ho0 && rho < ho1) {
         PK o;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < VP; ++h) {
           o.set(2 * h, acc[k3][h].x);
           o.set(2 * h + 1, acc[k3][h].y);
         }
         if (comp) o.store_out(dxn + rho * rstr);
         if constexpr (RED) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < VP; ++h) {
             const dw_f2 ov = dw_f2{o.get(2 * h), o.get(2 * h + 1)};
             const dw_f2 g = ov * em[h];
             sg[h] += g;
@@ -2168,7 +2191,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
         }
       }
 #pragma unroll
-      for (int h = 0; h < 2; ++h) acc[k3][h] = dw_f2{0.f, 0.f};
+      for (int h = 0; h < VP; ++h) acc[k3][h] = dw_f2{0.f, 0.f};
     }
   }
 
@@ -2176,14 +2199,14 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused2_kernel(const T* __restri
   float* red = (float*)smem;
   const int Cc = CVb * V;
   const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
-  auto colsum = [&](const dw_f2 (&a)[2], float* dst) {
+  auto colsum = [&](const dw_f2 (&a)[VP], float* dst) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < VP; ++h) {
       red[tid * V + 2 * h] = comp ? a[h].x : 0.f;
       red[tid * V + 2 * h + 1] = comp ? a[h].y : 0.f;
     }
     __syncthreads();
-    for (int e = tid; e < Cc; e += 256) {
+    for (int e = tid; e < Cc; e += TB) {
       const int cve = e / V, v = e - cve * V;
       float s = 0.f;
       for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
@@ -2478,12 +2501,17 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
   float* slab = (float*)workspace;
   auto go = [&](auto tag) {
     typedef decltype(tag) T;
-    // stride-1 prefetch ring depth (steps in flight): 3; ROD_DWF_RING=6 (measurement switch)
-    // measured 3.27 ms (3) vs 3.34 ms (6) over the step's bf16 shapes (tools/dwfused_bench.py)
+    // 4-channel stride-1 forms: prefetch ring depth 3; ROD_DWF_RING=6 (measurement switch)
+    // measured 3.27 ms (3) vs 3.34 ms (6) for the first form over the step's bf16 shapes
     static const int ring_env = getenv("ROD_DWF_RING") ? atoi(getenv("ROD_DWF_RING")) : 0;
     const int ring = ring_env == 6 ? 6 : 3;
     // stride 1: the issue-lean kernel; ROD_DWF_V1=1 (A/B switch) the first form
     static const bool v1 = getenv("ROD_DWF_V1") && atoi(getenv("ROD_DWF_V1")) == 1;
+    // bf16 default: 2 channels per thread in 512-thread blocks (120 VGPRs, 4 waves/SIMD) with a
+    // 6-step ring, stride-1 shapes 3.76 -> 3.70 ms in total (tools/dwfused_bench.py);
+    // ROD_DWF_C2=0 the 4-channel form, ROD_DWF_RING=3 the 3-step ring
+    static const bool v2 = !(getenv("ROD_DWF_C2") && atoi(getenv("ROD_DWF_C2")) == 0);
+    const int vring = ring_env == 3 ? 3 : 6;
 #define DWF1(PA, R, D)                                                                                               \
   hipLaunchKernelGGL((dw3x3_bwd_fused_kernel<T, PA, R, D>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,      \
                      (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)
@@ -2493,8 +2521,23 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
   hipLaunchKernelGGL((dw3x3_bwd_fused_s2_kernel<T, PA, R, D2>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,   \
                      (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, pad_t, pad_l, Ho, Wo, t, pv, bd)
 #define DWV2(PA, R, BA)                                                                                              \
-  hipLaunchKernelGGL((dw3x3_bwd_fused2_kernel<T, PA, R, BA>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,     \
-                     (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)
+  do {                                                                                                              \
+    if constexpr (sizeof(T) == 2) {                                                                                 \
+      if (v2 && vring == 6)                                                                                         \
+        hipLaunchKernelGGL((dw3x3_bwd_fused2_kernel<T, PA, R, BA, 2, 6>), grid, dim3(512), 0, s, (const T*)ye,      \
+                           (const T*)dz, (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd);                \
+      else if (v2)                                                                                                  \
+        hipLaunchKernelGGL((dw3x3_bwd_fused2_kernel<T, PA, R, BA, 2>), grid, dim3(512), 0, s, (const T*)ye,         \
+                           (const T*)dz, (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd);                \
+      if (v2) break;                                                                                                \
+    }                                                                                                               \
+    if (ring == 6)                                                                                                  \
+      hipLaunchKernelGGL((dw3x3_bwd_fused2_kernel<T, PA, R, BA, 4, 6>), grid, dim3(256), 0, s, (const T*)ye,        \
+                         (const T*)dz, (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd);                  \
+    else                                                                                                            \
+      hipLaunchKernelGGL((dw3x3_bwd_fused2_kernel<T, PA, R, BA>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz, \
+                         (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd);                                \
+  } while (0)
 #define DWF2(PA, R)                                                                                                  \
   do {                                                                                                              \
     if (stride == 2) DWS2(PA, R);                                                                                   \
