@@ -1990,11 +1990,12 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
   constexpr int VP = V / 2;  // V channels per thread = VP packed pairs
   constexpr int TB = 1024 / V;      // threads per block (the tile of the 4-channel plan)
   typedef PackV<T, V> PK;
-  constexpr int XS = 2 * 2 * TB * (int)sizeof(PK);
+  // the row exchange holds the rounded fp32 pairs (no pack / unpack around the LDS trip)
+  constexpr int XS = 2 * 2 * TB * VP * (int)sizeof(dw_f2);
   constexpr int SS = TB * V * 4;
   __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
-  PK* xs = (PK*)smem;
-  PK* dsl = xs + 2 * TB;
+  dw_f2* xs = (dw_f2*)smem;
+  dw_f2* dsl = xs + 2 * TB * VP;
   const int tid = threadIdx.x;
   const int CVb = tl.CVb * (4 / V), P = tl.P;
   const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
@@ -2124,23 +2125,21 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
           dv[h] = dok ? round2(o, T{}) : dw_f2{0.f, 0.f};
         }
       }
-      PK px, pd;
+      issue(k, q + D);
 #pragma unroll
       for (int h = 0; h < VP; ++h) {
-        px.set(2 * h, xv[h].x);
-        px.set(2 * h + 1, xv[h].y);
-        pd.set(2 * h, dv[h].x);
-        pd.set(2 * h + 1, dv[h].y);
+        xs[(buf * TB + tid) * VP + h] = xv[h];
+        dsl[(buf * TB + tid) * VP + h] = dv[h];
       }
-      issue(k, q + D);
-      xs[buf * TB + tid] = px;
-      dsl[buf * TB + tid] = pd;
       __syncthreads();
       dw_f2 xl[VP], xr[VP], dl[VP], dr[VP];
-      unpackv(xs[buf * TB + li], xl);
-      unpackv(xs[buf * TB + ri], xr);
-      unpackv(dsl[buf * TB + li], dl);
-      unpackv(dsl[buf * TB + ri], dr);
+#pragma unroll
+      for (int h = 0; h < VP; ++h) {
+        xl[h] = xs[(buf * TB + li) * VP + h];
+        xr[h] = xs[(buf * TB + ri) * VP + h];
+        dl[h] = dsl[(buf * TB + li) * VP + h];
+        dr[h] = dsl[(buf * TB + ri) * VP + h];
+      }
       // backward-data: dy row rho+1 is tap row 0 of dx row rho, 1 of rho+1, 2 of rho+2
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
