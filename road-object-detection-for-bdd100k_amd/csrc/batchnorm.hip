@@ -354,7 +354,10 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------- backward
-template <typename T, bool VEC, bool PM = false, int U = 4>
+// PIPE: the row batches are software-pipelined (batch k+1's loads issued before batch k's
+// arithmetic, ping-pong registers), so a wave keeps loads in flight while it computes; same
+// rows in the same order as the plain loop (sums bit-identical)
+template <typename T, bool VEC, bool PM = false, int U = 4, bool PIPE = false>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
@@ -393,15 +396,51 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
       }
     };
     long r = r0 + pln;
-    for (; r + (U - 1L) * lanes < r1; r += (long)U * lanes) {
-      float xa[U][V], ga[U][V];
+    if constexpr (PIPE) {
+      const long step = (long)U * lanes;
+      auto full = [&](long rr) { return rr + (U - 1L) * lanes < r1; };
+      static_assert(VEC, "the pipelined form holds raw 16-byte vectors");
+      Vec16<T> xa[2][U], ga[2][U];  // raw (bf16: 4 VGPRs per 8 values), widened at use
+      auto ld = [&](int b, long rr) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        load_v<T, VEC>(x + (r + (long)u * lanes) * ldx + c, xa[u]);
-        load_v<T, VEC>(dy + (r + (long)u * lanes) * lddy + c, ga[u]);
+        for (int u = 0; u < U; ++u) {
+          xa[b][u].load(x + (rr + (long)u * lanes) * ldx + c);
+          ga[b][u].load(dy + (rr + (long)u * lanes) * lddy + c);
+        }
+      };
+      auto use = [&](int b) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float xv[V], gv[V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            xv[v] = xa[b][u].get(v);
+            gv[v] = ga[b][u].get(v);
+          }
+          acc(xv, gv);
+        }
+      };
+      if (full(r)) ld(0, r);
+      while (full(r)) {
+        if (full(r + step)) ld(1, r + step);
+        use(0);
+        r += step;
+        if (!full(r)) break;
+        if (full(r + step)) ld(0, r + step);
+        use(1);
+        r += step;
       }
+    } else {
+      for (; r + (U - 1L) * lanes < r1; r += (long)U * lanes) {
+        float xa[U][V], ga[U][V];
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc(xa[u], ga[u]);
+        for (int u = 0; u < U; ++u) {
+          load_v<T, VEC>(x + (r + (long)u * lanes) * ldx + c, xa[u]);
+          load_v<T, VEC>(dy + (r + (long)u * lanes) * lddy + c, ga[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc(xa[u], ga[u]);
+      }
     }
     for (; r < r1; r += lanes) {
       float xv[V], gv[V];
@@ -1001,7 +1040,15 @@ int rod_bn_bwd_reduce(const void* dz, const void* y, const float* mean, const fl
     // ROD_BN_RED_U=4 / 8 forces one form
     static const int red_u = getenv("ROD_BN_RED_U") ? atoi(getenv("ROD_BN_RED_U")) : 0;
     const bool u8 = red_u == 8 || (red_u == 0 && (long)M * C >= (64L << 20));
-    if (vec && u8)
+    // the large tensors take the software-pipelined form (4-row batches, ping-pong): the step's
+    // shapes in tools/bn_bench.py 7372800 x 96 1459 -> 1369 us, x 32 480 -> 448, x 16 248 -> 231,
+    // 1843200 x 144 571 -> 528, 460800 x 192 203 -> 187 (reduce + apply, bit-identical); the
+    // mid-size ones are neutral to +3 us.  ROD_BN_RED_PIPE=0 keeps the 8-row form
+    static const bool red_pipe = !(getenv("ROD_BN_RED_PIPE") && atoi(getenv("ROD_BN_RED_PIPE")) == 0);
+    if (vec && u8 && red_pipe)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, false, 4, true>), grid, dim3(256), lds, s, (const T*)dz,
+                         (const T*)y, mean, rstd, gamma, beta, M, C, C, C, act, pl.CVb, pl.lanes, pl.chunk, slab);
+    else if (vec && u8)
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, false, 8>), grid, dim3(256), lds, s, (const T*)dz,
                          (const T*)y, mean, rstd, gamma, beta, M, C, C, C, act, pl.CVb, pl.lanes, pl.chunk, slab);
     else if (vec)
