@@ -47,9 +47,16 @@ def parse():
                     help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
     ap.add_argument('--graph', dest='graph', action='store_true', default=True,
                     help='replay the training step as a HIP graph (Trainer.step_graphed; bit-identical to the '
-                         'eager step); at N>1 the bucketed RCCL all-reduces are captured into the graph with the '
-                         'kernels (gloo rehearsals run eager)')
+                         'eager step).  N>1 default (\'split\'): forward + backward replay as a graph with no '
+                         'collective inside, then the bucketed RCCL all-reduce and SGD are issued eagerly')
     ap.add_argument('--no-graph', dest='graph', action='store_false')
+    ap.add_argument('--graph-dp', dest='graph_dp', action='store_true', default=False,
+                    help='N>1 over RCCL: capture the whole step, bucketed all-reduces included (\'full\'; '
+                         'verified bit-identical on a 1-rank group only)')
+    ap.add_argument('--dp-leg', dest='dp_leg', action='store_true', default=True,
+                    help='N=1: time the graphed step with a 1-rank RCCL GradReducer (split and full capture) and '
+                         'with SyncBatchNorm against the step without a reducer ("dp_overhead")')
+    ap.add_argument('--no-dp-leg', dest='dp_leg', action='store_false')
     ap.add_argument('--sync-bn', dest='sync_bn', action='store_true', default=False,
                     help='N>1: BatchNorm statistics over the global batch (rod.ddp.SyncBatchNorm; default per rank)')
     ap.add_argument('--probe', default='rod_dw3x3_bwd_fused',
@@ -201,40 +208,60 @@ def synthetic_jpeg_tfrecord(path, n, H=720, W=1280, seed=5):
 
 def tfrecord_leg(args, tr, dev, dtype, steps=8, n_img=48):
     """The train.py input path (TFRecord scan + CRC, host JPEG decode on the reference's 4
-    reader threads, process_raw_data_train on the GPU) feeding the training step as train.py
-    runs it (eager Trainer.step: the boxes' padded count changes per batch, so there is no
-    fixed graph to replay).  Reports the host decode rate alone and the fed training rate:
-    when decode is slower than the step, the fed rate falls to the decode rate."""
-    step = tr.step
+    reader threads, process_raw_data_train on the GPU) feeding the training step exactly as
+    train.py runs it: the source pads the boxes to a fixed count (so the step's HIP graph is
+    captured once and replayed whatever each batch's real box count), decodes the next batch on
+    a background thread during the current step, and the loop reads each step's losses one
+    step late (train._loss_copy / _loss_values).  Reports the host decode rate alone (a
+    non-prefetching source) and the fed training rate."""
+    step = tr.step_graphed if args.graph else tr.step
     import tempfile
     from rod.dataio import TFRecordSource
+    from train import _loss_copy, _loss_values
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, 'bdd100k_train_000.tfrecord')
         t0 = time.perf_counter()
         synthetic_jpeg_tfrecord(path, n_img, args.height, args.width)
         t_write = time.perf_counter() - t0
         nbytes = os.path.getsize(path)
+        dec = TFRecordSource([path], args.batch, (args.height, args.width), dev, dtype, train=True, seed=SEED_TF,
+                             num_readers=4, prefetch=False)
+        dec._host()
+        t0 = time.perf_counter()
+        for _ in range(steps):   # the host half of a batch: record reads + JPEG decode on the pool + draws
+            dec._host()
+        t_dec = (time.perf_counter() - t0) / steps
+        dec.close()
         src = TFRecordSource([path], args.batch, (args.height, args.width), dev, dtype, train=True, seed=SEED_TF,
                              num_readers=4)
+        n_graphs = len(getattr(tr, '_graphs', {}))
         for _ in range(2):
             step(*next(src))
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):   # the host half of next(src): record reads + JPEG decode on the pool
-            list(src.pool.map(src._load, src._take()))
-        t_dec = (time.perf_counter() - t0) / steps
-        torch.cuda.synchronize()
+        counts = []
+        pending = None
         t0 = time.perf_counter()
         for _ in range(steps):
-            losses = step(*next(src))
+            x, bo, lo, n = next(src)
+            counts.append(n)
+            losses = step(x, bo, lo, n)
+            entry = _loss_copy(losses, 1)
+            if pending is not None:
+                _loss_values(pending)
+            pending = entry
+        last = _loss_values(pending)
         torch.cuda.synchronize()
         t_fed = (time.perf_counter() - t0) / steps
-        src.pool.shutdown()
+        src.close()
+        new_graphs = len(getattr(tr, '_graphs', {})) - n_graphs
+    real = sorted({int(v) for c in counts for v in c.tolist()})
     return {'metric': 'training images/sec fed from TFRecord (host JPEG decode, 4 reader threads, GPU augmentation)',
             'value': round(args.batch / t_fed, 2), 'unit': 'images/s', 'ms_per_step': round(t_fed * 1e3, 2),
             'host_decode_images_per_s': round(args.batch / t_dec, 2), 'decode_ms_per_batch': round(t_dec * 1e3, 2),
             'num_readers': 4, 'records': n_img, 'mean_record_kb': round(nbytes / n_img / 1024, 1),
-            'write_s': round(t_write, 1), 'loss': round(float(losses[0].item()), 4),
+            'hip_graph': bool(args.graph), 'graphs_captured': new_graphs, 'gt_padded_to': int(bo.shape[1]),
+            'real_box_counts_seen': [real[0], real[-1]] if real else None,
+            'write_s': round(t_write, 1), 'loss': round(float(last[0]), 4),
             'data': 'synthetic 1280x720 JPEG frames (smooth colour fields + noise), BDD-shaped boxes'}
 
 
@@ -263,6 +290,55 @@ def fp32_leg(args, dev, steps=10, warmup=2):
 
 
 SEED_TF = 4242
+
+
+def dp_overhead_leg(args, dev, dtype, batch, base_ms, steps=10):
+    """The data-parallel machinery's cost on one GPU: the headline step (no reducer) against
+    the same step with a 1-rank RCCL GradReducer (4 MB buckets) in each graph mode —
+    'split' (the N>1 default: forward + backward replayed, all-reduce + SGD eager), 'full'
+    (--graph-dp: the in-backward bucket all-reduces captured too) — and with SyncBatchNorm
+    ('full': its ~280 all-gathers captured; 'eager': issued from the host).  A 1-rank
+    all-reduce moves no data over xGMI: this prices launch, synchronisation and lost overlap,
+    not the link."""
+    import socket
+    import torch.distributed as dist
+    import config
+    from rod import ops
+    from rod.ddp import GradReducer
+    from rod.trainer import Trainer
+    from utils import net_tools
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1, device_id=dev)
+    out = {'baseline_ms_per_step': round(base_ms, 3), 'world': 1, 'bucket_mb': 4.0, 'steps': steps}
+    try:
+        from rod.data import C2_WEIGHT_SEED
+        for name, kw, graphed in (('split', {}, True), ('full', {'graph_dp': True}, True),
+                                  ('sync_bn_full', {'graph_dp': True, 'sync_bn': True}, True),
+                                  ('sync_bn_eager', {'sync_bn': True}, False)):
+            tr = Trainer((args.height, args.width), args.batch, dtype=dtype, device=dev, world_size=1,
+                         reducer=GradReducer(1), seed=C2_WEIGHT_SEED, **kw)
+            step = tr.step_graphed if graphed else tr.step
+            for _ in range(3):
+                step(*batch)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step(*batch)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / steps * 1e3
+            out[name] = {'ms_per_step': round(ms, 3), 'overhead_frac': round(ms / base_ms - 1, 4),
+                         'graph_mode': tr.graph_mode() if graphed else 'eager'}
+            del tr, step
+            torch.cuda.empty_cache()
+    finally:
+        ops.SYNC_BN = None          # Trainer globals: back to the single-process state
+        net_tools.HNM_EXCHANGE = None
+        dist.destroy_process_group()
+    return out
 
 
 def inference_fps(args, dev, dtype, batch=32, steps=5, warmup=2, hw=None):
@@ -391,7 +467,7 @@ def main():
         reducer = GradReducer(world)  # bucketed RCCL all-reduce, launched during backward
     tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
                  world_size=world, reducer=reducer, fix_refine=args.fix_refine, sync_bn=args.sync_bn,
-                 seed=C2_WEIGHT_SEED)
+                 seed=C2_WEIGHT_SEED, graph_dp=args.graph_dp)
     # rank 0's batch and the initial weights are the ones tests/test_gpu_fullsize.py pins
     batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=C2_BATCH_SEED + rank)
     source = None
@@ -399,9 +475,10 @@ def main():
         from rod.dataio import AugmentedSource
         source = AugmentedSource(args.batch, (args.height, args.width), dev, dtype, seed=SEED + rank, n_distinct=2)
     next_batch = (lambda: next(source)) if source is not None else (lambda: batch)
-    # the DP step is captured with its RCCL collectives (Trainer.step_graphed); gloo (host-side
-    # collectives, the one-box rehearsal) cannot be captured and runs eager
-    use_graph = args.graph and (world == 1 or backend == 'nccl')
+    # Trainer.graph_mode decides what the graph holds: the whole step (N=1, or --graph-dp over
+    # RCCL), forward + backward only ('split', the N>1 default: no collective in the graph, so
+    # the gloo rehearsal replays it too), or nothing (collectives inside the step)
+    use_graph = args.graph and tr.graph_mode() != 'eager'
     step = tr.step_graphed if use_graph else tr.step
 
     # graphed: the capture happens on the second call (after one eager set-up step), so at
@@ -458,6 +535,9 @@ def main():
     fp32 = None
     if args.fp32_leg and world == 1 and dtype == torch.bfloat16:
         fp32 = fp32_leg(args, dev)
+    dp_over = None
+    if args.dp_leg and world == 1 and args.graph and tr_range is config.train_range.REFINE:
+        dp_over = dp_overhead_leg(args, dev, dtype, batch, base_ms=elapsed / args.steps * 1e3)
     if args.probe_table and rank == 0:
         # per-entry live timing (every call bracketed by events; the step itself is slower
         # in this mode, so ms_per_step of such a run is not a bench number)
@@ -540,6 +620,7 @@ def main():
                        'global_batch': args.batch * world, 'img_hw': [args.height, args.width],
                        'train_range': args.train_range, 'parallelism': f'dp{world}',
                        'augment': bool(args.augment), 'hip_graph': bool(use_graph),
+                       'graph_mode': tr.graph_mode() if use_graph else 'eager',
                        **({'dist_backend': 'rccl' if backend == 'nccl' else backend,
                            'batchnorm': 'sync (global batch)' if args.sync_bn else 'per rank'} if world > 1 else {}),
                        **({} if args.train_range == 'REFINE' else {'fix_refine': args.fix_refine})},
@@ -554,6 +635,8 @@ def main():
             out['training_fp32'] = fp32
         if tf_leg is not None:
             out['tfrecord'] = tf_leg
+        if dp_over is not None:
+            out['dp_overhead'] = dp_over
         if args.cpu_baseline and world == 1:
             if inf is not None:
                 inf['cpu_baseline'] = cpu_baseline_inference(args.height, args.width)

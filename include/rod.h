@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 14
+#define ROD_ABI_VERSION 15
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -530,10 +530,15 @@ int rod_sgd_clip(float* param, const float* grad, long n, float lr, float clip, 
  * the gradient outputs alive, unmodified, until the flush); rod_slab_flush runs every queued
  * sum on `stream` as one batched launch per 32 sums, bit-identical to the immediate launches;
  * rod_slab_defer(0) stops queueing (queued sums stay queued until flushed).  rod_slab_defer
- * returns the previous mode, rod_slab_pending the queue length. */
+ * returns the previous mode, rod_slab_pending the queue length.
+ * rod_slab_flush_range (ABI 15) runs only the queued sums whose output lies entirely in the
+ * byte range [lo, hi) — the data-parallel bucket about to be all-reduced (the reduce point,
+ * net_tools.py:645-651) — and leaves the others queued, so a bucket launched from inside
+ * backward does not split the rest of the step's batched sums. */
 int rod_slab_defer(int on);
 int rod_slab_pending(void);
 int rod_slab_flush(void* stream);
+int rod_slab_flush_range(const void* lo, const void* hi, void* stream);
 
 #ifdef __cplusplus
 }

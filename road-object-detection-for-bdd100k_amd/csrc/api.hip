@@ -294,14 +294,7 @@ int rod_slab_pending(void) {
   return g_slab_jobs ? (int)g_slab_jobs->size() : 0;
 }
 
-int rod_slab_flush(void* stream) {
-  hipStream_t s = ROD_STREAM(stream);
-  std::vector<SlabJob> jobs;
-  {
-    std::lock_guard<std::mutex> lk(g_slab_mu);
-    if (!g_slab_jobs || g_slab_jobs->empty()) return 0;
-    jobs.swap(*g_slab_jobs);
-  }
+static int slab_launch(std::vector<SlabJob>& jobs, hipStream_t s) {
   for (size_t k0 = 0; k0 < jobs.size(); k0 += SLAB_BATCH) {
     SlabBatch b{};
     b.cnt = (int)std::min<size_t>(SLAB_BATCH, jobs.size() - k0);
@@ -318,6 +311,35 @@ int rod_slab_flush(void* stream) {
     if (rc) return rc;
   }
   return 0;
+}
+
+int rod_slab_flush(void* stream) {
+  hipStream_t s = ROD_STREAM(stream);
+  std::vector<SlabJob> jobs;
+  {
+    std::lock_guard<std::mutex> lk(g_slab_mu);
+    if (!g_slab_jobs || g_slab_jobs->empty()) return 0;
+    jobs.swap(*g_slab_jobs);
+  }
+  return slab_launch(jobs, s);
+}
+
+int rod_slab_flush_range(const void* lo, const void* hi, void* stream) {
+  hipStream_t s = ROD_STREAM(stream);
+  ROD_CHECK_ARG((const char*)lo <= (const char*)hi, "rod_slab_flush_range: lo > hi");
+  std::vector<SlabJob> jobs;
+  {
+    std::lock_guard<std::mutex> lk(g_slab_mu);
+    if (!g_slab_jobs || g_slab_jobs->empty()) return 0;
+    std::vector<SlabJob> keep;
+    for (const SlabJob& j : *g_slab_jobs) {
+      const char* o = (const char*)j.out;
+      const bool in = o >= (const char*)lo && o + j.n * sizeof(float) <= (const char*)hi;
+      (in ? jobs : keep).push_back(j);
+    }
+    g_slab_jobs->swap(keep);
+  }
+  return jobs.empty() ? 0 : slab_launch(jobs, s);
 }
 
 int rod_sgd_clip(float* param, const float* grad, long n, float lr, float clip, void* stream) {

@@ -22,6 +22,8 @@ import torch
 
 from rod.data import SEED, synthetic_batch, synthetic_boxes
 
+GMAX = 64   # padded ground-truth boxes per training image; larger batches: next multiple
+
 log = logging.getLogger(__name__)
 
 
@@ -92,10 +94,21 @@ class TFRecordSource(object):
     train=False: file order (shuffle=False, evaluate.py:103), resize to img_size only
     (data_pileline_tools.py:39-40), normalised into `dtype`; boxes unchanged.  The number of
     ground-truth boxes varies per image: batches are zero-padded to the largest count
-    (dynamic_pad=True, evaluate.py:109-114) with the counts in n."""
+    (dynamic_pad=True, evaluate.py:109-114) with the counts in n.
+
+    Training batches are padded to a FIXED box count instead: `gmax` (64), or the
+    next multiple of 64 above it for a batch that holds more.  The batch shapes then do not
+    change from step to step, so the captured training step (Trainer.step_graphed) replays
+    without re-capture; the matching kernel reads only the first n[b] boxes of each row, so
+    the padding changes no result.
+
+    prefetch (default: on for training): the host half of the NEXT batch (record reads,
+    JPEG decode on the reader pool, pinned staging, augmentation sampling) runs on a
+    background thread while the current step runs on the GPU; the device half (upload,
+    augmentation kernels) is issued from the caller's thread, stream-ordered behind it."""
 
     def __init__(self, files, batch_size, img_size, device, dtype, train=True, seed=SEED, num_readers=4,
-                 verify=True, max_images=None, rank=0, world=1):
+                 verify=True, max_images=None, rank=0, world=1, gmax=GMAX, prefetch=None):
         from rod import tfrecord
         if not files:
             raise FileNotFoundError('no TFRecord files')
@@ -112,7 +125,9 @@ class TFRecordSource(object):
         # pass over the data set (the reference reads it on one device); each rank keeps
         # len // world records per epoch (the remainder is dropped, as DistributedSampler's
         # drop_last) so the ranks' epochs stay in step
-        self.rank, self.world = int(rank), max(1, int(world))
+        # (evaluation is never sharded: every record is read once, in file order)
+        self.rank, self.world = (int(rank), max(1, int(world))) if train else (0, 1)
+        self.gmax = int(gmax) if train else 0
         self.rng = np.random.default_rng(seed)
         self.order = self._shard(self.rng.permutation(len(self.index)) if train else np.arange(len(self.index)))
         self.pos = 0
@@ -122,9 +137,18 @@ class TFRecordSource(object):
         if train:
             from utils.data_pileline_tools import TrainAugmenter
             self.aug = TrainAugmenter(self.img_size, seed=seed + 1000 * self.rank)   # per-rank augmentation draws
+        self.prefetch = train if prefetch is None else bool(prefetch)
+        self._ahead = ThreadPoolExecutor(max_workers=1) if self.prefetch else None
+        self._next_host = None
 
     def __len__(self):
-        return len(self.index)
+        """Records this rank reads per epoch."""
+        return len(self.order)
+
+    def close(self):
+        if self._ahead is not None:
+            self._ahead.shutdown(wait=True)
+        self.pool.shutdown(wait=True)
 
     def __iter__(self):
         return self
@@ -155,11 +179,15 @@ class TFRecordSource(object):
             self.pos += 1
         return ks
 
-    def __next__(self):
-        from rod import ops
+    def _host(self):
+        """Host half of a batch: record reads + JPEG decode (reader pool), the padded box arrays,
+        the pinned staging buffer and, for training, the augmentation draws (in batch order, so
+        the sequence of batches does not depend on prefetching)."""
         items = list(self.pool.map(self._load, self._take()))
         B = len(items)
         G = max(1, max(len(b) for _, b, _ in items))
+        if self.gmax:
+            G = max(self.gmax, -(-G // GMAX) * GMAX)
         boxes = np.zeros((B, G, 4), np.float32)
         labels = np.zeros((B, G), np.int32)
         n = np.zeros(B, np.int32)
@@ -176,9 +204,16 @@ class TFRecordSource(object):
         fl = flat.numpy()
         for b, (img, _, _) in enumerate(items):
             fl[offs[b]:offs[b] + img.size] = img.reshape(-1)
+        draws = self.aug.sample(hw, boxes, n) if self.train else None
+        return flat, boxes, labels, n, hw, offs, draws
+
+    def _device(self, host):
+        from rod import ops
+        flat, boxes, labels, n, hw, offs, draws = host
+        B = len(n)
         src = flat.to(self.device, non_blocking=True)
         if self.train:
-            crop, ref, mode, colour = self.aug.sample(hw, boxes, n)
+            crop, ref, mode, colour = draws
             x = ops.augment_images(src, crop, mode, colour, self.img_size, dtype=self.dtype, normalize=True,
                                    src_hw=hw, src_off=offs)
             bo, lo, no = ops.augment_boxes(boxes, labels, n, ref, mode, threshold=0.3)
@@ -189,6 +224,14 @@ class TFRecordSource(object):
                                normalize=True, src_hw=hw, src_off=offs)
         dev = lambda a: torch.from_numpy(a).to(self.device)
         return x, dev(boxes), dev(labels), dev(n)
+
+    def __next__(self):
+        if self._ahead is None:
+            return self._device(self._host())
+        fut = self._next_host if self._next_host is not None else self._ahead.submit(self._host)
+        host = fut.result()
+        self._next_host = self._ahead.submit(self._host)   # decode the next batch during this step
+        return self._device(host)
 
 
 def make_source(dataset_dir, batch_size, img_size, device, split='train', seed=SEED, augment_dtype=None,

@@ -26,6 +26,9 @@ class GradReducer(object):
         self.group = group
         self.store = None
         self.buckets = []
+        # True while Trainer.step_graphed captures a 'split' step: the captured backward launches
+        # no collective, every bucket is reduced after the replay (__call__)
+        self.defer = False
 
     def attach(self, store):
         """Build buckets over the trainable parameters (in reverse registration order,
@@ -56,22 +59,46 @@ class GradReducer(object):
     def _launch(self, b):
         if b['work'] is None:
             from . import ops
-            ops.SLAB.flush()   # deferred weight-gradient sums land before the bucket is reduced
             view = self.store.flat_grad[b['lo']:b['hi']]
+            # the deferred weight-gradient sums INTO this bucket land before it is reduced; the
+            # rest of the step's sums stay queued for the batched flush at the end of backward
+            ops.SLAB.flush_range(view)
             b['work'] = dist.all_reduce(view, group=self.group, async_op=True)
 
     def _on_grad(self, p):
         b = getattr(p, '_rod_bucket', None)
-        if b is None or p._rod_seen:
+        if b is None or p._rod_seen or self.defer:
             return
         p._rod_seen = True
         b['pending'] -= 1
         if b['pending'] == 0:
             self._launch(b)
 
+    def spans(self):
+        """The buckets' ranges of the flat gradient merged where they touch: [(lo, hi)]."""
+        out = []
+        for lo, hi in sorted((b['lo'], b['hi']) for b in self.buckets):
+            if out and out[-1][1] == lo:
+                out[-1] = (out[-1][0], hi)
+            else:
+                out.append((lo, hi))
+        return out
+
     def __call__(self, flat_grad):
         if self.store is None:
             raise RuntimeError('GradReducer.attach(store) was not called')
+        if all(b['work'] is None for b in self.buckets):
+            # nothing launched from inside backward (a 'split' graph replay, or hooks that never
+            # fired): nothing left to overlap with, so one all-reduce per contiguous span (one
+            # for the usual contiguous trainable set) instead of one per bucket
+            from . import ops
+            ops.SLAB.flush()
+            works = [dist.all_reduce(self.store.flat_grad[lo:hi], group=self.group, async_op=True)
+                     for lo, hi in self.spans()]
+            for w in works:
+                w.wait()
+            self.reset()
+            return
         for b in self.buckets:
             self._launch(b)
         for b in self.buckets:

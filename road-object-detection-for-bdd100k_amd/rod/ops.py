@@ -117,6 +117,13 @@ class SlabDefer(object):
         _abi.call("rod_slab_flush", stream())
         _abi.KEEP = []    # the flush is enqueued: stream order protects the slabs from here on
 
+    def flush_range(self, t):
+        """Enqueue only the queued sums that write into tensor t (a gradient bucket, ABI 15).
+        The slabs of the sums left queued stay referenced until the full flush."""
+        if not self.active:
+            return
+        _abi.call("rod_slab_flush_range", t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), stream())
+
     def end(self):
         if not self.active:
             return

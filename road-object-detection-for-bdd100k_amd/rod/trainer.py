@@ -26,11 +26,13 @@ from utils.common_tools import cornerBboxes_2_centerBboxes
 
 
 class Trainer:
+    MAX_GRAPHS = 4   # captured step graphs kept (one per batch signature), oldest dropped first
+
     def __init__(self, img_size, batch_size, dtype=torch.bfloat16, train_range=config.train_range.REFINE,
                  learning_rate=1e-3, device='cuda', fix_refine=True, seed=0, world_size=1, reducer=None,
                  deconv_method=config.deconv_method.LEARN_HALF, merge_method=config.merge_method.ADD,
                  sync_bn=False, backbone_name='mobilenet_v2',
-                 process_backbone_method=config.process_backbone_method.NONE):
+                 process_backbone_method=config.process_backbone_method.NONE, graph_dp=False):
         self.img_size = tuple(img_size)
         self.batch_size = batch_size          # per-rank batch
         self.world_size = world_size
@@ -79,8 +81,22 @@ class Trainer:
         ops.DROPOUT_RANK[:] = [rank, world_size]
         self._eager_steps = 0
         self._dropout_seen = False   # the step draws dropout masks (vgg_16 training): never graphed
+        # data parallel + step_graphed: capture the RCCL collectives into the graph too (opt-in,
+        # 'full'); by default only the collective-free compute is captured ('split', see
+        # graph_mode)
+        self.graph_dp = bool(graph_dp)
 
     def step(self, img_u8, gt_corner, gt_labels, gt_n):
+        losses = self._compute(img_u8, gt_corner, gt_labels, gt_n)
+        if self.reducer is not None:
+            self.reducer(self.net.store.flat_grad)
+        self.opt.step()
+        self._eager_steps += 1
+        return losses
+
+    def _compute(self, img_u8, gt_corner, gt_labels, gt_n):
+        """Forward + backward of one step: the parameter gradients in the flat buffer (the
+        data-parallel buckets launch from inside backward unless the reducer is deferred)."""
         calls = ops._DROPOUT_CALLS[0]
         losses = self.losses(img_u8, gt_corner, gt_labels, gt_n)
         self._dropout_seen |= ops._DROPOUT_CALLS[0] != calls
@@ -93,11 +109,32 @@ class Trainer:
                 graph.backward(losses[0])
             finally:
                 ops.SLAB.end()
-        if self.reducer is not None:
-            self.reducer(self.net.store.flat_grad)
-        self.opt.step()
-        self._eager_steps += 1
         return losses
+
+    def graph_mode(self):
+        """How step_graphed runs this trainer's step:
+        'full'  — the whole step is one graph: single process, or data parallel over RCCL with
+                  graph_dp=True (the bucketed all-reduces, SyncBatchNorm all-gathers and the
+                  hard-negative exchange are captured with the kernels);
+        'split' — data parallel, default: forward + backward (no collective inside: REFINE
+                  mode without SyncBatchNorm) replay as a graph, then the gradient all-reduce
+                  (buckets launched back to back) and the SGD update are issued eagerly.  The
+                  graph holds no collective, so every rank's capture is the single-process
+                  one; what is lost is the overlap of the ~22 MB all-reduce with backward;
+        'eager' — steps with collectives inside forward/backward: ALL mode's global hard
+                  negatives (always), SyncBatchNorm (unless graph_dp); gloo with graph_dp;
+                  dropout."""
+        if self._dropout_seen:
+            return 'eager'
+        if self.reducer is None:
+            return 'full'
+        hnm = self.train_range is not config.train_range.REFINE and net_tools.HNM_EXCHANGE is not None
+        if self.graph_dp:
+            # the hard-negative exchange's blocking all-reduces inside a capture raced RCCL's
+            # watchdog (hipErrorCapturedEvent on a 1-rank group, round 4): ALL mode stays eager
+            return 'full' if self._nccl() and not hnm else 'eager'
+        mid = self.sync_bn or hnm
+        return 'eager' if mid or not hasattr(self.reducer, 'defer') else 'split'
 
     def step_graphed(self, img_u8, gt_corner, gt_labels, gt_n):
         """One training step replayed as a HIP graph: the whole forward / backward / SGD launch
@@ -114,35 +151,54 @@ class Trainer:
         (RCCL collectives are stream-ordered and capturable; each bucket joins the compute
         stream before SGD, so the capture closes on one stream) and replay with them.  gloo
         runs on the host and cannot be captured: with it the step stays eager."""
-        if self._eager_steps == 0 or self._dropout_seen or not self._graphable():
+        mode = self.graph_mode()
+        if self._eager_steps == 0 or mode == 'eager':
             return self.step(img_u8, gt_corner, gt_labels, gt_n)
         new = (img_u8, gt_corner, gt_labels, gt_n)
-        if getattr(self, '_graph', None) is None or any(a.shape != b.shape or a.dtype != b.dtype
-                                                          for a, b in zip(self._graph[1], new)):
+        key = tuple((tuple(t.shape), t.dtype) for t in new)
+        graphs = self.__dict__.setdefault('_graphs', {})
+        if key not in graphs:
+            # one graph per batch signature (the TFRecord source pads the boxes to a fixed count,
+            # so a run normally has one; a batch with more boxes gets its own), all on one memory
+            # pool: replays are serialised on the compute stream, so they can share temporaries
+            if len(graphs) >= self.MAX_GRAPHS:
+                graphs.pop(next(iter(graphs)))
             static = tuple(t.clone() for t in new)
             self.net.store.build_prep_tables()   # host -> device set-up stays outside the capture
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
             st = self.net.store
             gstep, eager, version = self.opt.global_step, self._eager_steps, st.version
+            if getattr(self, '_pool', None) is None:
+                self._pool = torch.cuda.graph_pool_handle()
             # thread_local: RCCL's watchdog thread may query its events while this thread captures
-            with torch.cuda.graph(g, capture_error_mode='thread_local' if self.reducer is not None else 'global'):
-                out = self.step(*static)
+            if mode == 'split':
+                self.reducer.defer = True   # no bucket launches from inside the captured backward
+            try:
+                with torch.cuda.graph(g, pool=self._pool,
+                                      capture_error_mode='thread_local' if self.reducer is not None else 'global'):
+                    out = self.step(*static) if mode == 'full' else self._compute(*static)
+            finally:
+                if mode == 'split':
+                    self.reducer.defer = False
             # the capture recorded the step without running it: host counters as before
             self.opt.global_step, self._eager_steps, st.version = gstep, eager, version
-            self._graph = (g, static, out)
-        g, static, out = self._graph
+            graphs[key] = (g, static, out)
+        g, static, out = graphs[key]
+        self._graph = graphs[key]
         for a, b in zip(static, new):
             if a.data_ptr() != b.data_ptr():
                 a.copy_(b)
         g.replay()
+        if mode == 'split':
+            self.reducer(self.net.store.flat_grad)   # every bucket, back to back, then SGD
+            self.opt.step()
+            return out
         self.opt.global_step += 1
         self.net.store.version += 1   # the replay's SGD changed the parameters (derived layouts stale)
         return out
 
-    def _graphable(self):
-        if self.reducer is None:
-            return True
+    def _nccl(self):
         import torch.distributed as dist
         return dist.is_initialized() and dist.get_backend(getattr(self.reducer, 'group', None)) == 'nccl'
 

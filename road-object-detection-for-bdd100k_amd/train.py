@@ -67,6 +67,14 @@ def parse(argv=None):
                     help='checkpoint format: torch file, or a TF-1.x tensor bundle the reference can restore')
     ap.add_argument('--augment', type=str2bool, default=True,
                     help='process_raw_data_train on the GPU (random crop / flip / colour); False = raw batches')
+    ap.add_argument('--hip_graph', type=str2bool, default=True,
+                    help='replay the training step as a HIP graph (Trainer.step_graphed, bit-identical to the '
+                         'eager step; dropout steps run eager).  Data parallel: forward + backward replay, the '
+                         'gradient all-reduce and SGD follow eagerly; steps with collectives inside (ALL mode, '
+                         '--sync_bn) run eager unless --graph_dp')
+    ap.add_argument('--graph_dp', type=str2bool, default=False,
+                    help='data parallel over RCCL: capture the whole step, collectives included (opt-in: '
+                         'multi-rank capture is verified on a 1-rank group only)')
     return ap.parse_args(argv)
 
 
@@ -80,6 +88,63 @@ def load_ckpt(store, path, names_regex=None):
 def save_ckpt(store, path, step, fmt='torch'):
     from rod.checkpoint import save_variables
     save_variables(store, path, step, fmt)
+
+
+def _loss_copy(losses, world):
+    """The step's loss values as one small device tensor (a copy: a replayed graph overwrites
+    its outputs on the next replay).  Data parallel: each rank holds its shard's sum / global
+    batch, so the global loss is the all-reduced sum."""
+    lv = torch.stack([l.detach().float().reshape(()) for l in losses])
+    if world > 1:
+        torch.distributed.all_reduce(lv)
+    if lv.device.type != 'cuda':
+        return lv, None
+    host = torch.empty(lv.shape, dtype=lv.dtype, pin_memory=True)
+    host.copy_(lv, non_blocking=True)   # queued before the next step: reading it waits for this step only
+    ev = torch.cuda.Event()
+    ev.record()
+    return host, ev
+
+
+def _loss_values(entry):
+    host, ev = entry
+    if ev is not None:
+        ev.synchronize()
+    return host.tolist()
+
+
+class StepLog(object):
+    """Running averages and the log / summary lines of train.py:292-320 (formats kept)."""
+
+    def __init__(self, F, trainer, tr_range, rank, summ):
+        self.F, self.trainer, self.tr_range, self.rank, self.summ = F, trainer, tr_range, rank, summ
+        self.avg = [0., 0., 0.]
+        self.avg_t = 0.
+
+    def __call__(self, current_step, vals, t):
+        F, avg = self.F, self.avg
+        if F.log_every_n_steps is not None:
+            s = current_step % F.log_every_n_steps
+            if self.tr_range is config.train_range.ALL:
+                tot, _, dl, cl = vals
+                avg[:] = [(avg[0] * s + tot) / (s + 1.), (avg[1] * s + dl) / (s + 1.), (avg[2] * s + cl) / (s + 1.)]
+            else:
+                avg[0] = (avg[0] * s + vals[0]) / (s + 1.)
+            self.avg_t = (self.avg_t * s + t) / (s + 1.)
+            if current_step % F.log_every_n_steps == F.log_every_n_steps - 1 and self.rank == 0:
+                if self.tr_range is config.train_range.ALL:
+                    logger.info('Step%s total_loss:%s det_loss:%s clf_loss:%s time_each_step:%s' %
+                                (str(current_step + 1), str(avg[0]), str(avg[1]), str(avg[2]), str(self.avg_t)))
+                else:
+                    logger.info('Step_%s refine_loss:%s time:%s' % (str(current_step + 1), str(avg[0]),
+                                                                    str(self.avg_t)))
+                avg[:] = [0., 0., 0.]
+                self.avg_t = 0.
+        if self.summ is not None and F.summary_every_n_steps is not None and \
+                current_step % F.summary_every_n_steps == F.summary_every_n_steps - 1:
+            rec = {'step': current_step, 'loss': vals, 'lr': self.trainer.opt.decayed_lr(current_step)}
+            self.summ.write(json.dumps(rec) + '\n')
+            self.summ.flush()
 
 
 def main(argv=None):
@@ -110,7 +175,7 @@ def main(argv=None):
     trainer = Trainer(config.img_size, F.batch_size, dtype=dtype, train_range=tr_range, learning_rate=F.learning_rate,
                       device=dev, fix_refine=F.fix_refine, seed=F.seed, world_size=world,
                       reducer=GradReducer(world) if world > 1 else None, backbone_name=F.backbone_name,
-                      sync_bn=F.sync_bn)
+                      sync_bn=F.sync_bn, graph_dp=F.graph_dp)
     store = trainer.net.store
     logger.info('Total trainable parameters:%s' % str(store.trainable_count()))
     step0 = 0
@@ -135,48 +200,40 @@ def main(argv=None):
 
     os.makedirs(F.summary_dir, exist_ok=True)
     summ = open(os.path.join(F.summary_dir, 'train_rank%d.jsonl' % rank), 'a') if rank == 0 else None
-    avg = [0., 0., 0.]
-    avg_t = 0.
+    log = StepLog(F, trainer, tr_range, rank, summ)
+    # Trainer.graph_mode: the whole step as one graph (one process), forward + backward only with
+    # the all-reduce and SGD after the replay (data parallel), or eager (collectives inside the
+    # step, unless --graph_dp; dropout)
+    step = trainer.step_graphed if F.hip_graph else trainer.step
+    # the host reads each step's losses (the reference's sess.run returns them) one step late:
+    # step k+1 is queued on the GPU before step k's values are read, so the GPU does not wait
+    # for the host's logging and next-batch work.  Checkpoints are written right after their
+    # step (before the next is queued), so they hold exactly that step's parameters.
+    pending = None
+    last = time.time()
     while True:
-        start = time.time()
-        losses = trainer.step(*next(source))
-        if world > 1:   # each rank holds its shard's sum / global batch: the global loss is their sum
-            lv = torch.stack([l.detach().float().reshape(()) for l in losses])
-            torch.distributed.all_reduce(lv)
-            vals = lv.tolist()
-        else:
-            vals = [float(l.item()) for l in losses]  # the reference's sess.run returns host values too
-        t = round(time.time() - start, 3)
+        losses = step(*next(source))
         current_step = trainer.opt.global_step - 1
-        if F.log_every_n_steps is not None:
-            s = current_step % F.log_every_n_steps
-            if tr_range is config.train_range.ALL:
-                tot, _, dl, cl = vals
-                avg = [(avg[0] * s + tot) / (s + 1.), (avg[1] * s + dl) / (s + 1.), (avg[2] * s + cl) / (s + 1.)]
-            else:
-                avg[0] = (avg[0] * s + vals[0]) / (s + 1.)
-            avg_t = (avg_t * s + t) / (s + 1.)
-            if current_step % F.log_every_n_steps == F.log_every_n_steps - 1 and rank == 0:
-                if tr_range is config.train_range.ALL:
-                    logger.info('Step%s total_loss:%s det_loss:%s clf_loss:%s time_each_step:%s' %
-                                (str(current_step + 1), str(avg[0]), str(avg[1]), str(avg[2]), str(avg_t)))
-                else:
-                    logger.info('Step_%s refine_loss:%s time:%s' % (str(current_step + 1), str(avg[0]), str(avg_t)))
-                avg = [0., 0., 0.]
-                avg_t = 0.
-        if summ is not None and F.summary_every_n_steps is not None and \
-                current_step % F.summary_every_n_steps == F.summary_every_n_steps - 1:
-            rec = {'step': current_step, 'loss': vals, 'lr': trainer.opt.decayed_lr(current_step)}
-            summ.write(json.dumps(rec) + '\n')
-            summ.flush()
+        entry = (current_step, _loss_copy(losses, world))
         if F.save_every_n_steps is not None and current_step % F.save_every_n_steps == F.save_every_n_steps - 1 \
                 and rank == 0:
             logger.info('Saving model...')
             save_ckpt(store, os.path.join(F.train_dir, F.backbone_name + '.model'), current_step + 1, F.save_format)
             logger.info('Save model sucess...')
+        if pending is not None:
+            vals = _loss_values(pending[1])   # waits for the previous step only
+            now = time.time()
+            log(pending[0], vals, round(now - last, 3))
+            last = now
+        pending = entry
         if F.max_number_of_steps is not None and current_step >= F.max_number_of_steps:
-            logger.info('Exit training...')
             break
+    vals = _loss_values(pending[1])
+    log(pending[0], vals, round(time.time() - last, 3))
+    logger.info('Exit training...')
+    close = getattr(source, 'close', None)
+    if close is not None:
+        close()
     if world > 1:
         torch.distributed.destroy_process_group()
 

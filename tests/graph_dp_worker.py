@@ -38,7 +38,7 @@ def main():
     runs = {}
     for mode in ('eager', 'graphed'):
         tr = Trainer((H, W), B, dtype=torch.bfloat16, train_range=tr_range, device=dev, seed=4, world_size=1,
-                     reducer=GradReducer(1, bucket_mb=1.0), sync_bn=True)
+                     reducer=GradReducer(1, bucket_mb=1.0), sync_bn=True, graph_dp=True)
         step = tr.step if mode == 'eager' else tr.step_graphed
         losses = []
         for i in range(a.steps):
@@ -52,8 +52,12 @@ def main():
               'params_equal': bool(torch.equal(fe, fg)), 'losses_equal': bool(torch.equal(le, lg)),
               'buffers_equal': all(torch.equal(v, bg[k]) for k, v in be.items()),
               'losses': le.float().tolist(), 'global_step': [te.opt.global_step, tg.opt.global_step]}
-    detail['ok'] = detail['captured'] and detail['params_equal'] and detail['losses_equal'] and \
-        detail['buffers_equal'] and detail['buckets'] > 3 and te.opt.global_step == tg.opt.global_step == a.steps
+    # ALL mode: the hard-negative exchange keeps the step eager even with graph_dp (Trainer.graph_mode)
+    detail['mode'] = tg.graph_mode()
+    want = 'full' if a.train_range == 'REFINE' else 'eager'
+    detail['ok'] = detail['mode'] == want and detail['captured'] == (want == 'full') and detail['params_equal'] and \
+        detail['losses_equal'] and detail['buffers_equal'] and detail['buckets'] > 3 and \
+        te.opt.global_step == tg.opt.global_step == a.steps
     torch.save(detail, a.out)
     dist.destroy_process_group()
 

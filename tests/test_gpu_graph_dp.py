@@ -1,9 +1,12 @@
-"""The data-parallel step as a HIP graph (Trainer.step_graphed with a GradReducer): bench.py
---gpus N replays it on every rank.  Captured on a 1-rank RCCL group on one MI355X — the
-bucketed all-reduces launched from inside backward, the SyncBatchNorm all-gathers and (ALL)
-the hard-negative count / histogram all-reduces all go into the graph — and replayed over
-alternating input batches: parameters, moving statistics and losses bit-identical to the
-eager data-parallel step (ref net_tools.py:642-651: clip after the reduction)."""
+"""The data-parallel step as a HIP graph (Trainer.step_graphed with a GradReducer).
+
+'full' (opt-in graph_dp): captured on a 1-rank RCCL group on one MI355X — the bucketed
+all-reduces launched from inside backward and the SyncBatchNorm all-gathers go into the graph —
+and replayed over alternating input batches: parameters, moving statistics and losses
+bit-identical to the eager data-parallel step (ref net_tools.py:642-651: clip after the
+reduction).  ALL mode (hard-negative exchange inside the step) stays eager.
+
+'split' (the default, what bench.py --gpus N replays): two ranks over gloo on one GPU."""
 import os
 import socket
 import subprocess
@@ -35,4 +38,22 @@ def test_dp_step_graph_capture_bit_identical(train_range, tmp_path, dev):
     assert r.returncode == 0, r.stderr[-3000:]
     d = torch.load(out, weights_only=True)
     print(train_range, d)
+    assert d['ok'], d
+
+
+SPLIT_WORKER = os.path.join(ROOT, 'tests', 'split_dp_worker.py')
+
+
+def test_split_graph_dp_two_ranks(tmp_path, dev):
+    """The default data-parallel graph mode ('split': forward + backward replayed, the bucketed
+    all-reduce + SGD issued after the replay) with TWO ranks (gloo on one GPU): bit-identical
+    to the eager DP step on each rank, ranks hold identical parameters; ALL mode stays eager."""
+    out = str(tmp_path / 's.pt')
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(_port()), SPLIT_WORKER, '--out', out]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = torch.load(out, weights_only=True)
+    print(d)
     assert d['ok'], d

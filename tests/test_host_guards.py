@@ -53,8 +53,9 @@ def test_tfrecord_source_ranks_read_disjoint_slices(golden_dir):
     files = tfrecord_files(os.path.join(golden_dir, 'tfrecord'))
     world = 2
     srcs = [TFRecordSource(files, 1, (32, 32), torch.device('cpu'), torch.float32, train=True, seed=9, rank=r,
-                           world=world) for r in range(world)]
-    n = len(srcs[0])
+                           world=world, prefetch=False) for r in range(world)]
+    n = len(srcs[0].index)
+    assert len(srcs[0]) == n // world   # records this rank reads per epoch
     for epoch in range(3):
         orders = [s.order.tolist() for s in srcs]
         assert all(len(o) == n // world for o in orders)
