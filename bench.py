@@ -410,7 +410,8 @@ def kernel_rooflines(tr, batch, steps, dtype):
     agg = _abi.PROBE.table()
     design = _abi.PROBE.design_table()
     by_shape = _abi.PROBE.table(by_shape=True)
-    totals = {'alg_bytes_per_step': sum(v[2] for v in agg.values()) // steps,
+    totals = {'cost_model': roofline.COST_MODEL_VERSION,
+              'alg_bytes_per_step': sum(v[2] for v in agg.values()) // steps,
               'alg_flops_per_step': sum(v[3] for v in agg.values()) // steps,
               'design_bytes_per_step': sum(design.values()) // steps,
               'launch_entries_per_step': sum(v[0] for v in agg.values()) // steps,
@@ -553,7 +554,7 @@ def main():
                 calls.append({'entry': name, 'args': list(shp), 'calls_per_step': n / args.steps,
                               'avg_us': 1e3 * t / n, 'alg_GBps': b / max(t, 1e-9) / 1e6,
                               'alg_TFLOPs': fl / max(t, 1e-9) / 1e9})
-            json.dump({'entries': rows, 'top_calls': calls}, f, indent=1)
+            json.dump({'cost_model': roofline.COST_MODEL_VERSION, 'entries': rows, 'top_calls': calls}, f, indent=1)
 
     # inference legs (configs[3], configs[4]): at N > 1 every rank runs the same predict path on
     # its own batch (inference does not shard: replicas); the aggregate is all ranks' images over
@@ -588,6 +589,7 @@ def main():
                                 max(1, sum(te['launches'] for te in tes)))
                 tsrc = os.path.relpath(args.traffic, ROOT)
         rl.update({'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, PMC)', 'traffic_source': tsrc,
+                   'cost_model': roofline.COST_MODEL_VERSION,
                    'alg_bytes_per_launch': byts // max(n_launch, 1), 'kernel': args.probe.replace(',', ' + '),
                    'launches_per_step': n_launch // max(probe_steps, 1),
                    'avg_launch_us': round(per_launch_ms * 1e3, 2), 'alg_bytes_per_step': byts // max(probe_steps, 1),

@@ -308,18 +308,28 @@ def _bn_backward(dz, y, mean, rstd, gamma, beta, act, need_g, need_b):
 # (_ConvBN) receives exactly that dx as its dz when the depthwise is the only consumer, and then
 # finalizes the sums instead of running rod_bn_bwd_reduce over (dz, y).  Entries hold their dx
 # (so its memory cannot be reused while listed) and are dropped when the backward ends.
+# An entry is accepted only for the very tensor it was made for, or a view of the same storage
+# whose version counter is unchanged: a gradient summed IN PLACE into dx (a second consumer of
+# the depthwise input) shares dx's pointer and shape but bumps its version, and then the
+# producer runs its own reduce over the summed dz instead of picking up stale sums.
 _BN_PARTS = {}
 
 
 def _put_bn_parts(dx, parts):
-    _BN_PARTS[dx.data_ptr()] = (dx, parts)
+    _BN_PARTS[dx.data_ptr()] = (dx, parts, dx._version)
 
 
 def _take_bn_parts(dz):
     e = _BN_PARTS.pop(dz.data_ptr(), None) if dz is not None else None
-    if e is None or e[0] is not dz and (e[0].shape != dz.shape or e[0].dtype != dz.dtype):
+    if e is None:
         return None
-    return e[1]
+    dx, parts, ver = e
+    if dx is dz:
+        return parts if dz._version == ver else None
+    if dx.shape != dz.shape or dx.dtype != dz.dtype or dz._version != ver or \
+            dx.untyped_storage().data_ptr() != dz.untyped_storage().data_ptr():
+        return None
+    return parts
 
 
 def clear_bn_parts():

@@ -25,6 +25,13 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
 
 _ES = {0: 4, 1: 2}
 
+# Version of the per-call cost model above, carried in every bench / probe JSON.  Figures are
+# comparable only within one version:
+#   1 (rounds 1-2): rod_bn_bwd_apply 3 passes; rod_dw3x3_bwd_fused es*(ye + dz + yd + dx)
+#   2 (round 3 on): rod_bn_bwd_apply 1 pass (write dy) and rod_dw3x3_bwd_fused es*(ye + dx) —
+#     their reads of (dz, y) are the BatchNorm backward's second pass, reported as design bytes
+COST_MODEL_VERSION = 2
+
 MI355X_HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 MI355X_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec, no sparsity)
 MI355X_F32_PEAK_TFLOPS = 157.3    # f32 MFMA / vector

@@ -47,9 +47,31 @@ def _nerr(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
+R6, NONE, LEAKY, RELU = ops.ROD_ACT_RELU6, ops.ROD_ACT_NONE, ops.ROD_ACT_LEAKY, 3
+# the run-time activation forms (DW_ACT_RT) of both BatchNorms, stride 1 and 2
+ACT_CASES = [  # (N, H, W, C, dtype, stride, act of the output BatchNorm, act of the input BatchNorm)
+    (2, 37, 45, 96, torch.bfloat16, 1, NONE, LEAKY),
+    (2, 37, 45, 96, torch.bfloat16, 1, LEAKY, NONE),
+    (2, 20, 33, 32, torch.float32, 1, LEAKY, LEAKY),
+    (1, 23, 40, 64, torch.bfloat16, 1, RELU, R6),
+    (2, 36, 44, 96, torch.bfloat16, 2, NONE, LEAKY),
+    (2, 37, 45, 144, torch.bfloat16, 2, LEAKY, NONE),
+    (1, 45, 80, 32, torch.float32, 2, LEAKY, RELU),
+]
+
+
 @pytest.mark.parametrize('N,H,W,C,dt,pro,S', CASES)
 def test_fused_matches_unfused_chain(dev, N, H, W, C, dt, pro, S):
-    g = torch.Generator().manual_seed(N * 1000 + H * 10 + C)
+    _check(dev, N, H, W, C, dt, pro, S, R6, R6)
+
+
+@pytest.mark.parametrize('N,H,W,C,dt,S,act_d,act_e', ACT_CASES)
+def test_fused_runtime_activations(dev, N, H, W, C, dt, S, act_d, act_e):
+    _check(dev, N, H, W, C, dt, True, S, act_d, act_e)
+
+
+def _check(dev, N, H, W, C, dt, pro, S, act, act_e):
+    g = torch.Generator().manual_seed(N * 1000 + H * 10 + C + 7 * act + act_e)
     (Ho, pt), (Wo, pl) = _same(H, S), _same(W, S)
     ye = (torch.randn(N, H, W, C, generator=g) * 1.3 + 0.2).to(dev, dt)
     yd = (torch.randn(N, Ho, Wo, C, generator=g) * 2 + 0.4).to(dev, dt)
@@ -57,10 +79,9 @@ def test_fused_matches_unfused_chain(dev, N, H, W, C, dt, pro, S):
     w = (torch.randn(3, 3, C, generator=g) * 0.4).to(dev)
     f = lambda lo=0.5: (torch.rand(C, generator=g) + lo).to(dev)
     dmean, drstd, dgam, dbet = torch.randn(C, generator=g).to(dev) * 0.3, f(), f(), torch.randn(C, generator=g).to(dev)
-    act = ops.ROD_ACT_RELU6
     emean, erstd, egam, ebet = (torch.randn(C, generator=g).to(dev) * 0.1, f(), f(),
                                 torch.randn(C, generator=g).to(dev) * 0.1)
-    pargs = (emean, erstd, egam, ebet, act) if pro else (None, None, None, None, 0)
+    pargs = (emean, erstd, egam, ebet, act_e) if pro else (None, None, None, None, 0)
     M, Mo, st, code = N * H * W, N * Ho * Wo, ops.stream(), ops.dtcode(ye)
     coef = torch.empty(3 * C, device=dev)
     rws = ops.workspace(_abi.query('rod_bn_bwd_workspace', max(M, Mo), C), dev)
@@ -96,7 +117,7 @@ def test_fused_matches_unfused_chain(dev, N, H, W, C, dt, pro, S):
         # BN_e backward from the fused sums against rod_bn_bwd_reduce over (dx, ye)
         ce_ref, dg_ref, db_ref = torch.empty(3 * C, device=dev), torch.empty(C, device=dev), torch.empty(C, device=dev)
         rws2 = ops.workspace(_abi.query('rod_bn_bwd_workspace', M, C), dev)
-        _abi.call('rod_bn_bwd_reduce', dx_ref, ye, emean, erstd, egam, ebet, dg_ref, db_ref, ce_ref, rws2, M, C, act,
+        _abi.call('rod_bn_bwd_reduce', dx_ref, ye, emean, erstd, egam, ebet, dg_ref, db_ref, ce_ref, rws2, M, C, act_e,
                   code, st)
         ce, dg, db = torch.empty(3 * C, device=dev), torch.empty(C, device=dev), torch.empty(C, device=dev)
         _abi.call('rod_bn_bwd_finalize', gparts, nparts, M, C, erstd, egam, dg, db, ce, st)

@@ -115,3 +115,22 @@ def test_eval_views_checks_buffer_bounds():
     st.load_state_dict(sd)
     assert st.eval_views(st.buffers['b/moving_mean'], st.buffers['b/moving_variance'], 1e-3) is not None
     assert st.flat_buf[6:11].tolist() == [1.0] * 5
+
+
+def test_bn_parts_handoff_rejects_summed_gradient():
+    """The BatchNorm-sum hand-off from the fused depthwise backward to its producer (ops._BN_PARTS)
+    is taken only for the very gradient it was formed from: not after an in-place sum into it
+    (a second consumer of the depthwise input), not for another tensor of the same shape."""
+    dx = torch.zeros(4, 8)
+    parts = torch.ones(2, 2, 8)
+    ops._put_bn_parts(dx, parts)
+    assert ops._take_bn_parts(dx) is parts
+    ops._put_bn_parts(dx, parts)
+    dx.add_(torch.ones(4, 8))            # autograd accumulating a second branch in place
+    assert ops._take_bn_parts(dx) is None
+    ops._put_bn_parts(dx, parts)
+    other = torch.zeros(4, 8)            # same shape, different storage (an out-of-place sum)
+    assert ops._take_bn_parts(other) is None
+    ops._put_bn_parts(dx, parts)
+    assert ops._take_bn_parts(dx.view(4, 8)) is parts   # a view of the same, unchanged storage
+    ops.clear_bn_parts()
