@@ -21,6 +21,8 @@ constexpr int DW_ACT_RT = 99;
 template <typename T, int V> struct PackV;
 template <> struct PackV<float, 4> {
   f32x4 v;
+  __device__ __forceinline__ void bload(rsrc_t r, unsigned vo, unsigned so) { v = buf_ld<decltype(v)>(r, vo, so); }
+  __device__ __forceinline__ void bstore(rsrc_t r, unsigned vo, unsigned so) const { buf_st(v, r, vo, so); }
   __device__ __forceinline__ void load(const float* p) { v = *(const f32x4*)p; }
   __device__ __forceinline__ void zero() { v = f32x4{0.f, 0.f, 0.f, 0.f}; }
   __device__ __forceinline__ float get(int i) const { return v[i]; }
@@ -30,6 +32,8 @@ template <> struct PackV<float, 4> {
 };
 template <> struct PackV<bf16_t, 4> {
   bf16x4 v;
+  __device__ __forceinline__ void bload(rsrc_t r, unsigned vo, unsigned so) { v = buf_ld<decltype(v)>(r, vo, so); }
+  __device__ __forceinline__ void bstore(rsrc_t r, unsigned vo, unsigned so) const { buf_st(v, r, vo, so); }
   __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x4*)p; }
   __device__ __forceinline__ void zero() { v = bf16x4{(bf16_t)0.f, (bf16_t)0.f, (bf16_t)0.f, (bf16_t)0.f}; }
   __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
@@ -39,6 +43,8 @@ template <> struct PackV<bf16_t, 4> {
 };
 template <> struct PackV<bf16_t, 8> {
   bf16x8 v;
+  __device__ __forceinline__ void bload(rsrc_t r, unsigned vo, unsigned so) { v = buf_ld<decltype(v)>(r, vo, so); }
+  __device__ __forceinline__ void bstore(rsrc_t r, unsigned vo, unsigned so) const { buf_st(v, r, vo, so); }
   __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x8*)p; }
   __device__ __forceinline__ void zero() {
 #pragma unroll
@@ -52,6 +58,8 @@ template <> struct PackV<bf16_t, 8> {
 template <> struct PackV<bf16_t, 2> {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   bf16x2_t v;
+  __device__ __forceinline__ void bload(rsrc_t r, unsigned vo, unsigned so) { v = buf_ld<decltype(v)>(r, vo, so); }
+  __device__ __forceinline__ void bstore(rsrc_t r, unsigned vo, unsigned so) const { buf_st(v, r, vo, so); }
   __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x2_t*)p; }
   __device__ __forceinline__ void zero() { v = bf16x2_t{(bf16_t)0.f, (bf16_t)0.f}; }
   __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
@@ -441,21 +449,41 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
     for (int v = 0; v < V; ++v) st.set(v, o[v]);
     st.store(xs + (buf * 256 + tid) * V);
   };
-  auto emit = [&](const float (&a)[V], int ho, bool first) {
+  // Buffer I/O (rod_common.h): every load is issued (rows / columns clamped into the map, uses
+  // masked by rok), every output store too (lane offset ROD_OOB off the strip and on halo lanes),
+  // and every lane runs the row arithmetic (neighbours from clamped slots; halo results are
+  // dropped), so no memory operation sits under a branch and the prefetch ring's wait counts
+  // stay exact.  The GRED form (opt-in) keeps its conditional y loads.
+  const unsigned es = sizeof(T);
+  const rsrc_t rxs = rod_rsrc(xn - c, (unsigned)((long)H * W * C * es));
+  const rsrc_t rys = rod_rsrc(yn - c, (unsigned)((long)Ho * Wo * C * es));
+  const int cc0 = ci0 < 0 ? 0 : (ci0 >= W ? W - 1 : ci0);
+  const int cc1 = ci0 + 1 < 0 ? 0 : (ci0 + 1 >= W ? W - 1 : ci0 + 1);
+  const unsigned vx0 = (unsigned)(((long)cc0 * C + c) * es), vx1 = (unsigned)(((long)cc1 * C + c) * es);
+  const unsigned vy = comp ? (unsigned)(((long)wo * C + c) * es) : ROD_OOB;
+  const unsigned rsx = (unsigned)(W * C * es), rsy = (unsigned)(Wo * C * es);
+  const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < 256 ? tid + CVb : tid;
+  auto emit = [&](const float (&a)[V], int ho, bool valid, bool first) {
     PK o;
 #pragma unroll
     for (int v = 0; v < V; ++v) o.set(v, a[v]);
-    o.store_out(yn + ((long)ho * Wo + wo) * C);
+    // the statistics read the rounded outputs BEFORE the store: with the store first, the fp32
+    // form (dwordx4 store, then VALU reading its data registers) returned corrupted element-1
+    // outputs on the MI355X, different run to run (tests/test_gpu_kernels.py::
+    // test_dw_epilogue_bn_stats); every buffer store here is the last use of its data
     if constexpr (STATS) {
+      if (valid) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const float ov = o.get(v);
-        if (first) piv[v] = ov;
-        const float d = ov - piv[v];
-        s1[v] += d;
-        s2[v] = fmaf(d, d, s2[v]);
+        for (int v = 0; v < V; ++v) {
+          const float ov = o.get(v);
+          if (first) piv[v] = ov;
+          const float d = ov - piv[v];
+          s1[v] += d;
+          s2[v] = fmaf(d, d, s2[v]);
+        }
       }
     }
+    o.bstore(rys, valid ? vy : ROD_OOB, (unsigned)(valid ? ho : 0) * rsy);
   };
   auto emit_g = [&](const float (&a)[V], int ho, int gslot) {  // GRED: y of row ho is in gring[gslot]
     PackV<T, V> o;
@@ -477,11 +505,14 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
     auto issue = [&](int k, int q) {
       const int hi = hi0 + q;
       rok[k] = cok0 && q < nin && hi >= 0 && hi < H;
-      if (rok[k]) ring[k].load(xn + ((long)hi * W + ci0) * C);
+      const int hc = hi < 0 ? 0 : (hi >= H ? H - 1 : hi);
+      ring[k].bload(rxs, vx0, (unsigned)hc * rsx);
     };
-    issue(0, 0);
-    issue(1, 1);
-    issue(2, 2);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {   // slot order, so the loop header's wait is the same on entry
+      issue(k, k);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // GRED: y of output row m is loaded at input row q = m into slot m % 3 (two rows ahead)
     auto gissue = [&](int k, int m) {
       if constexpr (GRED) {
@@ -500,37 +531,36 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
         const int buf = q & 1;
         float cen[V];
         cvt(ring[k], rok[k], cen);
+        __builtin_amdgcn_sched_barrier(0);   // the slot's reload stays after its last read
         issue(k, q + 3);
         gissue(k, q);
         publish(cen, buf);
         __syncthreads();
-        if (comp) {
-          PK L, R;
-          L.load(xs + (buf * 256 + tid - CVb) * V);
-          R.load(xs + (buf * 256 + tid + CVb) * V);
-          // row q feeds output m = q - i with weight row i: slot (k - i) mod 3
+        PK L, R;
+        L.load(xs + (buf * 256 + li) * V);
+        R.load(xs + (buf * 256 + ri) * V);
+        // row q feeds output m = q - i with weight row i: slot (k - i) mod 3
 #pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const int sl = (k - i + 3) % 3;
+        for (int i = 0; i < 3; ++i) {
+          const int sl = (k - i + 3) % 3;
 #pragma unroll
-            for (int v = 0; v < V; ++v) {
-              float a = acc[sl][v];
-              a = fmaf(L.get(v), wr[i * 3][v], a);
-              a = fmaf(cen[v], wr[i * 3 + 1][v], a);
-              a = fmaf(R.get(v), wr[i * 3 + 2][v], a);
-              acc[sl][v] = a;
-            }
+          for (int v = 0; v < V; ++v) {
+            float a = acc[sl][v];
+            a = fmaf(L.get(v), wr[i * 3][v], a);
+            a = fmaf(cen[v], wr[i * 3 + 1][v], a);
+            a = fmaf(R.get(v), wr[i * 3 + 2][v], a);
+            acc[sl][v] = a;
           }
-          const int sd = (k + 1) % 3;  // output m = q - 2 is complete
-          const int m = q - 2;
-          if constexpr (GRED) {
-            if (m >= 0 && ho0 + m < ho1) emit_g(acc[sd], ho0 + m, sd);
-          } else {
-            if (m >= 0 && ho0 + m < ho1) emit(acc[sd], ho0 + m, m == 0);
-          }
-#pragma unroll
-          for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
         }
+        const int sd = (k + 1) % 3;  // output m = q - 2 is complete
+        const int m = q - 2;
+        if constexpr (GRED) {
+          if (comp && m >= 0 && ho0 + m < ho1) emit_g(acc[sd], ho0 + m, sd);
+        } else {
+          emit(acc[sd], ho0 + m, m >= 0 && ho0 + m < ho1, m == 0);
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
       }
     }
   } else {
@@ -543,11 +573,15 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
       const bool rowok = q < nin && hi >= 0 && hi < H;
       rok[k][0] = rowok && cok0;
       rok[k][1] = rowok && cok1;
-      if (rok[k][0]) ring[k][0].load(xn + ((long)hi * W + ci0) * C);
-      if (rok[k][1]) ring[k][1].load(xn + ((long)hi * W + ci0 + 1) * C);
+      const int hc = hi < 0 ? 0 : (hi >= H ? H - 1 : hi);
+      ring[k][0].bload(rxs, vx0, (unsigned)hc * rsx);
+      ring[k][1].bload(rxs, vx1, (unsigned)hc * rsx);
     };
 #pragma unroll
-    for (int k = 0; k < 4; ++k) issue(k, k);
+    for (int k = 0; k < 4; ++k) {
+      issue(k, k);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     float acc[2][V];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -561,36 +595,35 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
         float c0[V], c1[V];
         cvt(ring[k][0], rok[k][0], c0);
         cvt(ring[k][1], rok[k][1], c1);
+        __builtin_amdgcn_sched_barrier(0);
         issue(k, q + 4);
         publish(c0, buf);
         __syncthreads();
-        if (comp) {
-          PK R;
-          R.load(xs + (buf * 256 + tid + CVb) * V);
-          // q = q0 + k, q0 % 4 == 0: k even -> weight row 0 into output q/2 (slot k/2) and
-          // row 2 into output q/2 - 1 (slot 1 - k/2, then complete); k odd -> row 1 into
-          // output (q-1)/2 (slot k/2)
-          auto addrow = [&](int i, int sl) {
+        PK R;
+        R.load(xs + (buf * 256 + ri) * V);
+        // q = q0 + k, q0 % 4 == 0: k even -> weight row 0 into output q/2 (slot k/2) and
+        // row 2 into output q/2 - 1 (slot 1 - k/2, then complete); k odd -> row 1 into
+        // output (q-1)/2 (slot k/2)
+        auto addrow = [&](int i, int sl) {
 #pragma unroll
-            for (int v = 0; v < V; ++v) {
-              float a = acc[sl][v];
-              a = fmaf(c0[v], wr[i * 3][v], a);
-              a = fmaf(c1[v], wr[i * 3 + 1][v], a);
-              a = fmaf(R.get(v), wr[i * 3 + 2][v], a);
-              acc[sl][v] = a;
-            }
-          };
-          if ((k & 1) == 0) {
-            const int sn = k >> 1, sd = 1 - (k >> 1);
-            addrow(2, sd);
-            const int m = (q >> 1) - 1;
-            if (m >= 0 && ho0 + m < ho1) emit(acc[sd], ho0 + m, m == 0);
-#pragma unroll
-            for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
-            addrow(0, sn);
-          } else {
-            addrow(1, k >> 1);
+          for (int v = 0; v < V; ++v) {
+            float a = acc[sl][v];
+            a = fmaf(c0[v], wr[i * 3][v], a);
+            a = fmaf(c1[v], wr[i * 3 + 1][v], a);
+            a = fmaf(R.get(v), wr[i * 3 + 2][v], a);
+            acc[sl][v] = a;
           }
+        };
+        if ((k & 1) == 0) {
+          const int sn = k >> 1, sd = 1 - (k >> 1);
+          addrow(2, sd);
+          const int m = (q >> 1) - 1;
+          emit(acc[sd], ho0 + m, m >= 0 && ho0 + m < ho1, m == 0);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
+          addrow(0, sn);
+        } else {
+          addrow(1, k >> 1);
         }
       }
     }
@@ -2052,25 +2085,39 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
   dw_f2 sg[VP], sgx[VP];
 #pragma unroll
   for (int h = 0; h < VP; ++h) sg[h] = sgx[h] = dw_f2{0.f, 0.f};
-  const long nb = (long)n * H * W * C + c;
-  const T* yen = ye + nb + (long)colc * C;
-  const T* dzn = dz + nb + (long)colc * C;
-  const T* ydn = yd + nb + (long)colc * C;
-  T* dxn = dx + nb + (long)colc * C;
-  const long rstr = (long)W * C;
+  // buffer resources over this image (wave-uniform base); lane offset = its (clamped) column and
+  // channels, the row goes in the scalar offset
+  const long img = (long)n * H * W * C;
+  const unsigned ib = (unsigned)((long)H * W * C * sizeof(T));
+  const rsrc_t rye = rod_rsrc(ye + img, ib), rdz = rod_rsrc(dz + img, ib), ryd = rod_rsrc(yd + img, ib);
+  const rsrc_t rdx = rod_rsrc(dx + img, ib);
+  const unsigned vo = (unsigned)(((long)colc * C + c) * sizeof(T));
+  const unsigned vox = comp ? vo : ROD_OOB;   // halo lanes store nothing
+  const unsigned rstrb = (unsigned)(W * C * sizeof(T));
 
   PK rx[D], rz[D], ry[D];
-  auto issue = [&](int k, int q) {  // row conditions are block-uniform
+  // every step loads all three rows unconditionally, rows clamped into [xlo, xhi] (a clamped row
+  // re-reads one the block just read: a cache hit; the xok / dok masks zero its use), and the dx
+  // store is a buffer store every step (dropped by the range check off the strip / on halo
+  // lanes): with no memory operation under a branch the compiler counts the ring exactly
+  // (s_waitcnt vmcnt(N) for the step being consumed) instead of draining every load in flight
+  // (vmcnt(0)) at each step.
+  auto issue = [&](int k, int q) {
     const int rho = ho0 - 2 + q;
-    if (rho >= xlo && rho <= xhi) rx[k].load(yen + rho * rstr);
-    if (rho + 1 >= xlo && rho + 1 <= xhi) {
-      rz[k].load(dzn + (rho + 1) * rstr);
-      ry[k].load(ydn + (rho + 1) * rstr);
-    }
+    const int rx_ = rho < xlo ? xlo : (rho > xhi ? xhi : rho);
+    const int rd_ = rho + 1 < xlo ? xlo : (rho + 1 > xhi ? xhi : rho + 1);
+    rx[k].bload(rye, vo, (unsigned)rx_ * rstrb);
+    rz[k].bload(rdz, vo, (unsigned)rd_ * rstrb);
+    ry[k].bload(ryd, vo, (unsigned)rd_ * rstrb);
   };
   const int nst = ho1 - ho0 + 3;
+  // the prologue issues the slots in order (slot 0 first), so that the loop header's wait for
+  // slot 0 is the same count on entry as around the back-edge
 #pragma unroll
-  for (int k = 0; k < D; ++k) issue(k, k);
+  for (int k = 0; k < D; ++k) {
+    issue(k, k);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   dw_f2 acc[3][VP], fa[9][VP], q1[VP], q2[VP];
 #pragma unroll
   for (int h = 0; h < VP; ++h) {
@@ -2082,8 +2129,8 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       const int q = q0 + k;
-      if constexpr (D > 3) {  // the deep ring's tail steps are empty (block-uniform)
-        if (q >= nst) break;
+      if constexpr (D > 3) {  // the deep ring's tail: whole 3-step groups only (block-uniform), so
+        if (k % 3 == 0 && q >= nst) break;   // every path to the back-edge issued the same loads
       }
       const int rho = ho0 - 2 + q;
       const int buf = q & 1;
@@ -2125,6 +2172,10 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
           dv[h] = dok ? round2(o, T{}) : dw_f2{0.f, 0.f};
         }
       }
+      // keep the ring slot's reload after its last read: the scheduler hoisting it would make the
+      // slot's old and new values overlap, and the copy that resolves that at the loop back-edge
+      // has to wait for the load in flight (s_waitcnt vmcnt(0))
+      __builtin_amdgcn_sched_barrier(0);
       issue(k, q + D);
 #pragma unroll
       for (int h = 0; h < VP; ++h) {
@@ -2171,14 +2222,14 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
         q1[h] = f0;
       }
       // dx row rho is complete
-      if (rho >= ho0 && rho < ho1) {
-        PK o;
+      const bool rowout = rho >= ho0 && rho < ho1;
+      PK o;
 #pragma unroll
-        for (int h = 0; h < VP; ++h) {
-          o.set(2 * h, acc[k3][h].x);
-          o.set(2 * h + 1, acc[k3][h].y);
-        }
-        if (comp) o.store_out(dxn + rho * rstr);
+      for (int h = 0; h < VP; ++h) {
+        o.set(2 * h, acc[k3][h].x);
+        o.set(2 * h + 1, acc[k3][h].y);
+      }
+      if (rowout) {   // BN_e sums from the rounded dx, before the store (its last use)
         if constexpr (RED) {
 #pragma unroll
           for (int h = 0; h < VP; ++h) {
@@ -2189,6 +2240,7 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
           }
         }
       }
+      o.bstore(rdx, rowout ? vox : ROD_OOB, (unsigned)(rho < 0 ? 0 : rho) * rstrb);
 #pragma unroll
       for (int h = 0; h < VP; ++h) acc[k3][h] = dw_f2{0.f, 0.f};
     }
@@ -2506,11 +2558,12 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
     const int ring = ring_env == 6 ? 6 : 3;
     // stride 1: the issue-lean kernel; ROD_DWF_V1=1 (A/B switch) the first form
     static const bool v1 = getenv("ROD_DWF_V1") && atoi(getenv("ROD_DWF_V1")) == 1;
-    // bf16 default: 2 channels per thread in 512-thread blocks (120 VGPRs, 4 waves/SIMD) with a
-    // 6-step ring, stride-1 shapes 3.76 -> 3.70 ms in total (tools/dwfused_bench.py);
-    // ROD_DWF_C2=0 the 4-channel form, ROD_DWF_RING=3 the 3-step ring
+    // bf16 default: 2 channels per thread in 512-thread blocks (122 VGPRs, 4 waves/SIMD) with a
+    // 3-step ring: with branch-free buffer loads / stores the ring's wait counts are exact, and a
+    // 6-step ring needs 131 VGPRs (3 waves/SIMD; capped at 128 it spills).  ROD_DWF_C2=0 the
+    // 4-channel form, ROD_DWF_RING=6 the 6-step ring
     static const bool v2 = !(getenv("ROD_DWF_C2") && atoi(getenv("ROD_DWF_C2")) == 0);
-    const int vring = ring_env == 3 ? 3 : 6;
+    const int vring = ring_env == 6 ? 6 : 3;
 #define DWF1(PA, R, D)                                                                                               \
   hipLaunchKernelGGL((dw3x3_bwd_fused_kernel<T, PA, R, D>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,      \
                      (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)

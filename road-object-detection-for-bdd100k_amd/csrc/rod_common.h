@@ -66,6 +66,36 @@ template <> struct Vec16<bf16_t> {
   __device__ __forceinline__ void set(int i, float x) { v[i] = (bf16_t)x; }
 };
 
+// Buffer-resource I/O for streaming kernels with a register prefetch ring.  A load or store
+// inside a branch (a row outside the strip, a halo lane) makes the compiler's wait-count pass
+// lose track of how many vector-memory operations are in flight, and it then drains them all
+// (s_waitcnt vmcnt(0)) every step — the ring prefetches nothing.  With buffer instructions every
+// load / store is issued unconditionally: the 32-bit lane offset `vo` carries the per-lane
+// column, the wave-uniform `so` (SGPR) the row; a store that must not happen gets vo = ROD_OOB,
+// which the hardware range check (offset >= num_records) drops.  Base and size must be
+// wave-uniform; the byte range of one resource must fit in 31 bits.
+constexpr unsigned ROD_OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t rod_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+template <typename V> __device__ __forceinline__ V buf_ld(rsrc_t r, unsigned vo, unsigned so) {
+  constexpr int NB = sizeof(V);
+  static_assert(NB == 4 || NB == 8 || NB == 16, "buffer load of 4 / 8 / 16 bytes");
+  if constexpr (NB == 4) return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+  else if constexpr (NB == 8) return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+  else return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+}
+template <typename V> __device__ __forceinline__ void buf_st(const V& v, rsrc_t r, unsigned vo, unsigned so) {
+  constexpr int NB = sizeof(V);
+  static_assert(NB == 4 || NB == 8 || NB == 16, "buffer store of 4 / 8 / 16 bytes");
+  if constexpr (NB == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+  else if constexpr (NB == 8) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, vo, so, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, vo, so, 0);
+}
+
 // Correctly-rounded f32 transcendental functions (evaluated in f64 and
 // rounded once).  The oracle uses the same definition (np.float64 then cast),
 // so integer decisions downstream of exp/log are reproducible bit for bit.
