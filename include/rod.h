@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 15
+#define ROD_ABI_VERSION 16
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -539,6 +539,19 @@ int rod_slab_defer(int on);
 int rod_slab_pending(void);
 int rod_slab_flush(void* stream);
 int rod_slab_flush_range(const void* lo, const void* hi, void* stream);
+
+/* ------------------------------------------------ data-parallel reduce point (ABI 16)
+ * The exchange the reference's single-device optimizer step becomes under data parallelism
+ * (net_tools.py:645-651: the gradient is summed over the ranks before the clip + SGD).  One
+ * RCCL communicator per process (RCCL bound at run time: the process's already loaded
+ * librccl.so.1 is reused).  rod_rccl_unique_id writes the 128-byte id rank 0 creates; the
+ * caller distributes it (any rendezvous) and every rank calls rod_rccl_init with it.
+ * rod_allreduce_bucket sums `count` elements (ROD_F32 / ROD_BF16) in place over all ranks,
+ * ordered on `stream` (capturable into a HIP graph).  rod_rccl_destroy frees the communicator. */
+int rod_rccl_unique_id(void* uid128);
+int rod_rccl_init(int rank, int world, const void* uid128);
+int rod_allreduce_bucket(void* ptr, long count, int dtype, void* stream);
+int rod_rccl_destroy(void);
 
 #ifdef __cplusplus
 }

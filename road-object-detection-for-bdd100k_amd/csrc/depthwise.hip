@@ -797,18 +797,15 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
   // GP: per-channel constants of the BatchNorm-backward apply, and the raw (dz, y) loads of
   // the rows still in flight (their apply runs when they enter the contraction queue)
   constexpr int GV = GP ? V : 1;
-  float gmu[GV], grs[GV], gsc[GV], gsh[GV], ga[GV], gmg[GV], gmx[GV];
+  float gsc[GV], gsh[GV], ga[GV], gmg[GV], gmx[GV];
   const T* yn = nullptr;
   T* dyo = nullptr;
   if constexpr (GP) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      gmu[v] = gd.mean[c + v];
-      grs[v] = gd.rstd[c + v];
       bn_affine(gd.mean, gd.rstd, gd.gamma, gd.beta, c + v, gsc[v], gsh[v]);
       ga[v] = gd.coef[c + v];
-      gmg[v] = gd.coef[C + c + v];
-      gmx[v] = gd.coef[2 * C + c + v];
+      bn_bwd_k(ga[v], gd.mean[c + v], gd.rstd[c + v], gd.coef[C + c + v], gd.coef[2 * C + c + v], gmg[v], gmx[v]);
     }
     yn = (const T*)gd.y + (long)n * Ho * Wo * C + c;
     dyo = (T*)gd.dy + (long)n * Ho * Wo * C + c;
@@ -826,10 +823,9 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float xv = yv.get(v);
-        const float dd = xv - gmu[v];
         const float z = fmaf(xv, gsc[v], gsh[v]);
         const float g = d.get(v) * act_grad(z, gd.act);
-        d.set(v, ga[v] * (g - gmg[v] - (dd * grs[v]) * gmx[v]));
+        d.set(v, bn_bwd_apply1(ga[v], g, gmg[v], gmx[v], xv));   // gmg / gmx hold k1 / k0
       }
       d.store(dyo + ((long)(ho0 + m) * Wo + wo) * C);
     } else {
@@ -1803,15 +1799,12 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
     for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
   DwIn<T, V, PACT> in;
   in.init(pro, c);
-  float dmu[V], drs[V], dsc[V], dsh[V], da[V], dmg[V], dmx[V];
+  float dsc[V], dsh[V], da[V], dmg[V], dmx[V];   // dmg / dmx: the apply's k1 / k0
 #pragma unroll
   for (int v = 0; v < V; ++v) {
-    dmu[v] = bd.mean[c + v];
-    drs[v] = bd.rstd[c + v];
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c + v, dsc[v], dsh[v]);
     da[v] = bd.coef[c + v];
-    dmg[v] = bd.coef[C + c + v];
-    dmx[v] = bd.coef[2 * C + c + v];
+    bn_bwd_k(da[v], bd.mean[c + v], bd.rstd[c + v], bd.coef[C + c + v], bd.coef[2 * C + c + v], dmg[v], dmx[v]);
   }
   constexpr int RV = RED ? V : 1;
   float emu[RV], ers[RV], sg[RV], sgx[RV];
@@ -1879,10 +1872,9 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float yv = ry[k].get(v);
-        const float d = yv - dmu[v];
         const float z = fmaf(yv, dsc[v], dsh[v]);
         const float g = rz[k].get(v) * act_grad(z, bd.act);
-        const float o = da[v] * (g - dmg[v] - (d * drs[v]) * dmx[v]);
+        const float o = bn_bwd_apply1(da[v], g, dmg[v], dmx[v], yv);
         dv[v] = okd[k] ? to_f32(from_f32<T>(o)) : 0.f;
       }
       PK px, pd;
@@ -2006,8 +1998,21 @@ __device__ __forceinline__ void unpackv(const PackV<T, V>& p, dw_f2 (&o)[V / 2])
 #pragma unroll
   for (int h = 0; h < V / 2; ++h) o[h] = dw_f2{p.get(2 * h), p.get(2 * h + 1)};
 }
+// one v_cvt_pk_bf16_f32 for the pair (RNE, as (bf16_t)x per element), unpacked by a shift / mask
+typedef __bf16 dw_b2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ dw_f2 round2(dw_f2 v, bf16_t) {
-  return dw_f2{(float)(bf16_t)v.x, (float)(bf16_t)v.y};
+  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(v, dw_b2));
+  return dw_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
+// ReLU6 gradient gate (z > 0 && z < 6, NaN -> 0: agrad<ROD_ACT_RELU6>) as one unsigned compare
+// on the bits: positive floats order as integers, negative ones and NaN land above 6.0's bits
+__device__ __forceinline__ bool relu6_open(float z) {
+  return __builtin_bit_cast(unsigned, z) - 1u < 0x40BFFFFFu;
+}
+template <int ACT>
+__device__ __forceinline__ dw_f2 gate2(dw_f2 z, dw_f2 v, int act) {
+  if constexpr (ACT == ROD_ACT_RELU6) return dw_f2{relu6_open(z.x) ? v.x : 0.f, relu6_open(z.y) ? v.y : 0.f};
+  else return dw_f2{v.x * act_grad(z.x, act), v.y * act_grad(z.y, act)};
 }
 __device__ __forceinline__ dw_f2 round2(dw_f2 v, float) { return v; }
 
@@ -2023,12 +2028,14 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
   constexpr int VP = V / 2;  // V channels per thread = VP packed pairs
   constexpr int TB = 1024 / V;      // threads per block (the tile of the 4-channel plan)
   typedef PackV<T, V> PK;
-  // the row exchange holds the rounded fp32 pairs (no pack / unpack around the LDS trip)
-  constexpr int XS = 2 * 2 * TB * VP * (int)sizeof(dw_f2);
+  // the row exchange holds the rounded fp32 pairs (no pack / unpack around the LDS trip); three
+  // slots, one per step of the 3-step body, so every LDS address is the thread's base plus a
+  // compile-time offset
+  constexpr int XS = 3 * 2 * TB * VP * (int)sizeof(dw_f2);
   constexpr int SS = TB * V * 4;
   __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
   dw_f2* xs = (dw_f2*)smem;
-  dw_f2* dsl = xs + 2 * TB * VP;
+  dw_f2* dsl = xs + 3 * TB * VP;
   const int tid = threadIdx.x;
   const int CVb = tl.CVb * (4 / V), P = tl.P;
   const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
@@ -2067,20 +2074,20 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
       }
     }
   }
-  dw_f2 dmu[VP], drs[VP], dsc[VP], dsh[VP], da[VP], dmg[VP], dmx[VP];
+  dw_f2 dsc[VP], dsh[VP], da[VP], dmg[VP], dmx[VP];
 #pragma unroll
   for (int h = 0; h < VP; ++h) {
     const int c0 = c + 2 * h;
-    dmu[h] = dw_f2{bd.mean[c0], bd.mean[c0 + 1]};
-    drs[h] = dw_f2{bd.rstd[c0], bd.rstd[c0 + 1]};
-    float s0, t0, s1, t1;
+    float s0, t0, s1, t1, k10, k00, k11, k01;
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0, s0, t0);
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0 + 1, s1, t1);
     dsc[h] = dw_f2{s0, s1};
     dsh[h] = dw_f2{t0, t1};
     da[h] = dw_f2{bd.coef[c0], bd.coef[c0 + 1]};
-    dmg[h] = dw_f2{bd.coef[C + c0], bd.coef[C + c0 + 1]};
-    dmx[h] = dw_f2{bd.coef[2 * C + c0], bd.coef[2 * C + c0 + 1]};
+    bn_bwd_k(da[h].x, bd.mean[c0], bd.rstd[c0], bd.coef[C + c0], bd.coef[2 * C + c0], k10, k00);
+    bn_bwd_k(da[h].y, bd.mean[c0 + 1], bd.rstd[c0 + 1], bd.coef[C + c0 + 1], bd.coef[2 * C + c0 + 1], k11, k01);
+    dmg[h] = dw_f2{k10, k11};   // the apply's k1 / k0 (bn_bwd_k)
+    dmx[h] = dw_f2{k00, k01};
   }
   dw_f2 sg[VP], sgx[VP];
 #pragma unroll
@@ -2133,8 +2140,8 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
         if (k % 3 == 0 && q >= nst) break;   // every path to the back-edge issued the same loads
       }
       const int rho = ho0 - 2 + q;
-      const int buf = q & 1;
       const int k3 = k % 3;
+      const int buf = k3;
       const bool xok = cok && rho >= xlo && rho <= xhi;
       const bool dok = cok && rho + 1 >= xlo && rho + 1 <= xhi;
       // x row rho (prologue, rounded to T) and, with RED, BN_e's gradient mask at the same element
@@ -2152,7 +2159,7 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
             t = dw_f2{act_fwd(z.x, pact), act_fwd(z.y, pact)};
           }
           a = round2(t, T{});
-          if constexpr (RED) em[h] = dw_f2{agrad<PACT>(z.x, pact), agrad<PACT>(z.y, pact)};
+          if constexpr (RED) em[h] = z;   // BN_e's pre-activation: the gradient gate of this element
         }
         xv[h] = xok ? a : dw_f2{0.f, 0.f};
       }
@@ -2164,11 +2171,9 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
         unpackv(rz[k], zv);
 #pragma unroll
         for (int h = 0; h < VP; ++h) {
-          const dw_f2 d = yv[h] - dmu[h];
           const dw_f2 z = f2fma(yv[h], dsc[h], dsh[h]);
-          const dw_f2 m = dw_f2{agrad<BACT>(z.x, bd.act), agrad<BACT>(z.y, bd.act)};
-          const dw_f2 g = zv[h] * m;
-          const dw_f2 o = da[h] * ((g - dmg[h]) - (d * drs[h]) * dmx[h]);
+          const dw_f2 g = gate2<BACT>(z, zv[h], bd.act);
+          const dw_f2 o = f2fma(da[h], g, f2fma(dmg[h], yv[h], dmx[h]));   // bn_bwd_apply1, pairwise
           dv[h] = dok ? round2(o, T{}) : dw_f2{0.f, 0.f};
         }
       }
@@ -2226,15 +2231,21 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
       PK o;
 #pragma unroll
       for (int h = 0; h < VP; ++h) {
-        o.set(2 * h, acc[k3][h].x);
-        o.set(2 * h + 1, acc[k3][h].y);
+        if constexpr (sizeof(T) == 2) {   // one v_cvt_pk_bf16_f32 per pair
+          const dw_b2 b = __builtin_convertvector(acc[k3][h], dw_b2);
+          o.v[2 * h] = b.x;
+          o.v[2 * h + 1] = b.y;
+        } else {
+          o.set(2 * h, acc[k3][h].x);
+          o.set(2 * h + 1, acc[k3][h].y);
+        }
       }
       if (rowout) {   // BN_e sums from the rounded dx, before the store (its last use)
         if constexpr (RED) {
 #pragma unroll
           for (int h = 0; h < VP; ++h) {
             const dw_f2 ov = dw_f2{o.get(2 * h), o.get(2 * h + 1)};
-            const dw_f2 g = ov * em[h];
+            const dw_f2 g = gate2<PACT>(em[h], ov, pact);
             sg[h] += g;
             sgx[h] = f2fma(g, f2fma(yr[h], ers[h], enb[h]), sgx[h]);
           }
@@ -2320,15 +2331,12 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
     for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
   DwIn<T, V, PACT> in;
   in.init(pro, c);
-  float dmu[V], drs[V], dsc[V], dsh[V], da[V], dmg[V], dmx[V];
+  float dsc[V], dsh[V], da[V], dmg[V], dmx[V];   // dmg / dmx: the apply's k1 / k0
 #pragma unroll
   for (int v = 0; v < V; ++v) {
-    dmu[v] = bd.mean[c + v];
-    drs[v] = bd.rstd[c + v];
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c + v, dsc[v], dsh[v]);
     da[v] = bd.coef[c + v];
-    dmg[v] = bd.coef[C + c + v];
-    dmx[v] = bd.coef[2 * C + c + v];
+    bn_bwd_k(da[v], bd.mean[c + v], bd.rstd[c + v], bd.coef[C + c + v], bd.coef[2 * C + c + v], dmg[v], dmx[v]);
   }
   constexpr int RV = RED ? V : 1;
   float enb[RV], ers[RV], sg[RV], sgx[RV];  // xhat_e = fma(y_e, rstd, -mean * rstd)
@@ -2340,11 +2348,20 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
       sg[v] = sgx[v] = 0.f;
     }
   }
-  const T* yen = ye + (long)n * H * W * C + c;
-  T* dxn = dx + (long)n * H * W * C + c;
-  const long ob = (long)n * Ho * Wo * C + c;
-  const T* dzn = dz + ob;
-  const T* ydn = yd + ob;
+  // buffer resources over this image; every load is issued (rows / columns clamped into the
+  // map, uses masked by okd / okx) and every dx store too (vo = ROD_OOB where nothing is to be
+  // written), so the wait counts of the prefetch ring stay exact (see rod_common.h)
+  const unsigned es = sizeof(T);
+  const rsrc_t rye = rod_rsrc(ye + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
+  const rsrc_t rdx = rod_rsrc(dx + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
+  const rsrc_t rdz = rod_rsrc(dz + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
+  const rsrc_t ryd = rod_rsrc(yd + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
+  const int bc = b < 0 ? 0 : (b >= Wo ? Wo - 1 : b);
+  const int x0c = ci0 < 0 ? 0 : (ci0 >= W ? W - 1 : ci0), x1c = ci0 + 1 < 0 ? 0 : (ci0 + 1 >= W ? W - 1 : ci0 + 1);
+  const unsigned vod = (unsigned)(((long)bc * C + c) * es);
+  const unsigned vox0 = (unsigned)(((long)x0c * C + c) * es), vox1 = (unsigned)(((long)x1c * C + c) * es);
+  const unsigned vst0 = comp && cok0 ? vox0 : ROD_OOB, vst1 = comp && cok1 ? vox1 : ROD_OOB;
+  const unsigned rsx = (unsigned)(W * C * es), rsd = (unsigned)(Wo * C * es);
 
   // ring slot: dy (dz, yd) of row a, x (ye) at rows 2a-pt, 2a+1-pt x columns ci0, ci0+1
   PK rz[D], ry[D], rx[D][4];
@@ -2354,21 +2371,24 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
   auto issue = [&](int k, int q) {
     const int a = a0 - 1 + q;
     okd[k] = cokd && a >= dlo && a <= dhi;
-    if (okd[k]) {
-      rz[k].load(dzn + ((long)a * Wo + b) * C);
-      ry[k].load(ydn + ((long)a * Wo + b) * C);
-    }
+    const int ac = a < dlo ? dlo : (a > dhi ? dhi : a);
+    rz[k].bload(rdz, vod, (unsigned)ac * rsd);
+    ry[k].bload(ryd, vod, (unsigned)ac * rsd);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int h = 2 * a - pt + (i >> 1);
       const bool rowok = a >= a0 && (i < 2 ? a <= a1 : a < a1) && h >= 0 && h < H;
       okx[k][i] = rowok && ((i & 1) ? cok1 : cok0);
-      if (okx[k][i]) rx[k][i].load(yen + ((long)h * W + ci0 + (i & 1)) * C);
+      const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h);
+      rx[k][i].bload(rye, (i & 1) ? vox1 : vox0, (unsigned)hc * rsx);
     }
   };
   const int nst = a1 - a0 + 2;
 #pragma unroll
-  for (int k = 0; k < D; ++k) issue(k, k);
+  for (int k = 0; k < D; ++k) {   // slot order (the loop header's wait is then the same on entry)
+    issue(k, k);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   float fa[9][V], pv[V], pL[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
@@ -2386,10 +2406,9 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float yv = ry[k].get(v);
-        const float d = yv - dmu[v];
         const float z = fmaf(yv, dsc[v], dsh[v]);
         const float g = rz[k].get(v) * act_grad(z, bd.act);
-        const float o = da[v] * (g - dmg[v] - (d * drs[v]) * dmx[v]);
+        const float o = bn_bwd_apply1(da[v], g, dmg[v], dmx[v], yv);
         dv[v] = okd[k] ? to_f32(from_f32<T>(o)) : 0.f;
       }
       float xv[4][V], yr[4][V];
@@ -2409,49 +2428,54 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
         p0.set(v, xv[0][v]);
         p1.set(v, xv[2][v]);
       }
+      __builtin_amdgcn_sched_barrier(0);   // the slots' reloads stay after their last reads
       issue(k, q + D);
       dsl[buf * 256 + tid] = pd;
       x0s[buf * 256 + tid] = p0;
       x1s[buf * 256 + tid] = p1;
       __syncthreads();
-      if (comp) {
-        const PK dlp = dsl[buf * 256 + tid - CVb];
-        const PK r0 = x0s[buf * 256 + tid + CVb], r1 = x1s[buf * 256 + tid + CVb];
+      {
+        // every lane computes (halo lanes' results are dropped: stores out of range, column sums
+        // masked by comp), so no memory operation sits under a branch
+        const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < 256 ? tid + CVb : tid;
+        const PK dlp = dsl[buf * 256 + li];
+        const PK r0 = x0s[buf * 256 + ri], r1 = x1s[buf * 256 + ri];
         float dL[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) dL[v] = dlp.get(v);
-        if (a >= a0 && a < a1) {
-          // dx block: taps as dw3x3_bwd_data_s2_kernel (c1 = dy[a][b], c0 = dy[a][b-1], p1, p0 = row a-1)
-          float o[4][V];
+        const bool own = a >= a0 && a < a1, ownp = a - 1 >= a0 && a - 1 < a1;
+        // dx block: taps as dw3x3_bwd_data_s2_kernel (c1 = dy[a][b], c0 = dy[a][b-1], p1, p0 = row a-1)
+        float o[4][V];
 #pragma unroll
-          for (int v = 0; v < V; ++v) {
-            const float c1 = dv[v], c0 = dL[v], p1v = pv[v], p0v = pL[v];
-            o[0][v] = fmaf(p0v, wr[8][v], fmaf(p1v, wr[6][v], fmaf(c0, wr[2][v], c1 * wr[0][v])));
-            o[1][v] = fmaf(p1v, wr[7][v], c1 * wr[1][v]);
-            o[2][v] = fmaf(c0, wr[5][v], c1 * wr[3][v]);
-            o[3][v] = c1 * wr[4][v];
-          }
+        for (int v = 0; v < V; ++v) {
+          const float c1 = dv[v], c0 = dL[v], p1v = pv[v], p0v = pL[v];
+          o[0][v] = fmaf(p0v, wr[8][v], fmaf(p1v, wr[6][v], fmaf(c0, wr[2][v], c1 * wr[0][v])));
+          o[1][v] = fmaf(p1v, wr[7][v], c1 * wr[1][v]);
+          o[2][v] = fmaf(c0, wr[5][v], c1 * wr[3][v]);
+          o[3][v] = c1 * wr[4][v];
+        }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int h = 2 * a - pt + (i >> 1), ww = ci0 + (i & 1);
-            if (h < 0 || h >= H || ww < 0 || ww >= W) continue;
-            PK pk;
+        for (int i = 0; i < 4; ++i) {
+          const int h = 2 * a - pt + (i >> 1);
+          const bool hok = own && h >= 0 && h < H;
+          PK pk;
 #pragma unroll
-            for (int v = 0; v < V; ++v) pk.set(v, o[i][v]);
-            pk.store_out(dxn + ((long)h * W + ww) * C);
-            if constexpr (RED) {
+          for (int v = 0; v < V; ++v) pk.set(v, o[i][v]);
+          if constexpr (RED) {   // BN_e sums from the rounded dx, before the store (its last use)
+            if (hok) {
+              const bool cc = (i & 1) ? cok1 : cok0;
 #pragma unroll
               for (int v = 0; v < V; ++v) {
                 const float z = fmaf(yr[i][v], in.sc[v], in.sh[v]);
-                const float g = pk.get(v) * act_grad(z, pro.act);
+                const float g = cc ? pk.get(v) * act_grad(z, pro.act) : 0.f;
                 sg[v] += g;
                 sgx[v] = fmaf(g, fmaf(yr[i][v], ers[v], enb[v]), sgx[v]);
               }
             }
           }
+          pk.bstore(rdx, hok ? ((i & 1) ? vst1 : vst0) : ROD_OOB, (unsigned)(hok ? h : 0) * rsx);
         }
         // filter: dy[a] with x rows 2a-pt (tap row 0) and 2a+1-pt (1), dy[a-1] with 2a-pt (2)
-        const bool own = a >= a0 && a < a1, ownp = a - 1 >= a0 && a - 1 < a1;
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           const float f0 = own ? dv[v] : 0.f, f2 = ownp ? pv[v] : 0.f;
@@ -2479,6 +2503,279 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
   auto colsum = [&](const float (&acc)[V], float* dst) {
 #pragma unroll
     for (int v = 0; v < V; ++v) red[tid * V + v] = comp ? acc[v] : 0.f;
+    __syncthreads();
+    for (int e = tid; e < Cc; e += 256) {
+      const int cve = e / V, v = e - cve * V;
+      float s = 0.f;
+      for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
+      dst[cg * Cc + e] = s;
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int k = 0; k < 9; ++k) colsum(fa[k], slab + (part * 9 + k) * C);
+  if constexpr (RED) {
+    colsum(sg, gparts + part * 2 * C);
+    colsum(sgx, gparts + part * 2 * C + C);
+  }
+}
+
+// Packed stride-2 form (bf16, the default): the same tile, step order, dx accumulation order
+// (bit-identical dx) and filter / BN_e sums as dw3x3_bwd_fused_s2_kernel, with the four channels
+// of a thread as two packed fp32 pairs (v_pk_fma / v_pk_mul: one instruction per pair), the
+// BatchNorm-backward apply in its two-FMA form, one v_cvt_pk_bf16_f32 per rounded pair, the
+// ReLU6 gates as selects, the row exchange in fp32 pairs (no pack / unpack around the LDS trip)
+// with one LDS slot per step of the 2-step body (compile-time addresses), and the BN_e gate
+// taken from the prologue's own pre-activation.
+template <int PACT, bool RED, int BACT, int D = 2>
+__global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2p_kernel(
+    const bf16_t* __restrict__ ye, const bf16_t* __restrict__ dz, const bf16_t* __restrict__ yd,
+    const float* __restrict__ w, bf16_t* __restrict__ dx, float* __restrict__ slab, float* __restrict__ gparts, int H,
+    int W, int C, int pt, int pl, int Ho, int Wo, DwTile tl, BnPro pro, DwBwdBn bd) {
+  typedef bf16_t T;
+  constexpr int V = 4, VP = 2;
+  typedef PackV<T, V> PK;
+  static_assert(D == 2, "one LDS slot per step of the 2-step body");
+  // slots [D][3][256][VP] fp32 pairs: dy, x row 0, x row 1 (column ci0)
+  constexpr int XS = D * 3 * 256 * VP * (int)sizeof(dw_f2);
+  constexpr int SS = 256 * V * 4;
+  __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
+  dw_f2* sl = (dw_f2*)smem;
+  const int tid = threadIdx.x;
+  const int CVb = tl.CVb, P = tl.P;
+  const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
+  int bx, strip, n;
+  xcd_block(bx, strip, n);
+  const int cg = bx % tl.cgroups, ct = bx / tl.cgroups;
+  const int c = (cg * CVb + cvb) * V;
+  const int b = ct * tl.TWo + p - 1;
+  const int ci0 = 2 * b - pl;
+  const int A = ((H - 1 + pt) >> 1) + 1, B = ((W - 1 + pl) >> 1) + 1;
+  const bool comp = p >= 1 && p <= P - 2 && b < B;
+  const bool cokd = p < P && b >= 0 && b < Wo;
+  const bool cok0 = p < P && ci0 >= 0 && ci0 < W;
+  const bool cok1 = p < P && ci0 + 1 >= 0 && ci0 + 1 < W;
+  const int a0 = strip * tl.RB;
+  const int a1 = a0 + tl.RB < A ? a0 + tl.RB : A;
+  const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < 256 ? tid + CVb : tid;
+
+  dw_f2 wr[9][VP];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int h = 0; h < VP; ++h) wr[k][h] = dw_f2{w[k * C + c + 2 * h], w[k * C + c + 2 * h + 1]};
+  dw_f2 psc[VP], psh[VP], ers[VP], enb[VP];
+  int pact = 0;
+  if constexpr (PACT >= 0) {
+    pact = pro.act;
+#pragma unroll
+    for (int h = 0; h < VP; ++h) {
+      float a0_, b0_, a1_, b1_;
+      bn_pro_affine(pro, c + 2 * h, a0_, b0_);
+      bn_pro_affine(pro, c + 2 * h + 1, a1_, b1_);
+      psc[h] = dw_f2{a0_, a1_};
+      psh[h] = dw_f2{b0_, b1_};
+      if constexpr (RED) {
+        ers[h] = dw_f2{pro.rstd[c + 2 * h], pro.rstd[c + 2 * h + 1]};
+        enb[h] = dw_f2{-pro.mean[c + 2 * h] * ers[h].x, -pro.mean[c + 2 * h + 1] * ers[h].y};
+      }
+    }
+  }
+  dw_f2 dsc[VP], dsh[VP], da[VP], dk1[VP], dk0[VP];
+#pragma unroll
+  for (int h = 0; h < VP; ++h) {
+    const int c0 = c + 2 * h;
+    float s0, t0, s1, t1, k10, k00, k11, k01;
+    bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0, s0, t0);
+    bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0 + 1, s1, t1);
+    dsc[h] = dw_f2{s0, s1};
+    dsh[h] = dw_f2{t0, t1};
+    da[h] = dw_f2{bd.coef[c0], bd.coef[c0 + 1]};
+    bn_bwd_k(da[h].x, bd.mean[c0], bd.rstd[c0], bd.coef[C + c0], bd.coef[2 * C + c0], k10, k00);
+    bn_bwd_k(da[h].y, bd.mean[c0 + 1], bd.rstd[c0 + 1], bd.coef[C + c0 + 1], bd.coef[2 * C + c0 + 1], k11, k01);
+    dk1[h] = dw_f2{k10, k11};
+    dk0[h] = dw_f2{k00, k01};
+  }
+  dw_f2 sg[VP], sgx[VP];
+#pragma unroll
+  for (int h = 0; h < VP; ++h) sg[h] = sgx[h] = dw_f2{0.f, 0.f};
+
+  const unsigned es = sizeof(T);
+  const rsrc_t rye = rod_rsrc(ye + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
+  const rsrc_t rdx = rod_rsrc(dx + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
+  const rsrc_t rdz = rod_rsrc(dz + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
+  const rsrc_t ryd = rod_rsrc(yd + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
+  const int bc = b < 0 ? 0 : (b >= Wo ? Wo - 1 : b);
+  const int x0c = ci0 < 0 ? 0 : (ci0 >= W ? W - 1 : ci0), x1c = ci0 + 1 < 0 ? 0 : (ci0 + 1 >= W ? W - 1 : ci0 + 1);
+  const unsigned vod = (unsigned)(((long)bc * C + c) * es);
+  const unsigned vox0 = (unsigned)(((long)x0c * C + c) * es), vox1 = (unsigned)(((long)x1c * C + c) * es);
+  const unsigned vst0 = comp && cok0 ? vox0 : ROD_OOB, vst1 = comp && cok1 ? vox1 : ROD_OOB;
+  const unsigned rsx = (unsigned)(W * C * es), rsd = (unsigned)(Wo * C * es);
+
+  PK rz[D], ry[D], rx[D][4];
+  bool okd[D], okx[D][4];
+  const int dlo = a0 - 1 > 0 ? a0 - 1 : 0;
+  const int dhi = a1 - 1 < Ho - 1 ? a1 - 1 : Ho - 1;
+  auto issue = [&](int k, int q) {
+    const int a = a0 - 1 + q;
+    okd[k] = cokd && a >= dlo && a <= dhi;
+    const int ac = a < dlo ? dlo : (a > dhi ? dhi : a);
+    rz[k].bload(rdz, vod, (unsigned)ac * rsd);
+    ry[k].bload(ryd, vod, (unsigned)ac * rsd);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hh = 2 * a - pt + (i >> 1);
+      const bool rowok = a >= a0 && (i < 2 ? a <= a1 : a < a1) && hh >= 0 && hh < H;
+      okx[k][i] = rowok && ((i & 1) ? cok1 : cok0);
+      const int hc = hh < 0 ? 0 : (hh >= H ? H - 1 : hh);
+      rx[k][i].bload(rye, (i & 1) ? vox1 : vox0, (unsigned)hc * rsx);
+    }
+  };
+  const int nst = a1 - a0 + 2;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    issue(k, k);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  dw_f2 fa[9][VP], pv[VP], pL[VP];
+#pragma unroll
+  for (int h = 0; h < VP; ++h) {
+    pv[h] = pL[h] = dw_f2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) fa[k][h] = dw_f2{0.f, 0.f};
+  }
+  const dw_f2 zero2 = dw_f2{0.f, 0.f};
+  for (int q0 = 0; q0 < nst; q0 += D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int q = q0 + k;
+      const int a = a0 - 1 + q;
+      // dy[a][b]: BN_d backward apply (two-FMA form), rounded to bf16
+      dw_f2 dv[VP];
+      {
+        dw_f2 yv[VP], zv[VP];
+        unpackv(ry[k], yv);
+        unpackv(rz[k], zv);
+#pragma unroll
+        for (int h = 0; h < VP; ++h) {
+          const dw_f2 z = f2fma(yv[h], dsc[h], dsh[h]);
+          const dw_f2 g = gate2<BACT>(z, zv[h], bd.act);
+          const dw_f2 o = f2fma(da[h], g, f2fma(dk1[h], yv[h], dk0[h]));
+          dv[h] = okd[k] ? round2(o, T{}) : zero2;
+        }
+      }
+      // x at the 4 positions (prologue, rounded) and, with RED, BN_e's pre-activation (the gate)
+      dw_f2 xv[4][VP], yr[4][VP], ez[4][VP];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        unpackv(rx[k][i], yr[i]);
+#pragma unroll
+        for (int h = 0; h < VP; ++h) {
+          dw_f2 av = yr[i][h];
+          if constexpr (PACT >= 0) {
+            const dw_f2 z = f2fma(av, psc[h], psh[h]);
+            dw_f2 t;
+            if constexpr (PACT == ROD_ACT_RELU6) t = dw_f2{act_t<ROD_ACT_RELU6>(z.x), act_t<ROD_ACT_RELU6>(z.y)};
+            else t = dw_f2{act_fwd(z.x, pact), act_fwd(z.y, pact)};
+            av = round2(t, T{});
+            if constexpr (RED) ez[i][h] = z;
+          }
+          xv[i][h] = okx[k][i] ? av : zero2;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // the slots' reloads stay after their last reads
+      issue(k, q + D);
+      dw_f2* S = sl + k * 3 * 256 * VP;
+#pragma unroll
+      for (int h = 0; h < VP; ++h) {
+        S[tid * VP + h] = dv[h];
+        S[(256 + tid) * VP + h] = xv[0][h];
+        S[(512 + tid) * VP + h] = xv[2][h];
+      }
+      __syncthreads();
+      dw_f2 dL[VP], r0[VP], r1[VP];
+#pragma unroll
+      for (int h = 0; h < VP; ++h) {
+        dL[h] = S[li * VP + h];
+        r0[h] = S[(256 + ri) * VP + h];
+        r1[h] = S[(512 + ri) * VP + h];
+      }
+      const bool own = a >= a0 && a < a1, ownp = a - 1 >= a0 && a - 1 < a1;
+      // dx 2x2 block in the order of dw3x3_bwd_data_s2_kernel (bit-identical)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hh = 2 * a - pt + (i >> 1);
+        const bool hok = own && hh >= 0 && hh < H;
+        dw_f2 o[VP];
+#pragma unroll
+        for (int h = 0; h < VP; ++h) {
+          const dw_f2 c1 = dv[h], c0 = dL[h], p1v = pv[h], p0v = pL[h];
+          if (i == 0) o[h] = f2fma(p0v, wr[8][h], f2fma(p1v, wr[6][h], f2fma(c0, wr[2][h], c1 * wr[0][h])));
+          else if (i == 1) o[h] = f2fma(p1v, wr[7][h], c1 * wr[1][h]);
+          else if (i == 2) o[h] = f2fma(c0, wr[5][h], c1 * wr[3][h]);
+          else o[h] = c1 * wr[4][h];
+        }
+        PK pk;
+        dw_f2 orr[VP];
+#pragma unroll
+        for (int h = 0; h < VP; ++h) {
+          const dw_b2 bb = __builtin_convertvector(o[h], dw_b2);
+          pk.v[2 * h] = bb.x;
+          pk.v[2 * h + 1] = bb.y;
+          const unsigned u = __builtin_bit_cast(unsigned, bb);
+          orr[h] = dw_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+        }
+        if constexpr (RED) {   // BN_e sums from the rounded dx, before the store (its last use)
+          if (hok) {
+            const bool cc = (i & 1) ? cok1 : cok0;
+#pragma unroll
+            for (int h = 0; h < VP; ++h) {
+              const dw_f2 g = cc ? gate2<PACT>(ez[i][h], orr[h], pact) : zero2;
+              sg[h] += g;
+              sgx[h] = f2fma(g, f2fma(yr[i][h], ers[h], enb[h]), sgx[h]);
+            }
+          }
+        }
+        pk.bstore(rdx, hok ? ((i & 1) ? vst1 : vst0) : ROD_OOB, (unsigned)(hok ? hh : 0) * rsx);
+      }
+      // filter: dy[a] with x rows 2a-pt (tap row 0) and 2a+1-pt (1), dy[a-1] with 2a-pt (2)
+      if (own) {
+#pragma unroll
+        for (int h = 0; h < VP; ++h) {
+          fa[0][h] = f2fma(dv[h], xv[0][h], fa[0][h]);
+          fa[1][h] = f2fma(dv[h], xv[1][h], fa[1][h]);
+          fa[2][h] = f2fma(dv[h], r0[h], fa[2][h]);
+          fa[3][h] = f2fma(dv[h], xv[2][h], fa[3][h]);
+          fa[4][h] = f2fma(dv[h], xv[3][h], fa[4][h]);
+          fa[5][h] = f2fma(dv[h], r1[h], fa[5][h]);
+        }
+      }
+      if (ownp) {
+#pragma unroll
+        for (int h = 0; h < VP; ++h) {
+          fa[6][h] = f2fma(pv[h], xv[0][h], fa[6][h]);
+          fa[7][h] = f2fma(pv[h], xv[1][h], fa[7][h]);
+          fa[8][h] = f2fma(pv[h], r0[h], fa[8][h]);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < VP; ++h) {
+        pv[h] = dv[h];
+        pL[h] = dL[h];
+      }
+    }
+  }
+
+  __syncthreads();
+  float* red = (float*)smem;
+  const int Cc = CVb * V;
+  const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+  auto colsum = [&](const dw_f2 (&acc)[VP], float* dst) {
+#pragma unroll
+    for (int h = 0; h < VP; ++h) {
+      red[tid * V + 2 * h] = comp ? acc[h].x : 0.f;
+      red[tid * V + 2 * h + 1] = comp ? acc[h].y : 0.f;
+    }
     __syncthreads();
     for (int e = tid; e < Cc; e += 256) {
       const int cve = e / V, v = e - cve * V;
@@ -2567,11 +2864,30 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
 #define DWF1(PA, R, D)                                                                                               \
   hipLaunchKernelGGL((dw3x3_bwd_fused_kernel<T, PA, R, D>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,      \
                      (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, t, pv, bd)
-    // stride 2 ring: 3 steps (bf16), 2 (fp32: 16-byte slots; 3 spills to scratch)
-    constexpr int D2 = sizeof(T) == 2 ? 3 : 2;
+    // stride 2 ring (branch-free buffer I/O, exact wait counts): 2 steps for bf16 (238 VGPRs;
+    // 3 steps spill), 1 for fp32 (16-byte slots: 2 steps spill)
+    constexpr int D2 = sizeof(T) == 2 ? 2 : 1;
+    // bf16: the packed form (ROD_DWF_S2P=0: the scalar one)
+    static const bool s2p = !(getenv("ROD_DWF_S2P") && atoi(getenv("ROD_DWF_S2P")) == 0);
 #define DWS2(PA, R)                                                                                                  \
-  hipLaunchKernelGGL((dw3x3_bwd_fused_s2_kernel<T, PA, R, D2>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz,   \
-                     (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, pad_t, pad_l, Ho, Wo, t, pv, bd)
+  do {                                                                                                              \
+    if constexpr (sizeof(T) == 2) {                                                                                 \
+      if (s2p && bn_act == ROD_ACT_RELU6) {                                                                         \
+        hipLaunchKernelGGL((dw3x3_bwd_fused_s2p_kernel<PA, R, ROD_ACT_RELU6>), grid, dim3(256), 0, s,               \
+                           (const bf16_t*)ye, (const bf16_t*)dz, (const bf16_t*)yd, w, (bf16_t*)dx, slab, gparts, H,  \
+                           W, C, pad_t, pad_l, Ho, Wo, t, pv, bd);                                                  \
+        break;                                                                                                      \
+      }                                                                                                             \
+      if (s2p) {                                                                                                    \
+        hipLaunchKernelGGL((dw3x3_bwd_fused_s2p_kernel<PA, R, DW_ACT_RT>), grid, dim3(256), 0, s, (const bf16_t*)ye,  \
+                           (const bf16_t*)dz, (const bf16_t*)yd, w, (bf16_t*)dx, slab, gparts, H, W, C, pad_t, pad_l, \
+                           Ho, Wo, t, pv, bd);                                                                      \
+        break;                                                                                                      \
+      }                                                                                                             \
+    }                                                                                                               \
+    hipLaunchKernelGGL((dw3x3_bwd_fused_s2_kernel<T, PA, R, D2>), grid, dim3(256), 0, s, (const T*)ye, (const T*)dz, \
+                       (const T*)yd, w, (T*)dx, slab, gparts, H, W, C, pad_t, pad_l, Ho, Wo, t, pv, bd);             \
+  } while (0)
 #define DWV2(PA, R, BA)                                                                                              \
   do {                                                                                                              \
     if constexpr (sizeof(T) == 2) {                                                                                 \

@@ -83,8 +83,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
     t[2 * Cout] = sc;
     t[3 * Cout] = sh;
     t[4 * Cout] = a.coef[c];
-    t[5 * Cout] = a.coef[Cout + c];
-    t[6 * Cout] = a.coef[2 * Cout + c];
+    bn_bwd_k(a.coef[c], a.mean[c], a.rstd[c], a.coef[Cout + c], a.coef[2 * Cout + c], t[5 * Cout], t[6 * Cout]);
     t[7 * Cout] = 0.f;
   }
   if (prox) {
@@ -163,15 +162,14 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
           for (int h = 0; h < 2; ++h) {
             f32x4 f[7];
 #pragma unroll
-            for (int k = 0; k < 7; ++k) f[k] = *(const f32x4*)(ctab + k * Cout + cc * 8 + 4 * h);
+            for (int k = 2; k < 7; ++k) f[k] = *(const f32x4*)(ctab + k * Cout + cc * 8 + 4 * h);
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
               const int j = 4 * h + jj;
               const float yj = (float)yv[u][j];
-              const float d = yj - f[0][jj];
               const float z = fmaf(yj, f[2][jj], f[3][jj]);
               const float gj = (float)dv[u][j] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
-              o[j] = (bf16_t)(f[4][jj] * (gj - f[5][jj] - (d * f[1][jj]) * f[6][jj]));
+              o[j] = (bf16_t)bn_bwd_apply1(f[4][jj], gj, f[5][jj], f[6][jj], yj);   // fields 5, 6: k1, k0
             }
           }
         } else {

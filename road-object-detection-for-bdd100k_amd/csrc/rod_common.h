@@ -171,6 +171,21 @@ __device__ __forceinline__ void bn_affine(const float* mean, const float* rstd, 
   sh = (beta ? beta[c] : 0.f) - mean[c] * sc;
 }
 
+// ---- BatchNorm-backward apply --------------------------------------------------------
+// TF's FusedBatchNormGrad: dy = a*(g - mean(g) - yhat*mean(g*yhat)), yhat = (y - mean)*rstd,
+// with coef = (a, mean(g), mean(g*yhat)) per channel (rod_bn_bwd_finalize).  Every librod kernel
+// that applies it (rod_bn_bwd_apply, the one-launch small-tensor form, the fused depthwise and
+// 1x1 backwards) evaluates it as  fma(a, g, fma(k1, y, k0))  with the per-channel constants
+// below — two FMAs per element instead of five operations — so all of them round identically.
+__device__ __forceinline__ void bn_bwd_k(float a, float mu, float rs, float mg, float mgx, float& k1, float& k0) {
+  const float t = rs * mgx;
+  k1 = -(a * t);
+  k0 = a * fmaf(t, mu, -mg);
+}
+__device__ __forceinline__ float bn_bwd_apply1(float a, float g, float k1, float k0, float y) {
+  return fmaf(a, g, fmaf(k1, y, k0));
+}
+
 // ---- BatchNorm-apply prologue -----------------------------------------------------
 // A consumer kernel that reads the PRE-BatchNorm tensor y instead of the BatchNorm output:
 // z = act(fma(y, scale, offset)), rounded to the storage type — exactly the value

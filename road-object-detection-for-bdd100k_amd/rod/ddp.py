@@ -19,11 +19,31 @@ import torch
 import torch.distributed as dist
 
 
+def native_comm_init(rank, world, group=None):
+    """The C-ABI reduce point (include/rod.h ABI 16: rod_rccl_unique_id / rod_rccl_init): rank 0
+    makes the RCCL unique id, torch.distributed's store hands it to every rank (world > 1), and
+    every rank creates the library's communicator.  Returns nothing; rod_rccl_destroy frees it."""
+    import ctypes
+    from . import _abi
+    uid = (ctypes.c_char * 128)()
+    if rank == 0:
+        _abi.call('rod_rccl_unique_id', ctypes.addressof(uid))
+    if world > 1:
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0, group=group)
+        ctypes.memmove(uid, box[0], 128)
+    _abi.call('rod_rccl_init', rank, world, ctypes.addressof(uid))
+
+
 class GradReducer(object):
-    def __init__(self, world_size, bucket_mb=4.0, group=None):
+    def __init__(self, world_size, bucket_mb=4.0, group=None, native=False):
         self.world = world_size
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.group = group
+        # native=True: buckets are summed by the library's own communicator (rod_allreduce_bucket,
+        # native_comm_init first), in order on the compute stream; default: torch.distributed
+        # (RCCL as well), on its own stream, overlapping backward
+        self.native = bool(native)
         self.store = None
         self.buckets = []
         # True while Trainer.step_graphed captures a 'split' step: the captured backward launches
@@ -63,7 +83,7 @@ class GradReducer(object):
             # the deferred weight-gradient sums INTO this bucket land before it is reduced; the
             # rest of the step's sums stay queued for the batched flush at the end of backward
             ops.SLAB.flush_range(view)
-            b['work'] = dist.all_reduce(view, group=self.group, async_op=True)
+            b['work'] = self._allreduce(view)
 
     def _on_grad(self, p):
         b = getattr(p, '_rod_bucket', None)
@@ -93,8 +113,7 @@ class GradReducer(object):
             # for the usual contiguous trainable set) instead of one per bucket
             from . import ops
             ops.SLAB.flush()
-            works = [dist.all_reduce(self.store.flat_grad[lo:hi], group=self.group, async_op=True)
-                     for lo, hi in self.spans()]
+            works = [self._allreduce(self.store.flat_grad[lo:hi]) for lo, hi in self.spans()]
             for w in works:
                 w.wait()
             self.reset()
@@ -104,6 +123,13 @@ class GradReducer(object):
         for b in self.buckets:
             b['work'].wait()
         self.reset()
+
+    def _allreduce(self, view):
+        if not self.native:
+            return dist.all_reduce(view, group=self.group, async_op=True)
+        from . import _abi, ops
+        _abi.call('rod_allreduce_bucket', view, view.numel(), 0, ops.stream())
+        return _Done()
 
     def hnm_allreduce(self, tensors):
         """In-place SUM of small device int32 tensors over the ranks, on the compute stream
@@ -118,6 +144,13 @@ class GradReducer(object):
 
     def launched(self):
         return sum(1 for b in self.buckets if b['work'] is not None)
+
+
+class _Done(object):
+    """The handle of a stream-ordered (already enqueued) reduction."""
+
+    def wait(self):
+        return None
 
 
 def allgather(t, world, group=None):

@@ -5,9 +5,10 @@ oracle on the same seeded inputs:
       targets and the hard-negative selection — bit-exact (positive masks, argmax labels,
       offsets, matched boxes, IoU, k, the k-th value, the negative mask);
   (b) C2 step: one fp32 REFINE training step at B=8, 720x1280 — loss within 1e-4 relative of
-      the float64 oracle; head outputs within 1e-4 normwise on levels 1-5 and 2e-4 on level 6
-      (the 3x5 map, 24 layers + head deep: float32 itself lands there — PyTorch's fp32 CPU
-      evaluation of the same step measured 1.25e-4, this path 1.20e-4); moving statistics
+      the float64 oracle; head outputs within max(1e-4, 4x the float32 floor) normwise per level
+      (the floor: the oracle's own fp32 evaluation of the same step against float64; only the
+      3x5 map, 24 layers + head deep, has one above 1e-4 — measured 1.25e-4); the errors are
+      written to gpurun_out/parity_errors.json (kept under profiles/); moving statistics
       within 1e-4 (fixed bounds); parameter gradients within max(2e-3, 4x the error of an
       independent float32 evaluation) — float32 backprop through the deep BatchNorms is
       itself 1e-2..1e-1 off float64 there;
@@ -42,6 +43,18 @@ def _anchors(h=H, w=W):
     import utils.net_tools as nt
     config.img_size = (h, w)
     return nt.anchors_all_layer((h, w), config.feat_sizes((h, w)), nt.init_anchor(6))
+
+
+_PARITY = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out', 'parity_errors.json')
+
+
+def _record(key, value):
+    """Keep the measured errors of the full-size parity tests (copied to profiles/ per round)."""
+    os.makedirs(os.path.dirname(_PARITY), exist_ok=True)
+    d = json.load(open(_PARITY)) if os.path.exists(_PARITY) else {}
+    d[key] = value
+    with open(_PARITY, 'w') as f:
+        json.dump(d, f, indent=1)
 
 
 def _nerr(a, b):
@@ -179,13 +192,21 @@ def test_refine_step_fp32_720p_b8(dev):
     torch.cuda.synchronize()
     g64, mov64, ref64, l64 = _c2_truth(tr, snap, img, corner, labels, n, B)
     P64 = {k: _Grad(v) for k, v in g64.items()}
-    rep = [(l, _nerr(a, o64)) for l, (a, o64) in enumerate(zip(outs, ref64))]
-    print('per-level normwise error vs fp64:', rep)
+    # an independent float32 evaluation of the same step (the oracle, PyTorch-CPU fp32): its
+    # own distance from float64 is the float32 conditioning floor of each output
+    P32, _, ref32, _ = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float32)
+    rep = [(l, _nerr(a, o64), _nerr(o32, o64)) for l, (a, o32, o64) in enumerate(zip(outs, ref32, ref64))]
+    print('per-level normwise error vs fp64 (HIP fp32, oracle fp32):', rep)
     lrel = abs(loss.item() - l64) / abs(l64)
     print('loss', loss.item(), 'fp64', l64, 'rel', lrel)
-    # level 6 sits 24 backbone layers + 4 head convs deep; per-level float32 error roughly
-    # doubles per level (4e-6 ... 1.2e-4 measured, the fp32 PyTorch oracle alike)
-    assert all(e <= (1e-4 if l < 5 else 2e-4) for l, e in rep), rep
+    # north_star: fp32 logits / boxes within 1e-4 relative; where float32 itself (the oracle's
+    # own fp32 evaluation) is further than that from float64 — the deepest level sits 24
+    # backbone layers + 4 head convs deep — within 4x that float32 floor
+    bars = [max(1e-4, 4 * e32) for _, _, e32 in rep]
+    _record('c2_refine_step_fp32_720p_b8', {'levels': [{'level': l, 'err': e, 'oracle_fp32_err': e32, 'bar': bar}
+                                                      for (l, e, e32), bar in zip(rep, bars)],
+                                           'loss_rel_err': lrel})
+    assert all(e <= bar for (_, e, _), bar in zip(rep, bars)), (rep, bars)
     assert lrel <= 1e-4
     # moving means are judged on the scale of their update, (1 - decay) x the batch std: the
     # mean of a conv fed by a linear-BN output (project -> expand) is 0 up to rounding
@@ -207,9 +228,7 @@ def test_refine_step_fp32_720p_b8(dev):
     # within max(2e-3, 4x) the error of an independent float32 evaluation of the same step (the
     # oracle, PyTorch-CPU fp32).  Measured: worst ratio 3.7 (expanded_conv_22/expand/BatchNorm/
     # beta 0.152 vs 0.041); a third evaluation (the oracle's ops on the GPU) did not widen it.
-    P32, _, ref32, _ = _oracle_refine_step(tr, snap, img, corner, labels, n, B, torch.float32)
     Pg = P32
-    print('oracle fp32 per-level:', [(l, _nerr(a, o)) for l, (a, o) in enumerate(zip(ref32, ref64))])
     # gradients that are zero by construction (a bias or beta feeding a BatchNorm directly:
     # shift invariance) are judged on the scale of the step's gradients, not their own
     gscale = float(np.median([float(P64[k].grad.abs().max()) for k in tr.net.store.params]))
@@ -237,6 +256,11 @@ def test_refine_step_fp32_720p_b8(dev):
     for r in zero_rows[:3]:
         print('zero-by-construction grad |g|/scale %.3e  fp32 %.3e  %s' % r)
     print('worst parameter-gradient normwise error:', worst, 'over', len(tr.net.store.params), 'tensors')
+    d = json.load(open(_PARITY)) if os.path.exists(_PARITY) else {}
+    d.setdefault('c2_refine_step_fp32_720p_b8', {})['grads'] = {
+        'tensors': len(tr.net.store.params), 'worst_err': worst,
+        'top': [{'name': nm, 'err': e, 'oracle_fp32_err': e32} for e, e32, nm in rows[:12]]}
+    _record('c2_refine_step_fp32_720p_b8', d['c2_refine_step_fp32_720p_b8'])
     assert not bad, bad[:10]
 
 
@@ -392,7 +416,8 @@ def test_predict_1080p_fused_blocks_match_oracle(dev):
     fused inverted-residual blocks (rod_ir_block_fwd, ref conv_blocks.py:163-312) on, BatchNorm
     calibrated so the heads give a detector-like score distribution.
       * the fused kernel actually runs (probe);
-      * fp32 (the unfused path): head outputs (refine / det offsets, clf logits) within 1e-3
+      * fp32 (the unfused path): head outputs (refine / det offsets, clf logits) within
+        max(1e-4, 4x the oracle's own float32 distance from float64)
         normwise of the float64 oracle network in eval mode (ref predict.py:127-137);
       * bf16 with the fused blocks: no less accurate than the unfused bf16 chain (1.5x + 1e-3),
         and within 3x + 1e-2 of what bf16 storage allows — the oracle in fp32 arithmetic with
@@ -445,18 +470,30 @@ def test_predict_1080p_fused_blocks_match_oracle(dev):
                                       {k: v.float() for k, v in Bf.items()}, False, all_mode=True)
         finally:
             onet.set_storage(prev)
+        # the oracle's own float32 evaluation: the float32 conditioning floor of each output
+        r32, d32, c32 = onet.forward(x32, {k: v.float() for k, v in P.items()}, {k: v.float() for k, v in Bf.items()},
+                                     False, all_mode=True)
     cat = lambda ts, k: torch.cat([t.reshape(B, -1, k) for t in ts], 1)
     rep = []
-    for name, got, unf, f32o, q, want, k in (('refine', roff, u_roff, f_out[0], rq, r64, 4),
-                                            ('det', doff, u_doff, f_out[1], dq, d64, 4),
-                                            ('clf', logits, u_logits, f_out[2], cq, c64, 11)):
+    recs = []
+    for name, got, unf, f32o, q, o32, want, k in (('refine', roff, u_roff, f_out[0], rq, r32, r64, 4),
+                                                 ('det', doff, u_doff, f_out[1], dq, d32, d64, 4),
+                                                 ('clf', logits, u_logits, f_out[2], cq, c32, c64, 11)):
         want = cat(want, k)
         ef, eu, e32, eq = _nerr(got.float(), want), _nerr(unf.float(), want), _nerr(cat(f32o, k), want), \
             _nerr(cat(q, k), want)
-        rep.append((name, ef, eu, e32, eq))
-        assert e32 <= 1e-3, rep
+        eo = _nerr(cat(o32, k), want)
+        rep.append((name, ef, eu, e32, eq, eo))
+        # north_star: fp32 logits / boxes within 1e-4 relative, or within 4x the float32 floor
+        # (the oracle's own fp32 evaluation) where float32 itself is further from float64
+        bar = max(1e-4, 4 * eo)
+        recs.append({'output': name, 'hip_fp32_err': e32, 'oracle_fp32_err': eo, 'bar': bar, 'bf16_fused_err': ef,
+                     'bf16_unfused_err': eu, 'bf16_storage_oracle_err': eq})
+        assert e32 <= bar, rep
         assert ef <= 1.5 * eu + 1e-3 and ef <= 3 * eq + 1e-2, rep
-    print('1080p head outputs, normwise error vs fp64 (bf16 fused, bf16 unfused, fp32, bf16-storage oracle):', rep)
+    _record('c5_predict_1080p_b2', recs)
+    print('1080p head outputs, normwise error vs fp64 (bf16 fused, bf16 unfused, fp32, bf16-storage oracle, '
+          'oracle fp32):', rep)
     lg = logits.float().cpu().numpy()
     e, s_, _ = op.softmax_rows(lg)
     P_ = probs.cpu().numpy()

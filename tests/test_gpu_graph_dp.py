@@ -57,3 +57,18 @@ def test_split_graph_dp_two_ranks(tmp_path, dev):
     d = torch.load(out, weights_only=True)
     print(d)
     assert d['ok'], d
+
+
+NATIVE_WORKER = os.path.join(ROOT, 'tests', 'native_comm_worker.py')
+
+
+def test_native_comm_one_rank(tmp_path, dev):
+    """rod_rccl_init / rod_allreduce_bucket (the C-ABI reduce point) on a 1-rank communicator:
+    identity sums, graph capture and replay, and a training step reduced through it."""
+    out = str(tmp_path / 'n.pt')
+    r = subprocess.run([sys.executable, NATIVE_WORKER, '--out', out], cwd=ROOT, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = torch.load(out, weights_only=True)
+    print(d)
+    assert d['ok'], d

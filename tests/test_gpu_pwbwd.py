@@ -99,3 +99,61 @@ def test_pw_bwd_rejects_unsupported(dev):
     assert not ops.pw_bwd_supported(24, 36, bf16)        # Cout % 8
     assert not ops.pw_bwd_supported(320, 128, bf16)      # too many dW tiles
     assert not ops.pw_bwd_supported(24, 144, torch.float32)
+
+
+def test_pw_bwd_full_size_expand_vs_float64(dev):
+    """rod_pw_bwd at the step's largest expand (L3: 8 x 720 x 1280 = 7,372,800 rows, 16 -> 96,
+    ReLU6 BatchNorm, the input through its linear BatchNorm prologue) against a float64
+    restatement that keeps the product's two storage points (dy and the prologue output a,
+    both bf16).  Bars: dw normwise 1e-4 (fp32 partials over 7.4 M rows, f64 slab sum), dx
+    max |err| <= 2^-7 max |dx64| (bf16 output; a dy element whose rounding flips between the f32
+    and f64 coefficients moves it by one bf16 ulp).  Measured values printed and written to
+    gpurun_out/parity_errors.json."""
+    import json
+    import os
+    M, Cin, Cout, act = 8 * 720 * 1280, 16, 96, ops.ROD_ACT_RELU6
+    g = torch.Generator(device=dev).manual_seed(96)
+    x = (torch.randn(M, Cin, device=dev, generator=g) * 1.5 + 0.3).to(bf16)
+    y = (torch.randn(M, Cout, device=dev, generator=g) * 2 + 0.5).to(bf16)
+    dz = (torch.randn(M, Cout, device=dev, generator=g) * 1e-3).to(bf16)
+    w = torch.randn(Cout, 1, 1, Cin, device=dev, generator=g) * 0.2
+    mean = y.float().mean(0)
+    rstd = torch.rsqrt(y.float().var(0, unbiased=False) + 1e-3)
+    gamma = torch.rand(Cout, device=dev, generator=g) + 0.5
+    beta = torch.randn(Cout, device=dev, generator=g) * 0.3
+    xpro = (torch.randn(Cin, device=dev, generator=g) * 0.2, torch.rand(Cin, device=dev, generator=g) + 0.5,
+            torch.rand(Cin, device=dev, generator=g) + 0.5, torch.randn(Cin, device=dev, generator=g) * 0.2,
+            ops.ROD_ACT_NONE)
+    coef = ops.bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, False, False)
+    wt1 = ops._prep(w, 1, bf16, Cout, Cin, 1)
+    dw = torch.empty(Cout, Cin, device=dev)
+    dx = ops.pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, True, dw, None)
+    torch.cuda.synchronize()
+    d64 = torch.float64
+    sc = rstd.double() * gamma.double()
+    yd = y.double()
+    z = yd * sc + (beta.double() - mean.double() * sc)
+    gg = dz.double() * ((z > 0) & (z < 6))
+    del z
+    yh = (yd - mean.double()) * rstd.double()
+    del yd
+    dy = (sc * (gg - gg.mean(0) - yh * (gg * yh).mean(0))).to(bf16).to(d64)
+    del gg, yh
+    xs = xpro[1].double() * xpro[2].double()
+    a = (x.double() * xs + (xpro[3].double() - xpro[0].double() * xs)).to(bf16).to(d64)
+    dw64 = dy.t() @ a
+    del a
+    dx64 = dy @ wt1.double().t() if wt1.shape == (Cin, Cout) else dy @ w.double().reshape(Cout, Cin).to(bf16).to(d64)
+    ew = float((dw.double() - dw64).abs().max() / dw64.abs().max())
+    ex = float((dx.double() - dx64).abs().max() / dx64.abs().max())
+    rec = {'M': M, 'Cin': Cin, 'Cout': Cout, 'dw_err': ew, 'dx_err': ex, 'bars': {'dw': 1e-4, 'dx': 2 ** -7}}
+    print(rec)
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out',
+                        'parity_errors.json')
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    d['pw_bwd_expand_7372800x16x96'] = rec
+    with open(path, 'w') as f:
+        json.dump(d, f, indent=1)
+    assert ew <= 1e-4, rec
+    assert ex <= 2 ** -7, rec
