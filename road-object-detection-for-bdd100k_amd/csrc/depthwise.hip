@@ -457,6 +457,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
   const unsigned es = sizeof(T);
   const rsrc_t rxs = rod_rsrc(xn - c, (unsigned)((long)H * W * C * es));
   const rsrc_t rys = rod_rsrc(yn - c, (unsigned)((long)Ho * Wo * C * es));
+  const rsrc_t rnull = rod_rsrc(yn - c, 0u);   // rows off the strip: every store dropped
   const int cc0 = ci0 < 0 ? 0 : (ci0 >= W ? W - 1 : ci0);
   const int cc1 = ci0 + 1 < 0 ? 0 : (ci0 + 1 >= W ? W - 1 : ci0 + 1);
   const unsigned vx0 = (unsigned)(((long)cc0 * C + c) * es), vx1 = (unsigned)(((long)cc1 * C + c) * es);
@@ -467,10 +468,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
     PK o;
 #pragma unroll
     for (int v = 0; v < V; ++v) o.set(v, a[v]);
-    // the statistics read the rounded outputs BEFORE the store: with the store first, the fp32
-    // form (dwordx4 store, then VALU reading its data registers) returned corrupted element-1
-    // outputs on the MI355X, different run to run (tests/test_gpu_kernels.py::
-    // test_dw_epilogue_bn_stats); every buffer store here is the last use of its data
+    // statistics of the rounded outputs, then the store (fenced: rod_common.h buf_st)
     if constexpr (STATS) {
       if (valid) {
 #pragma unroll
@@ -483,7 +481,7 @@ __device__ __forceinline__ void dw_lx_body(const T* __restrict__ x, const float*
         }
       }
     }
-    o.bstore(rys, valid ? vy : ROD_OOB, (unsigned)(valid ? ho : 0) * rsy);
+    o.bstore(valid ? rys : rnull, vy, (unsigned)(valid ? ho : 0) * rsy);
   };
   auto emit_g = [&](const float (&a)[V], int ho, int gslot) {  // GRED: y of row ho is in gring[gslot]
     PackV<T, V> o;
@@ -2097,7 +2095,7 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
   const long img = (long)n * H * W * C;
   const unsigned ib = (unsigned)((long)H * W * C * sizeof(T));
   const rsrc_t rye = rod_rsrc(ye + img, ib), rdz = rod_rsrc(dz + img, ib), ryd = rod_rsrc(yd + img, ib);
-  const rsrc_t rdx = rod_rsrc(dx + img, ib);
+  const rsrc_t rdx = rod_rsrc(dx + img, ib), rnull = rod_rsrc(dx + img, 0u);
   const unsigned vo = (unsigned)(((long)colc * C + c) * sizeof(T));
   const unsigned vox = comp ? vo : ROD_OOB;   // halo lanes store nothing
   const unsigned rstrb = (unsigned)(W * C * sizeof(T));
@@ -2251,7 +2249,7 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
           }
         }
       }
-      o.bstore(rdx, rowout ? vox : ROD_OOB, (unsigned)(rho < 0 ? 0 : rho) * rstrb);
+      o.bstore(rowout ? rdx : rnull, vox, (unsigned)(rho < 0 ? 0 : rho) * rstrb);
 #pragma unroll
       for (int h = 0; h < VP; ++h) acc[k3][h] = dw_f2{0.f, 0.f};
     }
@@ -2354,6 +2352,7 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
   const unsigned es = sizeof(T);
   const rsrc_t rye = rod_rsrc(ye + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
   const rsrc_t rdx = rod_rsrc(dx + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
+  const rsrc_t rnull = rod_rsrc(dx + (long)n * H * W * C, 0u);
   const rsrc_t rdz = rod_rsrc(dz + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
   const rsrc_t ryd = rod_rsrc(yd + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
   const int bc = b < 0 ? 0 : (b >= Wo ? Wo - 1 : b);
@@ -2473,7 +2472,7 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
               }
             }
           }
-          pk.bstore(rdx, hok ? ((i & 1) ? vst1 : vst0) : ROD_OOB, (unsigned)(hok ? h : 0) * rsx);
+          pk.bstore(hok ? rdx : rnull, (i & 1) ? vst1 : vst0, (unsigned)(hok ? h : 0) * rsx);
         }
         // filter: dy[a] with x rows 2a-pt (tap row 0) and 2a+1-pt (1), dy[a-1] with 2a-pt (2)
 #pragma unroll
@@ -2603,6 +2602,7 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2p_kernel(
   const unsigned es = sizeof(T);
   const rsrc_t rye = rod_rsrc(ye + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
   const rsrc_t rdx = rod_rsrc(dx + (long)n * H * W * C, (unsigned)((long)H * W * C * es));
+  const rsrc_t rnull = rod_rsrc(dx + (long)n * H * W * C, 0u);
   const rsrc_t rdz = rod_rsrc(dz + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
   const rsrc_t ryd = rod_rsrc(yd + (long)n * Ho * Wo * C, (unsigned)((long)Ho * Wo * C * es));
   const int bc = b < 0 ? 0 : (b >= Wo ? Wo - 1 : b);
@@ -2736,7 +2736,7 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2p_kernel(
             }
           }
         }
-        pk.bstore(rdx, hok ? ((i & 1) ? vst1 : vst0) : ROD_OOB, (unsigned)(hok ? hh : 0) * rsx);
+        pk.bstore(hok ? rdx : rnull, (i & 1) ? vst1 : vst0, (unsigned)(hok ? hh : 0) * rsx);
       }
       // filter: dy[a] with x rows 2a-pt (tap row 0) and 2a+1-pt (1), dy[a-1] with 2a-pt (2)
       if (own) {

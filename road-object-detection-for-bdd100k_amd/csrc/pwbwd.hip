@@ -270,11 +270,265 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
   }
 }
 
+
+// =====================================================================================
+// Streaming form (the expand shapes 16->96 and 24->144 without bias): every wave works on
+// its own 32-row tiles with no block barrier inside the row loop — the 64-row block-synchronous
+// steps above leave the memory system idle while all four waves sit in their MFMA phase.
+//   * lane constants: a lane owns ONE 8-channel chunk cc of dz / y (lanes = RG row groups x
+//     COUT/8 chunks) for the whole launch, so its BatchNorm-backward constants (sc, sh, a, k1,
+//     k0 of 8 channels) sit in registers — no per-element coefficient reads from LDS;
+//   * per 16-row half: dz / y / x arrive by buffer loads from a per-tile resource (rows past M
+//     read 0, their dx stores are dropped), dy = bn_bwd_apply (rounded to bf16, the arithmetic of
+//     the block kernel) goes to this wave's LDS tile, then the NEXT half's loads are issued into
+//     the same registers before the MFMA work of this one (one half in flight per wave, no extra
+//     registers);
+//   * dx = dy . W for the half (A fragments straight from the dy rows, W staged once per block),
+//     staged through a wave-private LDS slot and written as 16-byte row segments;
+//   * after the second half, dW += dy^T . x over the 32 rows (both operands read transposed,
+//     ds_read_b64_tr_b16, as above);
+//   * at the end the four waves' dW add in wave order in LDS (one partial per block, slab_sum).
+// dx is the block kernel's bit for bit (same dy, same MFMA k order); dW sums its rows in another
+// grouping (fp32, within the float64 bounds of tests/test_gpu_pwbwd.py).
+// =====================================================================================
+template <int CIN, int COUT>
+struct PbsGeo {
+  // CW channels per lane chunk: 4 (8-byte loads) where the chunks tile 64 lanes into whole rows
+  // without waste (96: 2 row groups x 24 chunks, 16 rows in 8 steps, 20 constant registers
+  // instead of 40), else 8
+  static constexpr int CW = (64 / (COUT / 4)) * (COUT / 4) >= 48 && 16 % (64 / (COUT / 4)) == 0 ? 4 : 8;
+  static constexpr int CCH = COUT / CW, RG = 64 / CCH, JN = (16 + RG - 1) / RG;
+  static constexpr int KT = (COUT + 31) / 32, KD = KT * 32, LDD = KD + 8;
+  static constexpr int NCO = COUT / 16, XCH = CIN / 8, NCI = (CIN + 15) / 16, LDX = NCI * 16 + 8;
+  static constexpr int LDC = CIN + 8;
+  static constexpr int WREG = 32 * LDD + 32 * LDX + 16 * LDC;    // bf16 elements per wave
+  static constexpr int WS = NCI * 16 * LDD;                       // wt1 image (bf16 elements)
+  static constexpr int XT = 2 * CIN * 2;                          // input-prologue table (bf16 slots)
+  static constexpr size_t lds() {
+    const size_t main = (size_t)(WS + XT + 4 * WREG) * 2;
+    const size_t red = (size_t)(WS + XT) * 2 + (size_t)COUT * NCI * 16 * 4;
+    return main > red ? main : red;
+  }
+};
+
+template <int CW> struct PbsVec;
+template <> struct PbsVec<4> { typedef bf16x4 T; };
+template <> struct PbsVec<8> { typedef bf16x8 T; };
+
+template <int CIN, int COUT, bool PRO, bool DX>
+__global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long ntiles) {
+  using G = PbsGeo<CIN, COUT>;
+  constexpr int CW = G::CW, CCH = G::CCH, RG = G::RG, JN = G::JN, KT = G::KT, LDD = G::LDD, NCO = G::NCO,
+                XCH = G::XCH, NCI = G::NCI, LDX = G::LDX, LDC = G::LDC;
+  typedef typename PbsVec<CW>::T VT;
+  static_assert(COUT % 16 == 0 && CIN % 8 == 0 && 16 * XCH <= 64, "streaming pw_bwd geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* Ws = (bf16_t*)smem;                                   // [NCI*16][LDD]: wt1 rows (ci), k = co
+  float* xtab = (float*)(Ws + G::WS);                           // [2][CIN]: input prologue scale, shift
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  bf16_t* Ds = Ws + G::WS + G::XT + wave * G::WREG;             // [32][LDD]  dy of the tile
+  bf16_t* Xs = Ds + 32 * LDD;                                   // [32][LDX]  conv input of the tile
+  bf16_t* Cx = Xs + 32 * LDX;                                   // [16][LDC]  dx staging
+  // zero everything once (dy columns >= COUT, x columns >= CIN stay 0), then the weights
+  for (int i = tid; i < (G::WS + G::XT + 4 * G::WREG) / 8; i += 256) {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (bf16_t)0.f;
+    ((bf16x8*)smem)[i] = z;
+  }
+  __syncthreads();
+  if constexpr (DX) {
+    for (int i = tid; i < CIN * (COUT / 8); i += 256) {
+      const int ci = i / (COUT / 8), c8 = i - ci * (COUT / 8);
+      *(bf16x8*)(Ws + ci * LDD + c8 * 8) = *(const bf16x8*)(a.wt1 + (long)ci * COUT + c8 * 8);
+    }
+  }
+  if constexpr (PRO) {
+    for (int c = tid; c < CIN; c += 256) bn_affine(a.xmean, a.xrstd, a.xgamma, a.xbeta, c, xtab[c], xtab[CIN + c]);
+  }
+  __syncthreads();
+
+  // ---- lane constants ---------------------------------------------------------------------
+  const int rg = lane / CCH, cc = lane - (lane / CCH) * CCH;
+  const bool dact = rg < RG;
+  const int c0 = dact ? cc * CW : 0;
+  float sc[CW], sh[CW], ca[CW], k1[CW], k0[CW];
+#pragma unroll
+  for (int e = 0; e < CW; ++e) {
+    const int c = c0 + e;
+    bn_affine(a.mean, a.rstd, a.gamma, a.beta, c, sc[e], sh[e]);
+    ca[e] = a.coef[c];
+    bn_bwd_k(ca[e], a.mean[c], a.rstd[c], a.coef[COUT + c], a.coef[2 * COUT + c], k1[e], k0[e]);
+  }
+  const float ghi = a.act == ROD_ACT_RELU6 ? 6.f : INFINITY;
+  const float glo = a.act == ROD_ACT_LEAKY ? 0.2f : a.act == ROD_ACT_NONE ? 1.f : 0.f;
+  const int xr = lane / XCH, xc = lane - (lane / XCH) * XCH;
+  const bool xact = lane < 16 * XCH;
+  // lane offset of chunk j inside a half (bytes): vd0 + j * RG rows; ROD_OOB: no row there
+  const unsigned vd0 = dact ? (unsigned)((rg * COUT + cc * CW) * 2) : ROD_OOB;
+  auto vdj = [&](int j) -> unsigned {
+    if constexpr (JN * RG == 16) return vd0 + (unsigned)(j * RG * COUT * 2);
+    else return rg + RG * j < 16 ? vd0 + (unsigned)(j * RG * COUT * 2) : ROD_OOB;
+  };
+  const unsigned vx = xact ? (unsigned)((xr * CIN + xc * 8) * 2) : ROD_OOB;
+  const long M = a.M;
+  auto rsrc_rows = [&](const void* base, long row0, int rowbytes) {   // rows [row0, min(row0 + 32, M))
+    const long rows = row0 < M ? (M - row0 < 32 ? M - row0 : 32) : 0;
+    return rod_rsrc((const char*)base + (row0 < M ? row0 : 0) * rowbytes, (unsigned)(rows * rowbytes));
+  };
+
+  f32x4 accw[NCO][NCI];
+#pragma unroll
+  for (int i = 0; i < NCO; ++i)
+#pragma unroll
+    for (int j = 0; j < NCI; ++j) accw[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const long wstride = (long)gridDim.x * 4;
+  long t = (long)blockIdx.x * 4 + wave;
+  VT dzv[JN], yv[JN];
+  bf16x8 xv;
+  {   // the first half (t >= ntiles: an empty resource, the loads return 0)
+    const rsrc_t rdz = rsrc_rows(a.dz, t * 32, COUT * 2), ry = rsrc_rows(a.y, t * 32, COUT * 2);
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      dzv[j] = buf_ld<VT>(rdz, vdj(j), 0u);
+      yv[j] = buf_ld<VT>(ry, vdj(j), 0u);
+    }
+    xv = buf_ld<bf16x8>(rsrc_rows(a.x, t * 32, CIN * 2), vx, 0u);
+  }
+  for (; t < ntiles; t += wstride) {
+    const long row0 = t * 32;
+    // not unrolled: the reloads land in the registers just consumed (unrolled, the compiler
+    // double-buffers them: +32 VGPRs)
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      // ---- dy = BatchNorm backward of (dz, y) -> Ds; x (+ prologue) -> Xs ------------------
+      // each chunk's registers are reloaded with the NEXT half's chunk as soon as they are
+      // consumed, so this wave keeps loads in flight through its VALU work as well
+      const long rown = (h == 0 ? t : t + wstride) * 32;
+      const rsrc_t ndz = rsrc_rows(a.dz, rown, COUT * 2), ny = rsrc_rows(a.y, rown, COUT * 2);
+      const unsigned nso = (unsigned)((1 - h) * 16 * COUT * 2);
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        const int r = rg + RG * j;
+        typename PbsVec<CW>::T o;
+#pragma unroll
+        for (int e = 0; e < CW; ++e) {
+          const float yj = (float)yv[j][e];
+          const float z = fmaf(yj, sc[e], sh[e]);
+          const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
+          o[e] = (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj);
+        }
+        dzv[j] = buf_ld<VT>(ndz, vdj(j), nso);
+        yv[j] = buf_ld<VT>(ny, vdj(j), nso);
+        if (dact && (JN * RG == 16 || r < 16)) *(VT*)(Ds + (h * 16 + r) * LDD + cc * CW) = o;
+      }
+      {
+        bf16x8 v = xv;
+        if constexpr (PRO) {
+          const bool rok = row0 + h * 16 + xr < M;   // rows past M stay 0 (not act(shift))
+          const f32x4 s0 = *(const f32x4*)(xtab + xc * 8), s1 = *(const f32x4*)(xtab + xc * 8 + 4);
+          const f32x4 h0 = *(const f32x4*)(xtab + CIN + xc * 8), h1 = *(const f32x4*)(xtab + CIN + xc * 8 + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = rok ? (bf16_t)act_fwd(fmaf((float)v[e], s0[e], h0[e]), a.xact) : (bf16_t)0.f;
+            v[4 + e] = rok ? (bf16_t)act_fwd(fmaf((float)v[4 + e], s1[e], h1[e]), a.xact) : (bf16_t)0.f;
+          }
+        }
+        xv = buf_ld<bf16x8>(rsrc_rows(a.x, rown, CIN * 2), vx, (unsigned)((1 - h) * 16 * CIN * 2));
+        if (xact) *(bf16x8*)(Xs + (h * 16 + xr) * LDX + xc * 8) = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if constexpr (DX) {
+        // ---- dx = dy . W for the 16 rows of this half -> Cx -> 16-byte row segments ---------
+        f32x4 accx[NCI];
+#pragma unroll
+        for (int j = 0; j < NCI; ++j) accx[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KT; ++s) {
+          const bf16x8 fa = *(const bf16x8*)(Ds + (h * 16 + li) * LDD + s * 32 + 8 * g);
+#pragma unroll
+          for (int j = 0; j < NCI; ++j) {
+            const bf16x8 fb = *(const bf16x8*)(Ws + (j * 16 + li) * LDD + s * 32 + 8 * g);
+            accx[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, accx[j], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NCI; ++j) {
+          const int col = j * 16 + li;
+          if (col < CIN) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Cx[(4 * g + r) * LDC + col] = (bf16_t)accx[j][r];
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const rsrc_t rdx = rsrc_rows(a.dx, row0, CIN * 2);
+        const bf16x8 ov = *(const bf16x8*)(Cx + (xact ? xr : 0) * LDC + xc * 8);
+        buf_st(ov, rdx, vx, (unsigned)(h * 16 * CIN * 2));
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    // ---- dW += dy^T . x over the tile's 32 rows ---------------------------------------------
+#pragma unroll
+    for (int ct = 0; ct < NCO; ++ct) {
+      const bf16_t* pd = Ds + (8 * g + q) * LDD + ct * 16 + 4 * p;
+      const bf16x4 lo = pb_tr_read(pd), hi = pb_tr_read(pd + 4 * LDD);
+      const bf16x8 fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int it = 0; it < NCI; ++it) {
+        const bf16_t* px = Xs + (8 * g + q) * LDX + it * 16 + 4 * p;
+        const bf16x4 l2 = pb_tr_read(px), h2 = pb_tr_read(px + 4 * LDX);
+        const bf16x8 fb = {l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
+        accw[ct][it] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, accw[ct][it], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();   // the next tile's dy / x writes stay after these reads
+  }
+  // ---- the block's dW: the four waves add in wave order -> part blockIdx.x -----------------
+  float* red = (float*)(smem + (size_t)(G::WS + G::XT) * 2);   // [COUT][NCI*16]
+  constexpr int LR = NCI * 16;
+  __syncthreads();
+#pragma unroll 1
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int ct = 0; ct < NCO; ++ct)
+#pragma unroll
+        for (int it = 0; it < NCI; ++it)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* d = red + (ct * 16 + 4 * g + r) * LR + it * 16 + li;
+            *d = w == 0 ? accw[ct][it][r] : *d + accw[ct][it][r];
+          }
+    }
+    __syncthreads();
+  }
+  float* pw = a.partw + (long)blockIdx.x * COUT * CIN;
+  for (int i = tid; i < COUT * CIN; i += 256) {
+    const int co = i / CIN, ci = i - co * CIN;
+    pw[i] = red[co * LR + ci];
+  }
+}
+
 struct PwBwdPlan {
   int kd, nci, nco, nxt, nx, wt, nblk;
   long chunk;
   size_t lds;
 };
+
+// the streaming kernel's shapes (expand convs without bias); ROD_PWB_STREAM=0 turns it off
+static bool pw_bwd_stream_ok(int Cin, int Cout, bool bias) {
+  static const bool off = getenv("ROD_PWB_STREAM") && atoi(getenv("ROD_PWB_STREAM")) == 0;
+  // 32->192 stays on the block kernel: 248 VGPRs (2 waves / SIMD), measured slower (168 vs 152 us)
+  return !off && !bias && ((Cin == 16 && Cout == 96) || (Cin == 24 && Cout == 144));
+}
+// blocks of the streaming launch: 3 per CU (the register budget of the 16->96 form), at most one
+// 4-wave group per 4 tiles
+static int pw_bwd_stream_blocks(long M) {
+  const long ntiles = cdivl(M, 32);
+  return (int)std::max<long>(1, std::min<long>(cdivl(ntiles, 4), 3L * 256));
+}
 
 static bool pw_bwd_ok(int Cin, int Cout) {
   if (Cin <= 0 || Cout <= 0 || Cin % 8 || Cout % 8 || Cin > 192 || Cout > 512) return false;
@@ -313,7 +567,8 @@ int rod_pw_bwd_supported(int Cin, int Cout, int dtype) { return dtype == ROD_BF1
 size_t rod_pw_bwd_workspace(long M, int Cin, int Cout) {
   if (!pw_bwd_ok(Cin, Cout) || M <= 0) return 0;
   const PwBwdPlan p = pw_bwd_plan(M, Cin, Cout, true);
-  return (size_t)p.nblk * Cout * (Cin + 1) * sizeof(float) + 64;
+  const size_t blk = pw_bwd_stream_ok(Cin, Cout, false) ? (size_t)std::max(p.nblk, pw_bwd_stream_blocks(M)) : p.nblk;
+  return blk * Cout * (Cin + 1) * sizeof(float) + 64;
 }
 
 int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
@@ -331,6 +586,32 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
   ROD_CHECK_ARG(p.lds <= 160 * 1024, "rod_pw_bwd: LDS plan too large");
   hipStream_t s = ROD_STREAM(stream);
   float* partw = (float*)workspace;
+  if (pw_bwd_stream_ok(Cin, Cout, db != nullptr)) {
+    const int nblk = pw_bwd_stream_blocks(M);
+    PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw, nullptr,
+                mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0};
+    const long ntiles = cdivl(M, 32);
+#define PBS(CI, CO, PR, DXF)                                                                                 \
+  do {                                                                                                       \
+    const size_t lds = PbsGeo<CI, CO>::lds();                                                                \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, PR, DXF>,                            \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
+    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, PR, DXF>), dim3(nblk), dim3(256), lds, s, a, ntiles);   \
+  } while (0)
+#define PBS2(CI, CO)                                        \
+  if (Cin == CI) {                                          \
+    if (xmean) {                                            \
+      if (dx) PBS(CI, CO, true, true); else PBS(CI, CO, true, false);   \
+    } else {                                                \
+      if (dx) PBS(CI, CO, false, true); else PBS(CI, CO, false, false); \
+    }                                                       \
+  }
+    PBS2(16, 96) else PBS2(24, 144)
+#undef PBS2
+#undef PBS
+    slab_sum(partw, dw, nblk, (long)Cout * Cin, s);
+    return check_launch("rod_pw_bwd");
+  }
   float* partb = db ? partw + (size_t)p.nblk * Cout * Cin : nullptr;
   PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw, partb,
               mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, p.chunk,

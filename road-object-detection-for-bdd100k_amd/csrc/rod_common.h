@@ -71,9 +71,17 @@ template <> struct Vec16<bf16_t> {
 // lose track of how many vector-memory operations are in flight, and it then drains them all
 // (s_waitcnt vmcnt(0)) every step — the ring prefetches nothing.  With buffer instructions every
 // load / store is issued unconditionally: the 32-bit lane offset `vo` carries the per-lane
-// column, the wave-uniform `so` (SGPR) the row; a store that must not happen gets vo = ROD_OOB,
-// which the hardware range check (offset >= num_records) drops.  Base and size must be
-// wave-uniform; the byte range of one resource must fit in 31 bits.
+// column, the wave-uniform `so` (SGPR) the row.  A lane that must not store has vo = ROD_OOB
+// (fixed for the whole kernel), which the hardware range check (offset >= num_records) drops;
+// a whole row that must not store goes to an empty resource (rod_rsrc(base, 0), chosen in
+// SGPRs).  Store hazard: the compiler inserts the wait state between a >8-byte buffer store and
+// a VALU overwrite of its data registers only for stores whose SGPR offset is the constant 0 (its
+// MUBUF rule); these stores carry the row in an SGPR offset, and a VALU write of the data
+// registers in the very next instruction corrupted stored elements on the MI355X (fp32
+// depthwise outputs, different run to run; tests/test_gpu_dwsweep.py).  buf_st therefore fences
+// every store with s_nop 4 (5 wait states) between scheduling barriers, so nothing that writes a
+// VGPR issues within 5 cycles of the store.  Base and size must be wave-uniform; one resource's
+// byte range fits in 31 bits.
 constexpr unsigned ROD_OOB = 0x80000000u;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t rod_rsrc(const void* base, unsigned bytes) {
@@ -94,6 +102,9 @@ template <typename V> __device__ __forceinline__ void buf_st(const V& v, rsrc_t 
   if constexpr (NB == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
   else if constexpr (NB == 8) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, vo, so, 0);
   else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, vo, so, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // Correctly-rounded f32 transcendental functions (evaluated in f64 and

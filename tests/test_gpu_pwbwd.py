@@ -18,6 +18,8 @@ bf16 = torch.bfloat16
 SHAPES = [  # (M, Cin, Cout, act, pro_x, bias)
     (4096 + 37, 24, 144, ops.ROD_ACT_RELU6, True, False),     # project 144->24's consumer side: expand 24->144
     (3000, 16, 96, ops.ROD_ACT_RELU6, False, False),          # L3 expand
+    (700, 32, 192, ops.ROD_ACT_RELU6, True, False),           # L5 expand (streaming kernel, ragged tail)
+    (31, 16, 96, ops.ROD_ACT_RELU6, True, False),             # fewer rows than one streaming tile
     (1111, 144, 24, ops.ROD_ACT_NONE, True, False),           # project (linear BN)
     (777, 64, 128, ops.ROD_ACT_LEAKY, False, True),           # head 1x1 (bias + BN beta only)
     (5000, 192, 32, ops.ROD_ACT_NONE, True, False),           # project 192->32
