@@ -382,7 +382,7 @@ def replicated(r, world, dev):
 
 
 NORTH_STAR = ('rod_dw3x3_fwd', 'rod_dw3x3_bwd_fused', 'rod_dw3x3_bwd_data', 'rod_dw3x3_bwd_filter', 'rod_conv_fwd',
-              'rod_conv_wgrad', 'rod_pw_bwd', 'rod_bn_bwd_reduce', 'rod_bn_bwd_apply', 'rod_bn_bwd')
+              'rod_conv_wgrad', 'rod_pw_bwd', 'rod_pw_bwd_gred', 'rod_bn_bwd_reduce', 'rod_bn_bwd_apply', 'rod_bn_bwd')
 
 
 def gpu_head_start(ms=120):

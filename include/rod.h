@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 16
+#define ROD_ABI_VERSION 17
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -378,6 +378,23 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
                const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
                void* dx, float* dw, float* db, void* workspace, long M, int Cin, int Cout, int dtype,
                void* stream);
+/* Project form (ABI 17): the same backward for a 1x1 conv whose input is the ReLU6(BatchNorm) of
+ * a depthwise output — the inverted-residual block's project conv (conv_blocks.py:287-294 after
+ * 238-247) — and, in the same pass, the backward sums of THAT input BatchNorm over (dx, x):
+ *   xparts[p][0][c] = sum g, xparts[p][1][c] = sum g*xhat,  g = dx*act_x'(x*sc_x + sh_x),
+ *   xhat = (x - xmean)*xrstd  (the [nparts][2][Cin] contract of rod_bn_bwd_finalize)
+ * so the depthwise BatchNorm's rod_bn_bwd_reduce pass over (dz, y) is not needed: x is read once
+ * for the weight gradient's prologue and for the sums, dx is summed as it is written.  No bias;
+ * xmean / xrstd, dx and wt1 required.  rod_pw_bwd_gred_parts() is the part count (0: shape not taken —
+ * bf16, Cout in {16, 24, 32, 64}, Cin a multiple of 32 or 48); workspace:
+ * rod_pw_bwd_gred_workspace() bytes.  dx is rod_pw_bwd's bit for bit. */
+long rod_pw_bwd_gred_parts(long M, int Cin, int Cout, int dtype);
+size_t rod_pw_bwd_gred_workspace(long M, int Cin, int Cout);
+int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                    const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                    const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                    void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
+                    void* stream);
 
 /* ------------------------------------------------ targets and losses
  * Anchor matching, JACCARD_BIGGER (utils/net_tools.py:270-428, branch 382-421).

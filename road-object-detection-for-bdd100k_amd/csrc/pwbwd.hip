@@ -511,6 +511,290 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
   }
 }
 
+
+// =====================================================================================
+// Project form with the input BatchNorm's backward sums (rod_pw_bwd_gred).  The conv input is
+// x_p = act_x(BN_x(x)) with x the raw depthwise output; the block's backward needs, besides
+// dx / dW, BN_x's backward sums over (dx, x) — which this kernel forms from the x it already
+// reads for the weight gradient and the dx it writes.  Cout is small (16..64) and Cin large, so
+// the grid splits Cin into groups of NW columns (blockIdx.y): a group re-reads only dz / y (4*Cout
+// bytes a row) and owns its columns of x, dx, dW and the sums.  Per wave, 32-row tiles in two
+// 16-row halves, no block barrier in the row loop:
+//   * dy: a lane owns one 4-channel chunk of dz / y (constants in registers), reloaded with the
+//     next half's chunk as soon as it is consumed; rows past M give dy = 0;
+//   * x: a lane owns one 8-column chunk of the group (BN_x constants in registers) for RGX row
+//     groups; x_p = act_x(BN_x(x)) (bf16) goes to LDS for the weight gradient, the raw x stays
+//     in registers for the sums;
+//   * dx = dy . W for the half (A fragments from the dy rows in LDS, W's group rows in LDS),
+//     staged in LDS, written by the x lanes, which add g and g*xhat of their chunk as they write;
+//   * after the second half dW += dy^T . x_p over the 32 rows (transposed LDS reads);
+//   * at the end the waves' dW and sums add in a fixed order -> part blockIdx.x.
+// =====================================================================================
+template <int COUT, int NW>
+struct PbgGeo {
+  static constexpr int CCH = COUT / 4, RG = 64 / CCH, JN = (16 + RG - 1) / RG;
+  static constexpr int KT = (COUT + 31) / 32, KD = KT * 32, LDD = KD + 8;
+  static constexpr int NCO = (COUT + 15) / 16;
+  static constexpr int XCH = NW / 8, RGX = 64 / XCH, JX = (16 + RGX - 1) / RGX, NWT = NW / 16;
+  static constexpr int LDX = NW + 8;
+  static constexpr int WREG = 32 * LDD + 32 * LDX + 16 * LDX;     // bf16 elements per wave
+  static constexpr int WS = NW * LDD;                              // the group's wt1 rows
+  static constexpr int RED = NCO * 16 * NW + 4 * RGX * 2 * NW;     // fp32 end-of-launch buffer
+  static constexpr size_t lds() {
+    const size_t main = (size_t)(WS + 4 * WREG) * 2;
+    const size_t red = (size_t)WS * 2 + (size_t)RED * 4;
+    return main > red ? main : red;
+  }
+};
+
+template <int COUT, int NW, bool DX>
+__global__ void __launch_bounds__(256) pw_bwd_gred_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
+  using G = PbgGeo<COUT, NW>;
+  constexpr int CCH = G::CCH, RG = G::RG, JN = G::JN, KT = G::KT, LDD = G::LDD, NCO = G::NCO, XCH = G::XCH,
+                RGX = G::RGX, JX = G::JX, NWT = G::NWT, LDX = G::LDX;
+  static_assert(COUT % 8 == 0 && NW % 16 == 0 && RG * CCH <= 64 && RGX * XCH <= 64, "gred pw_bwd geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Cin = a.Cin;
+  const int n0 = blockIdx.y * NW;                               // this group's first column
+  bf16_t* Ws = (bf16_t*)smem;                                   // [NW][LDD]: wt1 rows n0.., k = co
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  bf16_t* Ds = Ws + G::WS + wave * G::WREG;                     // [32][LDD]  dy of the tile
+  bf16_t* Xs = Ds + 32 * LDD;                                   // [32][LDX]  x_p of the tile
+  bf16_t* Cx = Xs + 32 * LDX;                                   // [16][LDX]  dx staging
+  for (int i = tid; i < (G::WS + 4 * G::WREG) / 8; i += 256) {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (bf16_t)0.f;
+    ((bf16x8*)smem)[i] = z;
+  }
+  __syncthreads();
+  if constexpr (DX) {
+    for (int i = tid; i < NW * (COUT / 8); i += 256) {
+      const int c = i / (COUT / 8), c8 = i - c * (COUT / 8);
+      *(bf16x8*)(Ws + c * LDD + c8 * 8) = *(const bf16x8*)(a.wt1 + (long)(n0 + c) * COUT + c8 * 8);
+    }
+  }
+  __syncthreads();
+
+  // ---- lane constants: dy chunk (4 channels of Cout) and x chunk (8 columns of the group) ----
+  const int rg = lane / CCH, cc = lane - (lane / CCH) * CCH;
+  const bool dact = rg < RG;
+  float sc[4], sh[4], ca[4], k1[4], k0[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = (dact ? cc * 4 : 0) + e;
+    bn_affine(a.mean, a.rstd, a.gamma, a.beta, c, sc[e], sh[e]);
+    ca[e] = a.coef[c];
+    bn_bwd_k(ca[e], a.mean[c], a.rstd[c], a.coef[COUT + c], a.coef[2 * COUT + c], k1[e], k0[e]);
+  }
+  const float ghi = a.act == ROD_ACT_RELU6 ? 6.f : INFINITY;
+  const float glo = a.act == ROD_ACT_LEAKY ? 0.2f : a.act == ROD_ACT_NONE ? 1.f : 0.f;
+  const int rx = lane / XCH, xc = lane - (lane / XCH) * XCH;
+  const bool xact = rx < RGX;
+  float xsc[8], xsh[8], xmu[8], xrs[8], sg[8], sgx[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = n0 + (xact ? xc * 8 : 0) + e;
+    bn_affine(a.xmean, a.xrstd, a.xgamma, a.xbeta, c, xsc[e], xsh[e]);
+    xmu[e] = a.xmean[c];
+    xrs[e] = a.xrstd[c];
+    sg[e] = sgx[e] = 0.f;
+  }
+  const unsigned vd0 = dact ? (unsigned)((rg * COUT + cc * 4) * 2) : ROD_OOB;
+  auto vdj = [&](int j) -> unsigned {
+    if constexpr (JN * RG == 16) return vd0 + (unsigned)(j * RG * COUT * 2);
+    else return rg + RG * j < 16 ? vd0 + (unsigned)(j * RG * COUT * 2) : ROD_OOB;
+  };
+  const unsigned vx0 = xact ? (unsigned)((rx * Cin + xc * 8) * 2) : ROD_OOB;
+  auto vxj = [&](int j) -> unsigned {
+    if constexpr (JX * RGX == 16) return vx0 + (unsigned)(j * RGX * Cin * 2);
+    else return rx + RGX * j < 16 ? vx0 + (unsigned)(j * RGX * Cin * 2) : ROD_OOB;
+  };
+  const long M = a.M;
+  auto rows_of = [&](long row0) -> long { return row0 < M ? (M - row0 < 32 ? M - row0 : 32) : 0; };
+  auto rsrc_d = [&](const void* base, long row0) {   // dz / y rows [row0, +32) of Cout channels
+    return rod_rsrc((const char*)base + (row0 < M ? row0 : 0) * COUT * 2, (unsigned)(rows_of(row0) * COUT * 2));
+  };
+  auto rsrc_x = [&](const void* base, long row0) {   // x / dx rows of this group's columns
+    const long r = rows_of(row0);
+    return rod_rsrc((const char*)base + ((row0 < M ? row0 : 0) * Cin + n0) * 2,
+                    r > 0 ? (unsigned)(((r - 1) * Cin + NW) * 2) : 0u);
+  };
+
+  f32x4 accw[NCO][NWT];
+#pragma unroll
+  for (int i = 0; i < NCO; ++i)
+#pragma unroll
+    for (int j = 0; j < NWT; ++j) accw[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const long wstride = (long)gridDim.x * 4;
+  long t = (long)blockIdx.x * 4 + wave;
+  bf16x4 dzv[JN], yv[JN];
+  bf16x8 xv[JX];
+  {
+    const rsrc_t rdz = rsrc_d(a.dz, t * 32), ry = rsrc_d(a.y, t * 32), rxx = rsrc_x(a.x, t * 32);
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      dzv[j] = buf_ld<bf16x4>(rdz, vdj(j), 0u);
+      yv[j] = buf_ld<bf16x4>(ry, vdj(j), 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < JX; ++j) xv[j] = buf_ld<bf16x8>(rxx, vxj(j), 0u);
+  }
+  for (; t < ntiles; t += wstride) {
+    const long row0 = t * 32;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      const long rown = (h == 0 ? t : t + wstride) * 32;
+      // ---- dy -> Ds (rows past M: 0); the next half's dz / y chunks reload as consumed --------
+      {
+        const rsrc_t ndz = rsrc_d(a.dz, rown), ny = rsrc_d(a.y, rown);
+        const unsigned nso = (unsigned)((1 - h) * 16 * COUT * 2);
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int r = rg + RG * j;
+          const bool rok = row0 + h * 16 + r < M;
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float yj = (float)yv[j][e];
+            const float z = fmaf(yj, sc[e], sh[e]);
+            const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
+            o[e] = rok ? (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj) : (bf16_t)0.f;
+          }
+          dzv[j] = buf_ld<bf16x4>(ndz, vdj(j), nso);
+          yv[j] = buf_ld<bf16x4>(ny, vdj(j), nso);
+          if (dact && (JN * RG == 16 || r < 16)) *(bf16x4*)(Ds + (h * 16 + r) * LDD + cc * 4) = o;
+        }
+      }
+      // ---- x_p = act_x(BN_x(x)) -> Xs (rows past M: 0) -------------------------------------
+#pragma unroll
+      for (int j = 0; j < JX; ++j) {
+        const int r = rx + RGX * j;
+        const bool rok = row0 + h * 16 + r < M;
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = rok ? (bf16_t)act_fwd(fmaf((float)xv[j][e], xsc[e], xsh[e]), a.xact) : (bf16_t)0.f;
+        if (xact && (JX * RGX == 16 || r < 16)) *(bf16x8*)(Xs + (h * 16 + r) * LDX + xc * 8) = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- dx = dy . W for the half -> Cx; written by the x lanes with the BN_x sums ------------
+      {
+        f32x4 accx[NWT];
+#pragma unroll
+        for (int j = 0; j < NWT; ++j) accx[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KT; ++s) {
+          const bf16x8 fa = *(const bf16x8*)(Ds + (h * 16 + li) * LDD + s * 32 + 8 * g);
+#pragma unroll
+          for (int j = 0; j < NWT; ++j) {
+            const bf16x8 fb = *(const bf16x8*)(Ws + (j * 16 + li) * LDD + s * 32 + 8 * g);
+            accx[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, accx[j], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NWT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Cx[(4 * g + r) * LDX + j * 16 + li] = (bf16_t)accx[j][r];
+        __builtin_amdgcn_wave_barrier();
+        const rsrc_t rdx = rsrc_x(a.dx, row0);
+        const unsigned so = (unsigned)(h * 16 * Cin * 2);
+#pragma unroll
+        for (int j = 0; j < JX; ++j) {
+          const int r = rx + RGX * j;
+          const bool rok = row0 + h * 16 + r < M && xact && (JX * RGX == 16 || r < 16);
+          const bf16x8 dv = *(const bf16x8*)(Cx + (r < 16 ? r : 0) * LDX + xc * 8);
+          if constexpr (DX) buf_st(dv, rdx, vxj(j), so);
+          if (rok) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              gred_acc((float)dv[e], (float)xv[j][e], xsc[e], xsh[e], xmu[e], xrs[e], a.xact, sg[e], sgx[e]);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      // ---- the next half's x (its registers were needed until the sums above) -----------------
+      {
+        const rsrc_t nx = rsrc_x(a.x, rown);
+        const unsigned nso = (unsigned)((1 - h) * 16 * Cin * 2);
+#pragma unroll
+        for (int j = 0; j < JX; ++j) xv[j] = buf_ld<bf16x8>(nx, vxj(j), nso);
+      }
+    }
+    // ---- dW += dy^T . x_p over the tile's 32 rows -------------------------------------------
+#pragma unroll
+    for (int ct = 0; ct < NCO; ++ct) {
+      const bf16_t* pd = Ds + (8 * g + q) * LDD + ct * 16 + 4 * p;
+      const bf16x4 lo = pb_tr_read(pd), hi = pb_tr_read(pd + 4 * LDD);
+      const bf16x8 fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int it = 0; it < NWT; ++it) {
+        const bf16_t* px = Xs + (8 * g + q) * LDX + it * 16 + 4 * p;
+        const bf16x4 l2 = pb_tr_read(px), h2 = pb_tr_read(px + 4 * LDX);
+        const bf16x8 fb = {l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
+        accw[ct][it] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, accw[ct][it], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- end: dW (waves in order) and the BN_x sums (waves, then row groups, in order) -------
+  float* red = (float*)(smem + (size_t)G::WS * 2);              // [NCO*16][NW]
+  float* gbuf = red + NCO * 16 * NW;                            // [4][RGX][2][NW]
+  __syncthreads();
+  if (xact) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gbuf[((wave * RGX + rx) * 2 + 0) * NW + xc * 8 + e] = sg[e];
+      gbuf[((wave * RGX + rx) * 2 + 1) * NW + xc * 8 + e] = sgx[e];
+    }
+  }
+#pragma unroll 1
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int ct = 0; ct < NCO; ++ct)
+#pragma unroll
+        for (int it = 0; it < NWT; ++it)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* d = red + (ct * 16 + 4 * g + r) * NW + it * 16 + li;
+            *d = w == 0 ? accw[ct][it][r] : *d + accw[ct][it][r];
+          }
+    }
+    __syncthreads();
+  }
+  float* pw = a.partw + (long)blockIdx.x * COUT * Cin;
+  for (int i = tid; i < COUT * NW; i += 256) {
+    const int co = i / NW, c = i - co * NW;
+    pw[(long)co * Cin + n0 + c] = red[co * NW + c];
+  }
+  float* xp = xparts + (long)blockIdx.x * 2 * Cin;
+  for (int i = tid; i < 2 * NW; i += 256) {
+    const int k = i / NW, c = i - k * NW;
+    float s = 0.f;
+    for (int w = 0; w < 4; ++w)
+      for (int r = 0; r < RGX; ++r) s += gbuf[((w * RGX + r) * 2 + k) * NW + c];
+    xp[(long)k * Cin + n0 + c] = s;
+  }
+}
+
+// the group width of the gred form for (Cin, Cout); 0: not taken (ROD_PWB_GRED=0: never)
+static int pw_bwd_gred_nw(int Cin, int Cout) {
+  static const bool off = getenv("ROD_PWB_GRED") && atoi(getenv("ROD_PWB_GRED")) == 0;
+  if (off || !(Cout == 16 || Cout == 24 || Cout == 32 || Cout == 64)) return 0;
+  if (Cin % 48 == 0) return 48;
+  if (Cin % 32 == 0) return 32;
+  return 0;
+}
+static int pw_bwd_gred_rowblocks(long M, int Cin, int nw) {
+  const long ntiles = cdivl(M, 32);
+  const int groups = Cin / nw;
+  const long want = std::max<long>(1, 768 / groups);   // ~3 resident blocks per CU over all groups
+  return (int)std::max<long>(1, std::min<long>(cdivl(ntiles, 4), want));
+}
+
 struct PwBwdPlan {
   int kd, nci, nco, nxt, nx, wt, nblk;
   long chunk;
@@ -636,6 +920,56 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
   slab_sum(partw, dw, p.nblk, (long)Cout * Cin, s);
   if (db) slab_sum(partb, db, p.nblk, (long)Cout, s);
   return check_launch("rod_pw_bwd");
+}
+
+
+long rod_pw_bwd_gred_parts(long M, int Cin, int Cout, int dtype) {
+  const int nw = dtype == ROD_BF16 && M > 0 ? pw_bwd_gred_nw(Cin, Cout) : 0;
+  return nw ? pw_bwd_gred_rowblocks(M, Cin, nw) : 0;
+}
+
+size_t rod_pw_bwd_gred_workspace(long M, int Cin, int Cout) {
+  const int nw = M > 0 ? pw_bwd_gred_nw(Cin, Cout) : 0;
+  return nw ? (size_t)pw_bwd_gred_rowblocks(M, Cin, nw) * Cout * Cin * sizeof(float) + 64 : 0;
+}
+
+int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                    const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                    const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                    void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
+                    void* stream) {
+  const int nw = dtype == ROD_BF16 && M > 0 ? pw_bwd_gred_nw(Cin, Cout) : 0;
+  ROD_CHECK_ARG(nw, "rod_pw_bwd_gred: unsupported shape M=%ld Cin=%d Cout=%d dtype=%d", M, Cin, Cout, dtype);
+  ROD_CHECK_ARG(dz && y && mean && rstd && coef && x && xmean && xrstd && dw && xparts && workspace,
+                "rod_pw_bwd_gred: NULL argument");
+  ROD_CHECK_ARG(dx && wt1, "rod_pw_bwd_gred: dx and wt1 required (the sums are over dx)");
+  ROD_CHECK_ARG(((((uintptr_t)dz) | ((uintptr_t)y) | ((uintptr_t)x) | ((uintptr_t)wt1) | ((uintptr_t)dx)) & 15) == 0,
+                "rod_pw_bwd_gred: tensors must be 16-byte aligned");
+  ROD_CHECK_ARG(M * Cin * 2 < (1L << 31) && M * Cout * 2 < (1L << 31), "rod_pw_bwd_gred: tensor over 2 GiB");
+  hipStream_t s = ROD_STREAM(stream);
+  const int nblk = pw_bwd_gred_rowblocks(M, Cin, nw);
+  float* partw = (float*)workspace;
+  PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw, nullptr,
+              mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0};
+  const long ntiles = cdivl(M, 32);
+  const dim3 grid(nblk, Cin / nw);
+#define PBG(CO, NW_, DXF)                                                                                       \
+  do {                                                                                                          \
+    const size_t lds = PbgGeo<CO, NW_>::lds();                                                                  \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_gred_kernel<CO, NW_, DXF>,                                    \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
+    hipLaunchKernelGGL((pw_bwd_gred_kernel<CO, NW_, DXF>), grid, dim3(256), lds, s, a, ntiles, xparts);         \
+  } while (0)
+#define PBG2(CO)                                                                    \
+  if (Cout == CO) {                                                                 \
+    if (nw == 48) PBG(CO, 48, true);                                                \
+    else PBG(CO, 32, true);                                                         \
+  }
+  PBG2(16) else PBG2(24) else PBG2(32) else PBG2(64)
+#undef PBG2
+#undef PBG
+  slab_sum(partw, dw, nblk, (long)Cout * Cin, s);
+  return check_launch("rod_pw_bwd_gred");
 }
 
 }  // extern "C"

@@ -20,7 +20,7 @@ from . import _abi
 from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU, ROD_ACT_RELU6  # noqa: F401
 
 _DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
-# debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro
+# debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro, pwgred
 _DISABLE = set(os.environ.get("ROD_DISABLE", "").split(","))
 # opt-in paths (comma list): gred = BatchNorm-backward reduction fused into the backward-data
 # epilogues (measured slower than the separate streaming reduce on MI355X: DESIGN.md §6);
@@ -404,6 +404,27 @@ def pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, want_dx, dw,
     _abi.call("rod_pw_bwd", dz, y, mean, rstd, gamma, beta, act, coef, x, *_pro_args(xpro), wt1 if want_dx else None,
               dx, dw, db, ws, M, Cin, Cout, dtcode(y), stream())
     return dx
+
+
+def pw_bwd_gred_parts(M, Cin, Cout, dtype):
+    """Part count of rod_pw_bwd_gred for this project shape (0: not taken)."""
+    if "pwgred" in _DISABLE:
+        return 0
+    return int(_abi.lib().rod_pw_bwd_gred_parts(int(M), int(Cin), int(Cout), _DT[dtype]))
+
+
+def pw_bwd_gred(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, dw):
+    """rod_pw_bwd_gred: the project conv's backward through its BatchNorm (dx, dw written in
+    place) plus the input BatchNorm's backward sums over (dx, x) -> (dx, [nparts, 2, Cin])."""
+    Cin, Cout = x.shape[-1], y.shape[-1]
+    M = y.numel() // Cout
+    nparts = pw_bwd_gred_parts(M, Cin, Cout, y.dtype)
+    dx = torch.empty_like(x)
+    xparts = torch.empty((nparts, 2, Cin), dtype=torch.float32, device=y.device)
+    ws = workspace(_abi.query("rod_pw_bwd_gred_workspace", M, Cin, Cout), y.device)
+    _abi.call("rod_pw_bwd_gred", dz, y, mean, rstd, gamma, beta, act, coef, x, *_pro_args(xpro), wt1, dx, dw,
+              xparts, ws, M, Cin, Cout, dtcode(y), stream())
+    return dx, xparts
 
 
 def _bn_backward_parts(dz, y, mean, rstd, gamma, beta, act, parts, need_g, need_b):
@@ -807,6 +828,21 @@ class _ConvBN(torch.autograd.Function):
         dz = dz.contiguous()
         need_dx = ctx.needs_input_grad[0]
         parts = _take_bn_parts(dz)   # the BN sums a fused depthwise backward already formed
+        if ctx.ks == 1 and b is None and ctx.ipro is not None and need_dx and _needs(w) and \
+                M >= 65536 and SYNC_BN is None and pw_bwd_gred_parts(M, Cin, Cout, y.dtype) > 0:
+            # the project conv of an inverted-residual block (conv_blocks.py:287-294): one pass for
+            # its BatchNorm backward apply, dgrad and wgrad, which also forms the backward sums of
+            # the depthwise BatchNorm whose output it consumed (ipro) over (dx, x) — handed to that
+            # BatchNorm's node (_DWBN), which then skips its rod_bn_bwd_reduce pass
+            if parts is not None:
+                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))
+            else:
+                coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            wt1 = _prep(w, 1, x.dtype, Cout, Cin, 1)
+            dx, xparts = pw_bwd_gred(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, grad_slot(w))
+            _mark_written(w)
+            _put_bn_parts(dx, xparts)
+            return dx, None, None, None, None, None
         if ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w) or _needs(b)):
             if parts is not None:
                 coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))

@@ -18,6 +18,8 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
                          backward's SECOND pass (as for bn_bwd_apply): design traffic; dy is
                          never stored
   pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product
+  pw_bwd_gred (project): es*(2*M*Cout + 2*M*Cin) + W, 4*M*Cin*Cout + 10*M*Cout + 6*M*Cin (the
+                         input BatchNorm's sums ride on the x it reads and the dx it writes)
   match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
   ir_block_fwd (fused) : es*(N*H*W*Cin + N*Ho*Wo*Cout) + weights, 2*N*H*W*Cin*inner +
                          18*N*Ho*Wo*inner + 2*N*Ho*Wo*inner*Cout
@@ -99,6 +101,11 @@ def cost(name, a):
         want_dx = a[15] is not None
         byts = es * (2 * M * Cout + M * Cin + (M * Cin if want_dx else 0)) + Cout * Cin * (es + 4)
         return byts, 2 * M * Cin * Cout * (2 if want_dx else 1) + 10 * M * Cout
+    if name == "rod_pw_bwd_gred":
+        M, Cin, Cout, dt = a[19], a[20], a[21], a[22]
+        es = _ES[dt]
+        return es * (2 * M * Cout + 2 * M * Cin) + Cout * Cin * (es + 4), \
+            4 * M * Cin * Cout + 10 * M * Cout + 6 * M * Cin
     if name == "rod_ir_block_fwd":
         # fused inverted residual: x read once (the residual re-read is L2-served by design),
         # out written once, the expanded tensor never in HBM; expand flops over all input
@@ -192,7 +199,8 @@ ENTRY_KERNELS = {
     "rod_bn_apply": (("bn_apply_kernel",), ("bn_apply_kernel",)),
     "rod_bn_bwd_reduce": (("bn_bwd_reduce_kernel",), ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel")),
     "rod_bn_bwd_apply": (("bn_bwd_apply_kernel",), ("bn_bwd_apply_kernel",)),
-    "rod_pw_bwd": (("pw_bwd_kernel",), ("pw_bwd_kernel",)),
+    "rod_pw_bwd": (("pw_bwd_kernel", "pw_bwd_stream_kernel"), ("pw_bwd_kernel", "pw_bwd_stream_kernel")),
+    "rod_pw_bwd_gred": (("pw_bwd_gred_kernel",), ("pw_bwd_gred_kernel",)),
     "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),

@@ -159,3 +159,61 @@ def test_pw_bwd_full_size_expand_vs_float64(dev):
         json.dump(d, f, indent=1)
     assert ew <= 1e-4, rec
     assert ex <= 2 ** -7, rec
+
+
+GRED_SHAPES = [  # (M, Cin, Cout, act of the output BatchNorm): project convs of the blocks
+    (70000, 32, 16, ops.ROD_ACT_NONE),      # block 1 (32 -> 16), NW = 32
+    (3000 + 17, 96, 24, ops.ROD_ACT_NONE),  # stride-2 block's project, 2 groups of 48
+    (5000, 144, 24, ops.ROD_ACT_NONE),      # 3 groups, ragged tail
+    (4100, 192, 32, ops.ROD_ACT_NONE),
+    (2000, 384, 64, ops.ROD_ACT_NONE),      # 8 groups, Cout 64 (KT = 2)
+    (33, 48, 16, ops.ROD_ACT_LEAKY),        # fewer rows than one tile
+]
+
+
+@pytest.mark.parametrize('M,Cin,Cout,act', GRED_SHAPES)
+def test_pw_bwd_gred_matches_unfused_chain(dev, M, Cin, Cout, act):
+    """rod_pw_bwd_gred against the unfused chain (rod_bn_bwd_apply -> backward-data -> rod_conv_wgrad)
+    and the input BatchNorm's backward sums against a float64 reduction over the kernel's own dx:
+    dx bit-identical, dw 1e-5, sums 1e-5 normwise."""
+    nparts = ops.pw_bwd_gred_parts(M, Cin, Cout, bf16)
+    assert nparts > 0
+    g = torch.Generator().manual_seed(M + Cin * 5 + Cout)
+    x = (torch.randn(M, Cin, generator=g) * 1.5 + 0.3).to(dev, bf16)
+    y = (torch.randn(M, Cout, generator=g) * 2 + 0.5).to(dev, bf16)
+    dz = torch.randn(M, Cout, generator=g).to(dev, bf16)
+    w = (torch.randn(Cout, 1, 1, Cin, generator=g) * 0.2).to(dev)
+    mean = y.float().mean(0)
+    rstd = torch.rsqrt(y.float().var(0, unbiased=False) + 1e-3)
+    gamma = (torch.rand(Cout, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(Cout, generator=g) * 0.3).to(dev)
+    xm = x.float().mean(0) + (torch.randn(Cin, generator=g) * 0.05).to(dev)
+    xr = (torch.rand(Cin, generator=g) + 0.5).to(dev)
+    xpro = (xm, xr, (torch.rand(Cin, generator=g) + 0.5).to(dev), (torch.randn(Cin, generator=g) * 0.2).to(dev),
+            ops.ROD_ACT_RELU6)
+    coef = ops.bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, False, False)
+    wt1 = ops._prep(w, 1, bf16, Cout, Cin, 1)
+    dy = torch.empty_like(y)
+    ops._abi.call('rod_bn_bwd_apply', dz, y, mean, rstd, gamma, beta, coef, dy, M, Cout, act, ops.dtcode(y),
+                  ops.stream())
+    dx_ref = torch.empty_like(x)
+    ops.conv_fwd_raw(dy, wt1, None, dx_ref, 1, 1, M, Cout, Cin, 1)
+    dw_ref = torch.empty(Cout, Cin, device=dev)
+    wsz = ops._abi.query('rod_conv_wgrad_workspace', 1, 1, M, Cin, Cout, 1)
+    ops._abi.call('rod_conv_wgrad', x, *ops._pro_args(xpro), dy, dw_ref, None, ops.workspace(wsz, dev), 1, 1, M, Cin,
+                  Cout, 1, 0, 0, ops.dtcode(x), ops.stream())
+    dw = torch.full((Cout, Cin), float('nan'), device=dev)
+    dx, xparts = ops.pw_bwd_gred(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, dw)
+    assert xparts.shape == (nparts, 2, Cin)
+    assert torch.equal(dx, dx_ref), _nerr(dx.float(), dx_ref.float())
+    assert _nerr(dw, dw_ref) < 1e-5, _nerr(dw, dw_ref)
+    # the input BatchNorm's backward sums over (dx, x) in float64
+    xd = x.double()
+    xs = xr.double() * xpro[2].double()
+    zx = xd * xs + (xpro[3].double() - xm.double() * xs)
+    gx = dx.double() * ((zx > 0) & (zx < 6))
+    s_g = gx.sum(0)
+    s_gx = (gx * ((xd - xm.double()) * xr.double())).sum(0)
+    p = xparts.double().sum(0)
+    assert _nerr(p[0], s_g) < 1e-5, _nerr(p[0], s_g)
+    assert _nerr(p[1], s_gx) < 1e-5, _nerr(p[1], s_gx)
