@@ -524,7 +524,8 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
 //     next half's chunk as soon as it is consumed; rows past M give dy = 0;
 //   * x: a lane owns one 8-column chunk of the group (BN_x constants in registers) for RGX row
 //     groups; x_p = act_x(BN_x(x)) (bf16) goes to LDS for the weight gradient, the raw x stays
-//     in registers for the sums;
+//     in registers for the sums; the next half's x is loaded into a second register set at the
+//     start of each half (the first form loaded it after the sums: 2.5 TB/s on 96->24);
 //   * dx = dy . W for the half (A fragments from the dy rows in LDS, W's group rows in LDS),
 //     staged in LDS, written by the x lanes, which add g and g*xhat of their chunk as they write;
 //   * after the second half dW += dy^T . x_p over the 32 rows (transposed LDS reads);
@@ -548,7 +549,7 @@ struct PbgGeo {
 };
 
 template <int COUT, int NW, bool DX>
-__global__ void __launch_bounds__(256) pw_bwd_gred_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) pw_bwd_gred_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
   using G = PbgGeo<COUT, NW>;
   constexpr int CCH = G::CCH, RG = G::RG, JN = G::JN, KT = G::KT, LDD = G::LDD, NCO = G::NCO, XCH = G::XCH,
                 RGX = G::RGX, JX = G::JX, NWT = G::NWT, LDX = G::LDX;
@@ -592,13 +593,13 @@ __global__ void __launch_bounds__(256) pw_bwd_gred_kernel(PwBwdArgs a, long ntil
   const float glo = a.act == ROD_ACT_LEAKY ? 0.2f : a.act == ROD_ACT_NONE ? 1.f : 0.f;
   const int rx = lane / XCH, xc = lane - (lane / XCH) * XCH;
   const bool xact = rx < RGX;
-  float xsc[8], xsh[8], xmu[8], xrs[8], sg[8], sgx[8];
+  // sgx sums g*(x - mean); the rstd factor is applied once per column at the end
+  float xsc[8], xsh[8], xmu[8], sg[8], sgx[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = n0 + (xact ? xc * 8 : 0) + e;
     bn_affine(a.xmean, a.xrstd, a.xgamma, a.xbeta, c, xsc[e], xsh[e]);
     xmu[e] = a.xmean[c];
-    xrs[e] = a.xrstd[c];
     sg[e] = sgx[e] = 0.f;
   }
   const unsigned vd0 = dact ? (unsigned)((rg * COUT + cc * 4) * 2) : ROD_OOB;
@@ -647,6 +648,14 @@ __global__ void __launch_bounds__(256) pw_bwd_gred_kernel(PwBwdArgs a, long ntil
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
       const long rown = (h == 0 ? t : t + wstride) * 32;
+      // the next half's x, in flight through this whole half (xv is needed until its sums)
+      bf16x8 xn[JX];
+      {
+        const rsrc_t nx = rsrc_x(a.x, rown);
+        const unsigned nso = (unsigned)((1 - h) * 16 * Cin * 2);
+#pragma unroll
+        for (int j = 0; j < JX; ++j) xn[j] = buf_ld<bf16x8>(nx, vxj(j), nso);
+      }
       // ---- dy -> Ds (rows past M: 0); the next half's dz / y chunks reload as consumed --------
       {
         const rsrc_t ndz = rsrc_d(a.dz, rown), ny = rsrc_d(a.y, rown);
@@ -710,18 +719,13 @@ __global__ void __launch_bounds__(256) pw_bwd_gred_kernel(PwBwdArgs a, long ntil
           if (rok) {
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-              gred_acc((float)dv[e], (float)xv[j][e], xsc[e], xsh[e], xmu[e], xrs[e], a.xact, sg[e], sgx[e]);
+              gred_acc((float)dv[e], (float)xv[j][e], xsc[e], xsh[e], xmu[e], 1.f, a.xact, sg[e], sgx[e]);
           }
         }
         __builtin_amdgcn_wave_barrier();
       }
-      // ---- the next half's x (its registers were needed until the sums above) -----------------
-      {
-        const rsrc_t nx = rsrc_x(a.x, rown);
-        const unsigned nso = (unsigned)((1 - h) * 16 * Cin * 2);
 #pragma unroll
-        for (int j = 0; j < JX; ++j) xv[j] = buf_ld<bf16x8>(nx, vxj(j), nso);
-      }
+      for (int j = 0; j < JX; ++j) xv[j] = xn[j];
     }
     // ---- dW += dy^T . x_p over the tile's 32 rows -------------------------------------------
 #pragma unroll
@@ -776,7 +780,7 @@ __global__ void __launch_bounds__(256) pw_bwd_gred_kernel(PwBwdArgs a, long ntil
     float s = 0.f;
     for (int w = 0; w < 4; ++w)
       for (int r = 0; r < RGX; ++r) s += gbuf[((w * RGX + r) * 2 + k) * NW + c];
-    xp[(long)k * Cin + n0 + c] = s;
+    xp[(long)k * Cin + n0 + c] = k ? s * a.xrstd[n0 + c] : s;
   }
 }
 
@@ -784,6 +788,8 @@ __global__ void __launch_bounds__(256) pw_bwd_gred_kernel(PwBwdArgs a, long ntil
 static int pw_bwd_gred_nw(int Cin, int Cout) {
   static const bool off = getenv("ROD_PWB_GRED") && atoi(getenv("ROD_PWB_GRED")) == 0;
   if (off || !(Cout == 16 || Cout == 24 || Cout == 32 || Cout == 64)) return 0;
+  // Cout 64 at 48 columns spills under the 3-waves/SIMD bound (168 VGPRs); 32 columns fit (162)
+  if (Cout == 64) return Cin % 32 == 0 ? 32 : 0;
   if (Cin % 48 == 0) return 48;
   if (Cin % 32 == 0) return 32;
   return 0;
@@ -962,7 +968,7 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
   } while (0)
 #define PBG2(CO)                                                                    \
   if (Cout == CO) {                                                                 \
-    if (nw == 48) PBG(CO, 48, true);                                                \
+    if (nw == 48 && CO != 64) PBG(CO, 48, true);                                    \
     else PBG(CO, 32, true);                                                         \
   }
   PBG2(16) else PBG2(24) else PBG2(32) else PBG2(64)
