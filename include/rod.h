@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 17
+#define ROD_ABI_VERSION 18
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1 };
@@ -395,6 +395,18 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
                     const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
                     void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
                     void* stream);
+
+/* Stem weight gradient through its BatchNorm (ABI 18): rod_conv_wgrad of the 3x3, 3 -> 32 stem
+ * (mobilenet_v2.py:58 conv + mobilenet.py:417-420 batch_norm) with dy formed in the loader from
+ * the BatchNorm's (dz, y) by rod_bn_bwd_apply's arithmetic (coef from rod_bn_bwd_reduce or
+ * rod_bn_bwd_finalize) instead of read: the [M, 32] dy of the unfused path is never written or
+ * read.  dw fp32 [32][3][3][3] (overwritten); workspace: rod_conv_wgrad_workspace() of the same
+ * shape; x bf16 NHWC [N,H,W,3]; dz / y bf16 [N,H,W,32].  bf16, ksize 3, Cin 3, Cout 32 only
+ * (rod_stem_wgrad_bn_supported). */
+int rod_stem_wgrad_bn_supported(int Cin, int Cout, int ksize, int dtype);
+int rod_stem_wgrad_bn(const void* x, const void* dz, const void* y, const float* mean, const float* rstd,
+                      const float* gamma, const float* beta, int act, const float* coef, float* dw, void* workspace,
+                      int N, int H, int W, int Cin, int Cout, int ksize, int dtype, void* stream);
 
 /* ------------------------------------------------ targets and losses
  * Anchor matching, JACCARD_BIGGER (utils/net_tools.py:270-428, branch 382-421).

@@ -1441,9 +1441,18 @@ static StemWgradPlan stem_wgrad_plan(int N, int H, int W) {
   return p;
 }
 
+// BNB: dy is not read but formed in the loader from the stem BatchNorm's (dz, y) — the apply of
+// rod_bn_bwd_apply (bn_bwd_apply1, rounded to bf16), so dy never crosses HBM (rod_stem_wgrad_bn)
+struct StemBnb {
+  const bf16_t* dz;
+  const bf16_t* y;
+  const float *mean, *rstd, *gamma, *beta, *coef;
+  int act;
+};
+template <bool BNB>
 __global__ void __launch_bounds__(256) stem_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
                                                          float* __restrict__ part, int H, int W, int ldx, int lddy,
-                                                         int rb) {
+                                                         int rb, StemBnb bb) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * SW_TW * SW_LD];  // Ds [px][co] | Xs [px][tap]
   bf16_t* Ds = lds;
   bf16_t* Xs = lds + SW_TW * SW_LD;
@@ -1452,22 +1461,57 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const bf16_t* __restric
   const int n = blockIdx.z;
   const int ya = blockIdx.y * rb;
   const int yz = ya + rb < H ? ya + rb : H;
-  const int px = tid >> 1, half = tid & 1;  // dy loader: pixel, 16-channel half
+  // dy loader: pixel + 16-channel half (BNB: pixels px, px + 64 and a fixed 8-channel chunk, so
+  // the chunk's BatchNorm-backward constants stay in registers)
+  const int px = BNB ? tid >> 2 : tid >> 1, half = tid & 1, ck = tid & 3;
   const int xx = x0 + px;
-  const bool inx = xx < W;
+  const bool inx = xx < W, inx2 = xx + 64 < W;
   const int pg = tid & 127, hg = tid >> 7;  // gather: pixel, wave-uniform tap half
+  float sc[BNB ? 8 : 1], sh[BNB ? 8 : 1], ca[BNB ? 8 : 1], k1[BNB ? 8 : 1], k0[BNB ? 8 : 1];
+  float ghi = 0.f, glo = 0.f;
+  if constexpr (BNB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = ck * 8 + e;
+      bn_affine(bb.mean, bb.rstd, bb.gamma, bb.beta, c, sc[e], sh[e]);
+      ca[e] = bb.coef[c];
+      bn_bwd_k(ca[e], bb.mean[c], bb.rstd[c], bb.coef[32 + c], bb.coef[64 + c], k1[e], k0[e]);
+    }
+    ghi = bb.act == ROD_ACT_RELU6 ? 6.f : INFINITY;
+    glo = bb.act == ROD_ACT_LEAKY ? 0.2f : bb.act == ROD_ACT_NONE ? 1.f : 0.f;
+  }
+  auto apply = [&](const bf16x8& dzv, const bf16x8& yv) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float yj = (float)yv[e];
+      const float z = fmaf(yj, sc[e], sh[e]);
+      const float gj = (float)dzv[e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
+      o[e] = (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj);
+    }
+    return o;
+  };
 
-  bf16x8 d0, d1;
+  bf16x8 d0, d1, y0, y1;
   unsigned short tv[16];
   const unsigned short* Xu = (const unsigned short*)X;
   auto load_row = [&](int y) {
-    if (inx) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d0[j] = d1[j] = y0[j] = y1[j] = (bf16_t)0.f;
+    if constexpr (BNB) {   // (dz, y) of pixels xx and xx + 64, channels ck*8 .. +7
+      const long r = ((long)n * H + y) * W;
+      if (inx) {
+        d0 = *(const bf16x8*)(bb.dz + (r + xx) * 32 + ck * 8);
+        y0 = *(const bf16x8*)(bb.y + (r + xx) * 32 + ck * 8);
+      }
+      if (inx2) {
+        d1 = *(const bf16x8*)(bb.dz + (r + xx + 64) * 32 + ck * 8);
+        y1 = *(const bf16x8*)(bb.y + (r + xx + 64) * 32 + ck * 8);
+      }
+    } else if (inx) {
       const bf16_t* src = DY + (((long)n * H + y) * W + xx) * lddy + half * 16;
       d0 = *(const bf16x8*)src;
       d1 = *(const bf16x8*)(src + 8);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d0[j] = d1[j] = (bf16_t)0.f;
     }
     if (hg) stem_gather<1>(Xu, (long)n * H, y, x0 + pg, H, W, ldx, tv);
     else stem_gather<0>(Xu, (long)n * H, y, x0 + pg, H, W, ldx, tv);
@@ -1484,8 +1528,16 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const bf16_t* __restric
   if (ya < yz) load_row(ya);
   for (int y = ya; y < yz; ++y) {
     __syncthreads();
-    *(bf16x8*)(Ds + px * SW_LD + half * 16) = d0;
-    *(bf16x8*)(Ds + px * SW_LD + half * 16 + 8) = d1;
+    if constexpr (BNB) {   // pixels past W: dy 0 (the apply of zeros is not 0)
+      bf16x8 z8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z8[j] = (bf16_t)0.f;
+      *(bf16x8*)(Ds + px * SW_LD + ck * 8) = inx ? apply(d0, y0) : z8;
+      *(bf16x8*)(Ds + (px + 64) * SW_LD + ck * 8) = inx2 ? apply(d1, y1) : z8;
+    } else {
+      *(bf16x8*)(Ds + px * SW_LD + half * 16) = d0;
+      *(bf16x8*)(Ds + px * SW_LD + half * 16 + 8) = d1;
+    }
     {
       typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
       u16x8 t0, t1;
@@ -1893,8 +1945,8 @@ static void wgrad_typed(const void* x, const BnPro* pro, const void* dy, float* 
   if constexpr (sizeof(T) == 2) {
     if (!pro && ksize == 3 && Cin == 3 && Cout == 32 && vd && !old_stem) {
       const StemWgradPlan sp = stem_wgrad_plan(N, H, W);
-      hipLaunchKernelGGL(stem_wgrad_kernel, dim3(sp.xb, sp.yb, N), dim3(256), 0, s, (const bf16_t*)x,
-                         (const bf16_t*)dy, part, H, W, ldx, lddy, sp.rb);
+      hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(sp.xb, sp.yb, N), dim3(256), 0, s, (const bf16_t*)x,
+                         (const bf16_t*)dy, part, H, W, ldx, lddy, sp.rb, StemBnb{});
       p.splits = sp.nblk;
       stem = true;
     }
@@ -2000,6 +2052,29 @@ int rod_conv_wgrad(const void* x, const float* pro_mean, const float* pro_rstd, 
   ROD_DISPATCH_DTYPE(dtype, wgrad_typed<T>(x, pro_mean ? &pro : nullptr, dy, dw, db, (float*)workspace, N, H, W, Cin,
                                            Cout, ksize, ldx, lddy, ROD_STREAM(stream)));
   return check_launch("rod_conv_wgrad");
+}
+
+
+int rod_stem_wgrad_bn_supported(int Cin, int Cout, int ksize, int dtype) {
+  return dtype == ROD_BF16 && ksize == 3 && Cin == 3 && Cout == 32 ? 1 : 0;
+}
+
+int rod_stem_wgrad_bn(const void* x, const void* dz, const void* y, const float* mean, const float* rstd,
+                      const float* gamma, const float* beta, int act, const float* coef, float* dw, void* workspace,
+                      int N, int H, int W, int Cin, int Cout, int ksize, int dtype, void* stream) {
+  ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && rod_stem_wgrad_bn_supported(Cin, Cout, ksize, dtype),
+                "rod_stem_wgrad_bn: unsupported shape N=%d H=%d W=%d Cin=%d Cout=%d ksize=%d", N, H, W, Cin, Cout,
+                ksize);
+  ROD_CHECK_ARG(x && dz && y && mean && rstd && coef && dw && workspace, "rod_stem_wgrad_bn: NULL argument");
+  ROD_CHECK_ARG(((((uintptr_t)dz) | ((uintptr_t)y)) & 15) == 0, "rod_stem_wgrad_bn: dz / y must be 16-byte aligned");
+  hipStream_t s = ROD_STREAM(stream);
+  const StemWgradPlan sp = stem_wgrad_plan(N, H, W);
+  const StemBnb bb{(const bf16_t*)dz, (const bf16_t*)y, mean, rstd, gamma, beta, coef, act};
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(sp.xb, sp.yb, N), dim3(256), 0, s, (const bf16_t*)x, nullptr,
+                     part, H, W, Cin, Cout, sp.rb, bb);
+  slab_sum(part, dw, sp.nblk, (long)Cout * 27, s);
+  return check_launch("rod_stem_wgrad_bn");
 }
 
 }  // extern "C"

@@ -173,7 +173,7 @@ def _capturing():
 
 # entries whose parameter-gradient sums rod_slab_defer(1) may queue (include/rod.h, ABI 11)
 DEFERRING = frozenset(("rod_conv_wgrad", "rod_dw3x3_bwd_filter", "rod_dw3x3_bwd_filter_bn", "rod_pw_bwd",
-                       "rod_pw_bwd_gred", "rod_dw3x3_bwd_fused"))
+                       "rod_pw_bwd_gred", "rod_stem_wgrad_bn", "rod_dw3x3_bwd_fused"))
 # while sums are deferred: every tensor handed to such an entry (partial slabs, gradient outputs)
 # is kept referenced until rod_slab_flush has been enqueued (rod.ops.SlabDefer)
 KEEP = None

@@ -20,7 +20,7 @@ from . import _abi
 from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU, ROD_ACT_RELU6  # noqa: F401
 
 _DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
-# debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro, pwgred
+# debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro, pwgred, stembn
 _DISABLE = set(os.environ.get("ROD_DISABLE", "").split(","))
 # opt-in paths (comma list): gred = BatchNorm-backward reduction fused into the backward-data
 # epilogues (measured slower than the separate streaming reduce on MI355X: DESIGN.md §6);
@@ -843,6 +843,19 @@ class _ConvBN(torch.autograd.Function):
             _mark_written(w)
             _put_bn_parts(dx, xparts)
             return dx, None, None, None, None, None
+        if ctx.ks == 3 and not need_dx and b is None and ctx.ipro is None and _needs(w) and \
+                "stembn" not in _DISABLE and _abi.lib().rod_stem_wgrad_bn_supported(Cin, Cout, 3, dtcode(y)):
+            # the stem (mobilenet_v2.py:58 + its batch_norm): the weight gradient forms dy from the
+            # BatchNorm's (dz, y) in its loader — the [M, 32] dy is never written (rod_stem_wgrad_bn)
+            if parts is not None:
+                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))
+            else:
+                coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            ws = workspace(_abi.query("rod_conv_wgrad_workspace", N, H, W, Cin, Cout, 3), x.device)
+            _abi.call("rod_stem_wgrad_bn", x, dz, y, mean, rstd, gamma, beta, ctx.act, coef, grad_slot(w), ws, N, H,
+                      W, Cin, Cout, 3, dtcode(y), stream())
+            _mark_written(w)
+            return None, None, None, None, None, None
         if ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w) or _needs(b)):
             if parts is not None:
                 coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))

@@ -43,3 +43,34 @@ def test_stem_full_width(dev):
     torch.testing.assert_close(mm1, mm2, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(mv1, mv2, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(z1.float(), z2.float(), rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize('N,H,W', [(2, 37, 300), (1, 720, 1280)])
+def test_stem_wgrad_bn_matches_apply_then_wgrad(dev, N, H, W):
+    """rod_stem_wgrad_bn (dy formed from the stem BatchNorm's (dz, y) in the weight gradient's
+    loader) against rod_bn_bwd_apply -> rod_conv_wgrad: the same dy rounding and MFMA order, so
+    dw is bit-identical; ragged widths (W % 128 != 0) zero the pixels past W."""
+    bf16 = torch.bfloat16
+    g = torch.Generator().manual_seed(N * H + W)
+    x = (torch.rand(N, H, W, 3, generator=g) * 2 - 1).to(dev, bf16)
+    y = (torch.randn(N, H, W, 32, generator=g) * 2 + 0.5).to(dev, bf16)
+    dz = (torch.randn(N, H, W, 32, generator=g) * 0.1).to(dev, bf16)
+    mean = y.float().mean((0, 1, 2))
+    rstd = torch.rsqrt(y.float().var((0, 1, 2), unbiased=False) + 1e-3)
+    gamma = (torch.rand(32, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(32, generator=g) * 0.3).to(dev)
+    act = ops.ROD_ACT_RELU6
+    M = N * H * W
+    coef = ops.bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, False, False)
+    dy = torch.empty_like(y)
+    ops._abi.call('rod_bn_bwd_apply', dz, y, mean, rstd, gamma, beta, coef, dy, M, 32, act, ops.dtcode(y), ops.stream())
+    ws = ops.workspace(ops._abi.query('rod_conv_wgrad_workspace', N, H, W, 3, 32, 3), dev)
+    dw_ref = torch.empty(32, 3, 3, 3, device=dev)
+    ops._abi.call('rod_conv_wgrad', x, None, None, None, None, 0, dy, dw_ref, None, ws, N, H, W, 3, 32, 3, 0, 0,
+                  ops.dtcode(x), ops.stream())
+    dw = torch.full((32, 3, 3, 3), float('nan'), device=dev)
+    ws2 = ops.workspace(ops._abi.query('rod_conv_wgrad_workspace', N, H, W, 3, 32, 3), dev)
+    ops._abi.call('rod_stem_wgrad_bn', x, dz, y, mean, rstd, gamma, beta, act, coef, dw, ws2, N, H, W, 3, 32, 3,
+                  ops.dtcode(y), ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw_ref), float((dw - dw_ref).abs().max())
