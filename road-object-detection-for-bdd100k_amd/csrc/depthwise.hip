@@ -1398,22 +1398,25 @@ static long dw_lx_parts(int N, int Ho, int Wo, int C, int S, int V) {
   const DwTile t = dw_tile(N, Ho, Wo, C, S, V);
   return (long)N * t.strips * t.coltiles;
 }
-// channel pack of the forward LX kernel: 16-byte packs, or (bf16, output maps of <= 512K pixels)
-// 8-byte packs with half the per-thread weights / accumulators / statistics in registers (106
-// instead of 192 VGPRs with the prologue and statistics: 4 waves / SIMD instead of 2).  Measured
-// (tools/dw_bench.py fwdpro): 180x320x192 126 -> 109 us, 90x160x384 68 -> 60, 45x80x576 41 -> 33,
-// 23x40x960 26 -> 23; slower on the 720p / 360p maps (360x640x144 s2 188 -> 206), which keep 16.
+// channel pack of the forward LX kernel: 16-byte packs, or (bf16) 8-byte packs with half the
+// per-thread weights / accumulators / statistics in registers (106 instead of 192 VGPRs with the
+// prologue and statistics: 4 waves / SIMD instead of 2).  tools/dw_bench.py fwdpro, per shape
+// with ROD_DW_FWD_V=4 / 8 (round 4): 8 bytes on the narrow or small maps — 720x1280x32 s1 229.6
+// vs 258.3 us, 180x320x192 s1 104 vs 113, 90x160x384 52 vs 62, 45x80x576 30 vs 39 — and 16
+// bytes on the wide large ones — 720x1280x96 s2 387 vs 420, 360x640x144 s1 306 vs 341,
+// 360x640x144 s2 187 vs 206.  So 16 bytes when C >= 96 and the INPUT map has > 1M pixels.
 // ROD_DW_FWD_V=4 / 8 forces one width (A/B switch).
-static int dw_fwd_v(int dtype, long pixels) {
+static int dw_fwd_v(int dtype, long in_pixels, int C) {
   static const int env = getenv("ROD_DW_FWD_V") ? atoi(getenv("ROD_DW_FWD_V")) : 0;
   if (dtype == ROD_F32) return 4;
   if (env == 4 || env == 8) return env;
-  return pixels <= 512L * 1024 ? 4 : 8;
+  return C >= 96 && in_pixels > 1024L * 1024 ? 8 : 4;
 }
 template <typename T>
 static long dw_fwd_lx_launch(const void* x, const BnPro* pro, const float* w, void* y, float* parts, int N, int H,
                              int W, int C, int S, int pt, int pl, int Ho, int Wo, hipStream_t s) {
-  const int V = dw_fwd_v(sizeof(T) == 2 ? ROD_BF16 : ROD_F32, (long)N * Ho * Wo);
+  // input pixels as N*Ho*Wo*S*S: the same function of the output shape as rod_dw3x3_fwd_stat_parts
+  const int V = dw_fwd_v(sizeof(T) == 2 ? ROD_BF16 : ROD_F32, (long)N * Ho * Wo * S * S, C);
   const DwTile t = dw_tile(N, Ho, Wo, C, S, V);
   const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
   const BnPro pv = pro ? *pro : BnPro{};
@@ -1531,7 +1534,8 @@ int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C, int stride, int dtype
   // exactly the parts the launch for 16-byte-aligned x / y writes: the LDS-exchange kernel
   // when C fills 16-byte packs, else the register-strip kernel's grid
   const int V16 = dtype == ROD_F32 ? 4 : 8;
-  if (C % V16 == 0) return (int)dw_lx_parts(N, Ho, Wo, C, stride == 2 ? 2 : 1, dw_fwd_v(dtype, (long)N * Ho * Wo));
+  if (C % V16 == 0)
+    return (int)dw_lx_parts(N, Ho, Wo, C, stride == 2 ? 2 : 1, dw_fwd_v(dtype, (long)N * Ho * Wo * stride * stride, C));
   const int V = dtype == ROD_F32 ? (C % 4 == 0 ? 4 : 1) : (C % 4 == 0 ? 4 : 1);
   const dim3 g = dw_fwd_grid(N, Ho, Wo, C, V);
   return (int)(g.x * g.y * g.z);
