@@ -27,7 +27,7 @@ def test_training_batches_padded_to_fixed_count():
     files = tfrecord_files(GOLD)
     src = TFRecordSource(files, 3, (96, 160), CPU, torch.float32, train=True, seed=5, prefetch=False)
     counts = set()
-    for flat, boxes, labels, n, hw, offs, draws in _host_batches(src, 6):
+    for flat, boxes, labels, n, hw, offs, draws, _ in _host_batches(src, 6):
         assert boxes.shape == (3, GMAX, 4) and labels.shape == (3, GMAX)
         counts.add(tuple(n.tolist()))
         for b in range(3):   # zero past the real count
@@ -62,7 +62,7 @@ def test_batch_with_more_boxes_pads_to_next_multiple(tmp_path):
             c = np.sort(rng.uniform(0.05, 0.95, (g, 2, 2)), axis=1).reshape(g, 4)[:, [0, 2, 1, 3]].astype(np.float32)
             w.write(tfrecord.encode_detection_example(buf.getvalue(), (40, 64, 3), c, np.ones(g, np.int64)))
     src = TFRecordSource([path], 2, (32, 48), CPU, torch.float32, train=True, seed=1, prefetch=False)
-    _, boxes, labels, n, _, _, _ = src._host()
+    _, boxes, labels, n, _, _, _, _ = src._host()
     assert sorted(n.tolist()) == [3, 70] and boxes.shape == (2, 2 * GMAX, 4)
     src.close()
 
