@@ -548,7 +548,20 @@ struct PbgGeo {
   }
 };
 
-template <int COUT, int NW, bool DX>
+typedef float pb_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pb_b2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pb_f2 pb_unpack(unsigned u) {   // bf16 pair (low, high) -> fp32 pair
+  return pb_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
+__device__ __forceinline__ unsigned pb_round(pb_f2 v) {    // one v_cvt_pk_bf16_f32 (RNE per element)
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, pb_b2));
+}
+// ReLU6 gradient gate (0 < z < 6; NaN -> closed) as one unsigned compare on the bits
+__device__ __forceinline__ bool pb_relu6_open(float z) { return __builtin_bit_cast(unsigned, z) - 1u < 0x40BFFFFFu; }
+
+// FAST: the block's activations (linear output BatchNorm, ReLU6 input BatchNorm) at compile
+// time, channel pairs as packed fp32 ops; otherwise both activations at run time, per element
+template <int COUT, int NW, bool FAST>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) pw_bwd_gred_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
   using G = PbgGeo<COUT, NW>;
   constexpr int CCH = G::CCH, RG = G::RG, JN = G::JN, KT = G::KT, LDD = G::LDD, NCO = G::NCO, XCH = G::XCH,
@@ -570,11 +583,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
     ((bf16x8*)smem)[i] = z;
   }
   __syncthreads();
-  if constexpr (DX) {
-    for (int i = tid; i < NW * (COUT / 8); i += 256) {
-      const int c = i / (COUT / 8), c8 = i - c * (COUT / 8);
-      *(bf16x8*)(Ws + c * LDD + c8 * 8) = *(const bf16x8*)(a.wt1 + (long)(n0 + c) * COUT + c8 * 8);
-    }
+  for (int i = tid; i < NW * (COUT / 8); i += 256) {
+    const int c = i / (COUT / 8), c8 = i - c * (COUT / 8);
+    *(bf16x8*)(Ws + c * LDD + c8 * 8) = *(const bf16x8*)(a.wt1 + (long)(n0 + c) * COUT + c8 * 8);
   }
   __syncthreads();
 
@@ -602,6 +613,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
     xmu[e] = a.xmean[c];
     sg[e] = sgx[e] = 0.f;
   }
+  // FAST: the same constants as register pairs (packed operands without pair-building moves)
+  pb_f2 ca2[2], k12[2], k02[2], xsc2[4], xsh2[4], xmu2[4];
+  if constexpr (FAST) {
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      ca2[h2] = pb_f2{ca[2 * h2], ca[2 * h2 + 1]};
+      k12[h2] = pb_f2{k1[2 * h2], k1[2 * h2 + 1]};
+      k02[h2] = pb_f2{k0[2 * h2], k0[2 * h2 + 1]};
+    }
+#pragma unroll
+    for (int h2 = 0; h2 < 4; ++h2) {
+      xsc2[h2] = pb_f2{xsc[2 * h2], xsc[2 * h2 + 1]};
+      xsh2[h2] = pb_f2{xsh[2 * h2], xsh[2 * h2 + 1]};
+      xmu2[h2] = pb_f2{xmu[2 * h2], xmu[2 * h2 + 1]};
+    }
+  }
+  pb_f2 sg2[4] = {}, sgx2[4] = {};
   const unsigned vd0 = dact ? (unsigned)((rg * COUT + cc * 4) * 2) : ROD_OOB;
   auto vdj = [&](int j) -> unsigned {
     if constexpr (JN * RG == 16) return vd0 + (unsigned)(j * RG * COUT * 2);
@@ -665,12 +693,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
           const int r = rg + RG * j;
           const bool rok = row0 + h * 16 + r < M;
           bf16x4 o;
+          if constexpr (FAST) {   // linear output BatchNorm: g = dz; dy = fma(a, dz, fma(k1, y, k0))
+            const u32x2_t yu = __builtin_bit_cast(u32x2_t, yv[j]), du = __builtin_bit_cast(u32x2_t, dzv[j]);
+            u32x2_t ou;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float yj = (float)yv[j][e];
-            const float z = fmaf(yj, sc[e], sh[e]);
-            const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
-            o[e] = rok ? (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj) : (bf16_t)0.f;
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const pb_f2 y2 = pb_unpack(yu[h2]), d2 = pb_unpack(du[h2]);
+              const pb_f2 t2 = __builtin_elementwise_fma(k12[h2], y2, k02[h2]);
+              ou[h2] = rok ? pb_round(__builtin_elementwise_fma(ca2[h2], d2, t2)) : 0u;
+            }
+            o = __builtin_bit_cast(bf16x4, ou);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float yj = (float)yv[j][e];
+              const float z = fmaf(yj, sc[e], sh[e]);
+              const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
+              o[e] = rok ? (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj) : (bf16_t)0.f;
+            }
           }
           dzv[j] = buf_ld<bf16x4>(ndz, vdj(j), nso);
           yv[j] = buf_ld<bf16x4>(ny, vdj(j), nso);
@@ -683,9 +723,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
         const int r = rx + RGX * j;
         const bool rok = row0 + h * 16 + r < M;
         bf16x8 v;
+        if constexpr (FAST) {   // ReLU6 input BatchNorm
+          const u32x4_t xu = __builtin_bit_cast(u32x4_t, xv[j]);
+          u32x4_t vu;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          v[e] = rok ? (bf16_t)act_fwd(fmaf((float)xv[j][e], xsc[e], xsh[e]), a.xact) : (bf16_t)0.f;
+          for (int h2 = 0; h2 < 4; ++h2) {
+            const pb_f2 z2 = __builtin_elementwise_fma(pb_unpack(xu[h2]), xsc2[h2], xsh2[h2]);
+            const pb_f2 t2 = {act_t<ROD_ACT_RELU6>(z2.x), act_t<ROD_ACT_RELU6>(z2.y)};
+            vu[h2] = rok ? pb_round(t2) : 0u;
+          }
+          v = __builtin_bit_cast(bf16x8, vu);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = rok ? (bf16_t)act_fwd(fmaf((float)xv[j][e], xsc[e], xsh[e]), a.xact) : (bf16_t)0.f;
+        }
         if (xact && (JX * RGX == 16 || r < 16)) *(bf16x8*)(Xs + (h * 16 + r) * LDX + xc * 8) = v;
       }
       __builtin_amdgcn_wave_barrier();
@@ -715,11 +767,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
           const int r = rx + RGX * j;
           const bool rok = row0 + h * 16 + r < M && xact && (JX * RGX == 16 || r < 16);
           const bf16x8 dv = *(const bf16x8*)(Cx + (r < 16 ? r : 0) * LDX + xc * 8);
-          if constexpr (DX) buf_st(dv, rdx, vxj(j), so);
+          buf_st(dv, rdx, vxj(j), so);
           if (rok) {
+            if constexpr (FAST) {   // g = dx where 0 < z < 6; sums of g and g*(x - mean), in pairs
+              const u32x4_t du = __builtin_bit_cast(u32x4_t, dv), xu = __builtin_bit_cast(u32x4_t, xv[j]);
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              gred_acc((float)dv[e], (float)xv[j][e], xsc[e], xsh[e], xmu[e], 1.f, a.xact, sg[e], sgx[e]);
+              for (int h2 = 0; h2 < 4; ++h2) {
+                const pb_f2 x2 = pb_unpack(xu[h2]), d2 = pb_unpack(du[h2]);
+                const pb_f2 z2 = __builtin_elementwise_fma(x2, xsc2[h2], xsh2[h2]);
+                const pb_f2 g2 = {pb_relu6_open(z2.x) ? d2.x : 0.f, pb_relu6_open(z2.y) ? d2.y : 0.f};
+                sg2[h2] += g2;
+                sgx2[h2] = __builtin_elementwise_fma(g2, x2 - xmu2[h2], sgx2[h2]);
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                gred_acc((float)dv[e], (float)xv[j][e], xsc[e], xsh[e], xmu[e], 1.f, a.xact, sg[e], sgx[e]);
+            }
           }
         }
         __builtin_amdgcn_wave_barrier();
@@ -747,6 +811,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
   float* red = (float*)(smem + (size_t)G::WS * 2);              // [NCO*16][NW]
   float* gbuf = red + NCO * 16 * NW;                            // [4][RGX][2][NW]
   __syncthreads();
+  if constexpr (FAST) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sg[e] = sg2[e >> 1][e & 1];
+      sgx[e] = sgx2[e >> 1][e & 1];
+    }
+  }
   if (xact) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -790,8 +861,12 @@ static int pw_bwd_gred_nw(int Cin, int Cout) {
   if (off || !(Cout == 16 || Cout == 24 || Cout == 32 || Cout == 64)) return 0;
   // Cout 64 at 48 columns spills under the 3-waves/SIMD bound (168 VGPRs); 32 columns fit (162)
   if (Cout == 64) return Cin % 32 == 0 ? 32 : 0;
-  if (Cin % 48 == 0) return 48;
+  // 32-column groups wherever Cin allows (tools/pwgred_bench.py: 96->24 289 -> 256 us, 192->32
+  // 139 -> 121 us against 48: no idle row group, 4 waves / SIMD), 48 for Cin = 144
+  static const int force = getenv("ROD_PWB_GRED_NW") ? atoi(getenv("ROD_PWB_GRED_NW")) : 0;   // A/B switch
+  if (force == 48 && Cin % 48 == 0) return 48;
   if (Cin % 32 == 0) return 32;
+  if (Cin % 48 == 0) return 48;
   return 0;
 }
 static int pw_bwd_gred_rowblocks(long M, int Cin, int nw) {
@@ -959,20 +1034,28 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
               mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0};
   const long ntiles = cdivl(M, 32);
   const dim3 grid(nblk, Cin / nw);
-#define PBG(CO, NW_, DXF)                                                                                       \
+  // the inverted-residual block's case; at 48 columns the packed form measured slower (144->24:
+  // 569 vs 433 us), so there the per-element form runs (ROD_PWB_GRED_FAST48=1: packed, A/B)
+  static const bool fast48 = getenv("ROD_PWB_GRED_FAST48") && atoi(getenv("ROD_PWB_GRED_FAST48")) == 1;
+  const bool fast = act == ROD_ACT_NONE && xact == ROD_ACT_RELU6 && (nw == 32 || fast48);
+#define PBG(CO, NW_, F)                                                                                         \
   do {                                                                                                          \
     const size_t lds = PbgGeo<CO, NW_>::lds();                                                                  \
-    (void)hipFuncSetAttribute((const void*)pw_bwd_gred_kernel<CO, NW_, DXF>,                                    \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_gred_kernel<CO, NW_, F>,                                      \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
-    hipLaunchKernelGGL((pw_bwd_gred_kernel<CO, NW_, DXF>), grid, dim3(256), lds, s, a, ntiles, xparts);         \
+    hipLaunchKernelGGL((pw_bwd_gred_kernel<CO, NW_, F>), grid, dim3(256), lds, s, a, ntiles, xparts);           \
   } while (0)
+#define PBG1(CO, NW_)                        \
+  if (fast) PBG(CO, NW_, true);              \
+  else PBG(CO, NW_, false);
 #define PBG2(CO)                                                                    \
   if (Cout == CO) {                                                                 \
-    if (nw == 48 && CO != 64) PBG(CO, 48, true);                                    \
-    else PBG(CO, 32, true);                                                         \
+    if (nw == 48 && CO != 64) { PBG1(CO, 48) }                                      \
+    else { PBG1(CO, 32) }                                                           \
   }
   PBG2(16) else PBG2(24) else PBG2(32) else PBG2(64)
 #undef PBG2
+#undef PBG1
 #undef PBG
   slab_sum(partw, dw, nblk, (long)Cout * Cin, s);
   return check_launch("rod_pw_bwd_gred");
