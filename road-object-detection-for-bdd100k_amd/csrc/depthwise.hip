@@ -2530,22 +2530,23 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
 // ReLU6 gates as selects, the row exchange in fp32 pairs (no pack / unpack around the LDS trip)
 // with one LDS slot per step of the 2-step body (compile-time addresses), and the BN_e gate
 // taken from the prologue's own pre-activation.
-template <int PACT, bool RED, int BACT, int D = 2>
-__global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2p_kernel(
+template <int PACT, bool RED, int BACT, int D = 2, int V = 4>
+__global__ void __launch_bounds__(1024 / V, V == 4 ? 2 : 1) dw3x3_bwd_fused_s2p_kernel(
     const bf16_t* __restrict__ ye, const bf16_t* __restrict__ dz, const bf16_t* __restrict__ yd,
     const float* __restrict__ w, bf16_t* __restrict__ dx, float* __restrict__ slab, float* __restrict__ gparts, int H,
     int W, int C, int pt, int pl, int Ho, int Wo, DwTile tl, BnPro pro, DwBwdBn bd) {
   typedef bf16_t T;
-  constexpr int V = 4, VP = 2;
+  constexpr int VP = V / 2;
+  constexpr int TB = 1024 / V;   // threads per block: the 4-channel tile with V channels a thread
   typedef PackV<T, V> PK;
-  static_assert(D == 2, "one LDS slot per step of the 2-step body");
+  static_assert(D >= 2, "one LDS slot per step of the D-step body");
   // slots [D][3][256][VP] fp32 pairs: dy, x row 0, x row 1 (column ci0)
-  constexpr int XS = D * 3 * 256 * VP * (int)sizeof(dw_f2);
-  constexpr int SS = 256 * V * 4;
+  constexpr int XS = D * 3 * TB * VP * (int)sizeof(dw_f2);
+  constexpr int SS = TB * V * 4;
   __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
   dw_f2* sl = (dw_f2*)smem;
   const int tid = threadIdx.x;
-  const int CVb = tl.CVb, P = tl.P;
+  const int CVb = tl.CVb * (4 / V), P = tl.P;
   const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
   int bx, strip, n;
   xcd_block(bx, strip, n);
@@ -2560,7 +2561,7 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2p_kernel(
   const bool cok1 = p < P && ci0 + 1 >= 0 && ci0 + 1 < W;
   const int a0 = strip * tl.RB;
   const int a1 = a0 + tl.RB < A ? a0 + tl.RB : A;
-  const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < 256 ? tid + CVb : tid;
+  const int li = tid >= CVb ? tid - CVb : tid, ri = tid + CVb < TB ? tid + CVb : tid;
 
   dw_f2 wr[9][VP];
 #pragma unroll
@@ -2689,20 +2690,20 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2p_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);   // the slots' reloads stay after their last reads
       issue(k, q + D);
-      dw_f2* S = sl + k * 3 * 256 * VP;
+      dw_f2* S = sl + k * 3 * TB * VP;
 #pragma unroll
       for (int h = 0; h < VP; ++h) {
         S[tid * VP + h] = dv[h];
-        S[(256 + tid) * VP + h] = xv[0][h];
-        S[(512 + tid) * VP + h] = xv[2][h];
+        S[(TB + tid) * VP + h] = xv[0][h];
+        S[(2 * TB + tid) * VP + h] = xv[2][h];
       }
       __syncthreads();
       dw_f2 dL[VP], r0[VP], r1[VP];
 #pragma unroll
       for (int h = 0; h < VP; ++h) {
         dL[h] = S[li * VP + h];
-        r0[h] = S[(256 + ri) * VP + h];
-        r1[h] = S[(512 + ri) * VP + h];
+        r0[h] = S[(TB + ri) * VP + h];
+        r1[h] = S[(2 * TB + ri) * VP + h];
       }
       const bool own = a >= a0 && a < a1, ownp = a - 1 >= a0 && a - 1 < a1;
       // dx 2x2 block in the order of dw3x3_bwd_data_s2_kernel (bit-identical)
@@ -2781,7 +2782,7 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2p_kernel(
       red[tid * V + 2 * h + 1] = comp ? acc[h].y : 0.f;
     }
     __syncthreads();
-    for (int e = tid; e < Cc; e += 256) {
+    for (int e = tid; e < Cc; e += TB) {
       const int cve = e / V, v = e - cve * V;
       float s = 0.f;
       for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
@@ -2873,9 +2874,26 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
     constexpr int D2 = sizeof(T) == 2 ? 2 : 1;
     // bf16: the packed form (ROD_DWF_S2P=0: the scalar one)
     static const bool s2p = !(getenv("ROD_DWF_S2P") && atoi(getenv("ROD_DWF_S2P")) == 0);
+    // packed stride-2 form with 2 channels a thread in 512-thread blocks (116 VGPRs: 4 waves /
+    // SIMD instead of 2 at 204): tools/dwfused_bench.py stride-2 shapes 1686 -> 1604 us, dx
+    // bit-identical.  ROD_DWF_S2P_V=4: the 4-channel form; ROD_DWF_S2P_D=3: a 3-step ring (A/B)
+    static const bool s2p2 = !(getenv("ROD_DWF_S2P_V") && atoi(getenv("ROD_DWF_S2P_V")) == 4);
+    static const bool s2pd3 = getenv("ROD_DWF_S2P_D") && atoi(getenv("ROD_DWF_S2P_D")) == 3;
 #define DWS2(PA, R)                                                                                                  \
   do {                                                                                                              \
     if constexpr (sizeof(T) == 2) {                                                                                 \
+      if (s2p && s2p2 && s2pd3 && bn_act == ROD_ACT_RELU6) {                                                        \
+        hipLaunchKernelGGL((dw3x3_bwd_fused_s2p_kernel<PA, R, ROD_ACT_RELU6, 3, 2>), grid, dim3(512), 0, s,         \
+                           (const bf16_t*)ye, (const bf16_t*)dz, (const bf16_t*)yd, w, (bf16_t*)dx, slab, gparts, H,  \
+                           W, C, pad_t, pad_l, Ho, Wo, t, pv, bd);                                                  \
+        break;                                                                                                      \
+      }                                                                                                             \
+      if (s2p && s2p2 && bn_act == ROD_ACT_RELU6) {                                                                 \
+        hipLaunchKernelGGL((dw3x3_bwd_fused_s2p_kernel<PA, R, ROD_ACT_RELU6, 2, 2>), grid, dim3(512), 0, s,         \
+                           (const bf16_t*)ye, (const bf16_t*)dz, (const bf16_t*)yd, w, (bf16_t*)dx, slab, gparts, H,  \
+                           W, C, pad_t, pad_l, Ho, Wo, t, pv, bd);                                                  \
+        break;                                                                                                      \
+      }                                                                                                             \
       if (s2p && bn_act == ROD_ACT_RELU6) {                                                                         \
         hipLaunchKernelGGL((dw3x3_bwd_fused_s2p_kernel<PA, R, ROD_ACT_RELU6>), grid, dim3(256), 0, s,               \
                            (const bf16_t*)ye, (const bf16_t*)dz, (const bf16_t*)yd, w, (bf16_t*)dx, slab, gparts, H,  \
