@@ -1134,8 +1134,14 @@ __global__ void __launch_bounds__(256) stem_fwd_mfma_kernel(const bf16_t* __rest
                                                             const float* __restrict__ bias, bf16_t* __restrict__ Y,
                                                             float* __restrict__ stats, int H, int W, int ldx,
                                                             int ldy, int rb) {
+  // input rows through an LDS ring of three (130 pixels x 3 channels each: one 2-byte load per
+  // element per row, issued a whole row ahead), the 3x3x3 patches gathered from LDS — the
+  // first form gathered every tap from global memory (16 two-byte loads per thread per row,
+  // each input element fetched 9 times)
+  constexpr int RIN = (SW_TW + 2) * 3;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[SW_TW * SW_LD];
   __shared__ __attribute__((aligned(16))) bf16_t Ys[SW_TW * SW_LD];
+  __shared__ unsigned short Rin[3][RIN + 2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int x0 = blockIdx.x * SW_TW, n = blockIdx.z;
   const int ya = blockIdx.y * rb;
@@ -1145,10 +1151,43 @@ __global__ void __launch_bounds__(256) stem_fwd_mfma_kernel(const bf16_t* __rest
   const bool inx = xx < W;
   const int pg = tid & 127, hg = tid >> 7;  // gather: pixel, wave-uniform tap half
   typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
-  unsigned short tv[16];
+  const unsigned short* Xu = (const unsigned short*)X;
+  unsigned short tv[16], rv[2];
+  auto load_in = [&](int iy) {   // this thread's elements of input row iy (zero outside the image)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * 256;
+      const int pxe = x0 - 1 + e / 3, ci = e - (e / 3) * 3;
+      rv[u] = 0;
+      if (e < RIN && iy >= 0 && iy < H && pxe >= 0 && pxe < W) rv[u] = Xu[(((long)n * H + iy) * W + pxe) * ldx + ci];
+    }
+  };
+  auto store_in = [&](int iy) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * 256;
+      if (e < RIN) Rin[(iy + 3) % 3][e] = rv[u];
+    }
+  };
+  // taps [16*HG, 16*HG + 16) of pixel pg's patch, tap = (r*3 + c)*3 + ci (HG constant: every
+  // tap's row / column / channel folds; callers pick HG = hg, which is wave-uniform)
+  auto gather_h = [&](auto hgc, int y) {
+    constexpr int HG = decltype(hgc)::value;
+    const unsigned short* rows[3] = {Rin[(y + 2) % 3], Rin[(y + 3) % 3], Rin[(y + 4) % 3]};   // y-1, y, y+1
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = HG * 16 + j;
+      if (k < 27) {
+        const int r = k / 9, c = (k / 3) % 3, ci = k % 3;
+        tv[j] = rows[r][(pg + c) * 3 + ci];
+      } else {
+        tv[j] = 0;
+      }
+    }
+  };
   auto gather = [&](int y) {
-    if (hg) stem_gather<1>((const unsigned short*)X, (long)n * H, y, x0 + pg, H, W, ldx, tv);
-    else stem_gather<0>((const unsigned short*)X, (long)n * H, y, x0 + pg, H, W, ldx, tv);
+    if (hg) gather_h(std::integral_constant<int, 1>{}, y);
+    else gather_h(std::integral_constant<int, 0>{}, y);
   };
   const int g = lane >> 4, i = lane & 15;
   bf16x8 fb[2];  // B[k = 8g + j][co = ct*16 + i] = Wt[co][k]
@@ -1162,9 +1201,26 @@ __global__ void __launch_bounds__(256) stem_fwd_mfma_kernel(const bf16_t* __rest
     }
     bv[ct] = bias ? bias[ct * 16 + i] : 0.f;
   }
-  if (ya < yz) gather(ya);
-  for (int y = ya; y < yz; ++y) {
+  if (ya < yz) {   // rows ya-1 .. ya+1 into the ring (loads issued together), row ya+2 in flight
+    unsigned short pre[3][2];
+#pragma unroll
+    for (int i3 = 0; i3 < 3; ++i3) {
+      load_in(ya - 1 + i3);
+      pre[i3][0] = rv[0];
+      pre[i3][1] = rv[1];
+    }
+#pragma unroll
+    for (int i3 = 0; i3 < 3; ++i3) {
+      rv[0] = pre[i3][0];
+      rv[1] = pre[i3][1];
+      store_in(ya - 1 + i3);
+    }
+    load_in(ya + 2);
     __syncthreads();
+    gather(ya);
+  }
+  for (int y = ya; y < yz; ++y) {
+    __syncthreads();   // Ys of the previous row stored; every gather of row y done
     {
       u16x8 t0, t1;
 #pragma unroll
@@ -1175,8 +1231,9 @@ __global__ void __launch_bounds__(256) stem_fwd_mfma_kernel(const bf16_t* __rest
       *(u16x8*)(Xs + pg * SW_LD + hg * 16) = t0;
       *(u16x8*)(Xs + pg * SW_LD + hg * 16 + 8) = t1;
     }
+    if (y + 1 < yz) store_in(y + 2);   // the slot of row y - 1 (no longer gathered)
     __syncthreads();
-    if (y + 1 < yz) gather(y + 1);  // next row's patch loads in flight under this row
+    if (y + 2 < yz) load_in(y + 3);    // a whole row ahead
     const int m0 = wave * 32;
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
@@ -1218,6 +1275,7 @@ __global__ void __launch_bounds__(256) stem_fwd_mfma_kernel(const bf16_t* __rest
                         (float)(m2 > 0.0 ? m2 : 0.0));
       }
     }
+    if (y + 1 < yz) gather(y + 1);   // rows y .. y+2 are in the ring (barrier above)
   }
 }
 

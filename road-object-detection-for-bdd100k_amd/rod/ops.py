@@ -20,7 +20,7 @@ from . import _abi
 from ._abi import ROD_ACT_LEAKY, ROD_ACT_NONE, ROD_ACT_RELU, ROD_ACT_RELU6  # noqa: F401
 
 _DT = {torch.float32: _abi.ROD_F32, torch.bfloat16: _abi.ROD_BF16}
-# debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro, pwgred, stembn
+# debug bisection switches (comma list): splitk, epistats, convstats, dwstats, bnpro, pwgred, stembn, pro3
 _DISABLE = set(os.environ.get("ROD_DISABLE", "").split(","))
 # opt-in paths (comma list): gred = BatchNorm-backward reduction fused into the backward-data
 # epilogues (measured slower than the separate streaming reduce on MI355X: DESIGN.md §6);
@@ -806,6 +806,15 @@ class _ConvBN(torch.autograd.Function):
         parts = None
         if training:
             parts = torch.empty((-(-(N * H * W) // 128), 3, Cout), dtype=torch.float32, device=x.device)
+        if ks == 3 and ipro is not None and N * H * W >= 16384 and "pro3" not in _DISABLE:
+            # a 3x3 conv gathers each input element for 9 taps, so its load prologue would apply
+            # the input BatchNorm 9 times per element: write act(BN(x)) once instead (the same
+            # rounded values) and use it for the forward and the weight gradient
+            # (the heads' 128 -> 128 convs, catch_net.py:301-304)
+            xb = torch.empty_like(x)
+            im, ir, ig, ib, ia = ipro
+            _abi.call("rod_bn_apply", x, im, ir, ig, ib, None, xb, N * H * W, Cin, 0, 0, 0, ia, dtcode(x), stream())
+            x, ipro = xb, None
         conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ks, parts, ipro)
         mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
         ctx.save_for_backward(x, w, b, y, mean, rstd)
