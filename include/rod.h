@@ -386,7 +386,8 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
  * so the depthwise BatchNorm's rod_bn_bwd_reduce pass over (dz, y) is not needed: x is read once
  * for the weight gradient's prologue and for the sums, dx is summed as it is written.  No bias;
  * xmean / xrstd, dx and wt1 required.  rod_pw_bwd_gred_parts() is the part count (0: shape not taken —
- * bf16, Cout in {16, 24, 32, 64}, Cin a multiple of 32 or 48); workspace:
+ * bf16, Cout in {16, 24, 32, 64}, Cin a multiple of 32 or 48; or the expand shape 16 -> 96, whose
+ * input is the previous block's project output: its linear BatchNorm's sums, ABI 18); workspace:
  * rod_pw_bwd_gred_workspace() bytes.  dx is rod_pw_bwd's bit for bit. */
 long rod_pw_bwd_gred_parts(long M, int Cin, int Cout, int dtype);
 size_t rod_pw_bwd_gred_workspace(long M, int Cin, int Cout);

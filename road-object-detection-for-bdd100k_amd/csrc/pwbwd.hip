@@ -303,10 +303,10 @@ struct PbsGeo {
   static constexpr int LDC = CIN + 8;
   static constexpr int WREG = 32 * LDD + 32 * LDX + 16 * LDC;    // bf16 elements per wave
   static constexpr int WS = NCI * 16 * LDD;                       // wt1 image (bf16 elements)
-  static constexpr int XT = 2 * CIN * 2;                          // input-prologue table (bf16 slots)
+  static constexpr int XT = 3 * CIN * 2;                          // input-prologue table (bf16 slots)
   static constexpr size_t lds() {
     const size_t main = (size_t)(WS + XT + 4 * WREG) * 2;
-    const size_t red = (size_t)(WS + XT) * 2 + (size_t)COUT * NCI * 16 * 4;
+    const size_t red = (size_t)(WS + XT) * 2 + (size_t)COUT * NCI * 16 * 4 + (size_t)4 * 16 * 2 * CIN * 4;
     return main > red ? main : red;
   }
 };
@@ -315,16 +315,21 @@ template <int CW> struct PbsVec;
 template <> struct PbsVec<4> { typedef bf16x4 T; };
 template <> struct PbsVec<8> { typedef bf16x8 T; };
 
-template <int CIN, int COUT, bool PRO, bool DX>
-__global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long ntiles) {
+// XG (with the input prologue): also the input BatchNorm's backward sums over (dx, x) — the
+// expand conv of a block whose input is the previous block's project output (linear BatchNorm):
+// that BatchNorm's gradient is this dx, so its rod_bn_bwd_reduce pass is not needed
+// (rod_pw_bwd_gred on the expand shapes); part blockIdx.x of [nblk][2][CIN]
+template <int CIN, int COUT, bool PRO, bool DX, bool XG = false>
+__global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
   using G = PbsGeo<CIN, COUT>;
+  static_assert(!XG || (PRO && DX), "the input sums need the prologue and dx");
   constexpr int CW = G::CW, CCH = G::CCH, RG = G::RG, JN = G::JN, KT = G::KT, LDD = G::LDD, NCO = G::NCO,
                 XCH = G::XCH, NCI = G::NCI, LDX = G::LDX, LDC = G::LDC;
   typedef typename PbsVec<CW>::T VT;
   static_assert(COUT % 16 == 0 && CIN % 8 == 0 && 16 * XCH <= 64, "streaming pw_bwd geometry");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ws = (bf16_t*)smem;                                   // [NCI*16][LDD]: wt1 rows (ci), k = co
-  float* xtab = (float*)(Ws + G::WS);                           // [2][CIN]: input prologue scale, shift
+  float* xtab = (float*)(Ws + G::WS);                           // [3][CIN]: input prologue scale, shift, mean
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   bf16_t* Ds = Ws + G::WS + G::XT + wave * G::WREG;             // [32][LDD]  dy of the tile
@@ -345,11 +350,15 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
     }
   }
   if constexpr (PRO) {
-    for (int c = tid; c < CIN; c += 256) bn_affine(a.xmean, a.xrstd, a.xgamma, a.xbeta, c, xtab[c], xtab[CIN + c]);
+    for (int c = tid; c < CIN; c += 256) {
+      bn_affine(a.xmean, a.xrstd, a.xgamma, a.xbeta, c, xtab[c], xtab[CIN + c]);
+      xtab[2 * CIN + c] = a.xmean[c];
+    }
   }
   __syncthreads();
 
   // ---- lane constants ---------------------------------------------------------------------
+  float xsg[XG ? 8 : 1] = {}, xsgx[XG ? 8 : 1] = {};   // XG: sums of g and g*(x - mean), this lane's chunk
   const int rg = lane / CCH, cc = lane - (lane / CCH) * CCH;
   const bool dact = rg < RG;
   const int c0 = dact ? cc * CW : 0;
@@ -424,6 +433,7 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
         yv[j] = buf_ld<VT>(ny, vdj(j), nso);
         if (dact && (JN * RG == 16 || r < 16)) *(VT*)(Ds + (h * 16 + r) * LDD + cc * CW) = o;
       }
+      const bf16x8 xcur = xv;   // XG: the raw x of this half, for the sums at the dx write-back
       {
         bf16x8 v = xv;
         if constexpr (PRO) {
@@ -466,6 +476,17 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
         const rsrc_t rdx = rsrc_rows(a.dx, row0, CIN * 2);
         const bf16x8 ov = *(const bf16x8*)(Cx + (xact ? xr : 0) * LDC + xc * 8);
         buf_st(ov, rdx, vx, (unsigned)(h * 16 * CIN * 2));
+        if constexpr (XG) {
+          if (xact && row0 + h * 16 + xr < M) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float xe = (float)xcur[e];
+              const float g = (float)ov[e] * act_grad(fmaf(xe, xtab[xc * 8 + e], xtab[CIN + xc * 8 + e]), a.xact);
+              xsg[e] += g;
+              xsgx[e] = fmaf(g, xe - xtab[2 * CIN + xc * 8 + e], xsgx[e]);
+            }
+          }
+        }
         __builtin_amdgcn_wave_barrier();
       }
     }
@@ -508,6 +529,25 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
   for (int i = tid; i < COUT * CIN; i += 256) {
     const int co = i / CIN, ci = i - co * CIN;
     pw[i] = red[co * LR + ci];
+  }
+  if constexpr (XG) {   // waves, then the 16 row lanes of each chunk, added in a fixed order
+    float* gbuf = red + COUT * LR;                                // [4][16][2][CIN]
+    if (xact) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        gbuf[((wave * 16 + xr) * 2 + 0) * CIN + xc * 8 + e] = xsg[e];
+        gbuf[((wave * 16 + xr) * 2 + 1) * CIN + xc * 8 + e] = xsgx[e];
+      }
+    }
+    __syncthreads();
+    float* xp = xparts + (long)blockIdx.x * 2 * CIN;
+    for (int i = tid; i < 2 * CIN; i += 256) {
+      const int k = i / CIN, c = i - k * CIN;
+      float sum = 0.f;
+      for (int w = 0; w < 4; ++w)
+        for (int r = 0; r < 16; ++r) sum += gbuf[((w * 16 + r) * 2 + k) * CIN + c];
+      xp[i] = k ? sum * a.xrstd[c] : sum;
+    }
   }
 }
 
@@ -961,7 +1001,8 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
     const size_t lds = PbsGeo<CI, CO>::lds();                                                                \
     (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, PR, DXF>,                            \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
-    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, PR, DXF>), dim3(nblk), dim3(256), lds, s, a, ntiles);   \
+    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, PR, DXF>), dim3(nblk), dim3(256), lds, s, a, ntiles,     \
+                       nullptr);                                                                             \
   } while (0)
 #define PBS2(CI, CO)                                        \
   if (Cin == CI) {                                          \
@@ -1004,12 +1045,19 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
 }
 
 
+// expand shapes the gred entry takes (the streaming kernel with the input sums): 16 -> 96 only
+// (168 VGPRs, 3 waves / SIMD); 24 -> 144 would need 268 (1 wave), and its input is usually also a
+// residual source, whose gradient is a sum the sums could not be handed to anyway
+static bool pw_bwd_xg_ok(int Cin, int Cout) { return Cin == 16 && Cout == 96 && pw_bwd_stream_ok(Cin, Cout, false); }
+
 long rod_pw_bwd_gred_parts(long M, int Cin, int Cout, int dtype) {
+  if (dtype == ROD_BF16 && M > 0 && pw_bwd_xg_ok(Cin, Cout)) return pw_bwd_stream_blocks(M);
   const int nw = dtype == ROD_BF16 && M > 0 ? pw_bwd_gred_nw(Cin, Cout) : 0;
   return nw ? pw_bwd_gred_rowblocks(M, Cin, nw) : 0;
 }
 
 size_t rod_pw_bwd_gred_workspace(long M, int Cin, int Cout) {
+  if (M > 0 && pw_bwd_xg_ok(Cin, Cout)) return (size_t)pw_bwd_stream_blocks(M) * Cout * Cin * sizeof(float) + 64;
   const int nw = M > 0 ? pw_bwd_gred_nw(Cin, Cout) : 0;
   return nw ? (size_t)pw_bwd_gred_rowblocks(M, Cin, nw) * Cout * Cin * sizeof(float) + 64 : 0;
 }
@@ -1019,8 +1067,10 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
                     const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
                     void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
                     void* stream) {
-  const int nw = dtype == ROD_BF16 && M > 0 ? pw_bwd_gred_nw(Cin, Cout) : 0;
-  ROD_CHECK_ARG(nw, "rod_pw_bwd_gred: unsupported shape M=%ld Cin=%d Cout=%d dtype=%d", M, Cin, Cout, dtype);
+  const bool sexp = dtype == ROD_BF16 && M > 0 && pw_bwd_xg_ok(Cin, Cout);
+  const int nw = dtype == ROD_BF16 && M > 0 && !sexp ? pw_bwd_gred_nw(Cin, Cout) : 0;
+  ROD_CHECK_ARG(nw || sexp, "rod_pw_bwd_gred: unsupported shape M=%ld Cin=%d Cout=%d dtype=%d", M, Cin, Cout,
+                dtype);
   ROD_CHECK_ARG(dz && y && mean && rstd && coef && x && xmean && xrstd && dw && xparts && workspace,
                 "rod_pw_bwd_gred: NULL argument");
   ROD_CHECK_ARG(dx && wt1, "rod_pw_bwd_gred: dx and wt1 required (the sums are over dx)");
@@ -1028,8 +1078,27 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
                 "rod_pw_bwd_gred: tensors must be 16-byte aligned");
   ROD_CHECK_ARG(M * Cin * 2 < (1L << 31) && M * Cout * 2 < (1L << 31), "rod_pw_bwd_gred: tensor over 2 GiB");
   hipStream_t s = ROD_STREAM(stream);
-  const int nblk = pw_bwd_gred_rowblocks(M, Cin, nw);
   float* partw = (float*)workspace;
+  if (sexp) {   // an expand shape: the streaming kernel with the input BatchNorm's sums
+    const int nb = pw_bwd_stream_blocks(M);
+    PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw,
+                nullptr, mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0,
+                0, 0};
+    const long nt = cdivl(M, 32);
+#define PBX(CI, CO)                                                                                       \
+  if (Cin == CI) {                                                                                        \
+    const size_t lds = PbsGeo<CI, CO>::lds();                                                             \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, true, true, true>,                \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                      \
+    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, true, true, true>), dim3(nb), dim3(256), lds, s, a, nt, \
+                       xparts);                                                                           \
+  }
+    PBX(16, 96)
+#undef PBX
+    slab_sum(partw, dw, nb, (long)Cout * Cin, s);
+    return check_launch("rod_pw_bwd_gred");
+  }
+  const int nblk = pw_bwd_gred_rowblocks(M, Cin, nw);
   PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw, nullptr,
               mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0};
   const long ntiles = cdivl(M, 32);

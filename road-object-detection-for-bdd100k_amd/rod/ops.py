@@ -842,7 +842,10 @@ class _ConvBN(torch.autograd.Function):
             # the project conv of an inverted-residual block (conv_blocks.py:287-294): one pass for
             # its BatchNorm backward apply, dgrad and wgrad, which also forms the backward sums of
             # the depthwise BatchNorm whose output it consumed (ipro) over (dx, x) — handed to that
-            # BatchNorm's node (_DWBN), which then skips its rod_bn_bwd_reduce pass
+            # BatchNorm's node (_DWBN), which then skips its rod_bn_bwd_reduce pass.  The expand
+            # 16 -> 96 takes the same entry: its input is the previous block's project output, whose
+            # linear BatchNorm then gets its sums from here (when dx is that BatchNorm's whole
+            # gradient: no residual path adds to it — _take_bn_parts checks)
             if parts is not None:
                 coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))
             else:

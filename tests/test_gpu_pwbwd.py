@@ -168,6 +168,8 @@ GRED_SHAPES = [  # (M, Cin, Cout, act of the output BatchNorm): project convs of
     (4100, 192, 32, ops.ROD_ACT_NONE),
     (2000, 384, 64, ops.ROD_ACT_NONE),      # 8 groups, Cout 64 (KT = 2)
     (33, 48, 16, ops.ROD_ACT_LEAKY),        # fewer rows than one tile
+    (70000, 16, 96, ops.ROD_ACT_RELU6),     # expand 16 -> 96: the streaming kernel with the input sums
+    (1000 + 7, 16, 96, ops.ROD_ACT_RELU6),  # ragged tail
 ]
 
 
