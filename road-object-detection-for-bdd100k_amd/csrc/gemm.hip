@@ -732,10 +732,15 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 // No block barrier after the weight staging.
 // =====================================================================================
 constexpr int PWS_WAVES = 4;
-template <int NT, int KT, int MODE>
+// PRO (KT == 1): the BatchNorm-apply prologue on x — act(fma(x, scale, offset)) rounded to bf16,
+// the value rod_bn_apply would have written — with the lane's 8 channels' constants in registers
+// (its k range is fixed: 8*(lane >> 4)); rows past M stay 0
+template <int NT, int KT, int MODE, bool PRO = false>
 __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                                                         bf16_t* __restrict__ Y, long M, int K, int Cout, int ldx,
-                                                        int ldy, float* __restrict__ part, BnGred gr) {
+                                                        int ldy, float* __restrict__ part, BnGred gr,
+                                                        BnPro pro = BnPro{}) {
+  static_assert(!PRO || KT == 1, "the prologue constants cover one 32-deep k step");
   constexpr int NP = NT * 16;       // columns of the N group
   constexpr int LDB = KT * 32 + 8;  // weight row stride in LDS (elements)
   constexpr int LDC = NP + 8;       // staging row stride (elements; 16-byte multiple)
@@ -780,6 +785,15 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
     }
   }
 
+  float psc[PRO ? 8 : 1], psh[PRO ? 8 : 1];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = lg * 8 + e;
+      psc[e] = psh[e] = 0.f;
+      if (k < K) bn_pro_affine(pro, k, psc[e], psh[e]);
+    }
+  }
   // A fragments of sub-step (tile, s): rows tile*128 + 16s + fr, k 32kt + 8lg
   auto load_a = [&](bf16x8 (&a)[KT], long tile, int s) {
     const long row = tile * 128 + s * 16 + fr;
@@ -791,6 +805,15 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[kt][e] = (bf16_t)0.f;
       }
+    }
+  };
+  // the prologue on a loaded fragment (at use, so the load stays in flight meanwhile)
+  auto pro_a = [&](bf16x8 (&a)[KT], long tile, int s) {
+    if constexpr (PRO) {
+      const bool ok = tile * 128 + s * 16 + fr < M && lg * 8 < K;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        a[0][e] = ok ? (bf16_t)act_fwd(fmaf((float)a[0][e], psc[e], psh[e]), pro.act) : (bf16_t)0.f;
     }
   };
   // gred: this lane's rows of gr.y for the sub-step starting at row rs (one sub-step ahead)
@@ -826,6 +849,7 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
           if constexpr (GRED) load_y(yn, tn * 128 + (s + 1 < SUB ? s + 1 : 0) * 16);
         }
       }
+      pro_a(ab, t, s);
       // the weight fragments are re-read from LDS every sub-step (kept out of registers)
       asm volatile("" ::: "memory");
       f32x4 acc[NT];
@@ -961,11 +985,12 @@ static int pw_stream_groups(long M, int K, int Cout, int& nt, bool gred = false)
   return 0;
 }
 static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long M, int K, int Cout, int ldx, int ldy,
-                             float* stats, const BnGred* gr, hipStream_t s) {
+                             float* stats, const BnGred* gr, hipStream_t s, const BnPro* pro = nullptr) {
   int nt = 0;
   const int ng = pw_stream_groups(M, K, Cout, nt, gr != nullptr);
   if (ng == 0 || (gr && (stats || ldy != Cout))) return false;
   const int kt = K > 64 ? 3 : K > 32 ? 2 : 1;
+  if (pro && (kt != 1 || gr)) return false;   // the prologue form: K <= 32, no gred epilogue
   const long ntiles = cdivl(M, 128);
   // waves: <= 3 blocks of 4 waves per CU (over all N groups), every wave the same number of
   // tiles (+-1)
@@ -975,6 +1000,17 @@ static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long 
   const BnGred g = gr ? *gr : BnGred{};
 #define PWS(NT_, KT_)                                                                                           \
   do {                                                                                                          \
+    if constexpr (KT_ == 1) {                                                                                   \
+      if (pro) {                                                                                                \
+        if (stats)                                                                                              \
+          hipLaunchKernelGGL((pw_stream_kernel<NT_, 1, 1, true>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout,  \
+                             ldx, ldy, stats, g, *pro);                                                         \
+        else                                                                                                    \
+          hipLaunchKernelGGL((pw_stream_kernel<NT_, 1, 0, true>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout,  \
+                             ldx, ldy, nullptr, g, *pro);                                                       \
+        return true;                                                                                            \
+      }                                                                                                         \
+    }                                                                                                           \
     if (gr)                                                                                                     \
       hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, 2>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, ldy, \
                          nullptr, g);                                                                           \
@@ -1946,8 +1982,11 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
     return;
   }
   if constexpr (sizeof(T) == 2) {
-    if (ksize == 1 && !pro && !bias && va && vb && vy &&
-        pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, gr, s))
+    // the prologue form only for the block-to-block case it serves (K <= 32 input channels of a
+    // project BatchNorm left pending: the 720p expand 16 -> 96)
+    if (ksize == 1 && !bias && va && vb && vy && (!pro || (K <= 32 && Cin <= PRO_MAXC)) &&
+        pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, gr, s,
+                         pro ? &pv : nullptr))
       return;
   }
   if (ksize == 1) {

@@ -109,7 +109,13 @@ class MobilenetV2:
         # backward runs the BatchNorm backward with the conv's own (fused for 1x1 where it pays).
         fuse = 'bnpro' not in ops._DISABLE
         keep = (lambda p: p) if fuse else ops.materialize
-        for (idx, kind, s, cin, inner, cout, res, sc) in self.plan:
+        # training with explicit taps (the detector): a project output that is no endpoint, has
+        # no residual and feeds only the next block's expand (itself without a residual: block 1
+        # -> block 2) stays Pending too — the expand applies it in its prologue and its backward
+        # hands that BatchNorm its sums (rod_pw_bwd_gred), so neither the 720p x 16 BatchNorm
+        # output nor its backward reduce crosses HBM
+        chain = fuse and is_training and bool(taps) and 'chainpro' not in ops._DISABLE
+        for i, (idx, kind, s, cin, inner, cout, res, sc) in enumerate(self.plan):
             base = '%s/%s' % (self.scope, sc)
             name = 'layer_%d' % idx
             tapped = name in taps or final_endpoint == name
@@ -133,8 +139,13 @@ class MobilenetV2:
                 x = keep(ops.dw3x3_bn(x, P[base + '/depthwise/depthwise_weights'], s,
                                       *self._bn_args(base + '/depthwise/BatchNorm'), ops.ROD_ACT_RELU6, is_training,
                                       BN_DECAY, BN_EPS))
-                x = ops.materialize(self._conv_bn(x, P[base + '/project/weights'], 1, base + '/project/BatchNorm',
-                                                  ops.ROD_ACT_NONE, is_training), inp)
+                x = self._conv_bn(x, P[base + '/project/weights'], 1, base + '/project/BatchNorm', ops.ROD_ACT_NONE,
+                                  is_training)
+                nxt = self.plan[i + 1] if i + 1 < len(self.plan) else None
+                pend = (chain and not res and not tapped and final_endpoint != name and nxt is not None and
+                        nxt[1] != 'conv' and nxt[4] > nxt[3] and not nxt[6])
+                if not pend:
+                    x = ops.materialize(x, inp)
             last = final_endpoint == name or idx == self.plan[-1][0]
             if name in taps and not last:
                 end_points[name], x = graph.fork(x, 2)

@@ -521,3 +521,18 @@ def test_head_chain_nodes_match_float64(dev, hw, cin):
     print('head chain', hw, cin, ['%d %.2e/%.2e' % r for r in rep])
     for i, e, e32 in rep:
         assert e <= max(1e-4, 4 * e32), rep
+
+
+@pytest.mark.parametrize('act', [ops.ROD_ACT_NONE, ops.ROD_ACT_RELU6])
+def test_pw_stream_prologue(dev, act):
+    """The streaming 1x1 forward with the BatchNorm-apply prologue (pw_stream_kernel PRO: the
+    720p expand 16 -> 96 whose input is block 1's project BatchNorm left pending, no bias,
+    M >= 65536) against writing the BatchNorm out first: forward bit-identical, gradients as the
+    materialised path."""
+    g = torch.Generator().manual_seed(21)
+    w = _param(torch.randn(96, 1, 1, 16, generator=g) / 4.0, dev)
+
+    def consumer(x):
+        w._rod_grad.zero_()
+        return ops.conv2d(x, w, None, 1), (lambda: w._rod_grad)
+    _fused_vs_materialised(dev, torch.bfloat16, (1, 257, 259, 16), act, True, consumer, 22)
