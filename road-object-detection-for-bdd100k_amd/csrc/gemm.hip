@@ -811,9 +811,24 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
   auto pro_a = [&](bf16x8 (&a)[KT], long tile, int s) {
     if constexpr (PRO) {
       const bool ok = tile * 128 + s * 16 + fr < M && lg * 8 < K;
+      if (pro.act == ROD_ACT_NONE) {   // the linear (project) BatchNorm: packed pairs, one rounding each
+        typedef float pf2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 pb2 __attribute__((ext_vector_type(2)));
+        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+        const u32x4v u = __builtin_bit_cast(u32x4v, a[0]);
+        u32x4v o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        a[0][e] = ok ? (bf16_t)act_fwd(fmaf((float)a[0][e], psc[e], psh[e]), pro.act) : (bf16_t)0.f;
+        for (int h = 0; h < 4; ++h) {
+          const pf2 x2 = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
+          const pf2 z2 = __builtin_elementwise_fma(x2, pf2{psc[2 * h], psc[2 * h + 1]}, pf2{psh[2 * h], psh[2 * h + 1]});
+          o[h] = ok ? __builtin_bit_cast(unsigned, __builtin_convertvector(z2, pb2)) : 0u;
+        }
+        a[0] = __builtin_bit_cast(bf16x8, o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          a[0][e] = ok ? (bf16_t)act_fwd(fmaf((float)a[0][e], psc[e], psh[e]), pro.act) : (bf16_t)0.f;
+      }
     }
   };
   // gred: this lane's rows of gr.y for the sub-step starting at row rs (one sub-step ahead)

@@ -291,6 +291,17 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
 // dx is the block kernel's bit for bit (same dy, same MFMA k order); dW sums its rows in another
 // grouping (fp32, within the float64 bounds of tests/test_gpu_pwbwd.py).
 // =====================================================================================
+typedef float pb_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pb_b2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pb_f2 pb_unpack(unsigned u) {   // bf16 pair (low, high) -> fp32 pair
+  return pb_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
+__device__ __forceinline__ unsigned pb_round(pb_f2 v) {    // one v_cvt_pk_bf16_f32 (RNE per element)
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, pb_b2));
+}
+// ReLU6 gradient gate (0 < z < 6; NaN -> closed) as one unsigned compare on the bits
+__device__ __forceinline__ bool pb_relu6_open(float z) { return __builtin_bit_cast(unsigned, z) - 1u < 0x40BFFFFFu; }
+
 template <int CIN, int COUT>
 struct PbsGeo {
   // CW channels per lane chunk: 4 (8-byte loads) where the chunks tile 64 lanes into whole rows
@@ -440,10 +451,25 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
           const bool rok = row0 + h * 16 + xr < M;   // rows past M stay 0 (not act(shift))
           const f32x4 s0 = *(const f32x4*)(xtab + xc * 8), s1 = *(const f32x4*)(xtab + xc * 8 + 4);
           const f32x4 h0 = *(const f32x4*)(xtab + CIN + xc * 8), h1 = *(const f32x4*)(xtab + CIN + xc * 8 + 4);
+          if (a.xact == ROD_ACT_NONE) {   // linear input BatchNorm: packed pairs
+            const u32x4_t u = __builtin_bit_cast(u32x4_t, v);
+            u32x4_t o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = rok ? (bf16_t)act_fwd(fmaf((float)v[e], s0[e], h0[e]), a.xact) : (bf16_t)0.f;
-            v[4 + e] = rok ? (bf16_t)act_fwd(fmaf((float)v[4 + e], s1[e], h1[e]), a.xact) : (bf16_t)0.f;
+            for (int h2 = 0; h2 < 4; ++h2) {
+              const f32x4& sc4 = h2 < 2 ? s0 : s1;
+              const f32x4& sh4 = h2 < 2 ? h0 : h1;
+              const int b = (h2 & 1) * 2;
+              const pb_f2 z2 = __builtin_elementwise_fma(pb_unpack(u[h2]), pb_f2{sc4[b], sc4[b + 1]},
+                                                         pb_f2{sh4[b], sh4[b + 1]});
+              o[h2] = rok ? pb_round(z2) : 0u;
+            }
+            v = __builtin_bit_cast(bf16x8, o);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = rok ? (bf16_t)act_fwd(fmaf((float)v[e], s0[e], h0[e]), a.xact) : (bf16_t)0.f;
+              v[4 + e] = rok ? (bf16_t)act_fwd(fmaf((float)v[4 + e], s1[e], h1[e]), a.xact) : (bf16_t)0.f;
+            }
           }
         }
         xv = buf_ld<bf16x8>(rsrc_rows(a.x, rown, CIN * 2), vx, (unsigned)((1 - h) * 16 * CIN * 2));
@@ -478,12 +504,21 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
         buf_st(ov, rdx, vx, (unsigned)(h * 16 * CIN * 2));
         if constexpr (XG) {
           if (xact && row0 + h * 16 + xr < M) {
+            if (a.xact == ROD_ACT_NONE) {   // linear input BatchNorm (the project's): g = dx
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float xe = (float)xcur[e];
-              const float g = (float)ov[e] * act_grad(fmaf(xe, xtab[xc * 8 + e], xtab[CIN + xc * 8 + e]), a.xact);
-              xsg[e] += g;
-              xsgx[e] = fmaf(g, xe - xtab[2 * CIN + xc * 8 + e], xsgx[e]);
+              for (int e = 0; e < 8; ++e) {
+                const float g = (float)ov[e];
+                xsg[e] += g;
+                xsgx[e] = fmaf(g, (float)xcur[e] - xtab[2 * CIN + xc * 8 + e], xsgx[e]);
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float xe = (float)xcur[e];
+                const float g = (float)ov[e] * act_grad(fmaf(xe, xtab[xc * 8 + e], xtab[CIN + xc * 8 + e]), a.xact);
+                xsg[e] += g;
+                xsgx[e] = fmaf(g, xe - xtab[2 * CIN + xc * 8 + e], xsgx[e]);
+              }
             }
           }
         }
@@ -587,17 +622,6 @@ struct PbgGeo {
     return main > red ? main : red;
   }
 };
-
-typedef float pb_f2 __attribute__((ext_vector_type(2)));
-typedef __bf16 pb_b2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ pb_f2 pb_unpack(unsigned u) {   // bf16 pair (low, high) -> fp32 pair
-  return pb_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
-}
-__device__ __forceinline__ unsigned pb_round(pb_f2 v) {    // one v_cvt_pk_bf16_f32 (RNE per element)
-  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, pb_b2));
-}
-// ReLU6 gradient gate (0 < z < 6; NaN -> closed) as one unsigned compare on the bits
-__device__ __forceinline__ bool pb_relu6_open(float z) { return __builtin_bit_cast(unsigned, z) - 1u < 0x40BFFFFFu; }
 
 // FAST: the block's activations (linear output BatchNorm, ReLU6 input BatchNorm) at compile
 // time, channel pairs as packed fp32 ops; otherwise both activations at run time, per element
