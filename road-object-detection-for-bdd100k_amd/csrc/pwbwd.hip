@@ -330,7 +330,10 @@ template <> struct PbsVec<8> { typedef bf16x8 T; };
 // expand conv of a block whose input is the previous block's project output (linear BatchNorm):
 // that BatchNorm's gradient is this dx, so its rod_bn_bwd_reduce pass is not needed
 // (rod_pw_bwd_gred on the expand shapes); part blockIdx.x of [nblk][2][CIN]
-template <int CIN, int COUT, bool PRO, bool DX, bool XG = false>
+// XL: the input BatchNorm is linear (act NONE; the project output chained into an expand) —
+// its prologue and sums compile without the activation (a runtime branch costs the XG form
+// 12 VGPRs and a wave per SIMD).
+template <int CIN, int COUT, bool PRO, bool DX, bool XG = false, bool XL = false>
 __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
   using G = PbsGeo<CIN, COUT>;
   static_assert(!XG || (PRO && DX), "the input sums need the prologue and dx");
@@ -451,7 +454,7 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
           const bool rok = row0 + h * 16 + xr < M;   // rows past M stay 0 (not act(shift))
           const f32x4 s0 = *(const f32x4*)(xtab + xc * 8), s1 = *(const f32x4*)(xtab + xc * 8 + 4);
           const f32x4 h0 = *(const f32x4*)(xtab + CIN + xc * 8), h1 = *(const f32x4*)(xtab + CIN + xc * 8 + 4);
-          if (a.xact == ROD_ACT_NONE) {   // linear input BatchNorm: packed pairs
+          if constexpr (XL) {   // linear input BatchNorm: packed pairs
             const u32x4_t u = __builtin_bit_cast(u32x4_t, v);
             u32x4_t o;
 #pragma unroll
@@ -504,7 +507,7 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
         buf_st(ov, rdx, vx, (unsigned)(h * 16 * CIN * 2));
         if constexpr (XG) {
           if (xact && row0 + h * 16 + xr < M) {
-            if (a.xact == ROD_ACT_NONE) {   // linear input BatchNorm (the project's): g = dx
+            if constexpr (XL) {   // linear input BatchNorm (the project's): g = dx
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
                 const float g = (float)ov[e];
@@ -1020,13 +1023,18 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
     PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw, nullptr,
                 mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0};
     const long ntiles = cdivl(M, 32);
-#define PBS(CI, CO, PR, DXF)                                                                                 \
+#define PBS1(CI, CO, PR, DXF, XLN)                                                                           \
   do {                                                                                                       \
     const size_t lds = PbsGeo<CI, CO>::lds();                                                                \
-    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, PR, DXF>,                            \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, PR, DXF, false, XLN>,                \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
-    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, PR, DXF>), dim3(nblk), dim3(256), lds, s, a, ntiles,     \
-                       nullptr);                                                                             \
+    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, PR, DXF, false, XLN>), dim3(nblk), dim3(256), lds, s, a, \
+                       ntiles, nullptr);                                                                     \
+  } while (0)
+#define PBS(CI, CO, PR, DXF)                                      \
+  do {                                                            \
+    if (PR && xact == ROD_ACT_NONE) PBS1(CI, CO, PR, DXF, true);  \
+    else PBS1(CI, CO, PR, DXF, false);                            \
   } while (0)
 #define PBS2(CI, CO)                                        \
   if (Cin == CI) {                                          \
@@ -1039,6 +1047,7 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
     PBS2(16, 96) else PBS2(24, 144)
 #undef PBS2
 #undef PBS
+#undef PBS1
     slab_sum(partw, dw, nblk, (long)Cout * Cin, s);
     return check_launch("rod_pw_bwd");
   }
@@ -1109,16 +1118,22 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
                 nullptr, mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0,
                 0, 0};
     const long nt = cdivl(M, 32);
-#define PBX(CI, CO)                                                                                       \
-  if (Cin == CI) {                                                                                        \
+#define PBX1(CI, CO, XLN)                                                                                 \
+  do {                                                                                                    \
     const size_t lds = PbsGeo<CI, CO>::lds();                                                             \
-    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, true, true, true>,                \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, true, true, true, XLN>,           \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                      \
-    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, true, true, true>), dim3(nb), dim3(256), lds, s, a, nt, \
-                       xparts);                                                                           \
+    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, true, true, true, XLN>), dim3(nb), dim3(256), lds, s, a, \
+                       nt, xparts);                                                                       \
+  } while (0)
+#define PBX(CI, CO)                                          \
+  if (Cin == CI) {                                           \
+    if (xact == ROD_ACT_NONE) PBX1(CI, CO, true);            \
+    else PBX1(CI, CO, false);                                \
   }
     PBX(16, 96)
 #undef PBX
+#undef PBX1
     slab_sum(partw, dw, nb, (long)Cout * Cin, s);
     return check_launch("rod_pw_bwd_gred");
   }

@@ -536,3 +536,53 @@ def test_pw_stream_prologue(dev, act):
         w._rod_grad.zero_()
         return ops.conv2d(x, w, None, 1), (lambda: w._rod_grad)
     _fused_vs_materialised(dev, torch.bfloat16, (1, 257, 259, 16), act, True, consumer, 22)
+
+
+@pytest.mark.parametrize('nparts,C', [(1, 16), (700, 16), (5000, 16), (57600, 16), (3000, 96), (900, 200), (40000, 1280)])
+def test_bn_finalize_one_launch_merge(dev, nparts, C):
+    """rod_bn_finalize over a producer's partial statistics (count, mean, M2 per part) in one
+    launch — several slices merged by the last block of each channel group — against a float64
+    Chan merge, incl. empty parts; a second call on the same parts is bit-identical (the slice
+    counters are back at 0), and so are calls inside a replayed graph."""
+    from rod import _abi
+    from rod.ops import workspace, stream
+    g = torch.Generator().manual_seed(nparts + C)
+    cnt = torch.randint(1, 129, (nparts, 1, C), generator=g).double()
+    cnt[3::7] = 0.
+    mu = torch.randn(nparts, 1, C, generator=g).double() * 0.5 + 3.0
+    m2 = torch.rand(nparts, 1, C, generator=g).double() * cnt
+    mu[cnt == 0] = 0.
+    parts = torch.cat([cnt, mu, m2], 1).float()
+    cd, md, qd = (t.double() for t in parts.unbind(1))
+    N = cd.sum(0)
+    mean = (cd * md).sum(0) / N
+    M2 = (qd + cd * (md - mean) ** 2).sum(0)
+    M = int(N.max())   # the call's M only scales the variance; use one M for every channel
+    var = M2 / M
+    pd = parts.to(dev)
+    nb = _abi.query("rod_bn_finalize_workspace", nparts, C)
+    ws = workspace(nb, dev) if nb else None
+
+    def run():
+        mo, ro = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        mm, mv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        _abi.call("rod_bn_finalize", pd, nparts, M, C, 1e-3, 0.9, mo, ro, mm, mv, ws, stream())
+        return mo, ro, mm, mv
+
+    a = run()
+    torch.testing.assert_close(a[0].double().cpu(), mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(a[1].double().cpu(), 1.0 / torch.sqrt(var.float().double() + 1e-3), rtol=1e-5, atol=1e-6)
+    for _ in range(20):   # a slice part read before it is visible would show as a changed bit
+        b = run()
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)
+    gr = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.cuda.graph(gr, stream=s):
+        c = run()
+    for _ in range(3):
+        gr.replay()
+        torch.cuda.synchronize()
+        for u, v in zip(a, c):
+            assert torch.equal(u, v)
