@@ -15,6 +15,8 @@ selected over the global batch (counts + radix histograms all-reduced, ops.hnm_l
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 
@@ -167,6 +169,12 @@ class Trainer:
             self.net.store.build_prep_tables()   # host -> device set-up stays outside the capture
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
+            if self._nccl():
+                # RCCL's watchdog thread polls the end events of the eager collectives until it has
+                # seen them complete (every ~100 ms); polled while the RCCL stream is joined into
+                # this capture, such an event fails the query and the watchdog aborts the process.
+                # The collectives are complete here: give the watchdog time to retire them.
+                time.sleep(0.5)
             st = self.net.store
             gstep, eager, version = self.opt.global_step, self._eager_steps, st.version
             if getattr(self, '_pool', None) is None:

@@ -162,6 +162,9 @@ def main(argv=None):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         torch.cuda.set_device(local)
+        # the step is captured with its RCCL collectives (Trainer.step_graphed): no event of an eager
+        # collective may be recycled into the capture while the watchdog still polls it
+        os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
         torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     from rod.dataio import make_source
