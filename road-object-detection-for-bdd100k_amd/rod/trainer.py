@@ -133,7 +133,9 @@ class Trainer:
         hnm = self.train_range is not config.train_range.REFINE and net_tools.HNM_EXCHANGE is not None
         if self.graph_dp:
             # the hard-negative exchange's blocking all-reduces inside a capture raced RCCL's
-            # watchdog (hipErrorCapturedEvent on a 1-rank group, round 4): ALL mode stays eager
+            # watchdog (hipErrorCapturedEvent on a 1-rank group, round 4; the same query error the
+            # retirement wait before capture in step_graphed now avoids for the eager collectives,
+            # not re-measured for this case): ALL mode stays eager
             return 'full' if self._nccl() and not hnm else 'eager'
         mid = self.sync_bn or hnm
         return 'eager' if mid or not hasattr(self.reducer, 'defer') else 'split'
