@@ -539,11 +539,11 @@ def test_pw_stream_prologue(dev, act):
 
 
 @pytest.mark.parametrize('nparts,C', [(1, 16), (700, 16), (5000, 16), (57600, 16), (3000, 96), (900, 200), (40000, 1280)])
-def test_bn_finalize_one_launch_merge(dev, nparts, C):
-    """rod_bn_finalize over a producer's partial statistics (count, mean, M2 per part) in one
-    launch — several slices merged by the last block of each channel group — against a float64
-    Chan merge, incl. empty parts; a second call on the same parts is bit-identical (the slice
-    counters are back at 0), and so are calls inside a replayed graph."""
+def test_bn_finalize_many_parts(dev, nparts, C):
+    """rod_bn_finalize over a producer's partial statistics (count, mean, M2 per part; one to
+    57,600 parts, so one to three merge levels) against a float64 Chan merge, incl. empty parts;
+    repeated calls on the same parts are bit-identical, and so are calls inside a replayed
+    graph."""
     from rod import _abi
     from rod.ops import workspace, stream
     g = torch.Generator().manual_seed(nparts + C)
@@ -572,7 +572,7 @@ def test_bn_finalize_one_launch_merge(dev, nparts, C):
     a = run()
     torch.testing.assert_close(a[0].double().cpu(), mean, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(a[1].double().cpu(), 1.0 / torch.sqrt(var.float().double() + 1e-3), rtol=1e-5, atol=1e-6)
-    for _ in range(20):   # a slice part read before it is visible would show as a changed bit
+    for _ in range(20):
         b = run()
         for u, v in zip(a, b):
             assert torch.equal(u, v)
