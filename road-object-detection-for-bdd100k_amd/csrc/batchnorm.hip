@@ -527,19 +527,19 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   const long stride = (long)gridDim.x * blockDim.x;
   const int c = (int)(t0 % CV) * V;
   const long rstep = stride / CV;
-  float sc[V], sh[V], a[V], k1[V], k0[V];
+  float sc[V], sh[V], a[V], k1[V], k0[V], km[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     bn_affine(mean, rstd, gamma, beta, c + v, sc[v], sh[v]);
     a[v] = coef[c + v];
-    bn_bwd_k(a[v], mean[c + v], rstd[c + v], coef[C + c + v], coef[2 * C + c + v], k1[v], k0[v]);
+    bn_bwd_k<T>(a[v], mean[c + v], rstd[c + v], coef[C + c + v], coef[2 * C + c + v], k1[v], k0[v], km[v]);
   }
   auto row = [&](float (&xv)[V], const float (&gv)[V]) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float z = fmaf(xv[v], sc[v], sh[v]);
       const float g = gv[v] * act_grad(z, act);
-      xv[v] = bn_bwd_apply1(a[v], g, k1[v], k0[v], xv[v]);
+      xv[v] = bn_bwd_apply1<T>(a[v], g, k1[v], k0[v], km[v], xv[v]);
     }
   };
   long r = t0 / CV;
@@ -688,17 +688,17 @@ __global__ void __launch_bounds__(SMALL_T) bn_bwd_small_kernel(const T* __restri
   if (dx == nullptr) return;
   __syncthreads();
   if (!active) return;
-  float a[V], k1[V], k0[V];
+  float a[V], k1[V], k0[V], km[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     a[v] = cf[0][cvl * V + v];
-    bn_bwd_k(a[v], mu[v], rs[v], cf[1][cvl * V + v], cf[2][cvl * V + v], k1[v], k0[v]);
+    bn_bwd_k<T>(a[v], mu[v], rs[v], cf[1][cvl * V + v], cf[2][cvl * V + v], k1[v], k0[v], km[v]);
   }
   auto row = [&](float (&xv)[V], const float (&gv)[V]) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float g = gv[v] * act_grad(fmaf(xv[v], sc[v], sh[v]), act);
-      xv[v] = bn_bwd_apply1(a[v], g, k1[v], k0[v], xv[v]);
+      xv[v] = bn_bwd_apply1<T>(a[v], g, k1[v], k0[v], km[v], xv[v]);
     }
   };
   long r = pln;

@@ -795,7 +795,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
   // GP: per-channel constants of the BatchNorm-backward apply, and the raw (dz, y) loads of
   // the rows still in flight (their apply runs when they enter the contraction queue)
   constexpr int GV = GP ? V : 1;
-  float gsc[GV], gsh[GV], ga[GV], gmg[GV], gmx[GV];
+  float gsc[GV], gsh[GV], ga[GV], gmg[GV], gmx[GV], gmm[GV];
   const T* yn = nullptr;
   T* dyo = nullptr;
   if constexpr (GP) {
@@ -803,7 +803,8 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
     for (int v = 0; v < V; ++v) {
       bn_affine(gd.mean, gd.rstd, gd.gamma, gd.beta, c + v, gsc[v], gsh[v]);
       ga[v] = gd.coef[c + v];
-      bn_bwd_k(ga[v], gd.mean[c + v], gd.rstd[c + v], gd.coef[C + c + v], gd.coef[2 * C + c + v], gmg[v], gmx[v]);
+      bn_bwd_k<T>(ga[v], gd.mean[c + v], gd.rstd[c + v], gd.coef[C + c + v], gd.coef[2 * C + c + v], gmg[v], gmx[v],
+                  gmm[v]);
     }
     yn = (const T*)gd.y + (long)n * Ho * Wo * C + c;
     dyo = (T*)gd.dy + (long)n * Ho * Wo * C + c;
@@ -823,7 +824,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwdw_lx_kernel(const T* __restrict_
         const float xv = yv.get(v);
         const float z = fmaf(xv, gsc[v], gsh[v]);
         const float g = d.get(v) * act_grad(z, gd.act);
-        d.set(v, bn_bwd_apply1(ga[v], g, gmg[v], gmx[v], xv));   // gmg / gmx hold k1 / k0
+        d.set(v, bn_bwd_apply1<T>(ga[v], g, gmg[v], gmx[v], gmm[v], xv));   // gmg / gmx hold k1 / k0
       }
       d.store(dyo + ((long)(ho0 + m) * Wo + wo) * C);
     } else {
@@ -1801,12 +1802,13 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
     for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
   DwIn<T, V, PACT> in;
   in.init(pro, c);
-  float dsc[V], dsh[V], da[V], dmg[V], dmx[V];   // dmg / dmx: the apply's k1 / k0
+  float dsc[V], dsh[V], da[V], dmg[V], dmx[V], dmm[V];   // dmg / dmx / dmm: the apply's k1 / k0 / m
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c + v, dsc[v], dsh[v]);
     da[v] = bd.coef[c + v];
-    bn_bwd_k(da[v], bd.mean[c + v], bd.rstd[c + v], bd.coef[C + c + v], bd.coef[2 * C + c + v], dmg[v], dmx[v]);
+    bn_bwd_k<T>(da[v], bd.mean[c + v], bd.rstd[c + v], bd.coef[C + c + v], bd.coef[2 * C + c + v], dmg[v], dmx[v],
+                dmm[v]);
   }
   constexpr int RV = RED ? V : 1;
   float emu[RV], ers[RV], sg[RV], sgx[RV];
@@ -1876,7 +1878,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
         const float yv = ry[k].get(v);
         const float z = fmaf(yv, dsc[v], dsh[v]);
         const float g = rz[k].get(v) * act_grad(z, bd.act);
-        const float o = bn_bwd_apply1(da[v], g, dmg[v], dmx[v], yv);
+        const float o = bn_bwd_apply1<T>(da[v], g, dmg[v], dmx[v], dmm[v], yv);
         dv[v] = okd[k] ? to_f32(from_f32<T>(o)) : 0.f;
       }
       PK px, pd;
@@ -2076,20 +2078,21 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
       }
     }
   }
-  dw_f2 dsc[VP], dsh[VP], da[VP], dmg[VP], dmx[VP];
+  dw_f2 dsc[VP], dsh[VP], da[VP], dmg[VP], dmx[VP], dmm[VP];
 #pragma unroll
   for (int h = 0; h < VP; ++h) {
     const int c0 = c + 2 * h;
-    float s0, t0, s1, t1, k10, k00, k11, k01;
+    float s0, t0, s1, t1, k10, k00, k11, k01, m0, m1;
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0, s0, t0);
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c0 + 1, s1, t1);
     dsc[h] = dw_f2{s0, s1};
     dsh[h] = dw_f2{t0, t1};
     da[h] = dw_f2{bd.coef[c0], bd.coef[c0 + 1]};
-    bn_bwd_k(da[h].x, bd.mean[c0], bd.rstd[c0], bd.coef[C + c0], bd.coef[2 * C + c0], k10, k00);
-    bn_bwd_k(da[h].y, bd.mean[c0 + 1], bd.rstd[c0 + 1], bd.coef[C + c0 + 1], bd.coef[2 * C + c0 + 1], k11, k01);
-    dmg[h] = dw_f2{k10, k11};   // the apply's k1 / k0 (bn_bwd_k)
+    bn_bwd_k<T>(da[h].x, bd.mean[c0], bd.rstd[c0], bd.coef[C + c0], bd.coef[2 * C + c0], k10, k00, m0);
+    bn_bwd_k<T>(da[h].y, bd.mean[c0 + 1], bd.rstd[c0 + 1], bd.coef[C + c0 + 1], bd.coef[2 * C + c0 + 1], k11, k01, m1);
+    dmg[h] = dw_f2{k10, k11};   // the apply's k1 / k0 / centring shift (bn_bwd_k)
     dmx[h] = dw_f2{k00, k01};
+    dmm[h] = dw_f2{m0, m1};
   }
   dw_f2 sg[VP], sgx[VP];
 #pragma unroll
@@ -2175,7 +2178,9 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
         for (int h = 0; h < VP; ++h) {
           const dw_f2 z = f2fma(yv[h], dsc[h], dsh[h]);
           const dw_f2 g = gate2<BACT>(z, zv[h], bd.act);
-          const dw_f2 o = f2fma(da[h], g, f2fma(dmg[h], yv[h], dmx[h]));   // bn_bwd_apply1, pairwise
+          // bn_bwd_apply1<T>, pairwise
+          const dw_f2 yc = sizeof(T) == 4 ? yv[h] - dmm[h] : yv[h];
+          const dw_f2 o = f2fma(da[h], g, f2fma(dmg[h], yc, dmx[h]));
           dv[h] = dok ? round2(o, T{}) : dw_f2{0.f, 0.f};
         }
       }
@@ -2333,12 +2338,13 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
     for (int v = 0; v < V; ++v) wr[k][v] = w[k * C + c + v];
   DwIn<T, V, PACT> in;
   in.init(pro, c);
-  float dsc[V], dsh[V], da[V], dmg[V], dmx[V];   // dmg / dmx: the apply's k1 / k0
+  float dsc[V], dsh[V], da[V], dmg[V], dmx[V], dmm[V];   // dmg / dmx / dmm: the apply's k1 / k0 / m
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     bn_affine(bd.mean, bd.rstd, bd.gamma, bd.beta, c + v, dsc[v], dsh[v]);
     da[v] = bd.coef[c + v];
-    bn_bwd_k(da[v], bd.mean[c + v], bd.rstd[c + v], bd.coef[C + c + v], bd.coef[2 * C + c + v], dmg[v], dmx[v]);
+    bn_bwd_k<T>(da[v], bd.mean[c + v], bd.rstd[c + v], bd.coef[C + c + v], bd.coef[2 * C + c + v], dmg[v], dmx[v],
+                dmm[v]);
   }
   constexpr int RV = RED ? V : 1;
   float enb[RV], ers[RV], sg[RV], sgx[RV];  // xhat_e = fma(y_e, rstd, -mean * rstd)
@@ -2411,7 +2417,7 @@ __global__ void __launch_bounds__(256, 2) dw3x3_bwd_fused_s2_kernel(const T* __r
         const float yv = ry[k].get(v);
         const float z = fmaf(yv, dsc[v], dsh[v]);
         const float g = rz[k].get(v) * act_grad(z, bd.act);
-        const float o = bn_bwd_apply1(da[v], g, dmg[v], dmx[v], yv);
+        const float o = bn_bwd_apply1<T>(da[v], g, dmg[v], dmx[v], dmm[v], yv);
         dv[v] = okd[k] ? to_f32(from_f32<T>(o)) : 0.f;
       }
       float xv[4][V], yr[4][V];
@@ -2595,8 +2601,10 @@ __global__ void __launch_bounds__(1024 / V, V == 4 ? 2 : 1) dw3x3_bwd_fused_s2p_
     dsc[h] = dw_f2{s0, s1};
     dsh[h] = dw_f2{t0, t1};
     da[h] = dw_f2{bd.coef[c0], bd.coef[c0 + 1]};
-    bn_bwd_k(da[h].x, bd.mean[c0], bd.rstd[c0], bd.coef[C + c0], bd.coef[2 * C + c0], k10, k00);
-    bn_bwd_k(da[h].y, bd.mean[c0 + 1], bd.rstd[c0 + 1], bd.coef[C + c0 + 1], bd.coef[2 * C + c0 + 1], k11, k01);
+    float m0, m1;   // bf16 storage: the folded form (m unused)
+    bn_bwd_k<bf16_t>(da[h].x, bd.mean[c0], bd.rstd[c0], bd.coef[C + c0], bd.coef[2 * C + c0], k10, k00, m0);
+    bn_bwd_k<bf16_t>(da[h].y, bd.mean[c0 + 1], bd.rstd[c0 + 1], bd.coef[C + c0 + 1], bd.coef[2 * C + c0 + 1], k11, k01,
+                     m1);
     dk1[h] = dw_f2{k10, k11};
     dk0[h] = dw_f2{k00, k01};
   }

@@ -1584,7 +1584,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const bf16_t* __restric
       const int c = ck * 8 + e;
       bn_affine(bb.mean, bb.rstd, bb.gamma, bb.beta, c, sc[e], sh[e]);
       ca[e] = bb.coef[c];
-      bn_bwd_k(ca[e], bb.mean[c], bb.rstd[c], bb.coef[32 + c], bb.coef[64 + c], k1[e], k0[e]);
+      bn_bwd_k_fold(ca[e], bb.mean[c], bb.rstd[c], bb.coef[32 + c], bb.coef[64 + c], k1[e], k0[e]);
     }
     ghi = bb.act == ROD_ACT_RELU6 ? 6.f : INFINITY;
     glo = bb.act == ROD_ACT_LEAKY ? 0.2f : bb.act == ROD_ACT_NONE ? 1.f : 0.f;
@@ -1596,7 +1596,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const bf16_t* __restric
       const float yj = (float)yv[e];
       const float z = fmaf(yj, sc[e], sh[e]);
       const float gj = (float)dzv[e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
-      o[e] = (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj);
+      o[e] = (bf16_t)bn_bwd_apply1<bf16_t>(ca[e], gj, k1[e], k0[e], 0.f, yj);
     }
     return o;
   };

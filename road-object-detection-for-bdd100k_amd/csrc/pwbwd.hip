@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
     t[2 * Cout] = sc;
     t[3 * Cout] = sh;
     t[4 * Cout] = a.coef[c];
-    bn_bwd_k(a.coef[c], a.mean[c], a.rstd[c], a.coef[Cout + c], a.coef[2 * Cout + c], t[5 * Cout], t[6 * Cout]);
+    bn_bwd_k_fold(a.coef[c], a.mean[c], a.rstd[c], a.coef[Cout + c], a.coef[2 * Cout + c], t[5 * Cout], t[6 * Cout]);
     t[7 * Cout] = 0.f;
   }
   if (prox) {
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) pw_bwd_kernel(PwBwdArgs a) {
               const float yj = (float)yv[u][j];
               const float z = fmaf(yj, f[2][jj], f[3][jj]);
               const float gj = (float)dv[u][j] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
-              o[j] = (bf16_t)bn_bwd_apply1(f[4][jj], gj, f[5][jj], f[6][jj], yj);   // fields 5, 6: k1, k0
+              o[j] = (bf16_t)bn_bwd_apply1<bf16_t>(f[4][jj], gj, f[5][jj], f[6][jj], 0.f, yj);   // fields 5, 6: k1, k0
             }
           }
         } else {
@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
     const int c = c0 + e;
     bn_affine(a.mean, a.rstd, a.gamma, a.beta, c, sc[e], sh[e]);
     ca[e] = a.coef[c];
-    bn_bwd_k(ca[e], a.mean[c], a.rstd[c], a.coef[COUT + c], a.coef[2 * COUT + c], k1[e], k0[e]);
+    bn_bwd_k_fold(ca[e], a.mean[c], a.rstd[c], a.coef[COUT + c], a.coef[2 * COUT + c], k1[e], k0[e]);
   }
   const float ghi = a.act == ROD_ACT_RELU6 ? 6.f : INFINITY;
   const float glo = a.act == ROD_ACT_LEAKY ? 0.2f : a.act == ROD_ACT_NONE ? 1.f : 0.f;
@@ -441,7 +441,7 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
           const float yj = (float)yv[j][e];
           const float z = fmaf(yj, sc[e], sh[e]);
           const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
-          o[e] = (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj);
+          o[e] = (bf16_t)bn_bwd_apply1<bf16_t>(ca[e], gj, k1[e], k0[e], 0.f, yj);
         }
         dzv[j] = buf_ld<VT>(ndz, vdj(j), nso);
         yv[j] = buf_ld<VT>(ny, vdj(j), nso);
@@ -665,7 +665,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
     const int c = (dact ? cc * 4 : 0) + e;
     bn_affine(a.mean, a.rstd, a.gamma, a.beta, c, sc[e], sh[e]);
     ca[e] = a.coef[c];
-    bn_bwd_k(ca[e], a.mean[c], a.rstd[c], a.coef[COUT + c], a.coef[2 * COUT + c], k1[e], k0[e]);
+    bn_bwd_k_fold(ca[e], a.mean[c], a.rstd[c], a.coef[COUT + c], a.coef[2 * COUT + c], k1[e], k0[e]);
   }
   const float ghi = a.act == ROD_ACT_RELU6 ? 6.f : INFINITY;
   const float glo = a.act == ROD_ACT_LEAKY ? 0.2f : a.act == ROD_ACT_NONE ? 1.f : 0.f;
@@ -776,7 +776,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
               const float yj = (float)yv[j][e];
               const float z = fmaf(yj, sc[e], sh[e]);
               const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
-              o[e] = rok ? (bf16_t)bn_bwd_apply1(ca[e], gj, k1[e], k0[e], yj) : (bf16_t)0.f;
+              o[e] = rok ? (bf16_t)bn_bwd_apply1<bf16_t>(ca[e], gj, k1[e], k0[e], 0.f, yj) : (bf16_t)0.f;
             }
           }
           dzv[j] = buf_ld<bf16x4>(ndz, vdj(j), nso);

@@ -186,15 +186,37 @@ __device__ __forceinline__ void bn_affine(const float* mean, const float* rstd, 
 // TF's FusedBatchNormGrad: dy = a*(g - mean(g) - yhat*mean(g*yhat)), yhat = (y - mean)*rstd,
 // with coef = (a, mean(g), mean(g*yhat)) per channel (rod_bn_bwd_finalize).  Every librod kernel
 // that applies it (rod_bn_bwd_apply, the one-launch small-tensor form, the fused depthwise and
-// 1x1 backwards) evaluates it as  fma(a, g, fma(k1, y, k0))  with the per-channel constants
-// below — two FMAs per element instead of five operations — so all of them round identically.
-__device__ __forceinline__ void bn_bwd_k(float a, float mu, float rs, float mg, float mgx, float& k1, float& k0) {
+// 1x1 backwards) evaluates it with the per-channel constants below, so all of them round
+// identically for a given storage type T:
+//   * bf16 storage:  fma(a, g, fma(k1, y, k0)), the mean folded into k0 (two FMAs per element).
+//     Folding costs ~|mean|/std * 2^-24 relative in k0; the bf16 input y itself carries
+//     |y| * 2^-9 ~ |mean| * 2^-9 of quantisation, 2^15 times more, so the fold is invisible;
+//   * fp32 storage:  fma(a, g, fma(k1, y - mean, k0')), k0' = -a*mean(g) — y is centred first,
+//     as FusedBatchNormGrad does ((y - mean) is exact near the mean), so a channel with
+//     |mean| >> std keeps full fp32 precision (tests/test_gpu_bnred.py, mean 50 / rstd 100).
+// `m` is the centring shift: the mean for fp32, unused (0) for bf16.
+template <typename T>
+__device__ __forceinline__ void bn_bwd_k(float a, float mu, float rs, float mg, float mgx, float& k1, float& k0,
+                                         float& m) {
   const float t = rs * mgx;
   k1 = -(a * t);
-  k0 = a * fmaf(t, mu, -mg);
+  if constexpr (sizeof(T) == 4) {
+    k0 = -(a * mg);
+    m = mu;
+  } else {
+    k0 = a * fmaf(t, mu, -mg);
+    m = 0.f;
+  }
 }
-__device__ __forceinline__ float bn_bwd_apply1(float a, float g, float k1, float k0, float y) {
-  return fmaf(a, g, fmaf(k1, y, k0));
+// bf16-only kernels (1x1 backwards, the stem weight gradient): the folded constants
+__device__ __forceinline__ void bn_bwd_k_fold(float a, float mu, float rs, float mg, float mgx, float& k1, float& k0) {
+  float m;
+  bn_bwd_k<bf16_t>(a, mu, rs, mg, mgx, k1, k0, m);
+}
+template <typename T>
+__device__ __forceinline__ float bn_bwd_apply1(float a, float g, float k1, float k0, float m, float y) {
+  if constexpr (sizeof(T) == 4) return fmaf(a, g, fmaf(k1, y - m, k0));
+  else return fmaf(a, g, fmaf(k1, y, k0));
 }
 
 // ---- BatchNorm-apply prologue -----------------------------------------------------

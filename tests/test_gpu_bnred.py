@@ -53,3 +53,39 @@ def test_bn_bwd_reduce_large(dev, M, C, act):
     assert nerr(coef[:C], (rstd * gamma).double()) < 1e-7
     assert nerr(coef[C:2 * C], db_ref / M) < 1e-5
     assert nerr(coef[2 * C:], dg_ref / M) < 1e-5
+
+
+@pytest.mark.parametrize('M,C', [(65_536, 64), (4096, 256)])
+def test_bn_bwd_fp32_large_mean_vs_float64(dev, M, C):
+    """fp32 BatchNorm backward on a channel whose |mean| is 5000x its std (mean 50, rstd 100):
+    the apply centres y before scaling (rod_common.h bn_bwd_k<float>), as FusedBatchNormGrad does,
+    so dx keeps fp32 precision; folding the mean into the constant (the bf16 form) would lose
+    ~log2(5000) bits here (~3e-4 relative).  dz is correlated with yhat so that the
+    mean(g * yhat) term — the one the fold degrades — carries weight.  (4096, 256) takes the
+    one-launch small-tensor kernel, (65536, 64) reduce -> finalize -> apply."""
+    g = torch.Generator(device=dev).manual_seed(M + C)
+    mean = 50.0 + torch.rand(C, device=dev, generator=g)
+    rstd = 100.0 * (torch.rand(C, device=dev, generator=g) + 0.5)
+    xh = torch.randn(M, C, device=dev, generator=g)
+    y = (mean + xh / rstd).float()
+    dz = (0.5 * xh + torch.randn(M, C, device=dev, generator=g)).float()
+    gamma = torch.rand(C, device=dev, generator=g) + 0.5
+    beta = torch.randn(C, device=dev, generator=g) * 0.2
+    act = ops.ROD_ACT_NONE
+    dx, dg, db = torch.empty_like(y), torch.empty(C, device=dev), torch.empty(C, device=dev)
+    ws = ops.workspace(_abi.query('rod_bn_bwd_workspace', M, C), dev)
+    _abi.call('rod_bn_bwd', dz, y, mean, rstd, gamma, beta, dx, dg, db, ws, M, C, C, C, C, act, ops.dtcode(y),
+              ops.stream())
+    coef = torch.empty(3 * C, device=dev)
+    _abi.call('rod_bn_bwd_reduce', dz, y, mean, rstd, gamma, beta, None, None, coef, ws, M, C, act, ops.dtcode(y),
+              ops.stream())
+    dx2 = torch.empty_like(y)
+    _abi.call('rod_bn_bwd_apply', dz, y, mean, rstd, gamma, beta, coef, dx2, M, C, act, ops.dtcode(y), ops.stream())
+    torch.cuda.synchronize()
+    yf, gf, mu, rs = y.double(), dz.double(), mean.double(), rstd.double()
+    xhat = (yf - mu) * rs
+    mg, mgx = gf.mean(0), (gf * xhat).mean(0)
+    ref = (rs * gamma.double()) * (gf - mg - xhat * mgx)
+    for out in (dx, dx2):
+        err = float((out.double() - ref).norm() / ref.norm())
+        assert err < 2e-6, err
