@@ -47,15 +47,13 @@ def parse():
                     help='ALL mode: train the backbone and refine heads too (train.py fix_refine=False)')
     ap.add_argument('--graph', dest='graph', action='store_true', default=True,
                     help='replay the training step as a HIP graph (Trainer.step_graphed; bit-identical to the '
-                         'eager step).  N>1 default (\'split\'): forward + backward replay as a graph with no '
-                         'collective inside, then the bucketed RCCL all-reduce and SGD are issued eagerly')
+                         'eager step).  N>1 over RCCL: the whole step, its bucketed all-reduces (on a side stream, '
+                         'overlapping backward) included, through the library\'s communicator (\'full\')')
     ap.add_argument('--no-graph', dest='graph', action='store_false')
-    ap.add_argument('--graph-dp', dest='graph_dp', action='store_true', default=False,
-                    help='N>1 over RCCL: capture the whole step, bucketed all-reduces included (\'full\'; '
-                         'verified bit-identical on a 1-rank group only)')
     ap.add_argument('--dp-leg', dest='dp_leg', action='store_true', default=True,
-                    help='N=1: time the graphed step with a 1-rank RCCL GradReducer (split and full capture) and '
-                         'with SyncBatchNorm against the step without a reducer ("dp_overhead")')
+                    help='N=1: time the graphed step with a 1-rank RCCL reducer (the N>1 default: native, full '
+                         'capture; with SyncBatchNorm; the torch.distributed split form) against the step without a '
+                         'reducer ("dp_overhead")')
     ap.add_argument('--no-dp-leg', dest='dp_leg', action='store_false')
     ap.add_argument('--sync-bn', dest='sync_bn', action='store_true', default=False,
                     help='N>1: BatchNorm statistics over the global batch (rod.ddp.SyncBatchNorm; default per rank)')
@@ -294,49 +292,49 @@ SEED_TF = 4242
 
 def dp_overhead_leg(args, dev, dtype, batch, base_ms, steps=10):
     """The data-parallel machinery's cost on one GPU: the headline step (no reducer) against
-    the same step with a 1-rank RCCL GradReducer (4 MB buckets) in each graph mode —
-    'split' (the N>1 default: forward + backward replayed, all-reduce + SGD eager), 'full'
-    (--graph-dp: the in-backward bucket all-reduces captured too) — and with SyncBatchNorm
-    ('full': its ~280 all-gathers captured; 'eager': issued from the host).  A 1-rank
-    all-reduce moves no data over xGMI: this prices launch, synchronisation and lost overlap,
-    not the link."""
+    the same step with a 1-rank reducer (4 MB buckets):
+      'full'        — the N>1 default over RCCL (rod.ddp.make_reducer): the library's
+                      communicator, the bucket all-reduces captured on their side stream;
+      'sync_bn_full'— the same with SyncBatchNorm (its ~280 rod_allgather calls captured);
+      'torch_split' — a torch.distributed reducer: forward + backward replayed, the all-reduce
+                      (one per contiguous span) and SGD issued after the replay.
+    A 1-rank all-reduce moves no data over xGMI: this prices launch, synchronisation and lost
+    overlap, not the link."""
     import socket
     import torch.distributed as dist
-    import config
-    from rod import ops
-    from rod.ddp import GradReducer
+    from rod import _abi, ops
+    from rod.ddp import GradReducer, make_reducer
     from rod.trainer import Trainer
     from utils import net_tools
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
     port = s.getsockname()[1]
     s.close()
-    os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
     dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1, device_id=dev)
     out = {'baseline_ms_per_step': round(base_ms, 3), 'world': 1, 'bucket_mb': 4.0, 'steps': steps}
     try:
         from rod.data import C2_WEIGHT_SEED
-        for name, kw, graphed in (('split', {}, True), ('full', {'graph_dp': True}, True),
-                                  ('sync_bn_full', {'graph_dp': True, 'sync_bn': True}, True),
-                                  ('sync_bn_eager', {'sync_bn': True}, False)):
+        for name, mk, kw in (('full', lambda: make_reducer(1, 0), {}),
+                             ('sync_bn_full', lambda: make_reducer(1, 0), {'sync_bn': True}),
+                             ('torch_split', lambda: GradReducer(1), {})):
             tr = Trainer((args.height, args.width), args.batch, dtype=dtype, device=dev, world_size=1,
-                         reducer=GradReducer(1), seed=C2_WEIGHT_SEED, **kw)
-            step = tr.step_graphed if graphed else tr.step
+                         reducer=mk(), seed=C2_WEIGHT_SEED, **kw)
             for _ in range(3):
-                step(*batch)
+                tr.step_graphed(*batch)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(steps):
-                step(*batch)
+                tr.step_graphed(*batch)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / steps * 1e3
             out[name] = {'ms_per_step': round(ms, 3), 'overhead_frac': round(ms / base_ms - 1, 4),
-                         'graph_mode': tr.graph_mode() if graphed else 'eager'}
-            del tr, step
+                         'graph_mode': tr.graph_mode(), 'native': bool(tr.reducer.native)}
+            del tr
             torch.cuda.empty_cache()
     finally:
         ops.SYNC_BN = None          # Trainer globals: back to the single-process state
         net_tools.HNM_EXCHANGE = None
+        _abi.call('rod_rccl_destroy')
         dist.destroy_process_group()
     return out
 
@@ -448,9 +446,6 @@ def main():
         local = local % torch.cuda.device_count() if backend != 'nccl' else local
         torch.cuda.set_device(local)
         if backend == 'nccl':
-            # the step is captured with its RCCL collectives (Trainer.step_graphed): no event of an eager
-            # collective may be recycled into the capture while the watchdog still polls it
-            os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
             torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             torch.distributed.init_process_group(backend)
@@ -464,11 +459,13 @@ def main():
     tr_range = config.train_range.REFINE if args.train_range == 'REFINE' else config.train_range.ALL
     reducer = None
     if world > 1:
-        from rod.ddp import GradReducer
-        reducer = GradReducer(world)  # bucketed RCCL all-reduce, launched during backward
+        # bucketed all-reduce launched during backward: over RCCL the library's communicator on a
+        # side stream (the whole step captured, 'full'); gloo (rehearsal): torch.distributed
+        from rod.ddp import make_reducer
+        reducer = make_reducer(world, rank)
     tr = Trainer((args.height, args.width), args.batch, dtype=dtype, train_range=tr_range, device=dev,
                  world_size=world, reducer=reducer, fix_refine=args.fix_refine, sync_bn=args.sync_bn,
-                 seed=C2_WEIGHT_SEED, graph_dp=args.graph_dp)
+                 seed=C2_WEIGHT_SEED)
     # rank 0's batch and the initial weights are the ones tests/test_gpu_fullsize.py pins
     batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=C2_BATCH_SEED + rank)
     source = None
@@ -476,9 +473,9 @@ def main():
         from rod.dataio import AugmentedSource
         source = AugmentedSource(args.batch, (args.height, args.width), dev, dtype, seed=SEED + rank, n_distinct=2)
     next_batch = (lambda: next(source)) if source is not None else (lambda: batch)
-    # Trainer.graph_mode decides what the graph holds: the whole step (N=1, or --graph-dp over
-    # RCCL), forward + backward only ('split', the N>1 default: no collective in the graph, so
-    # the gloo rehearsal replays it too), or nothing (collectives inside the step)
+    # Trainer.graph_mode decides what the graph holds: the whole step (N=1, or N>1 over RCCL
+    # through the library's communicator), forward + backward only ('split': the gloo
+    # rehearsal), or nothing (gloo with collectives inside the step)
     use_graph = args.graph and tr.graph_mode() != 'eager'
     step = tr.step_graphed if use_graph else tr.step
 
@@ -652,6 +649,8 @@ def main():
             out['cpu_baseline'] = cpu_baseline(args.height, args.width)
         print(json.dumps(out), flush=True)
     if world > 1:
+        if getattr(reducer, 'native', False):
+            _abi.call('rod_rccl_destroy')
         torch.distributed.destroy_process_group()
 
 

@@ -28,10 +28,10 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 18
+#define ROD_ABI_VERSION 19
 #define ROD_EINVAL (-1)
 
-enum { ROD_F32 = 0, ROD_BF16 = 1 };
+enum { ROD_F32 = 0, ROD_BF16 = 1, ROD_I32 = 2 /* collectives only (ABI 19) */ };
 /* activation applied after BatchNorm:
  *   NONE  = identity (project conv, conv_blocks.py:294)
  *   RELU6 = tf.nn.relu6 (mobilenet_v2.py:47)
@@ -576,11 +576,21 @@ int rod_slab_flush_range(const void* lo, const void* hi, void* stream);
  * RCCL communicator per process (RCCL bound at run time: the process's already loaded
  * librccl.so.1 is reused).  rod_rccl_unique_id writes the 128-byte id rank 0 creates; the
  * caller distributes it (any rendezvous) and every rank calls rod_rccl_init with it.
- * rod_allreduce_bucket sums `count` elements (ROD_F32 / ROD_BF16) in place over all ranks,
- * ordered on `stream` (capturable into a HIP graph).  rod_rccl_destroy frees the communicator. */
+ * rod_allreduce_bucket sums `count` elements (ROD_F32 / ROD_BF16; ABI 19: ROD_I32) in place
+ * over all ranks, ordered on `stream` (capturable into a HIP graph).  rod_rccl_destroy frees
+ * the communicator.
+ * ABI 19 — every collective a captured data-parallel step holds goes through this
+ * communicator, so no host-side watchdog ever polls a stream while it is being captured:
+ * the gradient buckets (rod_allreduce_bucket on a side stream, overlapping backward), the
+ * hard-negative counts / radix histograms (ROD_I32 sums; ref net_tools.py:557-587 selects
+ * over the whole batch) and SyncBatchNorm's partial statistics: rod_allgather concatenates
+ * every rank's `count` elements of `send` into `recv` ([world][count], rank order).
+ * rod_rccl_world returns the communicator's rank count (0: none). */
 int rod_rccl_unique_id(void* uid128);
 int rod_rccl_init(int rank, int world, const void* uid128);
 int rod_allreduce_bucket(void* ptr, long count, int dtype, void* stream);
+int rod_allgather(const void* send, void* recv, long count, int dtype, void* stream);
+int rod_rccl_world(void);
 int rod_rccl_destroy(void);
 
 #ifdef __cplusplus

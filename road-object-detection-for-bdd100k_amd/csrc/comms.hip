@@ -28,6 +28,7 @@ void* g_lib = nullptr;
 int (*g_get_uid)(Uid*) = nullptr;
 InitRankFn g_init_rank = nullptr;
 int (*g_allreduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+int (*g_allgather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
 int (*g_destroy)(void*) = nullptr;
 const char* (*g_errstr)(int) = nullptr;
 void* g_comm = nullptr;
@@ -45,14 +46,21 @@ bool bind() {
   g_get_uid = (int (*)(Uid*))dlsym(h, "ncclGetUniqueId");
   g_init_rank = (InitRankFn)dlsym(h, "ncclCommInitRank");
   g_allreduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclAllReduce");
+  g_allgather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(h, "ncclAllGather");
   g_destroy = (int (*)(void*))dlsym(h, "ncclCommDestroy");
   g_errstr = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
-  if (!g_get_uid || !g_init_rank || !g_allreduce || !g_destroy) {
+  if (!g_get_uid || !g_init_rank || !g_allreduce || !g_allgather || !g_destroy) {
     ::rod::set_error("rod_rccl: librccl.so.1 lacks the nccl* entry points");
     return false;
   }
   g_lib = h;
   return true;
+}
+
+// ncclDataType_t of a librod dtype code (-1: not a collective type)
+int nccl_type(int dtype) {
+  return dtype == ROD_F32 ? 7 /* ncclFloat32 */ : dtype == ROD_BF16 ? 9 /* ncclBfloat16 */
+                                                  : dtype == ROD_I32 ? 2 /* ncclInt32 */ : -1;
 }
 
 int fail(const char* what, int rc) {
@@ -94,12 +102,28 @@ int rod_rccl_init(int rank, int world, const void* uid) {
 int rod_allreduce_bucket(void* ptr, long count, int dtype, void* stream) {
   ROD_CHECK_ARG(g_comm, "rod_allreduce_bucket: no communicator (rod_rccl_init)");
   ROD_CHECK_ARG(ptr && count >= 0, "rod_allreduce_bucket: bad buffer");
-  ROD_CHECK_ARG(dtype == ROD_F32 || dtype == ROD_BF16, "rod_allreduce_bucket: bad dtype %d", dtype);
+  const int nt = nccl_type(dtype);
+  ROD_CHECK_ARG(nt >= 0, "rod_allreduce_bucket: bad dtype %d", dtype);
   if (count == 0) return 0;
-  const int nt = dtype == ROD_F32 ? 7 /* ncclFloat32 */ : 9 /* ncclBfloat16 */;
   const int rc = g_allreduce(ptr, ptr, (size_t)count, nt, 0 /* ncclSum */, g_comm, ROD_STREAM(stream));
   if (rc) return fail("rod_allreduce_bucket", rc);
   return 0;
+}
+
+int rod_allgather(const void* send, void* recv, long count, int dtype, void* stream) {
+  ROD_CHECK_ARG(g_comm, "rod_allgather: no communicator (rod_rccl_init)");
+  ROD_CHECK_ARG(send && recv && count >= 0, "rod_allgather: bad buffer");
+  const int nt = nccl_type(dtype);
+  ROD_CHECK_ARG(nt >= 0, "rod_allgather: bad dtype %d", dtype);
+  if (count == 0) return 0;
+  const int rc = g_allgather(send, recv, (size_t)count, nt, g_comm, ROD_STREAM(stream));
+  if (rc) return fail("rod_allgather", rc);
+  return 0;
+}
+
+int rod_rccl_world(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_comm ? g_world : 0;
 }
 
 int rod_rccl_destroy(void) {

@@ -4,12 +4,22 @@ The flat gradient buffer of rod.params.ParamStore is cut into contiguous buckets
 ~`bucket_mb` MB aligned to parameter boundaries.  Every rod.ops kernel that writes a
 parameter gradient calls the parameter's `_rod_on_grad` hook; when the last trainable
 parameter of a bucket has been written, that bucket's all-reduce (sum) is issued
-immediately with async_op=True.  RCCL runs it on its own stream, ordered after the
-kernels already enqueued on the compute stream, so the reduction of the head / late
-backbone buckets overlaps the early-backbone (depthwise) backward that is still running.
-`__call__` (after backward) issues any bucket not yet launched and makes the compute
-stream wait for all of them before the SGD update — clipping happens after the sum
-(net_tools.py:649).  Works with any torch.distributed backend (gloo in CPU tests).
+immediately, on a communication stream that waits (event) for the compute stream's work so
+far, so the reduction of the head / late-backbone buckets overlaps the early-backbone
+(depthwise) backward that is still running.  `__call__` (after backward) issues any bucket
+not yet launched and makes the compute stream wait for all of them before the SGD update —
+clipping happens after the sum (net_tools.py:649).
+
+Transports:
+  * native (the N > 1 default over RCCL, `make_reducer`): the library's own communicator
+    (include/rod.h ABI 16/19: rod_allreduce_bucket, rod_allgather), created from a unique id
+    handed over through torch.distributed's key-value store — no device collective of
+    torch.distributed runs in a training step, so no ProcessGroupNCCL watchdog ever polls an
+    event of a stream that is being captured, and the whole step (buckets, hard-negative
+    exchange, SyncBatchNorm gathers) is captured into one HIP graph ('full', rod.trainer);
+  * torch.distributed (gloo in the CPU tests and the one-GPU rehearsal): the same buckets via
+    dist.all_reduce(async_op=True); a graphed step then captures only the collective-free
+    compute ('split').
 
 xGMI note: 8 GPUs are fully connected point-to-point; a 22 MB (REFINE) / 35 MB (ALL) fp32
 gradient in ~4 MB buckets gives RCCL messages large enough to run its multi-channel rings
@@ -18,21 +28,44 @@ at link bandwidth while leaving room to overlap.
 import torch
 import torch.distributed as dist
 
+_UID_KEY = 'rod_rccl_uid'
+
 
 def native_comm_init(rank, world, group=None):
     """The C-ABI reduce point (include/rod.h ABI 16: rod_rccl_unique_id / rod_rccl_init): rank 0
-    makes the RCCL unique id, torch.distributed's store hands it to every rank (world > 1), and
-    every rank creates the library's communicator.  Returns nothing; rod_rccl_destroy frees it."""
+    makes the RCCL unique id and puts it in torch.distributed's key-value store (a host-side
+    TCP store: no device collective, nothing for a watchdog to poll), every rank reads it and
+    creates the library's communicator.  Idempotent: an existing communicator of this size is
+    kept (one per process).  rod_rccl_destroy frees it."""
     import ctypes
     from . import _abi
+    if _abi.lib().rod_rccl_world() == world:
+        return
+    if _abi.lib().rod_rccl_world() > 0:
+        _abi.call('rod_rccl_destroy')
     uid = (ctypes.c_char * 128)()
     if rank == 0:
         _abi.call('rod_rccl_unique_id', ctypes.addressof(uid))
     if world > 1:
-        box = [bytes(uid)]
-        dist.broadcast_object_list(box, src=0, group=group)
-        ctypes.memmove(uid, box[0], 128)
+        store = dist.distributed_c10d._get_default_store()
+        gen = getattr(native_comm_init, '_gen', 0) + 1    # a fresh key per communicator
+        native_comm_init._gen = gen
+        key = f'{_UID_KEY}_{gen}'
+        if rank == 0:
+            store.set(key, bytes(uid))
+        else:
+            ctypes.memmove(uid, store.get(key), 128)
     _abi.call('rod_rccl_init', rank, world, ctypes.addressof(uid))
+
+
+def make_reducer(world, rank=None, group=None, bucket_mb=4.0):
+    """The data-parallel reducer a job uses: over RCCL ('nccl' process group) the library's
+    communicator (native), over any other backend (gloo) torch.distributed."""
+    rank = dist.get_rank(group) if rank is None else rank
+    if dist.get_backend(group) == 'nccl':
+        native_comm_init(rank, world, group)
+        return GradReducer(world, bucket_mb, group, native=True)
+    return GradReducer(world, bucket_mb, group)
 
 
 class GradReducer(object):
@@ -40,10 +73,12 @@ class GradReducer(object):
         self.world = world_size
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.group = group
-        # native=True: buckets are summed by the library's own communicator (rod_allreduce_bucket,
-        # native_comm_init first), in order on the compute stream; default: torch.distributed
-        # (RCCL as well), on its own stream, overlapping backward
+        # native=True: every collective goes through the library's own communicator
+        # (native_comm_init first): the buckets on a communication stream joined by events,
+        # the hard-negative sums and SyncBatchNorm gathers on the compute stream; otherwise
+        # torch.distributed (async work handles)
         self.native = bool(native)
+        self._comm = None      # the native communication stream (created on first use)
         self.store = None
         self.buckets = []
         # True while Trainer.step_graphed captures a 'split' step: the captured backward launches
@@ -127,20 +162,34 @@ class GradReducer(object):
     def _allreduce(self, view):
         if not self.native:
             return dist.all_reduce(view, group=self.group, async_op=True)
-        from . import _abi, ops
-        _abi.call('rod_allreduce_bucket', view, view.numel(), 0, ops.stream())
-        return _Done()
+        from . import _abi
+        cur = torch.cuda.current_stream(view.device)
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=view.device)
+        ready = torch.cuda.Event()
+        ready.record(cur)                      # the bucket's gradients (and slab sums) are written
+        self._comm.wait_event(ready)
+        _abi.call('rod_allreduce_bucket', view, view.numel(), 0, self._comm.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(self._comm)
+        return _Joined(done, cur)
 
     def hnm_allreduce(self, tensors):
         """In-place SUM of small device int32 tensors over the ranks, on the compute stream
         (the hard-negative exchange of net_tools.det_clf_loss)."""
+        if self.native:
+            from . import _abi, ops
+            for t in tensors:
+                assert t.dtype == torch.int32 and t.is_contiguous()
+                _abi.call('rod_allreduce_bucket', t, t.numel(), 2, ops.stream())   # ROD_I32
+            return
         for t in tensors:
             dist.all_reduce(t, group=self.group)
 
     def bn_allgather(self, parts):
         """[world * nparts, ...] = every rank's BatchNorm partial statistics in rank order
         (SyncBatchNorm)."""
-        return allgather(parts, self.world, self.group)
+        return allgather(parts, self.world, self.group, native=self.native)
 
     def launched(self):
         return sum(1 for b in self.buckets if b['work'] is not None)
@@ -153,12 +202,28 @@ class _Done(object):
         return None
 
 
-def allgather(t, world, group=None):
+class _Joined(object):
+    """A bucket summed on the communication stream: wait() makes the compute stream wait for
+    it (an event edge — a graph dependency under capture), no host synchronisation."""
+
+    def __init__(self, done, stream):
+        self.done, self.stream = done, stream
+
+    def wait(self):
+        self.stream.wait_event(self.done)
+
+
+def allgather(t, world, group=None, native=False):
     """All-gather of a small device tensor into one [world * n, ...] buffer, rank-major, on the
-    compute stream (RCCL all_gather_into_tensor; the list form for gloo)."""
+    compute stream (native: rod_allgather; RCCL all_gather_into_tensor; the list form for
+    gloo)."""
     t = t.contiguous()
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    if dist.get_backend(group) == 'nccl':
+    if native:
+        from . import _abi, ops
+        code = {torch.float32: 0, torch.bfloat16: 1, torch.int32: 2}[t.dtype]
+        _abi.call('rod_allgather', t, out, t.numel(), code, ops.stream())
+    elif dist.get_backend(group) == 'nccl':
         dist.all_gather_into_tensor(out, t, group=group)
     else:
         dist.all_gather(list(out.chunk(world)), t, group=group)
@@ -175,9 +240,10 @@ class SyncBatchNorm(object):
     all-reduce adds up.  One all-gather of 3*C (forward) / 2*C (backward) floats per part and
     BatchNorm: a few KB to ~1 MB per layer, latency-bound on xGMI."""
 
-    def __init__(self, world, group=None):
+    def __init__(self, world, group=None, native=False):
         self.world = world
         self.group = group
+        self.native = native
 
     def gather(self, parts):
-        return allgather(parts, self.world, self.group)
+        return allgather(parts, self.world, self.group, native=self.native)

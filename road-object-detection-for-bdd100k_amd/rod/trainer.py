@@ -15,8 +15,6 @@ selected over the global batch (counts + radix histograms all-reduced, ops.hnm_l
 """
 from __future__ import annotations
 
-import time
-
 import numpy as np
 import torch
 
@@ -34,7 +32,7 @@ class Trainer:
                  learning_rate=1e-3, device='cuda', fix_refine=True, seed=0, world_size=1, reducer=None,
                  deconv_method=config.deconv_method.LEARN_HALF, merge_method=config.merge_method.ADD,
                  sync_bn=False, backbone_name='mobilenet_v2',
-                 process_backbone_method=config.process_backbone_method.NONE, graph_dp=False):
+                 process_backbone_method=config.process_backbone_method.NONE):
         self.img_size = tuple(img_size)
         self.batch_size = batch_size          # per-rank batch
         self.world_size = world_size
@@ -72,7 +70,8 @@ class Trainer:
         self.sync_bn = bool(sync_bn and (world_size > 1 or dp))
         if self.sync_bn:
             from rod.ddp import SyncBatchNorm
-            ops.SYNC_BN = SyncBatchNorm(world_size, getattr(reducer, 'group', None))
+            ops.SYNC_BN = SyncBatchNorm(world_size, getattr(reducer, 'group', None),
+                                        native=bool(getattr(reducer, 'native', False)))
         else:
             ops.SYNC_BN = None
         # weight gradients beside the backward-data chain (opt-in, ROD_ENABLE=side; single
@@ -83,10 +82,6 @@ class Trainer:
         ops.DROPOUT_RANK[:] = [rank, world_size]
         self._eager_steps = 0
         self._dropout_seen = False   # the step draws dropout masks (vgg_16 training): never graphed
-        # data parallel + step_graphed: capture the RCCL collectives into the graph too (opt-in,
-        # 'full'); by default only the collective-free compute is captured ('split', see
-        # graph_mode)
-        self.graph_dp = bool(graph_dp)
 
     def step(self, img_u8, gt_corner, gt_labels, gt_n):
         losses = self._compute(img_u8, gt_corner, gt_labels, gt_n)
@@ -115,28 +110,21 @@ class Trainer:
 
     def graph_mode(self):
         """How step_graphed runs this trainer's step:
-        'full'  — the whole step is one graph: single process, or data parallel over RCCL with
-                  graph_dp=True (the bucketed all-reduces, SyncBatchNorm all-gathers and the
-                  hard-negative exchange are captured with the kernels);
-        'split' — data parallel, default: forward + backward (no collective inside: REFINE
-                  mode without SyncBatchNorm) replay as a graph, then the gradient all-reduce
-                  (buckets launched back to back) and the SGD update are issued eagerly.  The
-                  graph holds no collective, so every rank's capture is the single-process
-                  one; what is lost is the overlap of the ~22 MB all-reduce with backward;
-        'eager' — steps with collectives inside forward/backward: ALL mode's global hard
-                  negatives (always), SyncBatchNorm (unless graph_dp); gloo with graph_dp;
-                  dropout."""
+        'full'  — the whole step is one graph: single process, or data parallel through the
+                  library's RCCL communicator (rod.ddp native reducer, the N > 1 default over
+                  RCCL): the bucketed all-reduces on their side stream (overlapping backward),
+                  the hard-negative exchange and the SyncBatchNorm gathers are captured with
+                  the kernels;
+        'split' — data parallel over torch.distributed (gloo: the CPU rehearsal): forward +
+                  backward (no collective inside: REFINE mode without SyncBatchNorm) replay as
+                  a graph, then the gradient all-reduce and SGD are issued eagerly;
+        'eager' — torch.distributed steps with collectives inside forward/backward (ALL mode's
+                  global hard negatives, SyncBatchNorm); dropout."""
         if self._dropout_seen:
             return 'eager'
-        if self.reducer is None:
+        if self.reducer is None or getattr(self.reducer, 'native', False):
             return 'full'
         hnm = self.train_range is not config.train_range.REFINE and net_tools.HNM_EXCHANGE is not None
-        if self.graph_dp:
-            # the hard-negative exchange's blocking all-reduces inside a capture raced RCCL's
-            # watchdog (hipErrorCapturedEvent on a 1-rank group, round 4; the same query error the
-            # retirement wait before capture in step_graphed now avoids for the eager collectives,
-            # not re-measured for this case): ALL mode stays eager
-            return 'full' if self._nccl() and not hnm else 'eager'
         mid = self.sync_bn or hnm
         return 'eager' if mid or not hasattr(self.reducer, 'defer') else 'split'
 
@@ -150,11 +138,18 @@ class Trainer:
         backbone in training) runs eager: its mask seed is a host counter that a replay would
         freeze.
 
-        Data parallel (RCCL): the bucketed gradient all-reduces that backward launches, the
-        hard-negative exchange and the SyncBatchNorm all-gathers are captured with the kernels
-        (RCCL collectives are stream-ordered and capturable; each bucket joins the compute
-        stream before SGD, so the capture closes on one stream) and replay with them.  gloo
-        runs on the host and cannot be captured: with it the step stays eager."""
+        Data parallel through the library's communicator: the bucketed gradient all-reduces that
+        backward launches (on the communication stream, forked from and joined back into the
+        compute stream by events), the hard-negative exchange and the SyncBatchNorm all-gathers
+        are captured with the kernels and replay with them.  No collective of torch.distributed
+        runs in the step, so RCCL's host watchdog has nothing to poll while the step is captured.
+        gloo runs on the host and cannot be captured: with it only forward + backward replay.
+
+        Graphs: one per batch signature (the TFRecord source pads the boxes to a fixed count, so
+        a run normally has one), each on its own memory pool — a graph's outputs (`out`) stay
+        valid until that same graph replays again, whatever other signature replays between.
+        Captures run in thread_local mode: a prefetching data source may allocate and copy on
+        its own thread meanwhile (rod.dataio), which is legal outside the capturing thread."""
         mode = self.graph_mode()
         if self._eager_steps == 0 or mode == 'eager':
             return self.step(img_u8, gt_corner, gt_labels, gt_n)
@@ -162,31 +157,18 @@ class Trainer:
         key = tuple((tuple(t.shape), t.dtype) for t in new)
         graphs = self.__dict__.setdefault('_graphs', {})
         if key not in graphs:
-            # one graph per batch signature (the TFRecord source pads the boxes to a fixed count,
-            # so a run normally has one; a batch with more boxes gets its own), all on one memory
-            # pool: replays are serialised on the compute stream, so they can share temporaries
             if len(graphs) >= self.MAX_GRAPHS:
-                graphs.pop(next(iter(graphs)))
+                graphs.pop(next(iter(graphs)))   # its graph and pool are freed with it
             static = tuple(t.clone() for t in new)
             self.net.store.build_prep_tables()   # host -> device set-up stays outside the capture
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
-            if self._nccl():
-                # RCCL's watchdog thread polls the end events of the eager collectives until it has
-                # seen them complete (every ~100 ms); polled while the RCCL stream is joined into
-                # this capture, such an event fails the query and the watchdog aborts the process.
-                # The collectives are complete here: give the watchdog time to retire them.
-                time.sleep(0.5)
             st = self.net.store
             gstep, eager, version = self.opt.global_step, self._eager_steps, st.version
-            if getattr(self, '_pool', None) is None:
-                self._pool = torch.cuda.graph_pool_handle()
-            # thread_local: RCCL's watchdog thread may query its events while this thread captures
             if mode == 'split':
                 self.reducer.defer = True   # no bucket launches from inside the captured backward
             try:
-                with torch.cuda.graph(g, pool=self._pool,
-                                      capture_error_mode='thread_local' if self.reducer is not None else 'global'):
+                with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle(), capture_error_mode='thread_local'):
                     out = self.step(*static) if mode == 'full' else self._compute(*static)
             finally:
                 if mode == 'split':
@@ -207,10 +189,6 @@ class Trainer:
         self.opt.global_step += 1
         self.net.store.version += 1   # the replay's SGD changed the parameters (derived layouts stale)
         return out
-
-    def _nccl(self):
-        import torch.distributed as dist
-        return dist.is_initialized() and dist.get_backend(getattr(self.reducer, 'group', None)) == 'nccl'
 
     def losses(self, img_u8, gt_corner, gt_labels, gt_n):
         """Forward of one step: (training loss, [refine, det, clf] in ALL mode)."""

@@ -69,12 +69,8 @@ def parse(argv=None):
                     help='process_raw_data_train on the GPU (random crop / flip / colour); False = raw batches')
     ap.add_argument('--hip_graph', type=str2bool, default=True,
                     help='replay the training step as a HIP graph (Trainer.step_graphed, bit-identical to the '
-                         'eager step; dropout steps run eager).  Data parallel: forward + backward replay, the '
-                         'gradient all-reduce and SGD follow eagerly; steps with collectives inside (ALL mode, '
-                         '--sync_bn) run eager unless --graph_dp')
-    ap.add_argument('--graph_dp', type=str2bool, default=False,
-                    help='data parallel over RCCL: capture the whole step, collectives included (opt-in: '
-                         'multi-rank capture is verified on a 1-rank group only)')
+                         'eager step; dropout steps run eager).  Data parallel over RCCL: the whole step, its '
+                         'collectives included (the library\'s communicator; gradient buckets on a side stream)')
     return ap.parse_args(argv)
 
 
@@ -162,13 +158,10 @@ def main(argv=None):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         torch.cuda.set_device(local)
-        # the step is captured with its RCCL collectives (Trainer.step_graphed): no event of an eager
-        # collective may be recycled into the capture while the watchdog still polls it
-        os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
         torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     from rod.dataio import make_source
-    from rod.ddp import GradReducer
+    from rod.ddp import make_reducer
     from rod.trainer import Trainer
 
     config.img_size = (F.img_height, F.img_width)
@@ -177,8 +170,8 @@ def main(argv=None):
     logger.info('Building model, using backbone---%s' % F.backbone_name)
     trainer = Trainer(config.img_size, F.batch_size, dtype=dtype, train_range=tr_range, learning_rate=F.learning_rate,
                       device=dev, fix_refine=F.fix_refine, seed=F.seed, world_size=world,
-                      reducer=GradReducer(world) if world > 1 else None, backbone_name=F.backbone_name,
-                      sync_bn=F.sync_bn, graph_dp=F.graph_dp)
+                      reducer=make_reducer(world, rank) if world > 1 else None, backbone_name=F.backbone_name,
+                      sync_bn=F.sync_bn)
     store = trainer.net.store
     logger.info('Total trainable parameters:%s' % str(store.trainable_count()))
     step0 = 0
@@ -204,9 +197,8 @@ def main(argv=None):
     os.makedirs(F.summary_dir, exist_ok=True)
     summ = open(os.path.join(F.summary_dir, 'train_rank%d.jsonl' % rank), 'a') if rank == 0 else None
     log = StepLog(F, trainer, tr_range, rank, summ)
-    # Trainer.graph_mode: the whole step as one graph (one process), forward + backward only with
-    # the all-reduce and SGD after the replay (data parallel), or eager (collectives inside the
-    # step, unless --graph_dp; dropout)
+    # Trainer.graph_mode: the whole step as one graph (one process, or data parallel through the
+    # library's RCCL communicator), forward + backward only (gloo), or eager (dropout)
     step = trainer.step_graphed if F.hip_graph else trainer.step
     # the host reads each step's losses (the reference's sess.run returns them) one step late:
     # step k+1 is queued on the GPU before step k's values are read, so the GPU does not wait
@@ -238,6 +230,9 @@ def main(argv=None):
     if close is not None:
         close()
     if world > 1:
+        if getattr(trainer.reducer, 'native', False):
+            from rod import _abi
+            _abi.call('rod_rccl_destroy')
         torch.distributed.destroy_process_group()
 
 

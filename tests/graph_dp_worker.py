@@ -1,8 +1,9 @@
-"""Worker of tests/test_gpu_graph_dp.py: the data-parallel training step (bucketed RCCL
-gradient all-reduce launched from inside backward, SyncBatchNorm all-gathers, the global
-hard-negative exchange in ALL mode) captured as a HIP graph and replayed (Trainer.step_graphed),
-against the same step run eager, on a 1-rank RCCL process group ('nccl' backend on cuda:0).
-Writes {'ok': bool, 'detail': ...} to <out>."""
+"""Worker of tests/test_gpu_graph_dp.py: the data-parallel training step as the N > 1 default
+runs it (rod.ddp.make_reducer over an RCCL process group: the library's communicator — bucketed
+gradient all-reduces launched from inside backward on a side stream, SyncBatchNorm all-gathers
+via rod_allgather, the global hard-negative exchange in ALL mode via int32 rod_allreduce_bucket)
+captured as ONE HIP graph and replayed (Trainer.step_graphed, 'full'), against the same step run
+eager, on a 1-rank group ('nccl' backend on cuda:0).  Writes {'ok': bool, 'detail': ...} to <out>."""
 import argparse
 import os
 import sys
@@ -24,13 +25,11 @@ def main():
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     import torch.distributed as dist
-    # the step is captured with its RCCL collectives (Trainer.step_graphed): no event of an eager
-    # collective may be recycled into the capture while the watchdog still polls it
-    os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
     dist.init_process_group('nccl', device_id=dev)
     import config
     from rod.data import synthetic_batch
-    from rod.ddp import GradReducer
+    from rod import _abi
+    from rod.ddp import make_reducer
     from rod.trainer import Trainer
     H, W, B = 160, 288, 2
     tr_range = getattr(config.train_range, a.train_range)
@@ -38,7 +37,7 @@ def main():
     runs = {}
     for mode in ('eager', 'graphed'):
         tr = Trainer((H, W), B, dtype=torch.bfloat16, train_range=tr_range, device=dev, seed=4, world_size=1,
-                     reducer=GradReducer(1, bucket_mb=1.0), sync_bn=True, graph_dp=True)
+                     reducer=make_reducer(1, 0, bucket_mb=1.0), sync_bn=True)
         step = tr.step if mode == 'eager' else tr.step_graphed
         losses = []
         for i in range(a.steps):
@@ -52,13 +51,15 @@ def main():
               'params_equal': bool(torch.equal(fe, fg)), 'losses_equal': bool(torch.equal(le, lg)),
               'buffers_equal': all(torch.equal(v, bg[k]) for k, v in be.items()),
               'losses': le.float().tolist(), 'global_step': [te.opt.global_step, tg.opt.global_step]}
-    # ALL mode: the hard-negative exchange keeps the step eager even with graph_dp (Trainer.graph_mode)
+    # every collective through the library's communicator: REFINE and ALL (its hard-negative
+    # exchange inside the step) are both captured whole
     detail['mode'] = tg.graph_mode()
-    want = 'full' if a.train_range == 'REFINE' else 'eager'
-    detail['ok'] = detail['mode'] == want and detail['captured'] == (want == 'full') and detail['params_equal'] and \
+    detail['native'] = bool(tg.reducer.native)
+    detail['ok'] = detail['mode'] == 'full' and detail['native'] and detail['captured'] and detail['params_equal'] and \
         detail['losses_equal'] and detail['buffers_equal'] and detail['buckets'] > 3 and \
         te.opt.global_step == tg.opt.global_step == a.steps
     torch.save(detail, a.out)
+    _abi.call('rod_rccl_destroy')
     dist.destroy_process_group()
 
 

@@ -2,7 +2,8 @@
 (rod_rccl_unique_id / rod_rccl_init / rod_allreduce_bucket, include/rod.h ABI 16) on a 1-rank
 communicator — in-place bucket sums (fp32 and bf16, identity at one rank), the same call captured
 into a HIP graph and replayed, and a REFINE training step whose GradReducer sums through the
-library (native=True, 'split' graph mode) bit-identical to the step without a reducer.  Writes
+library (native=True: buckets on a side stream, the whole step captured, 'full') bit-identical
+to the step without a reducer; ABI 19: int32 sums and rod_allgather (identity at one rank).  Writes
 {'ok': bool, ...} to <out>."""
 import argparse
 import os
@@ -35,6 +36,16 @@ def main():
     refb = xb.clone()
     _abi.call('rod_allreduce_bucket', xb, xb.numel(), 1, ops.stream())
     torch.cuda.synchronize()
+    xi = torch.randint(-1000, 1000, (1031,), device=dev, dtype=torch.int32)
+    refi = xi.clone()
+    _abi.call('rod_allreduce_bucket', xi, xi.numel(), 2, ops.stream())
+    src = torch.randn(3, 517, device=dev)
+    dst = torch.empty_like(src)
+    _abi.call('rod_allgather', src, dst, src.numel(), 0, ops.stream())
+    torch.cuda.synchronize()
+    det['i32_identity'] = bool(torch.equal(xi, refi))
+    det['allgather_identity'] = bool(torch.equal(src, dst))
+    det['world'] = int(_abi.lib().rod_rccl_world())
     det['f32_identity'] = bool(torch.equal(x, ref))
     det['bf16_identity'] = bool(torch.equal(xb, refb))
     g = torch.cuda.CUDAGraph()
@@ -59,8 +70,8 @@ def main():
         det['mode_' + ('none' if red is None else 'native')] = tr.graph_mode()
     det['step_equal'] = bool(torch.equal(flats[0], flats[1]))
     _abi.call('rod_rccl_destroy')
-    det['ok'] = det['f32_identity'] and det['bf16_identity'] and det['graph_replay'] and det['step_equal'] and \
-        det['mode_native'] == 'split'
+    det['ok'] = det['f32_identity'] and det['bf16_identity'] and det['i32_identity'] and det['allgather_identity'] \
+        and det['world'] == 1 and det['graph_replay'] and det['step_equal'] and det['mode_native'] == 'full'
     torch.save(det, a.out)
 
 

@@ -1,12 +1,13 @@
 """The data-parallel step as a HIP graph (Trainer.step_graphed with a GradReducer).
 
-'full' (opt-in graph_dp): captured on a 1-rank RCCL group on one MI355X — the bucketed
-all-reduces launched from inside backward and the SyncBatchNorm all-gathers go into the graph —
-and replayed over alternating input batches: parameters, moving statistics and losses
-bit-identical to the eager data-parallel step (ref net_tools.py:642-651: clip after the
-reduction).  ALL mode (hard-negative exchange inside the step) stays eager.
+'full' (the N > 1 default over RCCL, what bench.py --gpus N replays: rod.ddp.make_reducer, the
+library's communicator): captured on a 1-rank RCCL group on one MI355X — the bucketed
+all-reduces launched from inside backward on their side stream, the SyncBatchNorm all-gathers
+and (ALL mode) the hard-negative exchange go into the graph — and replayed over alternating
+input batches: parameters, moving statistics and losses bit-identical to the eager
+data-parallel step (ref net_tools.py:642-651: clip after the reduction).
 
-'split' (the default, what bench.py --gpus N replays): two ranks over gloo on one GPU."""
+'split' (torch.distributed reducers — the gloo rehearsal): two ranks over gloo on one GPU."""
 import os
 import socket
 import subprocess
@@ -45,7 +46,7 @@ SPLIT_WORKER = os.path.join(ROOT, 'tests', 'split_dp_worker.py')
 
 
 def test_split_graph_dp_two_ranks(tmp_path, dev):
-    """The default data-parallel graph mode ('split': forward + backward replayed, the bucketed
+    """The torch.distributed graph mode ('split': forward + backward replayed, the bucketed
     all-reduce + SGD issued after the replay) with TWO ranks (gloo on one GPU): bit-identical
     to the eager DP step on each rank, ranks hold identical parameters; ALL mode stays eager."""
     out = str(tmp_path / 's.pt')
