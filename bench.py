@@ -436,6 +436,10 @@ def kernel_rooflines(tr, batch, steps, dtype):
 
 def main():
     args = parse()
+    # stdout carries exactly ONE line, the JSON result: anything else written to fd 1 (RCCL's
+    # version banner at communicator init, library prints) goes to stderr
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -647,7 +651,8 @@ def main():
             out['inference_1080p'] = inf1080
         if args.cpu_baseline and world == 1:
             out['cpu_baseline'] = cpu_baseline(args.height, args.width)
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + '\n').encode())
     if world > 1:
         if getattr(reducer, 'native', False):
             _abi.call('rod_rccl_destroy')
