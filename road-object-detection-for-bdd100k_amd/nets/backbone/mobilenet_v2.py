@@ -101,6 +101,7 @@ class MobilenetV2:
         a graph.fork alias, so their gradient meets the backbone's own with rod_add."""
         P = self.store.params
         end_points = {}
+        self.tap_events = {}
         taps = set(taps or ())
         # The stem, expand and depthwise BatchNorms each feed exactly one consumer (the next
         # depthwise or project conv), so they stay Pending and are applied in that consumer's
@@ -151,6 +152,11 @@ class MobilenetV2:
                 end_points[name], x = graph.fork(x, 2)
             else:
                 end_points[name] = x
+            if name in taps and ops.LEVELS.active(end_points[name]):
+                # where a consumer on another stream (a detector head, ops.LEVELS) may start
+                ev = torch.cuda.Event()
+                ev.record()
+                self.tap_events[name] = ev
             if last:
                 break
         return end_points

@@ -15,6 +15,7 @@ Structure (reference line numbers):
 from __future__ import annotations
 
 import collections
+import contextlib
 
 import numpy as np
 import torch
@@ -217,24 +218,31 @@ class CatchNet:
         return ops.conv2d_bn(x, w, b, ks, None, P[name + '/beta'], B[name + '/moving_mean'],
                              B[name + '/moving_variance'], act, training, HEAD_BN_DECAY, HEAD_BN_EPS)
 
-    def head_out(self, feats, scope, k, training):
-        """__det_out / __clf_out (catch_net.py:276-342)."""
+    def head_out(self, feats, scope, k, training, ready=None):
+        """__det_out / __clf_out (catch_net.py:276-342).  The levels' chains are independent:
+        each runs on its own stream (ops.LEVELS), forked where its feature was produced
+        (`ready`: events recorded by the backbone at its taps) and joined before returning."""
         P = self.store.params
+        lv = ops.LEVELS if ops.LEVELS.active(feats[0]) else None
         outs = []
         for i, x in enumerate(feats):
             base = '%s/block_%d' % (scope, i + 1)
             n = 0
-            for ch in [128, k * self.n_anchor[i]]:
-                for ks in (1, 3):
-                    cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
-                    bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
-                    x = self._conv_bn(x, P[cname + '/weights'], P[cname + '/biases'], ks, bname, training)
-                    # the first three BatchNorms feed only the next conv of the head
-                    if n == 3 or 'bnpro' in ops._DISABLE:
-                        x = ops.materialize(x)
-                    n += 1
+            s = lv.fork(i, x, ready[i] if ready else None) if lv is not None else None
+            with torch.cuda.stream(s) if s is not None else contextlib.nullcontext():
+                for ch in [128, k * self.n_anchor[i]]:
+                    for ks in (1, 3):
+                        cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
+                        bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
+                        x = self._conv_bn(x, P[cname + '/weights'], P[cname + '/biases'], ks, bname, training)
+                        # the first three BatchNorms feed only the next conv of the head
+                        if n == 3 or 'bnpro' in ops._DISABLE:
+                            x = ops.materialize(x)
+                        n += 1
             B_, fh, fw, _ = x.shape
             outs.append(x.view(B_, fh, fw, self.n_anchor[i], k))
+        if lv is not None:
+            lv.join(outs)
         return outs
 
     def deconv_bone(self, feats, training):
@@ -306,13 +314,14 @@ class CatchNet:
         else:
             ep = self.backbone(inputs, is_training, taps=names)
             feats = [ep[n] for n in names]
+        ready = [getattr(self.backbone, 'tap_events', {}).get(n) for n in names] if not self.msf else None
         self.backbone_feats = collections.OrderedDict(('layer_%d' % (i + 1), f) for i, f in enumerate(feats))
         if not self.all_mode:
-            return self.head_out(feats, 'refine', 4, is_training)
+            return self.head_out(feats, 'refine', 4, is_training, ready)
         # multi-consumer tensors are forked so their gradients are summed by rod_add:
         # every feature feeds the refine head and the merge; the deepest one also the deconv
         forks = [graph.fork(f, 3 if i == len(feats) - 1 else 2) for i, f in enumerate(feats)]
-        refine_out = self.head_out([f[0] for f in forks], 'refine', 4, is_training)
+        refine_out = self.head_out([f[0] for f in forks], 'refine', 4, is_training, ready)
         deconv_in = feats[:-1] + [forks[-1][2]]     # the shallower ones contribute only their shape
         deconv = self.deconv_bone(deconv_in, is_training)
         self.deconv_feats = deconv

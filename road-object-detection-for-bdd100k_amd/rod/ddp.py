@@ -95,7 +95,7 @@ class GradReducer(object):
         cur = None
         for off, n, p in spans:
             if cur is None or (cur['hi'] - off) * 4 > self.bucket_bytes:
-                cur = {'lo': off, 'hi': off + n, 'params': [], 'pending': 0, 'work': None}
+                cur = {'lo': off, 'hi': off + n, 'params': [], 'pending': 0, 'work': None, 'streams': []}
                 self.buckets.append(cur)
             cur['lo'] = min(cur['lo'], off)
             cur['params'].append(p)
@@ -108,6 +108,7 @@ class GradReducer(object):
         for b in self.buckets:
             b['pending'] = len(b['params'])
             b['work'] = None
+            b['streams'] = []
             for p in b['params']:
                 p._rod_seen = False
 
@@ -115,6 +116,13 @@ class GradReducer(object):
         if b['work'] is None:
             from . import ops
             view = self.store.flat_grad[b['lo']:b['hi']]
+            # gradients of one bucket may be written on several streams (the detector heads run
+            # per level on their own, ops.LEVELS): the launching stream waits for all of them
+            cur = torch.cuda.current_stream(view.device)
+            for st in b['streams']:
+                if st != cur:
+                    cur.wait_stream(st)
+            b['streams'] = []
             # the deferred weight-gradient sums INTO this bucket land before it is reduced; the
             # rest of the step's sums stay queued for the batched flush at the end of backward
             ops.SLAB.flush_range(view)
@@ -125,6 +133,10 @@ class GradReducer(object):
         if b is None or p._rod_seen or self.defer:
             return
         p._rod_seen = True
+        if torch.cuda.is_available() and p.is_cuda:
+            st = torch.cuda.current_stream(p.device)
+            if st not in b['streams']:
+                b['streams'].append(st)
         b['pending'] -= 1
         if b['pending'] == 0:
             self._launch(b)

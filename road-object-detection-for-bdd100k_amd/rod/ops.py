@@ -91,6 +91,59 @@ class _Side:
 SIDE = _Side()
 
 
+class LevelStreams:
+    """Independent per-level chains (the detector heads: one chain of small convs per pyramid
+    level, catch_net.py:276-342) on their own HIP streams, so the latency-bound launches of the
+    small levels overlap each other and the backbone instead of queueing behind them.
+
+    fork(i, ready): the stream of chain i, made to wait for `ready` (an event recorded where the
+    chain's input was produced) or for everything the calling stream has queued; join(outs):
+    the calling stream waits for every chain stream used.  Tensors crossing streams are marked
+    with record_stream, so the caching allocator never hands their memory to another stream
+    while the consumer may still read it.  Fork and join are event edges, i.e. graph
+    dependencies under HIP-graph capture; autograd runs each backward node on its forward's
+    stream and synchronises the edges between streams itself.  ROD_HEAD_STREAMS=n chains
+    streams (0: every chain on the calling stream)."""
+
+    def __init__(self):
+        self.n = int(os.environ.get("ROD_HEAD_STREAMS", "3"))
+        self.pool = {}
+        self.used = []
+
+    def active(self, t):
+        return self.n > 0 and torch.is_tensor(t) and t.is_cuda
+
+    def stream(self, i, device):
+        key = (str(device), i % self.n)
+        if key not in self.pool:
+            self.pool[key] = torch.cuda.Stream(device=device)
+        return self.pool[key]
+
+    def fork(self, i, x, ready=None):
+        s = self.stream(i, x.device)
+        if ready is not None:
+            s.wait_event(ready)
+        else:
+            s.wait_stream(torch.cuda.current_stream(x.device))
+        x.record_stream(s)
+        if s not in self.used:
+            self.used.append(s)
+        return s
+
+    def join(self, outs):
+        if not self.used:
+            return
+        cur = torch.cuda.current_stream(self.used[0].device)
+        for s in self.used:
+            cur.wait_stream(s)
+        for o in outs:
+            o.record_stream(cur)
+        self.used = []
+
+
+LEVELS = LevelStreams()
+
+
 class SlabDefer(object):
     """Deferred parameter-gradient sums over one backward (rod_slab_defer / rod_slab_flush,
     include/rod.h ABI 11): the weight-gradient entries queue their final fixed-order slab sums
