@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 19
+#define ROD_ABI_VERSION 20
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1, ROD_I32 = 2 /* collectives only (ABI 19) */ };
@@ -140,6 +140,21 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
                         const float* coef, const float* w, void* dx, float* dw, float* gparts, void* workspace, int N,
                         int H, int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype,
                         void* stream);
+/* The same stride-1 pass without a materialised dz (ABI 20): in the inverted-residual block dz is
+ * the project conv's input gradient dy_p . W_p (conv_blocks.py:287-294 backward), so the kernel
+ * reads the cout-wide dy_p ([N*H*W][cout] bf16: the project BatchNorm's backward output, written
+ * by rod_pw_bwd_gred_dyp) and wt1 = W_p^T ([C][cout] bf16, the conv's mode-1 layout) and forms dz
+ * per row tile with the MFMA rod_pw_bwd_gred uses for it, rounded to bf16 once — dx, dw and gparts
+ * bit-identical to rod_pw_bwd_gred -> rod_dw3x3_bwd_fused, minus the 2*es*M*C bytes of dz.  Plans:
+ * rod_dw3x3_bwd_fused_pw_supported (bf16, both activations ReLU6, cout % 8 == 0 and <= 32, the
+ * stride-1 tile <= 32 columns x 48 channels); pad 1, Ho = H, Wo = W; workspace as
+ * rod_dw3x3_bwd_fused_workspace(N, H, W, C, 1, 1, 1); gparts as rod_dw3x3_bwd_fused_parts. */
+int rod_dw3x3_bwd_fused_pw_supported(int N, int H, int W, int C, int cout, int pro_act, int bn_act, int dtype);
+int rod_dw3x3_bwd_fused_pw(const void* ye, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                           const float* pro_beta, int pro_act, const void* dyp, const void* wt1, int cout,
+                           const void* yd, const float* bn_mean, const float* bn_rstd, const float* bn_gamma,
+                           const float* bn_beta, int bn_act, const float* coef, const float* w, void* dx, float* dw,
+                           float* gparts, void* workspace, int N, int H, int W, int C, int dtype, void* stream);
 
 /* The BatchNorm backward of the depthwise's output fused into its filter gradient (ABI 10):
  * dy = FusedBatchNormGrad-apply of (dz, y) with the coefficients coef[3][C] of
@@ -396,6 +411,17 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
                     const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
                     void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
                     void* stream);
+/* The same pass handing the consumer the project BatchNorm's backward output instead of dx
+ * (ABI 20): dyp [M][Cout] bf16 = dy (the values dx = dy . W is formed from, written once by the
+ * first column group), dx NOT written; dw and xparts exactly as rod_pw_bwd_gred (they are formed
+ * from the same in-register dx).  For a depthwise that recomputes dx = dy . W itself
+ * (rod_dw3x3_bwd_fused_pw): the Cin-wide dx never crosses HBM.  The shapes of rod_pw_bwd_gred
+ * other than the expand form (16 -> 96). */
+int rod_pw_bwd_gred_dyp(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                        const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                        const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                        void* dyp, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
+                        void* stream);
 
 /* Stem weight gradient through its BatchNorm (ABI 18): rod_conv_wgrad of the 3x3, 3 -> 32 stem
  * (mobilenet_v2.py:58 conv + mobilenet.py:417-420 batch_norm) with dy formed in the loader from

@@ -2020,15 +2020,33 @@ __device__ __forceinline__ dw_f2 gate2(dw_f2 z, dw_f2 v, int act) {
 }
 __device__ __forceinline__ dw_f2 round2(dw_f2 v, float) { return v; }
 
+// Project-gradient recompute (PW, ABI 20: rod_dw3x3_bwd_fused_pw).  In an inverted-residual block
+// dz — the gradient at act_d(BN_d(yd)), i.e. at the project conv's input — is dy_p . W_p with dy_p
+// the project BatchNorm's backward output [M][cout] (cout = 16..32) and W_p^T [C][cout].  Instead of
+// reading a materialised C-wide dz, the kernel reads the cout-wide dy_p (rod_pw_bwd_gred_dyp writes
+// it in place of dz) and forms each row step's dz tile [<=32 pixels][the block's channels] with the
+// MFMA rod_pw_bwd_gred uses for it — v_mfma_f32_16x16x32_bf16, k zero-padded to 32, one instruction
+// (cout <= 32) — rounded to bf16 once: bit-identical to the dz it would have written.  The tile is
+// computed one step ahead by waves 0 .. 2*ceil(Cc/16)-1 (one 16x16 tile each, A fragments from a
+// 3-step register ring like the other loads, B = W_p^T rows in registers) into a 3-slot LDS ring,
+// which the step's existing barrier publishes; the dz read and write of 2*es*M*C bytes disappear.
+struct DwPw {
+  const bf16_t* dyp;   // [N*H*W][cout] (rows = the depthwise output pixels)
+  const bf16_t* wt1;   // [C][cout]: W_p^T, the project conv's mode-1 GEMM layout
+  int cout;
+};
+constexpr int DWPW_LD = 52;   // LDS row stride (bf16) of the recomputed dz tile: <= 48 channels + pad
+
 // V = 2: the same tile with twice the threads (512 per block), each holding 2 channels — half the
 // per-thread weights, accumulators and BatchNorm constants, twice the waves in flight
-template <typename T, int PACT, bool RED, int BACT, int V = 4, int D = 3>
-__global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
+template <typename T, int PACT, bool RED, int BACT, int V = 4, int D = 3, bool PW = false>
+__global__ void __launch_bounds__(1024 / V, PW ? 4 : 1) dw3x3_bwd_fused2_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
                                                                const T* __restrict__ yd, const float* __restrict__ w,
                                                                T* __restrict__ dx, float* __restrict__ slab,
                                                                float* __restrict__ gparts, int H, int W, int C,
-                                                               DwTile tl, BnPro pro, DwBwdBn bd) {
+                                                               DwTile tl, BnPro pro, DwBwdBn bd, DwPw pw = DwPw{}) {
   static_assert(D % 3 == 0, "the ring steps a multiple of the 3 accumulator rows");
+  static_assert(!PW || (V == 2 && D == 3 && sizeof(T) == 2), "PW: the bf16 2-channel form, 3-step ring");
   constexpr int VP = V / 2;  // V channels per thread = VP packed pairs
   constexpr int TB = 1024 / V;      // threads per block (the tile of the 4-channel plan)
   typedef PackV<T, V> PK;
@@ -2107,7 +2125,46 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
   const unsigned vox = comp ? vo : ROD_OOB;   // halo lanes store nothing
   const unsigned rstrb = (unsigned)(W * C * sizeof(T));
 
-  PK rx[D], rz[D], ry[D];
+  // PW: the dz-tile MFMA roles.  Wave wv < 2*NTN owns tile (mt, nt): pixels mt*16 + l16 of the
+  // block's P columns (A: their dy_p rows, k = 8*g4 .. +7), channels nt*16 + l16 of the group
+  // (B: W_p^T rows); lanes past P / the group's Cc / cout load zeros (out-of-range buffer loads)
+  __shared__ __attribute__((aligned(16))) bf16_t dzs[PW ? 3 * 32 * DWPW_LD : 1];
+  const int Ccg = CVb * V;
+  const int lane = tid & 63, wv = tid >> 6, g4 = lane >> 4, l16 = lane & 15;
+  const int NTN = (Ccg + 15) >> 4;
+  const int mt = wv / NTN, nt = wv - (wv / NTN) * NTN;
+  const bool mfw = PW && mt < 2;                      // wave-uniform
+  bf16x8 fbw;
+  rsrc_t rdp = rnull;
+  unsigned voa = ROD_OOB, rstp = 0;
+  if constexpr (PW) {
+    const int pm = mt * 16 + l16, cm = nt * 16 + l16;
+    const int colm = ct * tl.TWo + pm - 1;
+    const int colmc = colm < 0 ? 0 : (colm >= W ? W - 1 : colm);
+    const bool kin = 8 * g4 < pw.cout;
+    voa = mfw && pm < P && kin ? (unsigned)(((long)colmc * pw.cout + 8 * g4) * 2) : ROD_OOB;
+    rdp = rod_rsrc(pw.dyp + (long)n * H * W * pw.cout, (unsigned)((long)H * W * pw.cout * 2));
+    rstp = (unsigned)(W * pw.cout * 2);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) fbw[e] = (bf16_t)0.f;
+    if (mfw && cm < Ccg && kin) fbw = *(const bf16x8*)(pw.wt1 + (long)(cg * Ccg + cm) * pw.cout + 8 * g4);
+  }
+  typedef unsigned dwpw_u4 __attribute__((ext_vector_type(4)));
+  dwpw_u4 ra[PW ? D : 1];
+  // the dz tile of the row whose dy_p fragment is `a` -> LDS slot `dst` (rounded to bf16 once)
+  auto dz_tile = [&](const dwpw_u4& a, int dst) {
+    if (mfw) {
+      f32x4 t4 = {0.f, 0.f, 0.f, 0.f};
+      t4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), fbw, t4, 0, 0, 0);
+      if (nt * 16 + l16 < Ccg) {
+        bf16_t* d = dzs + (dst * 32 + mt * 16 + 4 * g4) * DWPW_LD + nt * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r * DWPW_LD] = (bf16_t)t4[r];
+      }
+    }
+  };
+
+  PK rx[D], rz[PW ? 1 : D], ry[D];
   // every step loads all three rows unconditionally, rows clamped into [xlo, xhi] (a clamped row
   // re-reads one the block just read: a cache hit; the xok / dok masks zero its use), and the dx
   // store is a buffer store every step (dropped by the range check off the strip / on halo
@@ -2119,7 +2176,8 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
     const int rx_ = rho < xlo ? xlo : (rho > xhi ? xhi : rho);
     const int rd_ = rho + 1 < xlo ? xlo : (rho + 1 > xhi ? xhi : rho + 1);
     rx[k].bload(rye, vo, (unsigned)rx_ * rstrb);
-    rz[k].bload(rdz, vo, (unsigned)rd_ * rstrb);
+    if constexpr (PW) ra[k] = buf_ld<dwpw_u4>(rdp, voa, (unsigned)rd_ * rstp);
+    else rz[k].bload(rdz, vo, (unsigned)rd_ * rstrb);
     ry[k].bload(ryd, vo, (unsigned)rd_ * rstrb);
   };
   const int nst = ho1 - ho0 + 3;
@@ -2129,6 +2187,10 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
   for (int k = 0; k < D; ++k) {
     issue(k, k);
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (PW) {   // step 0's dz tile, published before the loop
+    dz_tile(ra[0], 0);
+    __syncthreads();
   }
   dw_f2 acc[3][VP], fa[9][VP], q1[VP], q2[VP];
 #pragma unroll
@@ -2173,7 +2235,12 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
       {
         dw_f2 yv[VP], zv[VP];
         unpackv(ry[k], yv);
-        unpackv(rz[k], zv);
+        if constexpr (PW) {   // this step's dz pair from the recomputed tile (slot k % 3)
+          const unsigned u = *(const unsigned*)(dzs + ((k % 3) * 32 + (p < 32 ? p : 31)) * DWPW_LD + cvb * 2);
+          zv[0] = dw_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+        } else {
+          unpackv(rz[k], zv);
+        }
 #pragma unroll
         for (int h = 0; h < VP; ++h) {
           const dw_f2 z = f2fma(yv[h], dsc[h], dsh[h]);
@@ -2189,6 +2256,7 @@ __global__ void __launch_bounds__(1024 / V) dw3x3_bwd_fused2_kernel(const T* __r
       // has to wait for the load in flight (s_waitcnt vmcnt(0))
       __builtin_amdgcn_sched_barrier(0);
       issue(k, q + D);
+      if constexpr (PW) dz_tile(ra[(k + 1) % D], (k + 1) % 3);   // the next step's dz, published below
 #pragma unroll
       for (int h = 0; h < VP; ++h) {
         xs[(buf * TB + tid) * VP + h] = xv[h];
@@ -2961,6 +3029,51 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
   if (rc) return rc;
   slab_sum(slab, dw, (int)((long)N * t.strips * t.coltiles), 9L * C, s);
   return check_launch("rod_dw3x3_bwd_fused");
+}
+
+// PW (ABI 20): the plan the recompute kernel supports — bf16, stride 1, both BatchNorms ReLU6 (the
+// inverted-residual block), cout a multiple of 8 up to 32 (one MFMA k step), and a tile of at most
+// 32 columns x 48 channels (2 x 3 MFMA tiles on the block's 8 waves)
+int rod_dw3x3_bwd_fused_pw_supported(int N, int H, int W, int C, int cout, int pro_act, int bn_act, int dtype) {
+  int A = 0, B = 0;
+  if (dtype != ROD_BF16 || cout <= 0 || cout > 32 || cout % 8 || pro_act != ROD_ACT_RELU6 ||
+      bn_act != ROD_ACT_RELU6 || !dw_fused_geom(N, H, W, C, 1, 1, 1, A, B))
+    return 0;
+  const DwTile t = dw_tile(N, A, B, C, 1, 4);
+  return t.P <= 32 && t.CVb * 4 <= 48 ? 1 : 0;
+}
+
+int rod_dw3x3_bwd_fused_pw(const void* ye, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                           const float* pro_beta, int pro_act, const void* dyp, const void* wt1, int cout,
+                           const void* yd, const float* bn_mean, const float* bn_rstd, const float* bn_gamma,
+                           const float* bn_beta, int bn_act, const float* coef, const float* w, void* dx, float* dw,
+                           float* gparts, void* workspace, int N, int H, int W, int C, int dtype, void* stream) {
+  ROD_CHECK_ARG(rod_dw3x3_bwd_fused_pw_supported(N, H, W, C, cout, pro_act, bn_act, dtype),
+                "rod_dw3x3_bwd_fused_pw: unsupported plan (N=%d H=%d W=%d C=%d cout=%d acts %d/%d dtype %d)", N, H, W,
+                C, cout, pro_act, bn_act, dtype);
+  ROD_CHECK_ARG(ye && pro_mean && pro_rstd && dyp && wt1 && yd && bn_mean && bn_rstd && coef && w && dx && dw &&
+                    workspace,
+                "rod_dw3x3_bwd_fused_pw: NULL tensor argument");
+  ROD_CHECK_ARG(((((uintptr_t)ye) | ((uintptr_t)yd) | ((uintptr_t)dx)) & 7) == 0 &&
+                    ((((uintptr_t)dyp) | ((uintptr_t)wt1)) & 15) == 0,
+                "rod_dw3x3_bwd_fused_pw: ye / yd / dx must be 8-byte, dyp / wt1 16-byte aligned");
+  hipStream_t s = ROD_STREAM(stream);
+  const DwTile t = dw_tile(N, H, W, C, 1, 4);
+  const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
+  const BnPro pv{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  const DwBwdBn bd{bn_mean, bn_rstd, bn_gamma, bn_beta, coef, bn_act};
+  const DwPw pw{(const bf16_t*)dyp, (const bf16_t*)wt1, cout};
+  float* slab = (float*)workspace;
+#define DWPW(R)                                                                                                     \
+  hipLaunchKernelGGL((dw3x3_bwd_fused2_kernel<bf16_t, ROD_ACT_RELU6, R, ROD_ACT_RELU6, 2, 3, true>), grid, dim3(512), \
+                     0, s, (const bf16_t*)ye, (const bf16_t*)nullptr, (const bf16_t*)yd, w, (bf16_t*)dx, slab, gparts,  \
+                     H, W, C, t, pv, bd, pw)
+  if (gparts) DWPW(true); else DWPW(false);
+#undef DWPW
+  const int rc = check_launch("rod_dw3x3_bwd_fused_pw");
+  if (rc) return rc;
+  slab_sum(slab, dw, (int)((long)N * t.strips * t.coltiles), 9L * C, s);
+  return check_launch("rod_dw3x3_bwd_fused_pw");
 }
 
 }  // extern "C"

@@ -43,6 +43,7 @@ struct PwBwdArgs {
   int act, xact;
   long M, chunk;
   int Cin, Cout, kd, nci, nco, nxt;
+  bf16_t* dyp = nullptr;   // rod_pw_bwd_gred_dyp: the BatchNorm-backward output rows [M][Cout] (dx not written)
 };
 
 typedef short pb_s16x4 __attribute__((ext_vector_type(4)));
@@ -755,6 +756,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
       {
         const rsrc_t ndz = rsrc_d(a.dz, rown), ny = rsrc_d(a.y, rown);
         const unsigned nso = (unsigned)((1 - h) * 16 * COUT * 2);
+        // dyp (column group 0 only; other blocks and rows past M: the empty / range-checked resource)
+        const rsrc_t rdp = a.dyp && blockIdx.y == 0 ? rsrc_d(a.dyp, row0) : rod_rsrc(a.dz, 0u);
+        const unsigned dpso = (unsigned)(h * 16 * COUT * 2);
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
           const int r = rg + RG * j;
@@ -781,6 +785,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
           }
           dzv[j] = buf_ld<bf16x4>(ndz, vdj(j), nso);
           yv[j] = buf_ld<bf16x4>(ny, vdj(j), nso);
+          buf_st(o, rdp, vdj(j), dpso);   // dropped unless the dyp form (empty resource)
           if (dact && (JN * RG == 16 || r < 16)) *(bf16x4*)(Ds + (h * 16 + r) * LDD + cc * 4) = o;
         }
       }
@@ -827,7 +832,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
 #pragma unroll
           for (int r = 0; r < 4; ++r) Cx[(4 * g + r) * LDX + j * 16 + li] = (bf16_t)accx[j][r];
         __builtin_amdgcn_wave_barrier();
-        const rsrc_t rdx = rsrc_x(a.dx, row0);
+        const rsrc_t rdx = a.dx ? rsrc_x(a.dx, row0) : rod_rsrc(a.x, 0u);   // dyp form: dx not stored
         const unsigned so = (unsigned)(h * 16 * Cin * 2);
 #pragma unroll
         for (int j = 0; j < JX; ++j) {
@@ -1095,19 +1100,21 @@ size_t rod_pw_bwd_gred_workspace(long M, int Cin, int Cout) {
   return nw ? (size_t)pw_bwd_gred_rowblocks(M, Cin, nw) * Cout * Cin * sizeof(float) + 64 : 0;
 }
 
-int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
-                    const float* beta, int act, const float* coef, const void* x, const float* xmean,
-                    const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
-                    void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
-                    void* stream) {
-  const bool sexp = dtype == ROD_BF16 && M > 0 && pw_bwd_xg_ok(Cin, Cout);
+static int pw_bwd_gred_run(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                           const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                           const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                           void* dx, void* dyp, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout,
+                           int dtype, void* stream) {
+  const bool sexp = dtype == ROD_BF16 && M > 0 && pw_bwd_xg_ok(Cin, Cout) && !dyp;
   const int nw = dtype == ROD_BF16 && M > 0 && !sexp ? pw_bwd_gred_nw(Cin, Cout) : 0;
   ROD_CHECK_ARG(nw || sexp, "rod_pw_bwd_gred: unsupported shape M=%ld Cin=%d Cout=%d dtype=%d", M, Cin, Cout,
                 dtype);
   ROD_CHECK_ARG(dz && y && mean && rstd && coef && x && xmean && xrstd && dw && xparts && workspace,
                 "rod_pw_bwd_gred: NULL argument");
-  ROD_CHECK_ARG(dx && wt1, "rod_pw_bwd_gred: dx and wt1 required (the sums are over dx)");
-  ROD_CHECK_ARG(((((uintptr_t)dz) | ((uintptr_t)y) | ((uintptr_t)x) | ((uintptr_t)wt1) | ((uintptr_t)dx)) & 15) == 0,
+  ROD_CHECK_ARG((dx != nullptr) != (dyp != nullptr) && wt1,
+                "rod_pw_bwd_gred: wt1 and exactly one of dx / dyp required (the sums are over dx)");
+  ROD_CHECK_ARG(((((uintptr_t)dz) | ((uintptr_t)y) | ((uintptr_t)x) | ((uintptr_t)wt1) | ((uintptr_t)dx) |
+                  ((uintptr_t)dyp)) & 15) == 0,
                 "rod_pw_bwd_gred: tensors must be 16-byte aligned");
   ROD_CHECK_ARG(M * Cin * 2 < (1L << 31) && M * Cout * 2 < (1L << 31), "rod_pw_bwd_gred: tensor over 2 GiB");
   hipStream_t s = ROD_STREAM(stream);
@@ -1139,7 +1146,8 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
   }
   const int nblk = pw_bwd_gred_rowblocks(M, Cin, nw);
   PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw, nullptr,
-              mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0};
+              mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0,
+              (bf16_t*)dyp};
   const long ntiles = cdivl(M, 32);
   const dim3 grid(nblk, Cin / nw);
   // the inverted-residual block's case; at 48 columns the packed form measured slower (144->24:
@@ -1167,6 +1175,26 @@ int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const floa
 #undef PBG
   slab_sum(partw, dw, nblk, (long)Cout * Cin, s);
   return check_launch("rod_pw_bwd_gred");
+}
+
+int rod_pw_bwd_gred(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                    const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                    const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                    void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
+                    void* stream) {
+  ROD_CHECK_ARG(dx, "rod_pw_bwd_gred: dx required");
+  return pw_bwd_gred_run(dz, y, mean, rstd, gamma, beta, act, coef, x, xmean, xrstd, xgamma, xbeta, xact, wt1, dx,
+                         nullptr, dw, xparts, workspace, M, Cin, Cout, dtype, stream);
+}
+
+int rod_pw_bwd_gred_dyp(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                        const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                        const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                        void* dyp, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
+                        void* stream) {
+  ROD_CHECK_ARG(dyp, "rod_pw_bwd_gred_dyp: dyp required");
+  return pw_bwd_gred_run(dz, y, mean, rstd, gamma, beta, act, coef, x, xmean, xrstd, xgamma, xbeta, xact, wt1,
+                         nullptr, dyp, dw, xparts, workspace, M, Cin, Cout, dtype, stream);
 }
 
 }  // extern "C"

@@ -66,8 +66,13 @@ def backward(loss):
     key = (loss.device, loss.dtype, tuple(loss.shape))
     if key not in _ONES:
         _ONES[key] = torch.ones_like(loss)
+    ok = False
     try:
         torch.autograd.backward(loss, grad_tensors=_ONES[key])
+        ok = True
     finally:
         from .ops import clear_bn_parts
-        clear_bn_parts()   # BatchNorm sums handed between nodes live for one backward
+        left = clear_bn_parts()   # BatchNorm sums / gradient recipes handed between nodes live for one backward
+    if ok and left:
+        raise RuntimeError("%d unmaterialised depthwise-input gradient(s) reached a node other than their "
+                           "depthwise (rod.ops._DZ_RECIPE)" % left)

@@ -386,7 +386,50 @@ def _take_bn_parts(dz):
 
 
 def clear_bn_parts():
+    """End of a backward: drop the hand-offs.  Returns how many unmaterialised depthwise-input
+    gradients (the project recipes below) were never consumed by their depthwise node."""
     _BN_PARTS.clear()
+    left = len(_DZ_RECIPE)
+    _DZ_RECIPE.clear()
+    return left
+
+
+# Unmaterialised depthwise-output gradients (ABI 20).  In an inverted-residual block the gradient
+# at the project conv's input is dz = dy_p . W_p; the project node (rod_pw_bwd_gred_dyp) hands the
+# depthwise node the cout-wide dy_p and W_p^T instead of writing the C-wide dz, and returns a
+# placeholder of dz's shape whose memory is never written.  The depthwise node takes the recipe
+# (rod_dw3x3_bwd_fused_pw recomputes dz per tile, or rod_conv_fwd materialises it for any other
+# path); a placeholder that reaches anything else is caught at the end of backward (graph.backward).
+_DZ_RECIPE = {}
+
+
+def _put_dz_recipe(dz, recipe):
+    _DZ_RECIPE[dz.data_ptr()] = (dz, recipe, dz._version)
+
+
+def _take_dz_recipe(dz):
+    if dz is None:
+        return None
+    e = _DZ_RECIPE.pop(dz.data_ptr(), None)
+    if e is None:
+        return None
+    ph, recipe, ver = e
+    same = ph is dz or (ph.shape == dz.shape and ph.dtype == dz.dtype and
+                        ph.untyped_storage().data_ptr() == dz.untyped_storage().data_ptr())
+    if not same or dz._version != ver:
+        raise RuntimeError("an unmaterialised depthwise-input gradient was modified or aliased before its "
+                           "depthwise node consumed it")
+    return recipe
+
+
+def _materialize_dz(recipe, shape, dtype):
+    """dz = dy_p . W_p^T with rod_conv_fwd (the MFMA rod_pw_bwd_gred forms it with, k zero-padded:
+    the same bf16 values) for a depthwise path other than rod_dw3x3_bwd_fused_pw."""
+    dyp, wt1, cout = recipe
+    N, H, W, C = shape
+    dz = torch.empty(shape, dtype=dtype, device=dyp.device)
+    conv_fwd_raw(dyp.view(N, H, W, cout), wt1, None, dz, N, H, W, cout, C, 1)
+    return dz
 
 
 def bn_bwd_coef_from_parts(parts, M, C, rstd, gamma, beta, need_g, need_b):
@@ -466,18 +509,32 @@ def pw_bwd_gred_parts(M, Cin, Cout, dtype):
     return int(_abi.lib().rod_pw_bwd_gred_parts(int(M), int(Cin), int(Cout), _DT[dtype]))
 
 
-def pw_bwd_gred(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, dw):
+def pw_bwd_gred(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, dw, dyp=False):
     """rod_pw_bwd_gred: the project conv's backward through its BatchNorm (dx, dw written in
-    place) plus the input BatchNorm's backward sums over (dx, x) -> (dx, [nparts, 2, Cin])."""
+    place) plus the input BatchNorm's backward sums over (dx, x) -> (dx, [nparts, 2, Cin]).
+    dyp=True: rod_pw_bwd_gred_dyp — (dy [M, Cout], parts), dx not written (ABI 20)."""
     Cin, Cout = x.shape[-1], y.shape[-1]
     M = y.numel() // Cout
     nparts = pw_bwd_gred_parts(M, Cin, Cout, y.dtype)
-    dx = torch.empty_like(x)
+    out = torch.empty((M, Cout), dtype=y.dtype, device=y.device) if dyp else torch.empty_like(x)
     xparts = torch.empty((nparts, 2, Cin), dtype=torch.float32, device=y.device)
     ws = workspace(_abi.query("rod_pw_bwd_gred_workspace", M, Cin, Cout), y.device)
-    _abi.call("rod_pw_bwd_gred", dz, y, mean, rstd, gamma, beta, act, coef, x, *_pro_args(xpro), wt1, dx, dw,
-              xparts, ws, M, Cin, Cout, dtcode(y), stream())
-    return dx, xparts
+    _abi.call("rod_pw_bwd_gred_dyp" if dyp else "rod_pw_bwd_gred", dz, y, mean, rstd, gamma, beta, act, coef, x,
+              *_pro_args(xpro), wt1, out, dw, xparts, ws, M, Cin, Cout, dtcode(y), stream())
+    return out, xparts
+
+
+def dw_pw_ok(src_dw, x, Cout, ipro):
+    """The project conv's input x comes from a stride-1 depthwise whose backward can recompute
+    its gradient from dy_p (rod_dw3x3_bwd_fused_pw_supported); src_dw = (stride, the depthwise's
+    input-prologue activation) recorded by _DWBN.forward."""
+    if src_dw is None or "dwpw" in _DISABLE or ipro is None:
+        return False
+    stride, pro_act = src_dw
+    N, H, W, C = x.shape
+    return stride == 1 and _dw_fused_ok(N, H, W, C, x.dtype, 1) and \
+        bool(_abi.lib().rod_dw3x3_bwd_fused_pw_supported(N, H, W, C, int(Cout), int(pro_act), int(ipro[4]),
+                                                         dtcode(x)))
 
 
 def _bn_backward_parts(dz, y, mean, rstd, gamma, beta, act, parts, need_g, need_b):
@@ -868,6 +925,7 @@ class _ConvBN(torch.autograd.Function):
             im, ir, ig, ib, ia = ipro
             _abi.call("rod_bn_apply", x, im, ir, ig, ib, None, xb, N * H * W, Cin, 0, 0, 0, ia, dtcode(x), stream())
             x, ipro = xb, None
+        ctx.src_dw = getattr(x, "_rod_dw", None)   # x is a depthwise output (_DWBN.forward)
         conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ks, parts, ipro)
         mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
         ctx.save_for_backward(x, w, b, y, mean, rstd)
@@ -904,6 +962,16 @@ class _ConvBN(torch.autograd.Function):
             else:
                 coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             wt1 = _prep(w, 1, x.dtype, Cout, Cin, 1)
+            if dw_pw_ok(ctx.src_dw, x, Cout, ctx.ipro):
+                # the depthwise recomputes dx = dy . W per tile (rod_dw3x3_bwd_fused_pw): hand it
+                # dy and W^T, return an unwritten placeholder of dx's shape (_DZ_RECIPE)
+                dyp, xparts = pw_bwd_gred(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1,
+                                          grad_slot(w), dyp=True)
+                _mark_written(w)
+                dx = torch.empty(1, dtype=x.dtype, device=x.device).expand(x.shape)
+                _put_dz_recipe(dx, (dyp, wt1, Cout))
+                _put_bn_parts(dx, xparts)
+                return dx, None, None, None, None, None
             dx, xparts = pw_bwd_gred(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, grad_slot(w))
             _mark_written(w)
             _put_bn_parts(dx, xparts)
@@ -961,6 +1029,7 @@ class _DWBN(torch.autograd.Function):
             parts = torch.empty((nparts, 3, C), dtype=torch.float32, device=x.device)
         _abi.call("rod_dw3x3_fwd", x, *_pro_args(ipro), w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x),
                   stream())
+        y._rod_dw = (stride, ipro[4] if ipro is not None else -1)   # for the consumer's backward (dw_pw_ok)
         mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
         ctx.save_for_backward(x, w, y, mean, rstd)
         ctx.geo = (N, H, W, C, stride, pt, pl, Ho, Wo)
@@ -981,6 +1050,29 @@ class _DWBN(torch.autograd.Function):
         # the BatchNorm-backward sums of (dz, y) when the consumer's backward-data formed them
         # (the project conv's streaming kernel, _conv_bwd_from_dy)
         parts = _take_bn_parts(dz)
+        recipe = _take_dz_recipe(dz)   # dz unmaterialised: dy_p, W_p^T of the project (ABI 20)
+        if recipe is not None and _needs(w) and ctx.needs_input_grad[0] and s == 1 and ctx.ipro is not None and \
+                _dw_fused_ok(N, Ho, Wo, C, x.dtype, s):
+            coef = bn_bwd_coef_from_parts(parts, N * Ho * Wo, C, rstd, gamma, beta, _needs(gamma), _needs(beta)) \
+                if parts is not None else None
+            if coef is not None:
+                dyp, wt1, cout = recipe
+                dx = torch.empty_like(x)
+                gparts = torch.empty((_abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C, 1, 1, 1), 2, C),
+                                     dtype=torch.float32, device=x.device)
+                ws = workspace(_abi.query("rod_dw3x3_bwd_fused_workspace", N, H, W, C, 1, 1, 1), x.device)
+                det = lambda t: None if t is None else t.detach()
+                _abi.call("rod_dw3x3_bwd_fused_pw", x, *_pro_args(ctx.ipro), dyp, wt1, cout, y, mean, rstd,
+                          det(gamma), det(beta), ctx.act, coef, w, dx, grad_slot(w), gparts, ws, N, H, W, C,
+                          dtcode(x), stream())
+                _mark_written(w)
+                _put_bn_parts(dx, gparts)
+                return dx, None, None, None, None
+        if recipe is not None:   # any other path: the dz the project would have written
+            dz = _materialize_dz(recipe, (N, Ho, Wo, C), y.dtype)
+            if parts is not None:
+                _put_bn_parts(dz, parts)
+                parts = _take_bn_parts(dz)
 
         def coef_d():
             if parts is not None:

@@ -17,9 +17,12 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
                          input BatchNorm's sums).  Its reads of dz and y are the BatchNorm
                          backward's SECOND pass (as for bn_bwd_apply): design traffic; dy is
                          never stored
+  dw3x3_bwd_fused_pw   : the same algorithmic bytes (ABI 20: dz is recomputed from the cout-wide dy_p;
+                         its reads of yd and dy_p are design traffic), flops + 2*N*H*W*C*cout
   pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product
   pw_bwd_gred (project): es*(2*M*Cout + 2*M*Cin) + W, 4*M*Cin*Cout + 10*M*Cout + 6*M*Cin (the
-                         input BatchNorm's sums ride on the x it reads and the dx it writes)
+                         input BatchNorm's sums ride on the x it reads and the dx it writes);
+                         the _dyp form writes the Cout-wide dy instead of dx: es*(3*M*Cout + M*Cin) + W
   match_anchors        : B*A*(16 + 16 + 16 + 4 + 4) + anchors, 15*G*A*B flops
   ir_block_fwd (fused) : es*(N*H*W*Cin + N*Ho*Wo*Cout) + weights, 2*N*H*W*Cin*inner +
                          18*N*Ho*Wo*inner + 2*N*Ho*Wo*inner*Cout
@@ -66,6 +69,11 @@ def cost(name, a):
         es = _ES[dt]
         red = 6 * N * H * W * C if a[17] is not None else 0
         return es * 2 * N * H * W * C + 72 * C, 44 * N * Ho * Wo * C + red
+    if name == "rod_dw3x3_bwd_fused_pw":
+        N, H, W, C, dt, cout = a[21], a[22], a[23], a[24], a[25], a[8]
+        es = _ES[dt]
+        red = 6 * N * H * W * C if a[19] is not None else 0
+        return es * 2 * N * H * W * C + 72 * C, 44 * N * H * W * C + red + 2 * N * H * W * C * cout
     if name == "rod_conv_fwd":
         N, H, W, Cin, Cout, ks, dt = a[18], a[19], a[20], a[21], a[22], a[23], a[26]
         es = _ES[dt]
@@ -105,6 +113,11 @@ def cost(name, a):
         M, Cin, Cout, dt = a[19], a[20], a[21], a[22]
         es = _ES[dt]
         return es * (2 * M * Cout + 2 * M * Cin) + Cout * Cin * (es + 4), \
+            4 * M * Cin * Cout + 10 * M * Cout + 6 * M * Cin
+    if name == "rod_pw_bwd_gred_dyp":
+        M, Cin, Cout, dt = a[19], a[20], a[21], a[22]
+        es = _ES[dt]
+        return es * (3 * M * Cout + M * Cin) + Cout * Cin * (es + 4), \
             4 * M * Cin * Cout + 10 * M * Cout + 6 * M * Cin
     if name == "rod_ir_block_fwd":
         # fused inverted residual: x read once (the residual re-read is L2-served by design),
@@ -187,6 +200,9 @@ def design_bytes(name, a):
     if name == "rod_dw3x3_bwd_fused":     # + the re-read of dz and y (BatchNorm backward pass 2)
         N, C, Ho, Wo, dt = a[19], a[22], a[26], a[27], a[28]
         return cost(name, a)[0] + _ES[dt] * 2 * N * Ho * Wo * C
+    if name == "rod_dw3x3_bwd_fused_pw":  # + the reads of yd and the cout-wide dy_p
+        N, H, W, C, dt, cout = a[21], a[22], a[23], a[24], a[25], a[8]
+        return cost(name, a)[0] + _ES[dt] * N * H * W * (C + cout)
     return cost(name, a)[0]
 
 
@@ -201,10 +217,12 @@ ENTRY_KERNELS = {
     "rod_bn_bwd_apply": (("bn_bwd_apply_kernel",), ("bn_bwd_apply_kernel",)),
     "rod_pw_bwd": (("pw_bwd_kernel", "pw_bwd_stream_kernel"), ("pw_bwd_kernel", "pw_bwd_stream_kernel")),
     "rod_pw_bwd_gred": (("pw_bwd_gred_kernel",), ("pw_bwd_gred_kernel",)),
+    "rod_pw_bwd_gred_dyp": (("pw_bwd_gred_kernel",), ("pw_bwd_gred_kernel",)),
     "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),
     "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused",), ("dw3x3_bwd_fused",)),
+    "rod_dw3x3_bwd_fused_pw": (("dw3x3_bwd_fused2",), ("dw3x3_bwd_fused2",)),
     "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
     "rod_conv_fwd": (("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel"),
                      ("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel")),

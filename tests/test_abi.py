@@ -60,3 +60,14 @@ def test_ir_block_policy_is_host_only():
     assert not _abi.lib().rod_ir_block_persistent(64, 384, 64, 1, 1, 1)    # parameters exceed LDS
     assert _abi.lib().rod_ir_block_persistent(32, 192, 32, 1, 1, 1)
     assert not ops.ir_block_preferred(24, 144, 24, 1, True, torch.float32)
+
+
+def test_dw_fused_pw_plan_query():
+    """Host-only plan query: bf16 stride-1 tiles of <= 32 columns x 48 channels, cout % 8 == 0 <= 32."""
+    from rod import ops
+    q = _abi.lib().rod_dw3x3_bwd_fused_pw_supported
+    assert q(8, 360, 640, 144, 24, ops.ROD_ACT_RELU6, ops.ROD_ACT_RELU6, 1) and q(8, 720, 1280, 32, 16, ops.ROD_ACT_RELU6, ops.ROD_ACT_RELU6, 1) and q(8, 180, 320, 192, 32, ops.ROD_ACT_RELU6, ops.ROD_ACT_RELU6, 1)
+    assert not q(8, 360, 640, 144, 24, ops.ROD_ACT_RELU6, ops.ROD_ACT_RELU6, 0)          # fp32
+    assert not q(8, 90, 160, 384, 64, ops.ROD_ACT_RELU6, ops.ROD_ACT_RELU6, 1)           # cout 64: two MFMA k steps
+    assert not q(8, 360, 640, 144, 20, ops.ROD_ACT_RELU6, ops.ROD_ACT_RELU6, 1)          # cout % 8
+    assert not q(8, 360, 640, 144, 24, ops.ROD_ACT_NONE, ops.ROD_ACT_RELU6, 1)

@@ -2,7 +2,9 @@
 (rod_bn_bwd_apply -> rod_dw3x3_bwd_data -> rod_dw3x3_bwd_filter -> the input BatchNorm's
 rod_bn_bwd_reduce) against rod_dw3x3_bwd_fused (+ rod_bn_bwd_finalize of its sums).  HIP-event
 timed on the launching stream; GB/s = the fused kernel's algorithmic bytes (read ye, dz, yd;
-write dx) over each path's time.   usage: python tools/dwfused_bench.py [--iters N] [--dtype bf16|f32]"""
+write dx) over each path's time.  Stride-1 bf16 shapes of the inverted-residual blocks also time
+rod_dw3x3_bwd_fused_pw (ABI 20: dz recomputed from the cout-wide dy_p, the block's project width).
+usage: python tools/dwfused_bench.py [--iters N] [--dtype bf16|f32]"""
 import argparse
 import os
 import sys
@@ -13,6 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'road-object-detection-for-bdd100k_amd'))
 from rod import _abi, ops  # noqa: E402
 
+PW_COUT = {32: 16, 144: 24, 192: 32}   # project width of the block whose depthwise has C channels
 SHAPES = [(8, 720, 1280, 32, 1), (8, 360, 640, 144, 1), (8, 180, 320, 192, 1), (8, 90, 160, 384, 1),
           (8, 90, 160, 576, 1), (8, 45, 80, 960, 1), (8, 23, 40, 960, 1),
           # the stride-2 blocks (input maps)
@@ -34,7 +37,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     st = ops.stream()
     act = ops.ROD_ACT_RELU6
-    tu = tf = 0.0
+    tu = tf = tp = 0.0
     for (N, H, W, C, S) in SHAPES:
         (Ho, pt), (Wo, pl) = _same(H, S), _same(W, S)
         M, Mo = N * H * W, N * Ho * Wo
@@ -69,8 +72,20 @@ def main():
                       coef, w, dx, dw, gparts, ws, N, H, W, C, S, pt, pl, Ho, Wo, code, st)
             _abi.call('rod_bn_bwd_finalize', gparts, nparts, M, C, erstd, egam, dg, db, ce, st)
 
+        cout = PW_COUT.get(C)
+        pw_ok = S == 1 and cout is not None and \
+            _abi.lib().rod_dw3x3_bwd_fused_pw_supported(N, H, W, C, cout, act, act, ops.dtcode(ye))
+        if pw_ok:
+            dyp = mk((M, cout))
+            wt1 = (torch.randn((C, cout), device=dev, generator=g) * 0.2).to(dt)
+
+        def fused_pw():
+            _abi.call('rod_dw3x3_bwd_fused_pw', ye, emean, erstd, egam, ebet, act, dyp, wt1, cout, yd, dmean, drstd, dgam,
+                      dbet, act, coef, w, dx, dw, gparts, ws, N, H, W, C, code, st)
+            _abi.call('rod_bn_bwd_finalize', gparts, nparts, M, C, erstd, egam, dg, db, ce, st)
+
         res = []
-        for fn in (unfused, fused):
+        for fn in (unfused, fused) + ((fused_pw,) if pw_ok else ()):
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -83,9 +98,11 @@ def main():
         byts = 2 * (M + Mo) * C * ye.element_size()
         tu += res[0]
         tf += res[1]
+        tp += res[2] if pw_ok else res[1]
+        pws = f'  fused_pw {res[2]:8.1f} us ({byts / res[2] / 1e3:5.0f} GB/s)' if pw_ok else ''
         print(f'{N}x{H}x{W}x{C:<5d} s{S} unfused {res[0]:8.1f} us  fused {res[1]:8.1f} us  x{res[0] / res[1]:5.2f}  '
-              f'fused-bytes GB/s: unfused {byts / res[0] / 1e3:7.0f} fused {byts / res[1] / 1e3:7.0f}', flush=True)
-    print(f'TOTAL unfused {tu:.1f} us fused {tf:.1f} us')
+              f'fused-bytes GB/s: unfused {byts / res[0] / 1e3:7.0f} fused {byts / res[1] / 1e3:7.0f}{pws}', flush=True)
+    print(f'TOTAL unfused {tu:.1f} us fused {tf:.1f} us  (fused_pw where supported) {tp:.1f} us')
 
 
 if __name__ == '__main__':
