@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 20
+#define ROD_ABI_VERSION 21
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1, ROD_I32 = 2 /* collectives only (ABI 19) */ };
@@ -325,6 +325,19 @@ int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, co
  * afterwards (the project conv's backward-data and the depthwise BatchNorm it feeds,
  * conv_blocks.py:287-294 -> 238-247); 0 otherwise.  M = N*H*W rows, K = Cin. */
 int rod_conv_fwd_stream_ok(long M, int K, int Cout, int dtype);
+/* Inference conv + BatchNorm-apply epilogue (ABI 21): rod_conv_fwd whose output is
+ *   z = act(fma(y, scale, offset)) (+ res),  y = the conv output rounded to bf16,
+ *   scale = bn_rstd*bn_gamma, offset = bn_beta - bn_mean*scale (bn_affine),
+ * rounded once — exactly what rod_conv_fwd followed by rod_bn_apply(y, ..., res, z) writes
+ * (slim.conv2d + slim.batch_norm(is_training=False) + act (+ the block's residual add),
+ * mobilenet.py:417-420, conv_blocks.py:302-311, catch_net.py:301-305), without y crossing HBM.
+ * bf16 only; res (nullable) [M][ldr] with 16-byte rows; the other arguments as rod_conv_fwd
+ * (no statistics / gred epilogue: inference). */
+int rod_conv_fwd_bnact(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                       const float* pro_beta, int pro_act, const void* wt, const float* bias, void* z, void* workspace,
+                       const float* bn_mean, const float* bn_rstd, const float* bn_gamma, const float* bn_beta,
+                       int bn_act, const void* res, int ldr, int N, int H, int W, int Cin, int Cout, int ksize,
+                       int ldx, int ldy, int dtype, void* stream);
 /* Weight layouts derived from the fp32 master weight w[Cout][ksize][ksize][Cin]:
  *   mode 0: forward operand      wt[co][i][j][ci]           (cast to dtype)
  *   mode 1: backward-data operand wt[ci][2-i][2-j][co]       (transposed, flipped)

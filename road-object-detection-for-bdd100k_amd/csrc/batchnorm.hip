@@ -192,10 +192,13 @@ struct MergePlan {
   int CB, PL, slice;
 };
 static MergePlan merge_plan(int C) {
+  // ROD_MERGE_LANE_PARTS (diagnosis switch): parts per lane per level (default 16) — a different
+  // slice grouping of the same fixed-order f64 merge
+  static const int lane_parts = getenv("ROD_MERGE_LANE_PARTS") ? atoi(getenv("ROD_MERGE_LANE_PARTS")) : 16;
   MergePlan p;
   p.CB = C < 64 ? C : 64;   // 64 channels x 16+ part lanes per block
   p.PL = MERGE_T / p.CB;
-  p.slice = 16 * p.PL;      // <= 16 parts per lane per level: short dependent load chains
+  p.slice = (lane_parts > 0 ? lane_parts : 16) * p.PL;   // <= 16 parts per lane per level: short load chains
   return p;
 }
 

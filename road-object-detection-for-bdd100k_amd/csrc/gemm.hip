@@ -297,12 +297,14 @@ __device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b
 // twice the MFMAs per wave between barriers — the deep-K 3x3 convs (K = 9 x 128), which at 32
 // were load-latency bound (a k step's MFMAs per SIMD shorter than the im2col gather latency).
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool SPLIT = false, bool STATS = false,
-          bool PRO = false, bool GRED = false, int BKT = BK>
+          bool PRO = false, bool GRED = false, int BKT = BK, bool EPI = false>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
                                                        const float* __restrict__ bias, T* __restrict__ Y, long M,
                                                        int H, int W, int Cin, int Cout, int ldx, int ldy,
                                                        float* __restrict__ part = nullptr, int kper = 0,
-                                                       BnPro pro = BnPro{}, BnGred gr = BnGred{}) {
+                                                       BnPro pro = BnPro{}, BnGred gr = BnGred{},
+                                                       BnEpi ep = BnEpi{}) {
+  static_assert(!EPI || (!SPLIT && !STATS && !GRED), "the BatchNorm-apply epilogue is inference-only");
   constexpr int BM = 128;
   constexpr int WN = BN >= 64 ? 2 : 1;
   constexpr int WM = 4 / WN;
@@ -581,6 +583,16 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         }
       }
     }
+    // EPI: the block's columns' BatchNorm (scale, offset), staged once (the store loop's first
+    // barrier publishes it)
+    __shared__ float2 etab[EPI ? BN : 1];
+    if constexpr (EPI) {
+      if (tid < BN && n0 + tid < Cout) {
+        float sc, sh;
+        bn_affine(ep.mean, ep.rstd, ep.gamma, ep.beta, n0 + tid, sc, sh);
+        etab[tid] = float2{sc, sh};
+      }
+    }
     constexpr int GV = GRED ? EV : 1;
     float gsc[GV], gsh[GV], gmu[GV], grs[GV], gs[GV], gsx[GV];
 #pragma unroll
@@ -635,7 +647,26 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
         if (row >= M || col >= Cout) continue;
         const T* src = Cs + rr * LDC + cc;
         T* dst = Y + row * ldy + col;
-        if (col + EV <= Cout) {
+        if constexpr (EPI) {   // z = act(BN(y)) (+ res) from the staged, already rounded y
+          if (col + EV <= Cout) {
+            Vec16<T> yv, rv, o;
+            yv.v = *(const decltype(yv.v)*)src;
+            if (ep.res) rv.load((const T*)ep.res + row * ep.ldr + col);
+#pragma unroll
+            for (int j = 0; j < EV; ++j) {
+              const float2 t = etab[cc + j];
+              float z = act_fwd(fmaf(yv.get(j), t.x, t.y), ep.act);
+              if (ep.res) z = z + rv.get(j);
+              o.set(j, z);
+            }
+            o.store(dst);
+          } else {
+            for (int j = 0; j < Cout - col; ++j) {
+              const float2 t = etab[cc + j];
+              dst[j] = from_f32<T>(bn_epi1<T>(ep, t.x, t.y, to_f32(src[j]), row, col + j));
+            }
+          }
+        } else if (col + EV <= Cout) {
           typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
           ROD_ST_OUT((u32x4*)dst, *(const u32x4*)src);
         } else {
@@ -687,12 +718,18 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
       const int col = n0 + wn * (BN / WN) + b * 16 + (lane & 15);
       if (col >= Cout) continue;
       const float bv = bias ? bias[col] : 0.f;
+      float esc = 1.f, esh = 0.f;
+      if constexpr (EPI) bn_affine(ep.mean, ep.rstd, ep.gamma, ep.beta, col, esc, esh);
 #pragma unroll
       for (int a = 0; a < MT; ++a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const long row = m0 + wm * (BM / WM) + a * 16 + (lane >> 4) * 4 + r;
-          if (row < M) Y[row * ldy + col] = from_f32<T>(acc[a][b][r] + bv);
+          if (row < M) {
+            float v = acc[a][b][r] + bv;
+            if constexpr (EPI) v = bn_epi1<T>(ep, esc, esh, v, row, col);
+            Y[row * ldy + col] = from_f32<T>(v);
+          }
         }
       }
     }
@@ -1050,9 +1087,9 @@ static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long 
 }
 
 // split-K combine: y[m, co] = round(sum_s part[s][m][co] + bias[co]), fixed split order
-template <typename T>
+template <typename T, bool EPI = false>
 __global__ void splitk_combine_kernel(const float* __restrict__ part, const float* __restrict__ bias,
-                                      T* __restrict__ Y, long M, int Cout, int ldy, int splits) {
+                                      T* __restrict__ Y, long M, int Cout, int ldy, int splits, BnEpi ep = BnEpi{}) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long n = M * Cout;
   if (i >= n) return;
@@ -1061,6 +1098,11 @@ __global__ void splitk_combine_kernel(const float* __restrict__ part, const floa
   float acc = 0.f;
   for (int z = 0; z < splits; ++z) acc += part[(long)z * n + i];
   if (bias) acc += bias[co];
+  if constexpr (EPI) {
+    float sc, sh;
+    bn_affine(ep.mean, ep.rstd, ep.gamma, ep.beta, co, sc, sh);
+    acc = bn_epi1<T>(ep, sc, sh, acc, m, co);
+  }
   Y[m * ldy + co] = from_f32<T>(acc);
 }
 
@@ -1835,10 +1877,18 @@ static bool aligned16(const void* p) {
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool PRO, int BKT = BK>
 static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
                             int Cout, int ldx, int ldy, float* stats, const BnPro& pro, const BnGred* gr,
-                            hipStream_t s) {
+                            hipStream_t s, const BnEpi* ep = nullptr) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
   if (grid.y > 1) grid.x = (grid.x + 7) / 8 * 8;  // XCD-aware N-tile order (see the kernel)
   const size_t lds = PRO ? 8 * (size_t)Cin : 0;
+  if constexpr (sizeof(T) == 2 && BKT == BK) {   // the inference BatchNorm-apply epilogue (bf16)
+    if (ep) {
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO, false, BKT, true>), grid,
+                         dim3(256), lds, s, (const T*)x, (const T*)wt, bias, (T*)y, M, H, W, Cin, Cout, ldx, ldy,
+                         nullptr, 0, pro, BnGred{}, *ep);
+      return;
+    }
+  }
   if constexpr (VY) {
     if (gr) {
       hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO, true, BKT>), grid, dim3(256), lds, s,
@@ -1874,14 +1924,14 @@ static int bk64_mode() {
 template <typename T, int KS, bool PRO>
 static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const void* wt, const float* bias, void* y,
                               long M, int H, int W, int Cin, int Cout, int ldx, int ldy, float* stats,
-                              const BnPro& pro, const BnGred* gr, hipStream_t s) {
+                              const BnPro& pro, const BnGred* gr, hipStream_t s, const BnEpi* ep = nullptr) {
 #define CF(BN_, VA_, VB_, VY_) \
-  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, gr, s)
+  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, gr, s, ep)
   if (va && vb && vy) {
     if constexpr (sizeof(T) == 2) {
       const int K = KS * KS * Cin;
       const int mode = bk64_mode();
-      if (mode > 0 && K % 64 == 0 && Cout > 96 && Cout <= 128 && (KS == 3 || (mode > 1 && K >= 256))) {
+      if (!ep && mode > 0 && K % 64 == 0 && Cout > 96 && Cout <= 128 && (KS == 3 || (mode > 1 && K >= 256))) {
         conv_fwd_launch<T, KS, 128, true, true, true, PRO, 64>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats,
                                                                 pro, gr, s);
         return;
@@ -1936,7 +1986,7 @@ static void conv_fwd_split(bool va, bool vb, const SplitPlan& p, const void* x, 
 template <typename T>
 static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, const float* bias, void* y, void* ws,
                            float* stats, const BnGred* gr, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
-                           int ldy, hipStream_t s) {
+                           int ldy, hipStream_t s, const BnEpi* ep = nullptr) {
   const long M = (long)N * H * W;
   const int K = ksize * ksize * Cin;
   const int eV = Vec16<T>::N;
@@ -1949,7 +1999,7 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
   const BnPro pv = pro ? *pro : BnPro{};
   static const bool old_stem_fwd = getenv("ROD_DEBUG_OLDSTEMFWD") != nullptr;  // A/B against the VALU kernel
   if constexpr (sizeof(T) == 2) {
-    if (!pro && !gr && ksize == 3 && Cin == 3 && Cout == 32 && vy && !old_stem_fwd) {
+    if (!pro && !gr && !ep && ksize == 3 && Cin == 3 && Cout == 32 && vy && !old_stem_fwd) {
       const bool fuse = stats != nullptr && W % SW_TW == 0;  // block == stat tile
       // rows per block: >= ~4 blocks' worth per CU of rows, pipelined within a block
       const int xb = cdiv(W, SW_TW);
@@ -1974,8 +2024,12 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
       if (pro) conv_fwd_split<T, 3, true>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
       else conv_fwd_split<T, 3, false>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
     }
-    hipLaunchKernelGGL(splitk_combine_kernel<T>, dim3(cdivl(M * Cout, 256)), dim3(256), 0, s, (const float*)part,
-                       bias, (T*)y, M, Cout, ldy, sp.splits);
+    if (ep)
+      hipLaunchKernelGGL((splitk_combine_kernel<T, true>), dim3(cdivl(M * Cout, 256)), dim3(256), 0, s,
+                         (const float*)part, bias, (T*)y, M, Cout, ldy, sp.splits, *ep);
+    else
+      hipLaunchKernelGGL(splitk_combine_kernel<T>, dim3(cdivl(M * Cout, 256)), dim3(256), 0, s, (const float*)part,
+                         bias, (T*)y, M, Cout, ldy, sp.splits);
     if (stats) stat_parts(dt, y, M, Cout, ldy, stats, nparts, s);
     if (gr) gred_parts(dt, y, gr->y, gr->p, M, Cout, gr->parts, nparts, s);
     return;
@@ -1987,7 +2041,7 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
     return;
   }
   static const bool no_stem = getenv("ROD_DEBUG_NOSTEM") != nullptr;  // debug bisection
-  if (!pro && !gr && ksize == 3 && Cin == 3 && (Cout == 32 || Cout == 64) && vy && !no_stem) {
+  if (!pro && !gr && !ep && ksize == 3 && Cin == 3 && (Cout == 32 || Cout == 64) && vy && !no_stem) {
     if (Cout == 32)
       hipLaunchKernelGGL((stem_conv_fwd_kernel<T, 32>), dim3(cdiv(W, 128), H, N), dim3(256), 0, s, (const T*)x,
                          (const T*)wt, bias, (T*)y, H, W, ldx, ldy);
@@ -1999,17 +2053,17 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
   if constexpr (sizeof(T) == 2) {
     // the prologue form only for the block-to-block case it serves (K <= 32 input channels of a
     // project BatchNorm left pending: the 720p expand 16 -> 96)
-    if (ksize == 1 && !bias && va && vb && vy && (!pro || (K <= 32 && Cin <= PRO_MAXC)) &&
+    if (!ep && ksize == 1 && !bias && va && vb && vy && (!pro || (K <= 32 && Cin <= PRO_MAXC)) &&
         pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, gr, s,
                          pro ? &pv : nullptr))
       return;
   }
   if (ksize == 1) {
-    if (pro) conv_fwd_dispatch<T, 1, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
-    else conv_fwd_dispatch<T, 1, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
+    if (pro) conv_fwd_dispatch<T, 1, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
+    else conv_fwd_dispatch<T, 1, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
   } else {
-    if (pro) conv_fwd_dispatch<T, 3, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
-    else conv_fwd_dispatch<T, 3, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s);
+    if (pro) conv_fwd_dispatch<T, 3, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
+    else conv_fwd_dispatch<T, 3, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
   }
 }
 
@@ -2123,6 +2177,29 @@ int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, co
                                               gred_parts ? &gr : nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy,
                                               ROD_STREAM(stream)));
   return check_launch("rod_conv_fwd");
+}
+
+int rod_conv_fwd_bnact(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                       const float* pro_beta, int pro_act, const void* wt, const float* bias, void* z, void* workspace,
+                       const float* bn_mean, const float* bn_rstd, const float* bn_gamma, const float* bn_beta,
+                       int bn_act, const void* res, int ldr, int N, int H, int W, int Cin, int Cout, int ksize,
+                       int ldx, int ldy, int dtype, void* stream) {
+  ROD_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "rod_conv_fwd_bnact: bad shape");
+  ROD_CHECK_ARG(ksize == 1 || ksize == 3, "rod_conv_fwd_bnact: ksize must be 1 or 3");
+  ROD_CHECK_ARG(dtype == ROD_BF16, "rod_conv_fwd_bnact: bf16 only (dtype %d)", dtype);
+  ROD_CHECK_ARG(bn_mean && bn_rstd && z, "rod_conv_fwd_bnact: BatchNorm mean / rstd and the output required");
+  ROD_CHECK_ARG(bn_act >= ROD_ACT_NONE && bn_act <= ROD_ACT_RELU, "rod_conv_fwd_bnact: bad act %d", bn_act);
+  if (ldx == 0) ldx = Cin;
+  if (ldy == 0) ldy = Cout;
+  if (ldr == 0) ldr = Cout;
+  ROD_CHECK_ARG(ldx >= Cin && ldy >= Cout && (!res || ldr >= Cout), "rod_conv_fwd_bnact: leading dim too small");
+  ROD_CHECK_ARG(!res || (((uintptr_t)res & 15) == 0 && ldr % 8 == 0), "rod_conv_fwd_bnact: res 16-byte rows");
+  ROD_CHECK_ARG(!pro_mean || (pro_rstd && Cin <= PRO_MAXC), "rod_conv_fwd_bnact: bad BatchNorm prologue (Cin %d)", Cin);
+  const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  const BnEpi ep{bn_mean, bn_rstd, bn_gamma, bn_beta, res, ldr, bn_act};
+  conv_fwd_typed<bf16_t>(x, pro_mean ? &pro : nullptr, wt, bias, z, workspace, nullptr, nullptr, N, H, W, Cin, Cout,
+                         ksize, ldx, ldy, ROD_STREAM(stream), &ep);
+  return check_launch("rod_conv_fwd_bnact");
 }
 
 int rod_conv_weight_prep(const float* w, void* wt, int Cout, int Cin, int ksize, int mode, int dtype,

@@ -236,6 +236,26 @@ __device__ __forceinline__ void bn_pro_affine(const BnPro& p, int c, float& sc, 
   bn_affine(p.mean, p.rstd, p.gamma, p.beta, c, sc, sh);
 }
 
+// BatchNorm-apply epilogue (ABI 21, inference): the producer of y writes z = act(BN(y)) (+ res)
+// instead of y — the value rod_bn_apply would write from the stored (rounded) y: y is rounded to
+// the storage type first, then z = act(fma(y, scale, offset)) (+ res) rounded once, so the
+// predict path's result is bit-identical to conv -> rod_bn_apply while y never crosses HBM.
+struct BnEpi {
+  const float* mean;
+  const float* rstd;
+  const float* gamma;  // NULL => 1
+  const float* beta;   // NULL => 0
+  const void* res;     // residual added after the activation (nullable), row stride ldr
+  int ldr;
+  int act;
+};
+template <typename T>
+__device__ __forceinline__ float bn_epi1(const BnEpi& e, float sc, float sh, float v, long row, int col) {
+  float z = act_fwd(fmaf(to_f32(from_f32<T>(v)), sc, sh), e.act);
+  if (e.res) z = z + to_f32(((const T*)e.res)[row * e.ldr + col]);
+  return z;
+}
+
 // Fallback: parts of y[M, C] computed by a separate pass (batchnorm.hip).
 void stat_parts(int dtype, const void* y, long M, int C, int ld, float* parts, int nparts, hipStream_t s);
 // Fallback: BatchNorm-backward partial sums [nparts][2][C] of (g, g*yhat) from dz and the

@@ -140,13 +140,16 @@ class MobilenetV2:
                 x = keep(ops.dw3x3_bn(x, P[base + '/depthwise/depthwise_weights'], s,
                                       *self._bn_args(base + '/depthwise/BatchNorm'), ops.ROD_ACT_RELU6, is_training,
                                       BN_DECAY, BN_EPS))
-                x = self._conv_bn(x, P[base + '/project/weights'], 1, base + '/project/BatchNorm', ops.ROD_ACT_NONE,
-                                  is_training)
                 nxt = self.plan[i + 1] if i + 1 < len(self.plan) else None
                 pend = (chain and not res and not tapped and final_endpoint != name and nxt is not None and
                         nxt[1] != 'conv' and nxt[4] > nxt[3] and not nxt[6])
-                if not pend:
-                    x = ops.materialize(x, inp)
+                if pend:
+                    x = self._conv_bn(x, P[base + '/project/weights'], 1, base + '/project/BatchNorm',
+                                      ops.ROD_ACT_NONE, is_training)
+                else:   # written out (+ the residual): in inference one launch (ops.conv2d_bn_act)
+                    x = ops.conv2d_bn_act(x, P[base + '/project/weights'], None, 1,
+                                          *self._bn_args(base + '/project/BatchNorm'), ops.ROD_ACT_NONE, is_training,
+                                          BN_DECAY, BN_EPS, residual=inp)
             last = final_endpoint == name or idx == self.plan[-1][0]
             if name in taps and not last:
                 end_points[name], x = graph.fork(x, 2)

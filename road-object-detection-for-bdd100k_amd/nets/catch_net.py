@@ -218,6 +218,12 @@ class CatchNet:
         return ops.conv2d_bn(x, w, b, ks, None, P[name + '/beta'], B[name + '/moving_mean'],
                              B[name + '/moving_variance'], act, training, HEAD_BN_DECAY, HEAD_BN_EPS)
 
+    def _conv_bn_out(self, x, w, b, ks, name, training, act=ops.ROD_ACT_LEAKY):
+        """_conv_bn written out (inference: the BatchNorm and leaky in the conv's epilogue)."""
+        P, B = self.store.params, self.store.buffers
+        return ops.conv2d_bn_act(x, w, b, ks, None, P[name + '/beta'], B[name + '/moving_mean'],
+                                 B[name + '/moving_variance'], act, training, HEAD_BN_DECAY, HEAD_BN_EPS)
+
     def head_out(self, feats, scope, k, training, ready=None):
         """__det_out / __clf_out (catch_net.py:276-342).  The levels' chains are independent:
         each runs on its own stream (ops.LEVELS), forked where its feature was produced
@@ -234,10 +240,15 @@ class CatchNet:
                     for ks in (1, 3):
                         cname = base + ('/Conv' if n == 0 else '/Conv_%d' % n)
                         bname = base + ('/BatchNorm' if n == 0 else '/BatchNorm_%d' % n)
-                        x = self._conv_bn(x, P[cname + '/weights'], P[cname + '/biases'], ks, bname, training)
-                        # the first three BatchNorms feed only the next conv of the head
-                        if n == 3 or 'bnpro' in ops._DISABLE:
-                            x = ops.materialize(x)
+                        # the first three BatchNorms feed only the next conv of the head (its prologue);
+                        # the last one is written out
+                        if n == 3:
+                            x = self._conv_bn_out(x, P[cname + '/weights'], P[cname + '/biases'], ks, bname,
+                                                  training)
+                        else:
+                            x = self._conv_bn(x, P[cname + '/weights'], P[cname + '/biases'], ks, bname, training)
+                            if 'bnpro' in ops._DISABLE:
+                                x = ops.materialize(x)
                         n += 1
             B_, fh, fw, _ = x.shape
             outs.append(x.view(B_, fh, fw, self.n_anchor[i], k))
@@ -257,8 +268,8 @@ class CatchNet:
         for i in range(n):
             base = 'deconv/block_%d' % (i + 1)
             if i == 0:
-                x = ops.materialize(self._conv_bn(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1,
-                                                  base + '/BatchNorm', training))
+                x = self._conv_bn_out(x, P[base + '/Conv/weights'], P[base + '/Conv/biases'], 1, base + '/BatchNorm',
+                                      training)
             elif half:
                 B_, h, w, _ = layers[i].shape
                 x_out, x_up, x_rs = xs

@@ -118,10 +118,11 @@ class GradReducer(object):
             view = self.store.flat_grad[b['lo']:b['hi']]
             # gradients of one bucket may be written on several streams (the detector heads run
             # per level on their own, ops.LEVELS): the launching stream waits for all of them
-            cur = torch.cuda.current_stream(view.device)
-            for st in b['streams']:
-                if st != cur:
-                    cur.wait_stream(st)
+            if view.is_cuda:
+                cur = torch.cuda.current_stream(view.device)
+                for st in b['streams']:
+                    if st != cur:
+                        cur.wait_stream(st)
             b['streams'] = []
             # the deferred weight-gradient sums INTO this bucket land before it is reduced; the
             # rest of the step's sums stay queued for the batched flush at the end of backward

@@ -1166,6 +1166,41 @@ def conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, ep
     return Pending(y, mean, rstd, gamma, beta, act, training, owned=True)
 
 
+def conv2d_bn_act(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, residual=None):
+    """conv2d_bn + materialize: act(BN(conv(x))) (+ residual) written out.  Inference in bf16:
+    ONE launch, rod_conv_fwd_bnact (ABI 21) — the conv's epilogue applies the eval BatchNorm
+    (moving statistics), the activation and the residual, bit-identical to conv -> rod_bn_apply
+    with y never written; otherwise (training, fp32, ROD_DISABLE=bnepi) the owned Pending and
+    rod_bn_apply."""
+    xt, ipro = _in_pro(x)
+    if training or xt.dtype != torch.bfloat16 or "bnepi" in _DISABLE or torch.is_grad_enabled() and \
+            (xt.requires_grad or w.requires_grad):
+        return materialize(conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps), residual)
+    N, H, W, Cin = xt.shape
+    Cout = w.shape[0]
+    if ksize == 1 and b is None and (ipro is None or Cin <= 32) and \
+            _abi.lib().rod_conv_fwd_stream_ok(N * H * W, Cin, Cout, dtcode(xt)):
+        # the streaming 1x1 kernel (no epilogue form) beats the tiled GEMM with the epilogue here
+        return materialize(conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps), residual)
+    if ksize == 3 and ipro is not None and N * H * W >= 16384 and "pro3" not in _DISABLE:
+        # as _ConvBN.forward: a 3x3 gathers every input element 9 times, so act(BN(x)) is written
+        # once instead of applied in the load prologue (the same rounded values)
+        xb = torch.empty_like(xt)
+        im, ir, ig, ib, ia = ipro
+        _abi.call("rod_bn_apply", xt, im, ir, ig, ib, None, xb, N * H * W, Cin, 0, 0, 0, ia, dtcode(xt), stream())
+        xt, ipro = xb, None
+    wt = _prep(w, 0, xt.dtype, Cout, Cin, ksize)
+    z = torch.empty((N, H, W, Cout), dtype=xt.dtype, device=xt.device)
+    mean, rstd = bn_statistics(z, mmean, mvar, False, decay, eps)
+    nb = 0 if "splitk" in _DISABLE else _abi.query("rod_conv_fwd_workspace", N, H, W, Cin, Cout, ksize)
+    ws = workspace(nb, xt.device) if nb else None
+    res = residual.contiguous() if residual is not None else None
+    det = lambda t: None if t is None else t.detach()
+    _abi.call("rod_conv_fwd_bnact", xt, *_pro_args(ipro), wt, det(b), z, ws, mean, rstd, det(gamma), det(beta), act,
+              res, 0, N, H, W, Cin, Cout, ksize, 0, 0, dtcode(xt), stream())
+    return z
+
+
 def dw3x3_bn(x, w, stride, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3):
     """depthwise 3x3 + slim.batch_norm(+act), left Pending (owned)."""
     xt, ipro = _in_pro(x)

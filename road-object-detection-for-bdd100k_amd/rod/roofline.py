@@ -3,7 +3,8 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
 
   dw3x3 fwd / bwd_data : es*(in + out) + 9*C*4 bytes, 18*N*Ho*Wo*C flops
   dw3x3 bwd_filter     : es*(x + dy) + 9*C*4, 18*N*Ho*Wo*C
-  conv fwd (1x1 / 3x3) : es*(M*Cin + M*Cout + Cout*K) (+4*Cout bias), 2*M*K*Cout
+  conv fwd (1x1 / 3x3) : es*(M*Cin + M*Cout + Cout*K) (+4*Cout bias), 2*M*K*Cout; the _bnact form
+                         (inference BatchNorm epilogue) + es*M*Cout for a residual
   conv wgrad           : es*(M*Cin + M*Cout) + 4*Cout*K, 2*M*K*Cout
   bn_stats             : es*M*C;  bn_apply: es*M*C*(2 + residual)
   bn_bwd               : es*M*C*3 (read dy, read x, write dx)
@@ -81,6 +82,14 @@ def cost(name, a):
         K = ks * ks * Cin
         gred = es * M * Cout if a[17] is not None else 0   # the gred epilogue reads y
         return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[7] is not None else 0) + gred, 2 * M * K * Cout
+    if name == "rod_conv_fwd_bnact":      # conv + eval BatchNorm / act (+ residual) epilogue (ABI 21)
+        N, H, W, Cin, Cout, ks, dt = a[17], a[18], a[19], a[20], a[21], a[22], a[25]
+        es = _ES[dt]
+        M = N * H * W
+        K = ks * ks * Cin
+        res = es * M * Cout if a[15] is not None else 0
+        return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[7] is not None else 0) + res, \
+            2 * M * K * Cout + 5 * M * Cout
     if name == "rod_conv_wgrad":
         N, H, W, Cin, Cout, ks, dt = a[10], a[11], a[12], a[13], a[14], a[15], a[18]
         es = _ES[dt]
