@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 21
+#define ROD_ABI_VERSION 22
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1, ROD_I32 = 2 /* collectives only (ABI 19) */ };
@@ -338,6 +338,19 @@ int rod_conv_fwd_bnact(const void* x, const float* pro_mean, const float* pro_rs
                        const float* bn_mean, const float* bn_rstd, const float* bn_gamma, const float* bn_beta,
                        int bn_act, const void* res, int ldr, int N, int H, int W, int Cin, int Cout, int ksize,
                        int ldx, int ldy, int dtype, void* stream);
+/* Backward-data of a 1x1 conv through its BatchNorm (ABI 22): the BatchNorm-backward apply
+ *   dy = rod_bn_bwd_apply(dz, y, mean, rstd, gamma, beta, coef, act)   [M][Cout], bf16, written
+ * formed in the GEMM's operand loader, and dx[M][Cin] = dy . wt1^T — bit for bit what
+ * rod_bn_bwd_apply followed by rod_conv_fwd(dy, wt1 (mode 1), ..., Cin = Cout, Cout = Cin, 1x1)
+ * writes (FusedBatchNormGrad + Conv2DBackpropInput of slim.conv2d + slim.batch_norm,
+ * conv_blocks.py:263-294 expand convs), in one launch: the deep expands' dy is produced where it
+ * is first consumed; the weight gradient then reads it (rod_conv_wgrad).  bf16, Cout % 8 == 0,
+ * Cin % 8 == 0, 16-byte aligned dense rows.  workspace: rod_conv_fwd_workspace(1, 1, M, Cout,
+ * Cin, 1) bytes (split-K partials; NULL when 0). */
+int rod_conv_bwd_data_bn_supported(int Cout, int Cin, int dtype);
+int rod_conv_bwd_data_bn(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                         const float* beta, int act, const float* coef, const void* wt1, void* dy, void* dx,
+                         void* workspace, long M, int Cout, int Cin, int dtype, void* stream);
 /* Weight layouts derived from the fp32 master weight w[Cout][ksize][ksize][Cin]:
  *   mode 0: forward operand      wt[co][i][j][ci]           (cast to dtype)
  *   mode 1: backward-data operand wt[ci][2-i][2-j][co]       (transposed, flipped)

@@ -159,7 +159,7 @@ static std::atomic<bool> g_slab_defer{false};
 static std::mutex g_slab_mu;
 static std::vector<SlabJob>* g_slab_jobs = nullptr;
 
-static int slab_cb(int nslab, long n) {
+int slab_cb(int nslab, long n) {
   if (n >= 256L * 32 || nslab <= 64) return 32;
   if (n >= 256L * 8) return 8;
   return 4;

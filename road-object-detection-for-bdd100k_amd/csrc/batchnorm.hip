@@ -287,6 +287,8 @@ static void finalize_launch(const float* parts, int nparts, long M, int C, float
                             float* rstd, float* mm, float* mv, float* ws, hipStream_t s) {
   const MergePlan p = merge_plan(C);
   const int s1 = cdiv(nparts, p.slice);
+  static const bool dbg = getenv("ROD_DEBUG_MERGE") != nullptr;
+  if (dbg) fprintf(stderr, "rod merge: nparts %d C %d M %ld levels %d\n", nparts, C, M, s1 > 1 ? 2 : 1);
   float* buf[2] = {ws, ws ? ws + (size_t)s1 * 3 * C : nullptr};
   int k = 0;
   while (true) {
@@ -854,18 +856,53 @@ static void bwd_launch(bool vec, const void* dy, const void* x, const float* mea
                        mean, rstd, gamma, beta, coef, (T*)dx, M, C, lddy, ldx, lddx, act);
 }
 
-// coef[3][C] from the merged sums held in coef[C..3C) (sum g, sum g*yhat): dbeta, dgamma and
-// (rstd*gamma, mean g, mean g*yhat) in place — the coefficients bn_bwd_apply_kernel uses
-__global__ void bn_bwd_coef_kernel(long M, int C, const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                   float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float sg = coef[C + c], sgx = coef[2 * C + c];
-  if (dbeta) dbeta[c] = sg;
-  if (dgamma) dgamma[c] = sgx;
-  coef[c] = gamma ? rstd[c] * gamma[c] : rstd[c];
-  coef[C + c] = (float)((double)sg / (double)M);
-  coef[2 * C + c] = (float)((double)sgx / (double)M);
+// rod_bn_bwd_finalize in one launch: block b owns channels [b*CB/2, (b+1)*CB/2) and both of their
+// columns (sum g at c, sum g*yhat at C + c) of the part-major [nparts][2][C] slab.  Every column
+// is summed exactly as slab_sum_kernel<CB> sums it — part rows ty, ty + L, ... over L = 256/CB
+// lanes, four chains per lane, the lanes added in ty order, rounded to float — so the sums, and
+// dbeta, dgamma and the coefficients bn_bwd_apply_kernel uses, (rstd*gamma, mean g, mean g*yhat),
+// formed from those rounded sums, are bit-identical to the round-4 two-launch form.
+template <int CB>
+__global__ void __launch_bounds__(256) bn_bwd_finalize1_kernel(const float* __restrict__ parts, int nparts, long M,
+                                                               int C, const float* __restrict__ rstd,
+                                                               const float* __restrict__ gamma,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               float* __restrict__ coef) {
+  constexpr int L = 256 / CB, H = CB / 2;
+  __shared__ double red[L][CB + 1];
+  __shared__ float tot[CB];
+  const int tx = threadIdx.x % CB, ty = threadIdx.x / CB;
+  const int c = blockIdx.x * H + tx % H;
+  const bool ok = c < C;
+  const long n = 2L * C;
+  const long i = (long)(tx / H) * C + c;   // the column slab_sum would give this sum
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (ok) {
+    int b = ty;
+    for (; b + 3 * L < nparts; b += 4 * L) {
+      s0 += (double)parts[(long)b * n + i];
+      s1 += (double)parts[(long)(b + L) * n + i];
+      s2 += (double)parts[(long)(b + 2 * L) * n + i];
+      s3 += (double)parts[(long)(b + 3 * L) * n + i];
+    }
+    for (; b < nparts; b += L) s0 += (double)parts[(long)b * n + i];
+  }
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ty == 0) {
+    double t = 0.0;
+    for (int k = 0; k < L; ++k) t += red[k][tx];
+    tot[tx] = (float)t;
+  }
+  __syncthreads();
+  if (ty == 0 && tx < H && ok) {
+    const float sg = tot[tx], sgx = tot[tx + H];
+    if (dbeta) dbeta[c] = sg;
+    if (dgamma) dgamma[c] = sgx;
+    coef[c] = gamma ? rstd[c] * gamma[c] : rstd[c];
+    coef[C + c] = (float)((double)sg / (double)M);
+    coef[2 * C + c] = (float)((double)sgx / (double)M);
+  }
 }
 
 // Backward partial sums [nparts][2][C] of g = dz*act'(u), g*yhat over exactly nparts row
@@ -902,8 +939,18 @@ int rod_bn_bwd_finalize(const float* parts, int nparts, long M, int C, const flo
   ROD_CHECK_ARG(parts != nullptr && nparts > 0 && M > 0 && C > 0 && coef != nullptr && rstd != nullptr,
                 "rod_bn_bwd_finalize: bad arguments");
   hipStream_t s = ROD_STREAM(stream);
-  slab_sum(parts, coef + C, nparts, 2L * C, s, false);  // f64, fixed order (read by the coef kernel)
-  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, M, C, rstd, gamma, dgamma, dbeta, coef);
+  // one launch: slab_sum's f64 fixed-order column sums and the coefficients
+  const int cb = slab_cb(nparts, 2L * C);
+  const dim3 grid(cdiv(C, cb / 2));
+  if (cb == 32)
+    hipLaunchKernelGGL(bn_bwd_finalize1_kernel<32>, grid, dim3(256), 0, s, parts, nparts, M, C, rstd, gamma, dgamma,
+                       dbeta, coef);
+  else if (cb == 8)
+    hipLaunchKernelGGL(bn_bwd_finalize1_kernel<8>, grid, dim3(256), 0, s, parts, nparts, M, C, rstd, gamma, dgamma,
+                       dbeta, coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize1_kernel<4>, grid, dim3(256), 0, s, parts, nparts, M, C, rstd, gamma, dgamma,
+                       dbeta, coef);
   return check_launch("rod_bn_bwd_finalize");
 }
 

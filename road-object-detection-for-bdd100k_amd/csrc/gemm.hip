@@ -275,6 +275,18 @@ __device__ __forceinline__ void stage_pro(float* pt, const BnPro& p, int Cin) {
   for (int c = threadIdx.x; c < Cin; c += blockDim.x) bn_pro_affine(p, c, pt[2 * c], pt[2 * c + 1]);
 }
 
+// BatchNorm-backward prologue of the backward-data GEMM of a 1x1 conv (rod_conv_bwd_data_bn):
+// the A operand is dy = the BatchNorm backward apply of (dz, y) (rod_bn_bwd_apply's arithmetic,
+// rounded to bf16), formed as each 8-element chunk of dz / y is staged; the block of N tile 0
+// also writes those rounded dy chunks out for the weight gradient.
+struct BnBwd {
+  const bf16_t* y;       // pre-BatchNorm conv output [M][K]
+  const float *mean, *rstd, *gamma, *beta, *coef;
+  int act;
+  bf16_t* dy;            // [M][K]
+};
+constexpr int BWD_CF = 8;   // floats per channel in the prologue's LDS table: sc, sh, a, k1, k0, m
+
 // ---- MFMA over one 32-deep k step for one 16x16 tile ---------------------------------
 __device__ __forceinline__ void mma32(f32x4& acc, const bf16_t* a, const bf16_t* b) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)a, *(const bf16x8*)b, acc, 0, 0, 0);
@@ -297,14 +309,16 @@ __device__ __forceinline__ void mma32(f32x4& acc, const float* a, const float* b
 // twice the MFMAs per wave between barriers — the deep-K 3x3 convs (K = 9 x 128), which at 32
 // were load-latency bound (a k step's MFMAs per SIMD shorter than the im2col gather latency).
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool SPLIT = false, bool STATS = false,
-          bool PRO = false, bool GRED = false, int BKT = BK, bool EPI = false>
+          bool PRO = false, bool GRED = false, int BKT = BK, bool EPI = false, bool BWD = false>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, const T* __restrict__ Wt,
                                                        const float* __restrict__ bias, T* __restrict__ Y, long M,
                                                        int H, int W, int Cin, int Cout, int ldx, int ldy,
                                                        float* __restrict__ part = nullptr, int kper = 0,
                                                        BnPro pro = BnPro{}, BnGred gr = BnGred{},
-                                                       BnEpi ep = BnEpi{}) {
+                                                       BnEpi ep = BnEpi{}, BnBwd bw = BnBwd{}) {
   static_assert(!EPI || (!SPLIT && !STATS && !GRED), "the BatchNorm-apply epilogue is inference-only");
+  static_assert(!BWD || (KS == 1 && VA && !PRO && !STATS && !GRED && !EPI && BKT == BK && sizeof(T) == 2),
+                "the BatchNorm-backward prologue: bf16 1x1 backward-data only");
   constexpr int BM = 128;
   constexpr int WN = BN >= 64 ? 2 : 1;
   constexpr int WM = 4 / WN;
@@ -351,13 +365,23 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
   RowSrc<T, KS> rows[ACH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) rows[i].init(X, m0 + tid / CPR + i * RPP, M, H, W, ldx);
-  extern __shared__ float pro_lds[];  // PRO: [Cin][2] prologue table (dynamic LDS)
+  extern __shared__ float pro_lds[];  // PRO: [Cin][2] prologue table; BWD: [K][BWD_CF] (dynamic LDS)
   if constexpr (PRO) {
     stage_pro(pro_lds, pro, Cin);
     __syncthreads();
   }
+  if constexpr (BWD) {
+    for (int c = tid; c < K; c += 256) {
+      float* t = pro_lds + c * BWD_CF;
+      bn_affine(bw.mean, bw.rstd, bw.gamma, bw.beta, c, t[0], t[1]);
+      t[2] = bw.coef[c];
+      bn_bwd_k<T>(t[2], bw.mean[c], bw.rstd[c], bw.coef[K + c], bw.coef[2 * K + c], t[3], t[4], t[5]);
+    }
+    __syncthreads();
+  }
 
   Chunk8<T> ra[ACH], rb[BCH];
+  Chunk8<T> ryb[BWD ? ACH : 1];   // BWD: the y chunks beside the dz chunks in ra
   // 3x3 with 16-byte A chunks: the k loop is sequential (k0 = kb, kb + BKT, ...), so the rows
   // walk their taps incrementally (RowSrc::walk_*); the state always matches the chunk held in ra
   constexpr bool WALK = KS == 3 && VA;
@@ -375,6 +399,13 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 #pragma unroll
       for (int i = 0; i < ACH; ++i)
         rows[i].template load<VA, PRO>(ra[i], k0 + kc, K, Cin, H, W, ldx, pro_lds, pro.act);
+      if constexpr (BWD) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+          if (rows[i].valid && k0 + kc < K) ryb[i].load_vec(bw.y + (rows[i].base - X) + k0 + kc);
+          else ryb[i].zero();
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
@@ -417,6 +448,21 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
     for (int i = 0; i < ACH; ++i) {
       if constexpr (WALK) rows[i].template walk_pro<PRO>(ra[i], pro_lds, pro.act);
       else rows[i].template pro_pending<PRO>(ra[i], k0 + kc, Cin, pro_lds, pro.act);
+      if constexpr (BWD) {
+        if (ra[i].ok) {   // a valid row and k < K (K % 8 == 0: whole chunks)
+          const int k = k0 + kc;
+          const float* t = pro_lds + k * BWD_CF;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const f32x4 c0 = *(const f32x4*)(t + j * BWD_CF), c1 = *(const f32x4*)(t + j * BWD_CF + 4);
+            const float yv = (float)ryb[i].v[j];
+            const float z = fmaf(yv, c0[0], c0[1]);
+            const float g = (float)ra[i].v[j] * act_grad(z, bw.act);
+            ra[i].v[j] = (bf16_t)bn_bwd_apply1<T>(c0[2], g, c0[3], c1[0], c1[1], yv);
+          }
+          if (nt == 0) *(bf16x8*)(bw.dy + (rows[i].base - X) + k) = ra[i].v;
+        }
+      }
       ra[i].store_lds(as + (tid / CPR + i * RPP) * LD + kc);
     }
 #pragma unroll
@@ -1877,10 +1923,18 @@ static bool aligned16(const void* p) {
 template <typename T, int KS, int BN, bool VA, bool VB, bool VY, bool PRO, int BKT = BK>
 static void conv_fwd_launch(const void* x, const void* wt, const float* bias, void* y, long M, int H, int W, int Cin,
                             int Cout, int ldx, int ldy, float* stats, const BnPro& pro, const BnGred* gr,
-                            hipStream_t s, const BnEpi* ep = nullptr) {
+                            hipStream_t s, const BnEpi* ep = nullptr, const BnBwd* bw = nullptr) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, BN));
   if (grid.y > 1) grid.x = (grid.x + 7) / 8 * 8;  // XCD-aware N-tile order (see the kernel)
   const size_t lds = PRO ? 8 * (size_t)Cin : 0;
+  if constexpr (sizeof(T) == 2 && BKT == BK && KS == 1 && !PRO && VA) {   // the backward-data BatchNorm prologue
+    if (bw) {
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, false, false, BKT, false, true>), grid,
+                         dim3(256), (size_t)Cin * BWD_CF * sizeof(float), s, (const T*)x, (const T*)wt, bias, (T*)y, M,
+                         H, W, Cin, Cout, ldx, ldy, nullptr, 0, pro, BnGred{}, BnEpi{}, *bw);
+      return;
+    }
+  }
   if constexpr (sizeof(T) == 2 && BKT == BK) {   // the inference BatchNorm-apply epilogue (bf16)
     if (ep) {
       hipLaunchKernelGGL((conv_fwd_kernel<T, KS, BN, VA, VB, VY, false, false, PRO, false, BKT, true>), grid,
@@ -1924,14 +1978,15 @@ static int bk64_mode() {
 template <typename T, int KS, bool PRO>
 static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const void* wt, const float* bias, void* y,
                               long M, int H, int W, int Cin, int Cout, int ldx, int ldy, float* stats,
-                              const BnPro& pro, const BnGred* gr, hipStream_t s, const BnEpi* ep = nullptr) {
+                              const BnPro& pro, const BnGred* gr, hipStream_t s, const BnEpi* ep = nullptr,
+                              const BnBwd* bw = nullptr) {
 #define CF(BN_, VA_, VB_, VY_) \
-  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, gr, s, ep)
+  conv_fwd_launch<T, KS, BN_, VA_, VB_, VY_, PRO>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pro, gr, s, ep, bw)
   if (va && vb && vy) {
     if constexpr (sizeof(T) == 2) {
       const int K = KS * KS * Cin;
       const int mode = bk64_mode();
-      if (!ep && mode > 0 && K % 64 == 0 && Cout > 96 && Cout <= 128 && (KS == 3 || (mode > 1 && K >= 256))) {
+      if (!ep && !bw && mode > 0 && K % 64 == 0 && Cout > 96 && Cout <= 128 && (KS == 3 || (mode > 1 && K >= 256))) {
         conv_fwd_launch<T, KS, 128, true, true, true, PRO, 64>(x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats,
                                                                 pro, gr, s);
         return;
@@ -1965,9 +2020,17 @@ static void conv_fwd_dispatch(bool va, bool vb, bool vy, const void* x, const vo
 
 template <typename T, int KS, bool PRO, bool VA, bool VB>
 static void conv_fwd_split_t(const SplitPlan& p, const void* x, const void* wt, float* part, long M, int H, int W,
-                             int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s) {
+                             int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s, const BnBwd* bw = nullptr) {
   dim3 grid(cdivl(M, 128), cdiv(Cout, 128), p.splits);
   const size_t lds = PRO ? 8 * (size_t)Cin : 0;
+  if constexpr (sizeof(T) == 2 && KS == 1 && !PRO && VA) {
+    if (bw) {
+      hipLaunchKernelGGL((conv_fwd_kernel<T, KS, 128, VA, VB, false, true, false, false, false, BK, false, true>), grid,
+                         dim3(256), (size_t)Cin * BWD_CF * sizeof(float), s, (const T*)x, (const T*)wt, nullptr,
+                         nullptr, M, H, W, Cin, Cout, ldx, 0, part, p.kper, pro, BnGred{}, BnEpi{}, *bw);
+      return;
+    }
+  }
   hipLaunchKernelGGL((conv_fwd_kernel<T, KS, 128, VA, VB, false, true, false, PRO>), grid, dim3(256), lds, s,
                      (const T*)x, (const T*)wt, nullptr, nullptr, M, H, W, Cin, Cout, ldx, 0, part, p.kper, pro);
 }
@@ -1976,9 +2039,10 @@ static void conv_fwd_split_t(const SplitPlan& p, const void* x, const void* wt, 
 // would otherwise walk all of K in a single workgroup (~50 us of load latency).
 template <typename T, int KS, bool PRO>
 static void conv_fwd_split(bool va, bool vb, const SplitPlan& p, const void* x, const void* wt, float* part, long M,
-                           int H, int W, int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s) {
-  if (va && vb) conv_fwd_split_t<T, KS, PRO, true, true>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
-  else if (va) conv_fwd_split_t<T, KS, PRO, true, false>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
+                           int H, int W, int Cin, int Cout, int ldx, const BnPro& pro, hipStream_t s,
+                           const BnBwd* bw = nullptr) {
+  if (va && vb) conv_fwd_split_t<T, KS, PRO, true, true>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s, bw);
+  else if (va) conv_fwd_split_t<T, KS, PRO, true, false>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s, bw);
   else if (vb) conv_fwd_split_t<T, KS, PRO, false, true>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
   else conv_fwd_split_t<T, KS, PRO, false, false>(p, x, wt, part, M, H, W, Cin, Cout, ldx, pro, s);
 }
@@ -1986,7 +2050,7 @@ static void conv_fwd_split(bool va, bool vb, const SplitPlan& p, const void* x, 
 template <typename T>
 static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, const float* bias, void* y, void* ws,
                            float* stats, const BnGred* gr, int N, int H, int W, int Cin, int Cout, int ksize, int ldx,
-                           int ldy, hipStream_t s, const BnEpi* ep = nullptr) {
+                           int ldy, hipStream_t s, const BnEpi* ep = nullptr, const BnBwd* bw = nullptr) {
   const long M = (long)N * H * W;
   const int K = ksize * ksize * Cin;
   const int eV = Vec16<T>::N;
@@ -1999,7 +2063,7 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
   const BnPro pv = pro ? *pro : BnPro{};
   static const bool old_stem_fwd = getenv("ROD_DEBUG_OLDSTEMFWD") != nullptr;  // A/B against the VALU kernel
   if constexpr (sizeof(T) == 2) {
-    if (!pro && !gr && !ep && ksize == 3 && Cin == 3 && Cout == 32 && vy && !old_stem_fwd) {
+    if (!pro && !gr && !ep && !bw && ksize == 3 && Cin == 3 && Cout == 32 && vy && !old_stem_fwd) {
       const bool fuse = stats != nullptr && W % SW_TW == 0;  // block == stat tile
       // rows per block: >= ~4 blocks' worth per CU of rows, pipelined within a block
       const int xb = cdiv(W, SW_TW);
@@ -2019,7 +2083,7 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
     float* part = (float*)ws;
     if (ksize == 1) {
       if (pro) conv_fwd_split<T, 1, true>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
-      else conv_fwd_split<T, 1, false>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
+      else conv_fwd_split<T, 1, false>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s, bw);
     } else {
       if (pro) conv_fwd_split<T, 3, true>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
       else conv_fwd_split<T, 3, false>(va, vb, sp, x, wt, part, M, H, W, Cin, Cout, ldx, pv, s);
@@ -2053,14 +2117,15 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
   if constexpr (sizeof(T) == 2) {
     // the prologue form only for the block-to-block case it serves (K <= 32 input channels of a
     // project BatchNorm left pending: the 720p expand 16 -> 96)
-    if (!ep && ksize == 1 && !bias && va && vb && vy && (!pro || (K <= 32 && Cin <= PRO_MAXC)) &&
+    if (!ep && !bw && ksize == 1 && !bias && va && vb && vy && (!pro || (K <= 32 && Cin <= PRO_MAXC)) &&
         pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, gr, s,
                          pro ? &pv : nullptr))
       return;
   }
   if (ksize == 1) {
     if (pro) conv_fwd_dispatch<T, 1, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
-    else conv_fwd_dispatch<T, 1, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
+    else conv_fwd_dispatch<T, 1, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep,
+                                        bw);
   } else {
     if (pro) conv_fwd_dispatch<T, 3, true>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
     else conv_fwd_dispatch<T, 3, false>(va, vb, vy, x, wt, bias, y, M, H, W, Cin, Cout, ldx, ldy, stats, pv, gr, s, ep);
@@ -2200,6 +2265,27 @@ int rod_conv_fwd_bnact(const void* x, const float* pro_mean, const float* pro_rs
   conv_fwd_typed<bf16_t>(x, pro_mean ? &pro : nullptr, wt, bias, z, workspace, nullptr, nullptr, N, H, W, Cin, Cout,
                          ksize, ldx, ldy, ROD_STREAM(stream), &ep);
   return check_launch("rod_conv_fwd_bnact");
+}
+
+int rod_conv_bwd_data_bn_supported(int Cout, int Cin, int dtype) {
+  return dtype == ROD_BF16 && Cout % 8 == 0 && Cin % 8 == 0 && Cout <= 4096 ? 1 : 0;
+}
+
+int rod_conv_bwd_data_bn(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+                         const float* beta, int act, const float* coef, const void* wt1, void* dy, void* dx,
+                         void* workspace, long M, int Cout, int Cin, int dtype, void* stream) {
+  ROD_CHECK_ARG(M > 0 && rod_conv_bwd_data_bn_supported(Cout, Cin, dtype),
+                "rod_conv_bwd_data_bn: unsupported M=%ld Cout=%d Cin=%d dtype=%d", M, Cout, Cin, dtype);
+  ROD_CHECK_ARG(dz && y && mean && rstd && coef && wt1 && dy && dx, "rod_conv_bwd_data_bn: NULL argument");
+  ROD_CHECK_ARG(act >= ROD_ACT_NONE && act <= ROD_ACT_RELU, "rod_conv_bwd_data_bn: bad act %d", act);
+  ROD_CHECK_ARG(((((uintptr_t)dz) | ((uintptr_t)y) | ((uintptr_t)wt1) | ((uintptr_t)dy) | ((uintptr_t)dx)) & 15) == 0,
+                "rod_conv_bwd_data_bn: tensors must be 16-byte aligned");
+  ROD_CHECK_ARG(M <= 0x7fffffffL, "rod_conv_bwd_data_bn: M too large");
+  const BnBwd bw{(const bf16_t*)y, mean, rstd, gamma, beta, coef, act, (bf16_t*)dy};
+  // the GEMM dx[M][Cin] = dy[M][Cout] . wt1[Cin][Cout]^T: rod_conv_fwd's 1x1 form with K = Cout
+  conv_fwd_typed<bf16_t>(dz, nullptr, wt1, nullptr, dx, workspace, nullptr, nullptr, 1, 1, (int)M, Cout, Cin, 1, Cout,
+                         Cin, ROD_STREAM(stream), nullptr, &bw);
+  return check_launch("rod_conv_bwd_data_bn");
 }
 
 int rod_conv_weight_prep(const float* w, void* wt, int Cout, int Cin, int ksize, int mode, int dtype,

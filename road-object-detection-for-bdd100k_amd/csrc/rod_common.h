@@ -26,6 +26,7 @@ int check_launch(const char* what);
 // deferrable: a parameter-gradient sum that rod_slab_defer(1) may queue for rod_slab_flush (its
 // output is read by no kernel before the flush); false for sums a later kernel of the same call reads.
 void slab_sum(const float* slab, float* out, int nslab, long n, hipStream_t s, bool deferrable = true);
+int slab_cb(int nslab, long n);  // the column-block width slab_sum launches with
 // Grid size for a grid-stride loop over rows x CV channel vectors in which every thread
 // keeps ONE channel vector: (blocks * 256) % CV == 0 and blocks ~ target.
 int const_channel_blocks(int CV, long total, int target = 2048);

@@ -859,6 +859,31 @@ def _pw_fused_ok(M, Cin, Cout, dtype):
     return M >= 200_000 and Cout >= 2 * Cin and pw_bwd_supported(Cin, Cout, dtype)
 
 
+def _bwd_data_bn_ok(M, Cout, Cin, dtype, ipro):
+    # the opt-in gred form of the backward-data (ROD_ENABLE=gredpw, below) keeps the two-launch
+    # chain, and so do the shapes whose plain backward-data takes the K <= 96 streaming kernel
+    return "bnbwd" not in _DISABLE and not (ipro is not None and "gredpw" in _ENABLE) and \
+        bool(_abi.lib().rod_conv_bwd_data_bn_supported(int(Cout), int(Cin), _DT[dtype])) and \
+        not _abi.lib().rod_conv_fwd_stream_ok(int(M), int(Cout), int(Cin), _DT[dtype])
+
+
+def conv_bwd_data_bn(dz, y, mean, rstd, gamma, beta, act, coef, w):
+    """rod_conv_bwd_data_bn (ABI 22): (dy, dx) of a 1x1 conv + BatchNorm — dy the BatchNorm-
+    backward apply of (dz, y) (written), dx = dy . W — bit-identical to rod_bn_bwd_apply followed
+    by rod_conv_fwd with the mode-1 weights."""
+    N, H, W_, Cout = y.shape
+    Cin = w.shape[-1]
+    M = N * H * W_
+    wt1 = _prep(w, 1, y.dtype, Cout, Cin, 1)
+    dy = torch.empty_like(y)
+    dx = torch.empty((N, H, W_, Cin), dtype=y.dtype, device=y.device)
+    nb = 0 if "splitk" in _DISABLE else _abi.query("rod_conv_fwd_workspace", 1, 1, M, Cout, Cin, 1)
+    ws = workspace(nb, y.device) if nb else None
+    _abi.call("rod_conv_bwd_data_bn", dz.contiguous(), y, mean, rstd, gamma, beta, act, coef, wt1, dy, dx, ws, M,
+              Cout, Cin, dtcode(y), stream())
+    return dy, dx
+
+
 def _conv_bwd_from_dy(x, w, b, ks, dy, pro, need_dx):
     """rod_conv_fwd (mode-1 weights) for dx and rod_conv_wgrad for dw / db from a dense dy
     (the weight gradient on the side stream when SIDE is on)."""
@@ -1002,6 +1027,17 @@ class _ConvBN(torch.autograd.Function):
                 _mark_written(w)
             if _needs(b):
                 _mark_written(b)
+        elif ctx.ks == 1 and need_dx and (parts is not None or M > 4096 or SYNC_BN is not None) and \
+                _bwd_data_bn_ok(M, Cout, Cin, y.dtype, ctx.ipro):
+            # the deep expand convs (64 -> 384, 96 -> 576, 160 -> 960, conv_blocks.py:263-294): the
+            # backward-data GEMM forms dy = the BatchNorm-backward apply in its loader and writes it
+            # once for the weight gradient (rod_conv_bwd_data_bn) — no rod_bn_bwd_apply launch
+            if parts is not None:
+                coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))
+            else:
+                coef = bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+            dy, dx = conv_bwd_data_bn(dz, y, mean, rstd, gamma, beta, ctx.act, coef, w)
+            _conv_bwd_from_dy(x, w, b, ctx.ks, dy, ctx.ipro, False)
         else:
             if parts is not None:
                 coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))

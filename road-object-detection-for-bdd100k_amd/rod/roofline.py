@@ -90,6 +90,10 @@ def cost(name, a):
         res = es * M * Cout if a[15] is not None else 0
         return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[7] is not None else 0) + res, \
             2 * M * K * Cout + 5 * M * Cout
+    if name == "rod_conv_bwd_data_bn":    # BatchNorm-backward apply in the backward-data loader (ABI 22)
+        M, Cout, Cin, dt = a[12], a[13], a[14], a[15]
+        es = _ES[dt]
+        return es * (3 * M * Cout + M * Cin + Cin * Cout), 2 * M * Cout * Cin + 8 * M * Cout
     if name == "rod_conv_wgrad":
         N, H, W, Cin, Cout, ks, dt = a[10], a[11], a[12], a[13], a[14], a[15], a[18]
         es = _ES[dt]
@@ -235,6 +239,7 @@ ENTRY_KERNELS = {
     "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
     "rod_conv_fwd": (("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel"),
                      ("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel")),
+    "rod_conv_bwd_data_bn": (("conv_fwd_kernel",), ("conv_fwd_kernel",)),
     "rod_bn_finalize": (("bn_parts_merge_kernel",), ("bn_parts_merge_kernel",)),
     "rod_ir_block_fwd": (("ir_block_fwd_kernel",), ("ir_block_fwd_kernel",)),
 }
