@@ -1972,6 +1972,26 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
   }
 }
 
+// Epilogue of the packed depthwise backward kernels: the per-block column sums of the nq staged
+// quantities (the 9 filter taps, then with the BatchNorm sums g and g*yhat; red = [nq][TB][V]
+// floats, halo lanes staged as 0) — every (quantity, channel) summed over the computing columns
+// 1 .. P-2 in column order by one thread, after ONE barrier for all quantities (the
+// one-quantity-at-a-time form took two barriers a quantity with Cc of the TB threads working;
+// the sums, and so the parts, are bit-identical).
+template <int V>
+__device__ __forceinline__ void dw_colsum_emit(const float* red, int q0, int nq, int TB, int Cc, int CVb, int P,
+                                               float* slab, float* gparts, long part, int C, int cg) {
+  for (int e = threadIdx.x; e < nq * Cc; e += TB) {
+    const int qs = e / Cc, ce = e - qs * Cc, qk = q0 + qs;
+    const int cve = ce / V, v = ce - cve * V;
+    const float* r = red + qs * TB * V;
+    float s = 0.f;
+    for (int pp = 1; pp <= P - 2; ++pp) s += r[(pp * CVb + cve) * V + v];
+    float* dst = qk < 9 ? slab + (part * 9 + qk) * C : gparts + (part * 2 + (qk - 9)) * C;
+    dst[cg * Cc + ce] = s;
+  }
+}
+
 // Issue-lean form of dw3x3_bwd_fused_kernel (the default; ROD_DWF_V1=1 selects the one above).
 // Same engine, same per-element arithmetic and accumulation order (dx bit-identical), cut for
 // the instruction stream (tools/dwfused_bench.py PMC: the step was ~230 VALU + ~90 SALU per
@@ -2035,7 +2055,10 @@ struct DwPw {
   const bf16_t* wt1;   // [C][cout]: W_p^T, the project conv's mode-1 GEMM layout
   int cout;
 };
-constexpr int DWPW_LD = 52;   // LDS row stride (bf16) of the recomputed dz tile: <= 48 channels + pad
+constexpr int DWPW_LD = 52;
+#ifndef DW_QG_PW
+#define DW_QG_PW 6
+#endif   // LDS row stride (bf16) of the recomputed dz tile: <= 48 channels + pad
 
 // V = 2: the same tile with twice the threads (512 per block), each holding 2 channels — half the
 // per-thread weights, accumulators and BatchNorm constants, twice the waves in flight
@@ -2054,7 +2077,9 @@ __global__ void __launch_bounds__(1024 / V, PW ? 4 : 1) dw3x3_bwd_fused2_kernel(
   // slots, one per step of the 3-step body, so every LDS address is the thread's base plus a
   // compile-time offset
   constexpr int XS = 3 * 2 * TB * VP * (int)sizeof(dw_f2);
-  constexpr int SS = TB * V * 4;
+  // the epilogue's staged column sums: all at once (dw_colsum_emit), or — PW, whose main loop
+  // is at the 128-VGPR bound and spills with the one-barrier epilogue — DW_QG_PW at a time
+  constexpr int SS = (PW ? DW_QG_PW : (RED ? 11 : 9)) * TB * V * 4;
   __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
   dw_f2* xs = (dw_f2*)smem;
   dw_f2* dsl = xs + 3 * TB * VP;
@@ -2336,26 +2361,27 @@ __global__ void __launch_bounds__(1024 / V, PW ? 4 : 1) dw3x3_bwd_fused2_kernel(
   float* red = (float*)smem;
   const int Cc = CVb * V;
   const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
-  auto colsum = [&](const dw_f2 (&a)[VP], float* dst) {
+  constexpr int NQ = RED ? 11 : 9;
+  // quantities per staging round: all at once, or (PW, whose row loop runs at the 128-VGPR
+  // bound and spills with an all-at-once epilogue) QG_PW at a time
+  constexpr int QG = PW ? DW_QG_PW : NQ;
+  auto stage = [&](const dw_f2 (&a)[VP], int slot) {
 #pragma unroll
     for (int h = 0; h < VP; ++h) {
-      red[tid * V + 2 * h] = comp ? a[h].x : 0.f;
-      red[tid * V + 2 * h + 1] = comp ? a[h].y : 0.f;
+      red[(slot * TB + tid) * V + 2 * h] = comp ? a[h].x : 0.f;
+      red[(slot * TB + tid) * V + 2 * h + 1] = comp ? a[h].y : 0.f;
     }
-    __syncthreads();
-    for (int e = tid; e < Cc; e += TB) {
-      const int cve = e / V, v = e - cve * V;
-      float s = 0.f;
-      for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
-      dst[cg * Cc + e] = s;
-    }
-    __syncthreads();
   };
 #pragma unroll
-  for (int k = 0; k < 9; ++k) colsum(fa[k], slab + (part * 9 + k) * C);
-  if constexpr (RED) {
-    colsum(sg, gparts + part * 2 * C);
-    colsum(sgx, gparts + part * 2 * C + C);
+  for (int q0 = 0; q0 < NQ; q0 += QG) {
+#pragma unroll
+    for (int qk = q0; qk < q0 + QG && qk < NQ; ++qk) {
+      if (qk < 9) stage(fa[qk], qk - q0);
+      else if constexpr (RED) stage(qk == 9 ? sg : sgx, qk - q0);
+    }
+    __syncthreads();
+    dw_colsum_emit<V>(red, q0, (q0 + QG < NQ ? q0 + QG : NQ) - q0, TB, Cc, CVb, P, slab, gparts, part, C, cg);
+    if (q0 + QG < NQ) __syncthreads();
   }
 }
 
@@ -2616,7 +2642,7 @@ __global__ void __launch_bounds__(1024 / V, V == 4 ? 2 : 1) dw3x3_bwd_fused_s2p_
   static_assert(D >= 2, "one LDS slot per step of the D-step body");
   // slots [D][3][256][VP] fp32 pairs: dy, x row 0, x row 1 (column ci0)
   constexpr int XS = D * 3 * TB * VP * (int)sizeof(dw_f2);
-  constexpr int SS = TB * V * 4;
+  constexpr int SS = (RED ? 11 : 9) * TB * V * 4;   // the epilogue's staged column sums
   __shared__ __attribute__((aligned(16))) char smem[XS > SS ? XS : SS];
   dw_f2* sl = (dw_f2*)smem;
   const int tid = threadIdx.x;
@@ -2851,27 +2877,21 @@ __global__ void __launch_bounds__(1024 / V, V == 4 ? 2 : 1) dw3x3_bwd_fused_s2p_
   float* red = (float*)smem;
   const int Cc = CVb * V;
   const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
-  auto colsum = [&](const dw_f2 (&acc)[VP], float* dst) {
+  auto stage = [&](const dw_f2 (&a)[VP], int qk) {
 #pragma unroll
     for (int h = 0; h < VP; ++h) {
-      red[tid * V + 2 * h] = comp ? acc[h].x : 0.f;
-      red[tid * V + 2 * h + 1] = comp ? acc[h].y : 0.f;
+      red[(qk * TB + tid) * V + 2 * h] = comp ? a[h].x : 0.f;
+      red[(qk * TB + tid) * V + 2 * h + 1] = comp ? a[h].y : 0.f;
     }
-    __syncthreads();
-    for (int e = tid; e < Cc; e += TB) {
-      const int cve = e / V, v = e - cve * V;
-      float s = 0.f;
-      for (int pp = 1; pp <= P - 2; ++pp) s += red[(pp * CVb + cve) * V + v];
-      dst[cg * Cc + e] = s;
-    }
-    __syncthreads();
   };
 #pragma unroll
-  for (int k = 0; k < 9; ++k) colsum(fa[k], slab + (part * 9 + k) * C);
+  for (int k = 0; k < 9; ++k) stage(fa[k], k);
   if constexpr (RED) {
-    colsum(sg, gparts + part * 2 * C);
-    colsum(sgx, gparts + part * 2 * C + C);
+    stage(sg, 9);
+    stage(sgx, 10);
   }
+  __syncthreads();
+  dw_colsum_emit<V>(red, 0, RED ? 11 : 9, TB, Cc, CVb, P, slab, gparts, part, C, cg);
 }
 
 // Both strides tile a map with one halo column each side (the S=1 plan geometry): stride 1
