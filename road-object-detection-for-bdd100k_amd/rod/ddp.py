@@ -139,8 +139,21 @@ class GradReducer(object):
             if st not in b['streams']:
                 b['streams'].append(st)
         b['pending'] -= 1
-        if b['pending'] == 0:
+        if b['pending'] == 0 and not self._on_chain_stream(p):
             self._launch(b)
+
+    @staticmethod
+    def _on_chain_stream(p):
+        """A gradient written on a detector-head chain stream (ops.LEVELS): a bucket completed
+        there is launched after backward, from the stream that runs the optimizer (__call__).
+        Forking the communication stream from a chain stream crashed the end of a HIP-graph
+        capture (hipStreamEndCapture, a segfault inside the runtime; tests/native_comm_worker.py
+        with ROD_HEAD_STREAMS=3), while the same step with the chains on the calling stream, or
+        with those buckets deferred, captures and replays bit-identically."""
+        if not (torch.cuda.is_available() and p.is_cuda):
+            return False
+        from . import ops
+        return torch.cuda.current_stream(p.device) in ops.LEVELS.pool.values()
 
     def spans(self):
         """The buckets' ranges of the flat gradient merged where they touch: [(lo, hi)]."""
@@ -216,14 +229,18 @@ class _Done(object):
 
 
 class _Joined(object):
-    """A bucket summed on the communication stream: wait() makes the compute stream wait for
-    it (an event edge — a graph dependency under capture), no host synchronisation."""
+    """A bucket summed on the communication stream: wait() makes the stream current at the
+    wait — the one that runs the optimizer step — wait for it (an event edge: a graph
+    dependency under capture), no host synchronisation.  Not the stream current at the launch:
+    a bucket is launched from inside backward, possibly on a detector-head chain stream
+    (ops.LEVELS) that nothing joins afterwards; joining the communication stream there left it
+    unjoined at the end of a HIP-graph capture (a crash in capture_end)."""
 
     def __init__(self, done, stream):
-        self.done, self.stream = done, stream
+        self.done, self.device = done, stream.device
 
     def wait(self):
-        self.stream.wait_event(self.done)
+        torch.cuda.current_stream(self.device).wait_event(self.done)
 
 
 def allgather(t, world, group=None, native=False):

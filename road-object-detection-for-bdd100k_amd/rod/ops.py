@@ -111,7 +111,9 @@ class LevelStreams:
         self.used = []
 
     def active(self, t):
-        return self.n > 0 and torch.is_tensor(t) and t.is_cuda
+        # not under SyncBatchNorm: its statistics all-gathers would run on the chain streams
+        # concurrently, and one RCCL communicator must not be driven from several streams at once
+        return self.n > 0 and SYNC_BN is None and torch.is_tensor(t) and t.is_cuda
 
     def stream(self, i, device):
         key = (str(device), i % self.n)
