@@ -219,9 +219,22 @@ def design_bytes(name, a):
     return cost(name, a)[0]
 
 
-# C-ABI entry -> (kernel-name substrings of which exactly one launches once per entry call,
-# substrings of every kernel the entry launches) for attributing rocprofv3 PMC counters
-# (tools/pmc_traffic.py); shared helper kernels (slab_sum, splitk_combine) are not attributed
+def kernel_match(name, pat):
+    """pat = 'a&b!c': the kernel name contains a and b and not c (demangled or mangled names: the
+    rocprofv3 CSVs hold both forms, e.g. '..., 2, 3, true>(' / '...Li2ELi3ELb1EE...')."""
+    inc, *exc = pat.split('!')
+    return all(t in name for t in inc.split('&')) and not any(t in name for t in exc)
+
+
+# template-argument tails that tell apart kernels of one name: the depthwise backward's
+# recompute form (PW, ABI 20) and the backward-data BatchNorm prologue (BWD, ABI 22)
+_PW = ('2, 3, true>', 'Li2ELi3ELb1EE')
+_BWD = ('32, false, true>', 'Li32ELb0ELb1EE')
+
+# C-ABI entry -> (kernel patterns of which exactly one launches once per entry call, patterns
+# of every kernel the entry launches; kernel_match) for attributing rocprofv3 PMC counters
+# (tools/pmc_traffic.py); shared helper kernels (slab_sum, splitk_combine) are not attributed.
+# rod_pw_bwd_gred and _dyp run the same kernel (dyp is an argument): PMC cannot tell them apart
 ENTRY_KERNELS = {
     # rod_bn_bwd runs only on small tensors on the training path (ops.bn_bwd_dy): the one-launch kernel
     "rod_bn_bwd": (("bn_bwd_small_kernel",), ("bn_bwd_small_kernel",)),
@@ -234,12 +247,12 @@ ENTRY_KERNELS = {
     "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),
-    "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused",), ("dw3x3_bwd_fused",)),
-    "rod_dw3x3_bwd_fused_pw": (("dw3x3_bwd_fused2",), ("dw3x3_bwd_fused2",)),
+    "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused!" + "!".join(_PW),), ("dw3x3_bwd_fused!" + "!".join(_PW),)),
+    "rod_dw3x3_bwd_fused_pw": tuple(tuple("dw3x3_bwd_fused2&" + t for t in _PW) for _ in range(2)),
     "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
-    "rod_conv_fwd": (("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel"),
-                     ("conv_fwd_kernel", "stem_fwd_mfma_kernel", "pw_stream_kernel")),
-    "rod_conv_bwd_data_bn": (("conv_fwd_kernel",), ("conv_fwd_kernel",)),
+    "rod_conv_fwd": (("conv_fwd_kernel!" + "!".join(_BWD), "stem_fwd_mfma_kernel", "pw_stream_kernel"),
+                     ("conv_fwd_kernel!" + "!".join(_BWD), "stem_fwd_mfma_kernel", "pw_stream_kernel")),
+    "rod_conv_bwd_data_bn": tuple(tuple("conv_fwd_kernel&" + t for t in _BWD) for _ in range(2)),
     "rod_bn_finalize": (("bn_parts_merge_kernel",), ("bn_parts_merge_kernel",)),
     "rod_ir_block_fwd": (("ir_block_fwd_kernel",), ("ir_block_fwd_kernel",)),
 }

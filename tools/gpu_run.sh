@@ -87,6 +87,13 @@ for step in "$@"; do
         f=$(ls $OUT/c5f_$TAG/*counter_collection.csv) && w=$(ls $OUT/c5w_$TAG/*counter_collection.csv) && m=$(ls $OUT/c5m_$TAG/*counter_collection.csv) &&
         python tools/c5_report.py pmc $OUT/${TAG}_c5_probe.json $f $w $m --out $OUT/${TAG}_c5_report.json &&
         gzip -f $f $w $m ;;
+    c5b32) run c5b32probe 300 python tools/c5_report.py probe --res 1080 --batch 32 --out $OUT/${TAG}_c5b32_probe.json &&
+        run c5b32f 200 timeout -s KILL 190 rocprofv3 --pmc FETCH_SIZE -d $OUT/c5b32f_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 32 --iters 2 --no-graph &&
+        run c5b32w 200 timeout -s KILL 190 rocprofv3 --pmc WRITE_SIZE -d $OUT/c5b32w_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 32 --iters 2 --no-graph &&
+        run c5b32m 200 timeout -s KILL 190 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/c5b32m_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 32 --iters 2 --no-graph &&
+        f=$(ls $OUT/c5b32f_$TAG/*counter_collection.csv) && w=$(ls $OUT/c5b32w_$TAG/*counter_collection.csv) && m=$(ls $OUT/c5b32m_$TAG/*counter_collection.csv) &&
+        python tools/c5_report.py pmc $OUT/${TAG}_c5b32_probe.json $f $w $m --out $OUT/${TAG}_c5b32_report.json &&
+        gzip -f $f $w $m ;;
     irpmc) run irpmc 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU -d $OUT/irpmc_$TAG -o run --output-format csv -- python3 tools/irblock_bench.py --iters 3 --res 1080 &&
            python tools/pmc_kernel_summary.py $OUT/irpmc_$TAG/run_counter_collection.csv ir_block_fwd > $OUT/${TAG}_irpmc.txt &&
            gzip -f $OUT/irpmc_$TAG/run_counter_collection.csv && cat $OUT/${TAG}_irpmc.txt ;;

@@ -19,7 +19,7 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..',
                                 'road-object-detection-for-bdd100k_amd'))
-from rod.roofline import ENTRY_KERNELS  # noqa: E402
+from rod.roofline import ENTRY_KERNELS, kernel_match  # noqa: E402
 
 
 def per_kernel(path, counter):
@@ -42,11 +42,11 @@ def main():
            'config': [sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7]), sys.argv[8]]
            if len(sys.argv) > 8 else ['REFINE', 8, 720, 1280, 'bf16']}
     for entry, (anchors, kernels) in ENTRY_KERNELS.items():
-        n = sum(c for k, (c, _) in fetch.items() if any(a in k for a in anchors))
+        n = sum(c for k, (c, _) in fetch.items() if any(kernel_match(k, a) for a in anchors))
         if n == 0:
             continue
-        rd = sum(b for k, (_, b) in fetch.items() if any(s in k for s in kernels)) * 2.0
-        wr = sum(b for k, (_, b) in write.items() if any(s in k for s in kernels))
+        rd = sum(b for k, (_, b) in fetch.items() if any(kernel_match(k, s) for s in kernels)) * 2.0
+        wr = sum(b for k, (_, b) in write.items() if any(kernel_match(k, s) for s in kernels))
         out['entries'][entry] = {'launches': n, 'read_bytes_per_launch': rd / n, 'write_bytes_per_launch': wr / n,
                                  'bytes_per_launch': (rd + wr) / n, 'kernels': list(kernels)}
     json.dump(out, open(sys.argv[3], 'w'), indent=1)
