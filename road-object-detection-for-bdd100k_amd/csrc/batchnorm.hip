@@ -12,6 +12,8 @@
 // 16-byte channel vector for the whole grid-stride loop (grid*256 is a multiple of the
 // channel-vector count), so the per-channel parameters live in registers and each
 // iteration is one 16-byte load per operand and one 16-byte store.
+#include <mutex>
+
 #include "rod_common.h"
 
 namespace rod {
@@ -216,25 +218,32 @@ static MergePlan merge_plan(int C, int nparts) {
 // channel (the mean of the slice's first non-empty part), every part contributes
 // n, S1 = n*(mean-k), S2 = M2 + n*(mean-k)^2 in f64; lanes and then the block's part lanes
 // are added in a fixed order, and the slice's (n, mean, M2) = (n, k + S1/n, S2 - S1^2/n).
-__global__ void __launch_bounds__(MERGE_T) bn_parts_merge_kernel(const float* __restrict__ parts, int nparts, int C, int CB,
-                                                             int slice, float* __restrict__ out, long M, float eps,
-                                                             float decay, float* __restrict__ mean,
-                                                             float* __restrict__ rstd, float* __restrict__ mmean,
-                                                             float* __restrict__ mvar) {
-  __shared__ double sn[MERGE_T], s1[MERGE_T], s2[MERGE_T];
-  __shared__ float piv[64];
+// One block's work: slice bx of the parts, channels [by*CB, (by+1)*CB); its part goes to part
+// bx of `out`, or (last) mean, rstd and the moving averages.  Slice parts are stored with
+// agent-scope (L2-coherent across the XCDs) stores, and COH reads them the same way: the
+// single-launch second level reads parts other blocks of the same launch wrote, with no
+// whole-cache write-back / invalidate (an agent-scope fence per block cost more than the launch
+// it saves: 93 launches at 13.5 us against 124 at 5.7 us).
+__device__ __forceinline__ float merge_ld(const float* p, bool coh) {
+  return coh ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+}
+template <bool COH>
+__device__ __forceinline__ void merge_slice(const float* parts, int nparts, int C, int CB, int slice, int bx, int by,
+                                            bool last, float* out, long M, float eps, float decay, float* mean,
+                                            float* rstd, float* mmean, float* mvar, double* sn, double* s1,
+                                            double* s2, float* piv) {
   const int tid = threadIdx.x;
   const int PL = MERGE_T / CB;
   const int cl = tid % CB, pl = tid / CB;
-  const int c = blockIdx.y * CB + cl;
+  const int c = by * CB + cl;
   const bool ok = pl < PL && c < C;
-  const int b0 = blockIdx.x * slice;
+  const int b0 = bx * slice;
   const int b1 = b0 + slice < nparts ? b0 + slice : nparts;
   if (pl == 0 && c < C) {  // pivot: mean of the first non-empty part of the slice
     float k = 0.f;
     for (int b = b0; b < b1; ++b) {
-      if (parts[(long)b * 3 * C + c] != 0.f) {
-        k = parts[(long)b * 3 * C + C + c];
+      if (merge_ld(parts + (long)b * 3 * C + c, COH) != 0.f) {
+        k = merge_ld(parts + (long)b * 3 * C + C + c, COH);
         break;
       }
     }
@@ -247,12 +256,12 @@ __global__ void __launch_bounds__(MERGE_T) bn_parts_merge_kernel(const float* __
 #pragma unroll 4
     for (int b = b0 + pl; b < b1; b += PL) {
       const float* p = parts + (long)b * 3 * C + c;
-      const double nb = (double)p[0];
-      const double d = (double)p[C] - k;
+      const double nb = (double)merge_ld(p, COH);
+      const double d = (double)merge_ld(p + C, COH) - k;
       const double q = nb * d;
       n += nb;
       a1 += q;
-      a2 += (double)p[2 * C] + q * d;
+      a2 += (double)merge_ld(p + 2 * C, COH) + q * d;
     }
   }
   sn[tid] = n;
@@ -299,8 +308,11 @@ __global__ void __launch_bounds__(MERGE_T) bn_parts_merge_kernel(const float* __
     const double k = (double)piv[cl];
     const double mu = n > 0.0 ? k + a1 / n : 0.0;
     const double m2 = n > 0.0 ? fmax(a2 - a1 * a1 / n, 0.0) : 0.0;
-    if (gridDim.x > 1) {
-      store_stat_part(out, C, blockIdx.x, c, (float)n, (float)mu, (float)m2);
+    if (!last) {
+      float* o = out + (long)bx * 3 * C + c;
+      __hip_atomic_store(o, (float)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + C, (float)mu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + 2 * C, (float)m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
     const double var = m2 / (double)M;
@@ -318,25 +330,103 @@ __global__ void __launch_bounds__(MERGE_T) bn_parts_merge_kernel(const float* __
   }
 }
 
+__global__ void __launch_bounds__(MERGE_T) bn_parts_merge_kernel(const float* parts, int nparts, int C, int CB,
+                                                             int slice, float* out, long M, float eps,
+                                                             float decay, float* __restrict__ mean,
+                                                             float* __restrict__ rstd, float* __restrict__ mmean,
+                                                             float* __restrict__ mvar, unsigned* cnt, int slice2) {
+  __shared__ double sn[MERGE_T], s1[MERGE_T], s2[MERGE_T];
+  __shared__ float piv[64];
+  __shared__ int is_last;
+  const bool one = gridDim.x == 1;
+  merge_slice<false>(parts, nparts, C, CB, slice, blockIdx.x, blockIdx.y, one, out, M, eps, decay, mean, rstd, mmean, mvar,
+              sn, s1, s2, piv);
+  if (cnt == nullptr || one) return;
+  // Second level in the same launch: the last block of channel group blockIdx.y to finish merges
+  // the gridDim.x slice parts as one slice of the next level's plan — the grouping and order of a
+  // second launch (bit-identical to it), without the launch.  The part's agent-scope stores have
+  // completed (vmcnt 0, before the barrier) when the block counts itself; the last block reads the
+  // parts with agent-scope loads issued after it has seen the count.
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = prev == gridDim.x - 1;
+    // self-cleaning: the counter is zero again for the next call (and every graph replay)
+    if (is_last) __hip_atomic_store(cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  merge_slice<true>(out, gridDim.x, C, CB, slice2, 0, blockIdx.y, true, nullptr, M, eps, decay, mean, rstd, mmean, mvar, sn,
+              s1, s2, piv);
+}
+
 // merge levels until one part remains; ws holds two ping-pong part buffers
 static size_t finalize_ws_bytes(int nparts, int C) {
   const MergePlan p = merge_plan(C, nparts);
   const int s1 = cdiv(nparts, p.slice);
   return s1 > 1 ? 2 * (size_t)s1 * 3 * C * sizeof(float) : 0;
 }
+// Zero-initialised per-device arrival counters of the single-launch two-level merge, handed out
+// round-robin (a 720p training step takes ~1,300 of the 65,536, so calls that may run at the same
+// time on the head-chain streams never share one); each counter is zero again when its launch
+// ends.  The pool is allocated on first use outside a stream capture; a call captured before
+// that falls back to two launches.  ROD_MERGE_TWO_LAUNCH=1 (read per call): always two launches.
+static unsigned* merge_counters(int n, hipStream_t s) {
+  const char* e = getenv("ROD_MERGE_TWO_LAUNCH");
+  if (e != nullptr && atoi(e) == 1) return nullptr;
+  constexpr int POOL = 1 << 16, MAXDEV = 64;
+  static unsigned* base[MAXDEV] = {};
+  static int next[MAXDEV] = {};
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (base[dev] == nullptr) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, POOL * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, POOL * sizeof(unsigned), s) != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    (void)hipStreamSynchronize(s);   // zeroed before any other stream takes a counter
+    base[dev] = (unsigned*)p;
+  }
+  if (next[dev] + n > POOL) next[dev] = 0;
+  unsigned* r = base[dev] + next[dev];
+  next[dev] += n;
+  return r;
+}
+
 static void finalize_launch(const float* parts, int nparts, long M, int C, float eps, float decay, float* mean,
                             float* rstd, float* mm, float* mv, float* ws, hipStream_t s) {
   const MergePlan p0 = merge_plan(C, nparts);
   const int s1 = cdiv(nparts, p0.slice);
-  static const bool dbg = getenv("ROD_DEBUG_MERGE") != nullptr;
-  if (dbg) fprintf(stderr, "rod merge: nparts %d C %d M %ld levels %d\n", nparts, C, M, s1 > 1 ? 2 : 1);
   float* buf[2] = {ws, ws ? ws + (size_t)s1 * 3 * C : nullptr};
+  unsigned* cnt = nullptr;
+  int slice2 = 0;
+  if (s1 > 1) {
+    // two levels in one launch when the second is one slice with the same channel blocks
+    const MergePlan p1 = merge_plan(C, s1);
+    if (p1.CB == p0.CB && s1 <= p1.slice && (cnt = merge_counters(cdiv(C, p0.CB), s)) != nullptr) slice2 = p1.slice;
+  }
+  static const bool dbg = getenv("ROD_DEBUG_MERGE") != nullptr;
+  if (dbg)
+    fprintf(stderr, "rod merge: nparts %d C %d M %ld levels %d launches %d\n", nparts, C, M, s1 > 1 ? 2 : 1,
+            s1 > 1 && cnt == nullptr ? 2 : 1);
+  if (cnt != nullptr) {
+    hipLaunchKernelGGL(bn_parts_merge_kernel, dim3(s1, cdiv(C, p0.CB)), dim3(MERGE_T), 0, s, parts, nparts, C, p0.CB,
+                       p0.slice, buf[0], M, eps, decay, mean, rstd, mm, mv, cnt, slice2);
+    return;
+  }
   int k = 0;
   while (true) {
     const MergePlan p = merge_plan(C, nparts);
     const int S = cdiv(nparts, p.slice);
     hipLaunchKernelGGL(bn_parts_merge_kernel, dim3(S, cdiv(C, p.CB)), dim3(MERGE_T), 0, s, parts, nparts, C, p.CB, p.slice,
-                       S > 1 ? buf[k] : nullptr, M, eps, decay, mean, rstd, mm, mv);
+                       S > 1 ? buf[k] : nullptr, M, eps, decay, mean, rstd, mm, mv, (unsigned*)nullptr, 0);
     if (S == 1) break;
     parts = buf[k];
     nparts = S;

@@ -538,12 +538,14 @@ def test_pw_stream_prologue(dev, act):
     _fused_vs_materialised(dev, torch.bfloat16, (1, 257, 259, 16), act, True, consumer, 22)
 
 
-@pytest.mark.parametrize('nparts,C', [(1, 16), (700, 16), (5000, 16), (57600, 16), (3000, 96), (900, 200), (40000, 1280)])
-def test_bn_finalize_many_parts(dev, nparts, C):
+@pytest.mark.parametrize('nparts,C', [(1, 16), (700, 16), (5000, 16), (57600, 16), (3000, 96), (900, 200), (40000, 1280),
+                                     (70000, 64)])
+def test_bn_finalize_many_parts(dev, nparts, C, monkeypatch):
     """rod_bn_finalize over a producer's partial statistics (count, mean, M2 per part; one to
-    57,600 parts, so one to three merge levels) against a float64 Chan merge, incl. empty parts;
+    70,000 parts, so one to three merge levels) against a float64 Chan merge, incl. empty parts;
     repeated calls on the same parts are bit-identical, and so are calls inside a replayed
-    graph."""
+    graph, calls on three streams at once, and the two-level merge in one launch (last-block
+    hand-off) against the same two levels in two launches (ROD_MERGE_TWO_LAUNCH=1)."""
     from rod import _abi
     from rod.ops import workspace, stream
     g = torch.Generator().manual_seed(nparts + C)
@@ -586,3 +588,24 @@ def test_bn_finalize_many_parts(dev, nparts, C):
         torch.cuda.synchronize()
         for u, v in zip(a, c):
             assert torch.equal(u, v)
+    # three streams at once, each with its own workspace (distinct arrival counters)
+    wss = [workspace(nb, dev) if nb else None for _ in range(3)]
+    outs = []
+    sts = [torch.cuda.Stream() for _ in range(3)]
+    for st, w in zip(sts, wss):
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            for _ in range(4):
+                mo, ro = torch.empty(C, device=dev), torch.empty(C, device=dev)
+                mm, mv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+                _abi.call("rod_bn_finalize", pd, nparts, M, C, 1e-3, 0.9, mo, ro, mm, mv, w, stream())
+                outs.append((mo, ro, mm, mv))
+    torch.cuda.synchronize()
+    for o in outs:
+        for u, v in zip(a, o):
+            assert torch.equal(u, v)
+    monkeypatch.setenv('ROD_MERGE_TWO_LAUNCH', '1')
+    d = run()
+    torch.cuda.synchronize()
+    for u, v in zip(a, d):
+        assert torch.equal(u, v)

@@ -59,11 +59,20 @@ def probe(a):
     rows = {}
     for name, (n, ms, b, fl) in _abi.PROBE.table().items():
         rows[name] = {'launches': n / a.iters, 'ms': ms / a.iters, 'alg_bytes': b / a.iters, 'alg_flops': fl / a.iters}
+    by_shape = _abi.PROBE.table(by_shape=True)
     shapes = [{'entry': k[0], 'args': list(k[1]), 'launches': v[0] / a.iters, 'ms': v[1] / a.iters}
-              for k, v in _abi.PROBE.table(by_shape=True).items() if k[0] == 'rod_ir_block_fwd']
+              for k, v in by_shape.items() if k[0] == 'rod_ir_block_fwd']
+    # the conv family per call shape (scalar args: M / N, H, W, Cin, Cout, ks ...), slowest first
+    convs = sorted(({'entry': k[0], 'args': list(k[1]), 'launches': v[0] / a.iters, 'ms': v[1] / a.iters,
+                     'alg_GBps': v[2] / max(v[1], 1e-9) * 1e-6, 'alg_TFLOPs': v[3] / max(v[1], 1e-9) * 1e-9}
+                    for k, v in by_shape.items() if k[0] in ('rod_conv_fwd', 'rod_conv_fwd_bnact')),
+                   key=lambda r: -r['ms'])
     out = {'img_hw': [H, W], 'batch': a.batch, 'iters': a.iters, 'eager_ms_per_batch': dt * 1e3,
-           'entries': rows, 'ir_block_calls': shapes}
+           'entries': rows, 'ir_block_calls': shapes, 'conv_calls': convs}
     json.dump(out, open(a.out, 'w'), indent=1)
+    for r in convs[:25]:
+        print('%-20s %-60s x%.0f %7.3f ms %7.0f GB/s %6.1f TF' % (r['entry'], r['args'], r['launches'], r['ms'],
+                                                               r['alg_GBps'], r['alg_TFLOPs']))
     print(json.dumps({k: round(v['ms'], 3) for k, v in sorted(rows.items(), key=lambda kv: -kv[1]['ms'])[:8]}))
 
 

@@ -30,6 +30,9 @@ for step in "$@"; do
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
     clitest) run clitest 400 python -m pytest tests/test_gpu_fullsize.py -m gpu -q -k cli --timeout=300 -p no:cacheprovider ;;
+    merge) run merge 400 python -u -m pytest tests/test_gpu_merge.py tests/test_gpu_kernels.py tests/test_gpu_defer.py -k "merge or finalize or defer" -m gpu -v --timeout=300 --timeout-method thread -p no:cacheprovider &&
+        run mergedbg 300 env ROD_DEBUG_MERGE=1 python bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 ;;
+    abmerge) for i in 1 2; do run abm2_$i 300 env ROD_MERGE_TWO_LAUNCH=1 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abm1_$i 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done; grep -h '"value"' $OUT/${TAG}_abm*.log | cut -c1-60 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchfast) run benchfast 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
@@ -80,6 +83,7 @@ for step in "$@"; do
     cbhead) run cbhead 300 python tools/conv_bench.py --shapes 7,13,14,15 ;;
     cball) run cball 300 python tools/conv_bench.py ;;
     convtests) run convtests 600 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_stem.py -m gpu -q -x --timeout=300 -p no:cacheprovider ;;
+    c5probe) run c5probe 300 python tools/c5_report.py probe --res 1080 --batch 8 --out $OUT/${TAG}_c5_probe.json ;;
     c5) run c5probe 300 python tools/c5_report.py probe --res 1080 --batch 8 --out $OUT/${TAG}_c5_probe.json &&
         run c5f 130 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/c5f_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 3 --no-graph &&
         run c5w 130 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/c5w_$TAG -o run --output-format csv -- python3 tools/predict_bench.py --res 1080 --batch 8 --iters 3 --no-graph &&
