@@ -815,15 +815,22 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 // No block barrier after the weight staging.
 // =====================================================================================
 constexpr int PWS_WAVES = 4;
-// PRO (KT == 1): the BatchNorm-apply prologue on x — act(fma(x, scale, offset)) rounded to bf16,
-// the value rod_bn_apply would have written — with the lane's 8 channels' constants in registers
-// (its k range is fixed: 8*(lane >> 4)); rows past M stay 0
-template <int NT, int KT, int MODE, bool PRO = false>
-__global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+// PRO: the BatchNorm-apply prologue on x — act(fma(x, scale, offset)) rounded to bf16, the value
+// rod_bn_apply would have written.  KT == 1: the lane's 8 channels' constants in registers (its k
+// range is fixed: 8*(lane >> 4)); KT > 1 (the projects, K = 96 .. 192): a [K][2] LDS table read
+// per chunk, the tiled kernel's Chunk8::pro_t (the same rounding), its activation a template
+// argument (ReLU6, the projects' depthwise BatchNorm: a runtime switch there kept every variant's
+// table reads live, 150-190 VGPRs).  Rows past M stay 0.
+// Cout need not fill the last 16-wide N tile (Cout % 8 == 0: the 24-channel projects): weight
+// rows past Cout are zero, their columns are neither stored nor counted.
+// (KT >= 5 with the table prologue: at least 4 waves per SIMD, 128 VGPRs — unbounded the compiler
+// took 144-172 and 2 waves per SIMD)
+template <int NT, int KT, int MODE, bool PRO = false, int PACT = ROD_ACT_RELU6>
+__global__ void __launch_bounds__(256, (PRO && KT >= 5) ? 4 : 1) pw_stream_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                                                         bf16_t* __restrict__ Y, long M, int K, int Cout, int ldx,
                                                         int ldy, float* __restrict__ part, BnGred gr,
                                                         BnPro pro = BnPro{}) {
-  static_assert(!PRO || KT == 1, "the prologue constants cover one 32-deep k step");
+  static_assert(!PRO || MODE != 2, "the prologue form has no gred epilogue");
   constexpr int NP = NT * 16;       // columns of the N group
   constexpr int LDB = KT * 32 + 8;  // weight row stride in LDS (elements)
   constexpr int LDC = NP + 8;       // staging row stride (elements; 16-byte multiple)
@@ -834,14 +841,17 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
   constexpr bool STATS = MODE == 1, GRED = MODE == 2;
   __shared__ __attribute__((aligned(16))) bf16_t Bs[NP * LDB];
   __shared__ __attribute__((aligned(16))) bf16_t Cs[PWS_WAVES][16 * LDC];
+  constexpr bool PTAB = PRO && KT > 1;
+  __shared__ __attribute__((aligned(16))) float Pt[PTAB ? KT * 32 * 2 : 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, lg = lane >> 4;
   const int n0 = blockIdx.y * NP;
 
-  for (int idx = tid; idx < NP * KT * 4; idx += 256) {  // weights -> LDS, k >= K zero
+  if constexpr (PTAB) stage_pro(Pt, pro, K);
+  for (int idx = tid; idx < NP * KT * 4; idx += 256) {  // weights -> LDS, k >= K / rows >= Cout zero
     const int r = idx / (KT * 4), k = (idx - r * (KT * 4)) * 8;
     bf16x8 v;
-    if (k < K) v = *(const bf16x8*)(Wt + (long)(n0 + r) * K + k);
+    if (k < K && n0 + r < Cout) v = *(const bf16x8*)(Wt + (long)(n0 + r) * K + k);
     else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (bf16_t)0.f;
@@ -868,8 +878,8 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
     }
   }
 
-  float psc[PRO ? 8 : 1], psh[PRO ? 8 : 1];
-  if constexpr (PRO) {
+  float psc[PRO && !PTAB ? 8 : 1], psh[PRO && !PTAB ? 8 : 1];
+  if constexpr (PRO && !PTAB) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int k = lg * 8 + e;
@@ -892,7 +902,9 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
   };
   // the prologue on a loaded fragment (at use, so the load stays in flight meanwhile)
   auto pro_a = [&](bf16x8 (&a)[KT], long tile, int s) {
-    if constexpr (PRO) {
+    if constexpr (PTAB) {
+      // applied per k step inside the MFMA loop (pro_k): one chunk's table reads live at a time
+    } else if constexpr (PRO) {
       const bool ok = tile * 128 + s * 16 + fr < M && lg * 8 < K;
       if (pro.act == ROD_ACT_NONE) {   // the linear (project) BatchNorm: packed pairs, one rounding each
         typedef float pf2 __attribute__((ext_vector_type(2)));
@@ -913,6 +925,14 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
           a[0][e] = ok ? (bf16_t)act_fwd(fmaf((float)a[0][e], psc[e], psh[e]), pro.act) : (bf16_t)0.f;
       }
     }
+  };
+  auto pro_k = [&](bf16x8& a, bool rok, int kt) {
+    const int k = kt * 32 + lg * 8;
+    Chunk8<bf16_t> c;
+    c.v = a;
+    if (rok && k < K) c.template pro_t<PACT>(Pt, k);
+    else c.zero();
+    a = c.v;
   };
   // gred: this lane's rows of gr.y for the sub-step starting at row rs (one sub-step ahead)
   auto load_y = [&](bf16x8 (&yv)[GRED ? JN : 1], long rs) {
@@ -954,12 +974,17 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
 #pragma unroll
       for (int b = 0; b < NT; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt)
+      for (int kt = 0; kt < KT; ++kt) {
+        if constexpr (PTAB) {
+          pro_k(ab[kt], rs + fr < M, kt);
+          asm volatile("" ::: "memory");   // the next chunk's table reads stay after this step
+        }
 #pragma unroll
         for (int b = 0; b < NT; ++b) {
           const bf16x8 bf = *(const bf16x8*)(Bs + (b * 16 + fr) * LDB + kt * 32 + lg * 8);
           acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab[kt], bf, acc[b], 0, 0, 0);
         }
+      }
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) ab[kt] = an[kt];
       // epilogue, one 16-wide N tile at a time: round once (the statistics and the staged value
@@ -1017,7 +1042,7 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
           if ((16 * CPR) % 64 != 0 && idx >= 16 * CPR) break;
           const int rr = idx / CPR, c8 = idx - rr * CPR;
           const u32x4 v = *(const u32x4*)(cs + rr * LDC + c8 * 8);
-          if (rs + rr < M) ROD_ST_OUT((u32x4*)(Y + (rs + rr) * ldy + n0 + c8 * 8), v);
+          if (rs + rr < M && n0 + c8 * 8 < Cout) ROD_ST_OUT((u32x4*)(Y + (rs + rr) * ldy + n0 + c8 * 8), v);
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -1035,7 +1060,7 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(const bf16_t* __restrict
         q += __shfl_xor(q, 16, 64);
         a += __shfl_xor(a, 32, 64);
         q += __shfl_xor(q, 32, 64);
-        if (lane < 16) {
+        if (lane < 16 && n0 + b * 16 + lane < Cout) {
           const float dm = full ? a * (1.0f / 128.0f) : a / n;
           store_stat_part(part, Cout, t, n0 + b * 16 + lane, n, piv[b] + dm, fmaxf(q - a * dm, 0.f));
         }
@@ -1129,6 +1154,55 @@ static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long 
   PWK(2) PWK(3) PWK(4) PWK(6) PWK(8) PWK(9) PWK(12)
 #undef PWK
 #undef PWS
+  return false;
+}
+
+// The projects (the streaming form past K = 96): a 1x1 conv whose input
+// BatchNorm is still pending (the prologue), K = 40 .. 192 input channels (ReLU6 prologue), Cout = 16 .. 32 outputs
+// (one N group of 1 or 2 MFMA tiles), M >= 65536 rows, with or without the statistics epilogue.
+// tools/conv_bench.py (fwd_stats, 8 images): 96 -> 24 at 360x640 100 -> 95 us, 144 -> 24 162 -> 139,
+// 192 -> 32 at 180x320 44 -> 42, 144 -> 32 44 -> 36 (3.7-4.7 -> 4.5-5.0 TB/s).
+// The tiled kernel ran these at 3.5-4.5 TB/s: a 128 x 32 output tile per block behind two barriers
+// per 32-deep k step.  Here each wave streams its 16-row sub-steps with all KT A fragments in
+// flight and no block barrier.  y is bit-identical (the same MFMA k order and prologue rounding);
+// the statistics parts are per 128-row tile as before, summed in another order.
+// ROD_PW_PROJ=0 turns it off (A/B switch).
+static bool pw_proj_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long M, int K, int Cout, int ldx, int ldy,
+                           float* stats, hipStream_t s, const BnPro& pro) {
+  const char* e = getenv("ROD_PW_PROJ");   // read per call (tests A/B it in one process)
+  const bool off = e != nullptr && atoi(e) == 0;
+  if (off || K > 192 || K % 8 || Cout > 32 || Cout % 8 || M < 65536) return false;
+  const int kt = cdiv(K, 32), nt = cdiv(Cout, 16);
+  // K <= 32 (the 720p block-1 project 32 -> 16, one 16-wide N tile) measured no faster here
+  // (229 vs 224 us): the tiled kernel keeps it; the table form is built for ReLU6
+  if (kt == 1 || pro.act != ROD_ACT_RELU6) return false;
+  const long ntiles = cdivl(M, 128);
+  const long maxw = 256L * 3 * PWS_WAVES;
+  const long per = cdivl(ntiles, maxw);
+  const dim3 grid((unsigned)cdivl(cdivl(ntiles, per), PWS_WAVES), 1);
+  const BnGred g{};
+#define PJ(NT_, KT_)                                                                                             \
+  do {                                                                                                           \
+    if (stats)                                                                                                   \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, 1, true>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, \
+                         ldy, stats, g, pro);                                                                    \
+    else                                                                                                         \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, KT_, 0, true>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, \
+                         ldy, nullptr, g, pro);                                                                  \
+    return true;                                                                                                 \
+  } while (0)
+#define PJK(NT_)                     \
+  switch (kt) {                      \
+    case 1: PJ(NT_, 1);              \
+    case 2: PJ(NT_, 2);              \
+    case 3: PJ(NT_, 3);              \
+    case 4: PJ(NT_, 4);              \
+    case 5: PJ(NT_, 5);              \
+    default: PJ(NT_, 6);             \
+  }
+  if (nt == 1) PJK(1) else PJK(2)
+#undef PJK
+#undef PJ
   return false;
 }
 
@@ -2115,6 +2189,9 @@ static void conv_fwd_typed(const void* x, const BnPro* pro, const void* wt, cons
     return;
   }
   if constexpr (sizeof(T) == 2) {
+    if (!ep && !bw && !gr && pro && ksize == 1 && !bias && va && vb && vy && Cin <= PRO_MAXC &&
+        pw_proj_launch((const bf16_t*)x, (const bf16_t*)wt, (bf16_t*)y, M, K, Cout, ldx, ldy, stats, s, pv))
+      return;
     // the prologue form only for the block-to-block case it serves (K <= 32 input channels of a
     // project BatchNorm left pending: the 720p expand 16 -> 96)
     if (!ep && !bw && ksize == 1 && !bias && va && vb && vy && (!pro || (K <= 32 && Cin <= PRO_MAXC)) &&

@@ -22,7 +22,9 @@ SHAPES = [(8, 720, 1280, 16, 96, 1, 0), (8, 360, 640, 96, 24, 1, 1), (8, 360, 64
           (8, 720, 1280, 3, 32, 3, 0), (8, 45, 80, 96, 576, 1, 0), (8, 45, 80, 576, 96, 1, 1),
           (8, 23, 40, 160, 960, 1, 0),
           # the heads' last 3x3 convs (Cin = Cout = k x anchors, not a multiple of 8)
-          (8, 90, 160, 66, 66, 3, 2), (8, 45, 80, 99, 99, 3, 2), (8, 45, 80, 36, 36, 3, 2)]
+          (8, 90, 160, 66, 66, 3, 2), (8, 45, 80, 99, 99, 3, 2), (8, 45, 80, 36, 36, 3, 2),
+          # projects with the depthwise BatchNorm prologue: 720p block 1, 180x320 blocks
+          (8, 720, 1280, 32, 16, 1, 1), (8, 180, 320, 192, 32, 1, 1), (8, 180, 320, 144, 32, 1, 1)]
 
 
 def main():

@@ -33,6 +33,10 @@ for step in "$@"; do
     merge) run merge 400 python -u -m pytest tests/test_gpu_merge.py tests/test_gpu_kernels.py tests/test_gpu_defer.py -k "merge or finalize or defer" -m gpu -v --timeout=300 --timeout-method thread -p no:cacheprovider &&
         run mergedbg 300 env ROD_DEBUG_MERGE=1 python bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 ;;
     abmerge) for i in 1 2; do run abm2_$i 300 env ROD_MERGE_TWO_LAUNCH=1 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abm1_$i 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done; grep -h '"value"' $OUT/${TAG}_abm*.log | cut -c1-60 ;;
+    abproj) for i in 1 2; do run abp0_$i 300 env ROD_PW_PROJ=0 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abp1_$i 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done; grep -h '"value"' $OUT/${TAG}_abp*.log | cut -c1-60 ;;
+    cbproj) run cbproj0 300 env ROD_PW_PROJ=0 python tools/conv_bench.py --ops fwd_stats --shapes 1,3,16,17,18 &&
+        run cbproj1 300 python tools/conv_bench.py --ops fwd_stats --shapes 1,3,16,17,18 ;;
+    projtest) run projtest 300 python -u -m pytest tests/test_gpu_pwproj.py -m gpu -v --timeout=200 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchfast) run benchfast 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
