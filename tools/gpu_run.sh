@@ -42,6 +42,8 @@ for step in "$@"; do
     abprev) for i in 1 2; do run abq0_$i 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abq1_$i 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done; grep -h '"value"' $OUT/${TAG}_abq*.log | cut -c1-60 ;;
     abprev3) run abr0_1 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abr1_1 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abr1_2 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abr0_2 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abr0_3 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abr1_3 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; grep -h '"value"' $OUT/${TAG}_abr*.log | cut -c1-60 ;;
     abproj3) run abs0_1 300 env ROD_PW_PROJ=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abs1_1 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abs1_2 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abs0_2 300 env ROD_PW_PROJ=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abs0_3 300 env ROD_PW_PROJ=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abs1_3 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; grep -h '"value"' $OUT/${TAG}_abs*.log | cut -c1-60 ;;
+    absplit3) run abt0_1 300 env ROD_SPLIT_FUSE=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abt1_1 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abt1_2 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abt0_2 300 env ROD_SPLIT_FUSE=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abt0_3 300 env ROD_SPLIT_FUSE=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run abt1_3 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; grep -h '"value"' $OUT/${TAG}_abt*.log | cut -c1-60 ;;
+    splittest) run splittest 400 python -u -m pytest tests/test_gpu_splitk.py tests/test_gpu_bwd_data_bn.py tests/test_gpu_kernels.py -k "split or bwd_data or prologue" -m gpu -v --timeout=200 --timeout-method thread -p no:cacheprovider ;;
     streamtest) run streamtest 300 python -u -m pytest tests/test_gpu_pwproj.py tests/test_gpu_kernels.py -k "pw_stream or pw_proj or prologue" -m gpu -v --timeout=200 --timeout-method thread -p no:cacheprovider ;;
     projtest) run projtest 300 python -u -m pytest tests/test_gpu_pwproj.py -m gpu -v --timeout=200 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
