@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ROD_ABI_VERSION 22
+#define ROD_ABI_VERSION 23
 #define ROD_EINVAL (-1)
 
 enum { ROD_F32 = 0, ROD_BF16 = 1, ROD_I32 = 2 /* collectives only (ABI 19) */ };
@@ -448,6 +448,25 @@ int rod_pw_bwd_gred_dyp(const void* dz, const void* y, const float* mean, const 
                         const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
                         void* dyp, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
                         void* stream);
+/* Expanded tensor recomputed, not read (ABI 23; ref conv_blocks.py:263-270 expand + 238-247): the
+ * same backward of an inverted-residual block's expand conv with y (its pre-BatchNorm output, the
+ * C-wide expanded tensor) NOT passed: each 16-row tile of it is recomputed as bf16(a . wt0^T) from
+ * the conv input a (x with the optional prologue) the kernel already reads for the weight gradient,
+ * with the forward's MFMA and rounding — bit for bit the y the forward would have stored.
+ * wt0 = the forward operand [Cout][Cin] bf16 (rod_conv_weight_prep mode 0).  The M x Cout y stream
+ * (1.42 GB at 720p b8 for 16 -> 96) is gone.  rod_pw_bwd_rc: the streaming shapes 16 -> 96 and
+ * 24 -> 144 (rod_pw_bwd_rc_supported), no bias, outputs identical to rod_pw_bwd; rod_pw_bwd_gred_rc:
+ * the 16 -> 96 expand form of rod_pw_bwd_gred (its parts / workspace queries apply). */
+int rod_pw_bwd_rc_supported(long M, int Cin, int Cout, int dtype);
+int rod_pw_bwd_rc(const void* dz, const void* wt0, const float* mean, const float* rstd, const float* gamma,
+                  const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                  const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1, void* dx,
+                  float* dw, void* workspace, long M, int Cin, int Cout, int dtype, void* stream);
+int rod_pw_bwd_gred_rc(const void* dz, const void* wt0, const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                       const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                       void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
+                       void* stream);
 
 /* Stem weight gradient through its BatchNorm (ABI 18): rod_conv_wgrad of the 3x3, 3 -> 32 stem
  * (mobilenet_v2.py:58 conv + mobilenet.py:417-420 batch_norm) with dy formed in the loader from

@@ -357,6 +357,12 @@ __global__ void __launch_bounds__(MERGE_T) bn_parts_merge_kernel(const float* pa
   }
   __syncthreads();
   if (!is_last) return;
+  // The release side: every block's parts went out as agent-scope (sc1, L2-coherent across the
+  // XCDs) stores, completed (vmcnt 0) before its thread 0 counted the block.  The acquire side,
+  // here: an agent-scope acquire fence in the last block (only one block per channel group pays
+  // for it) before its agent-scope loads of the parts, so the hand-off holds by the memory model,
+  // not only by how gfx950 compiles the relaxed accesses.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   merge_slice<true>(out, gridDim.x, C, CB, slice2, 0, blockIdx.y, true, nullptr, M, eps, decay, mean, rstd, mmean, mvar, sn,
               s1, s2, piv);
 }
@@ -367,32 +373,46 @@ static size_t finalize_ws_bytes(int nparts, int C) {
   const int s1 = cdiv(nparts, p.slice);
   return s1 > 1 ? 2 * (size_t)s1 * 3 * C * sizeof(float) : 0;
 }
-// Zero-initialised per-device arrival counters of the single-launch two-level merge, handed out
-// round-robin (a 720p training step takes ~1,300 of the 65,536, so calls that may run at the same
-// time on the head-chain streams never share one); each counter is zero again when its launch
-// ends.  The pool is allocated on first use outside a stream capture; a call captured before
-// that falls back to two launches.  ROD_MERGE_TWO_LAUNCH=1 (read per call): always two launches.
+// Zero-initialised per-device arrival counters of the single-launch two-level merge; each counter
+// is zero again when its launch ends.  Two ranges: eager calls take counters round-robin from the
+// first 65,536 (a 720p training step takes ~1,300, so calls that may run at the same time on the
+// head-chain streams never share one); a call being captured into a HIP graph takes counters of
+// its own from the second range, which are never handed out again — a graph's replays can then
+// overlap eager merges or another graph's replays without sharing a counter.  When the graph
+// range is used up (~800 captured training steps in one process) captured calls fall back to two
+// launches (bit-identical).  The pool is allocated on first use outside a stream capture; a call
+// captured before that also falls back.  ROD_MERGE_TWO_LAUNCH=1 (read per call): always two launches.
 static unsigned* merge_counters(int n, hipStream_t s) {
   const char* e = getenv("ROD_MERGE_TWO_LAUNCH");
   if (e != nullptr && atoi(e) == 1) return nullptr;
-  constexpr int POOL = 1 << 16, MAXDEV = 64;
+  constexpr int POOL = 1 << 16, GPOOL = 1 << 20, MAXDEV = 64;
   static unsigned* base[MAXDEV] = {};
   static int next[MAXDEV] = {};
+  static int gnext[MAXDEV] = {};
   static std::mutex mu;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV || n > POOL) return nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) return nullptr;
+  const bool capturing = st != hipStreamCaptureStatusNone;
   std::lock_guard<std::mutex> g(mu);
   if (base[dev] == nullptr) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    if (capturing) return nullptr;
     void* p = nullptr;
-    if (hipMalloc(&p, POOL * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(p, 0, POOL * sizeof(unsigned), s) != hipSuccess) {
+    const size_t bytes = (size_t)(POOL + GPOOL) * sizeof(unsigned);
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, bytes, s) != hipSuccess) {
       (void)hipFree(p);
       return nullptr;
     }
     (void)hipStreamSynchronize(s);   // zeroed before any other stream takes a counter
     base[dev] = (unsigned*)p;
+  }
+  if (capturing) {
+    if (gnext[dev] + n > GPOOL) return nullptr;
+    unsigned* r = base[dev] + POOL + gnext[dev];
+    gnext[dev] += n;
+    return r;
   }
   if (next[dev] + n > POOL) next[dev] = 0;
   unsigned* r = base[dev] + next[dev];

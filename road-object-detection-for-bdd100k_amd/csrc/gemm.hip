@@ -2344,8 +2344,24 @@ int rod_conv_fwd_bnact(const void* x, const float* pro_mean, const float* pro_rs
   return check_launch("rod_conv_fwd_bnact");
 }
 
+// The BWD loader's per-channel table takes Cout * BWD_CF floats of dynamic LDS beside the GEMM's
+// static tiles (<= BWD_STATIC_LDS bytes for every tile configuration): the bound is the device's
+// LDS per workgroup (160 KB on gfx950 -> Cout <= 4096), read once.
+constexpr int BWD_STATIC_LDS = 32 * 1024;
+static int bwd_data_bn_max_cout() {
+  static int cached = -1;
+  if (cached < 0) {
+    int dev = 0, lds = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || lds <= 0)
+      lds = 64 * 1024;   // no device (CPU-side query): the smallest LDS of any target
+    cached = (lds - BWD_STATIC_LDS) / (BWD_CF * (int)sizeof(float)) / 8 * 8;
+  }
+  return cached;
+}
+
 int rod_conv_bwd_data_bn_supported(int Cout, int Cin, int dtype) {
-  return dtype == ROD_BF16 && Cout % 8 == 0 && Cin % 8 == 0 && Cout <= 4096 ? 1 : 0;
+  return dtype == ROD_BF16 && Cout % 8 == 0 && Cin % 8 == 0 && Cout > 0 && Cout <= bwd_data_bn_max_cout() ? 1 : 0;
 }
 
 int rod_conv_bwd_data_bn(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,

@@ -44,6 +44,7 @@ struct PwBwdArgs {
   long M, chunk;
   int Cin, Cout, kd, nci, nco, nxt;
   bf16_t* dyp = nullptr;   // rod_pw_bwd_gred_dyp: the BatchNorm-backward output rows [M][Cout] (dx not written)
+  const bf16_t* wt0 = nullptr;   // RC (ABI 23): the forward weights [Cout][Cin]; y is recomputed, never read
 };
 
 typedef short pb_s16x4 __attribute__((ext_vector_type(4)));
@@ -316,9 +317,12 @@ struct PbsGeo {
   static constexpr int WREG = 32 * LDD + 32 * LDX + 16 * LDC;    // bf16 elements per wave
   static constexpr int WS = NCI * 16 * LDD;                       // wt1 image (bf16 elements)
   static constexpr int XT = 3 * CIN * 2;                          // input-prologue table (bf16 slots)
-  static constexpr size_t lds() {
-    const size_t main = (size_t)(WS + XT + 4 * WREG) * 2;
-    const size_t red = (size_t)(WS + XT) * 2 + (size_t)COUT * NCI * 16 * 4 + (size_t)4 * 16 * 2 * CIN * 4;
+  static constexpr int LDW = 40;                                  // RC: forward weight rows, k zero-padded to 32
+  static constexpr int WF = COUT * LDW;                           // RC: forward weight image (bf16 elements)
+  static constexpr size_t lds(bool rc = false) {
+    const size_t main = (size_t)(WS + XT + 4 * WREG + (rc ? WF : 0)) * 2;
+    const size_t red = (size_t)(WS + XT + (rc ? WF : 0)) * 2 + (size_t)COUT * NCI * 16 * 4 +
+                       (size_t)4 * 16 * 2 * CIN * 4;
     return main > red ? main : red;
   }
 };
@@ -334,10 +338,18 @@ template <> struct PbsVec<8> { typedef bf16x8 T; };
 // XL: the input BatchNorm is linear (act NONE; the project output chained into an expand) —
 // its prologue and sums compile without the activation (a runtime branch costs the XG form
 // 12 VGPRs and a wave per SIMD).
-template <int CIN, int COUT, bool PRO, bool DX, bool XG = false, bool XL = false>
+// RC (ABI 23, rod_pw_bwd_rc / rod_pw_bwd_gred_rc): the pre-BatchNorm y = x_act . W^T is not read
+// but recomputed per 16-row half from the conv input already staged for the weight gradient — the
+// forward's MFMA (v_mfma_f32_16x16x32_bf16, k zero-padded to 32) with the operands swapped, so the
+// lane holds 4 consecutive channels of one row, rounded to bf16 once: the stored y bit for bit.
+// It is written into the half's dy rows in LDS, where each lane reads its chunk and overwrites it
+// with dy in place (the same lane reads and writes an element).  Saves the M x COUT y stream (the
+// expanded tensor of an inverted-residual block: 1.42 GB at 720p b8 for 16 -> 96).
+template <int CIN, int COUT, bool PRO, bool DX, bool XG = false, bool XL = false, bool RC = false>
 __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
   using G = PbsGeo<CIN, COUT>;
   static_assert(!XG || (PRO && DX), "the input sums need the prologue and dx");
+  static_assert(!RC || CIN <= 32, "the recompute is one k step");
   constexpr int CW = G::CW, CCH = G::CCH, RG = G::RG, JN = G::JN, KT = G::KT, LDD = G::LDD, NCO = G::NCO,
                 XCH = G::XCH, NCI = G::NCI, LDX = G::LDX, LDC = G::LDC;
   typedef typename PbsVec<CW>::T VT;
@@ -350,8 +362,9 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
   bf16_t* Ds = Ws + G::WS + G::XT + wave * G::WREG;             // [32][LDD]  dy of the tile
   bf16_t* Xs = Ds + 32 * LDD;                                   // [32][LDX]  conv input of the tile
   bf16_t* Cx = Xs + 32 * LDX;                                   // [16][LDC]  dx staging
+  bf16_t* Wf = Ws + G::WS + G::XT + 4 * G::WREG;                // RC: [COUT][LDW] forward weights
   // zero everything once (dy columns >= COUT, x columns >= CIN stay 0), then the weights
-  for (int i = tid; i < (G::WS + G::XT + 4 * G::WREG) / 8; i += 256) {
+  for (int i = tid; i < (G::WS + G::XT + 4 * G::WREG + (RC ? G::WF : 0)) / 8; i += 256) {
     bf16x8 z;
 #pragma unroll
     for (int j = 0; j < 8; ++j) z[j] = (bf16_t)0.f;
@@ -368,6 +381,12 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
     for (int c = tid; c < CIN; c += 256) {
       bn_affine(a.xmean, a.xrstd, a.xgamma, a.xbeta, c, xtab[c], xtab[CIN + c]);
       xtab[2 * CIN + c] = a.xmean[c];
+    }
+  }
+  if constexpr (RC) {
+    for (int i = tid; i < COUT * (CIN / 8); i += 256) {
+      const int co = i / (CIN / 8), k8 = i - co * (CIN / 8);
+      *(bf16x8*)(Wf + co * G::LDW + k8 * 8) = *(const bf16x8*)(a.wt0 + (long)co * CIN + k8 * 8);
     }
   }
   __syncthreads();
@@ -410,14 +429,14 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const long wstride = (long)gridDim.x * 4;
   long t = (long)blockIdx.x * 4 + wave;
-  VT dzv[JN], yv[JN];
+  VT dzv[JN], yv[RC ? 1 : JN];
   bf16x8 xv;
   {   // the first half (t >= ntiles: an empty resource, the loads return 0)
-    const rsrc_t rdz = rsrc_rows(a.dz, t * 32, COUT * 2), ry = rsrc_rows(a.y, t * 32, COUT * 2);
+    const rsrc_t rdz = rsrc_rows(a.dz, t * 32, COUT * 2);
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
       dzv[j] = buf_ld<VT>(rdz, vdj(j), 0u);
-      yv[j] = buf_ld<VT>(ry, vdj(j), 0u);
+      if constexpr (!RC) yv[j] = buf_ld<VT>(rsrc_rows(a.y, t * 32, COUT * 2), vdj(j), 0u);
     }
     xv = buf_ld<bf16x8>(rsrc_rows(a.x, t * 32, CIN * 2), vx, 0u);
   }
@@ -430,24 +449,34 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
       // ---- dy = BatchNorm backward of (dz, y) -> Ds; x (+ prologue) -> Xs ------------------
       // each chunk's registers are reloaded with the NEXT half's chunk as soon as they are
       // consumed, so this wave keeps loads in flight through its VALU work as well
+      // (RC: x first, then y recomputed from it into the dy rows, then dy over it in place)
       const long rown = (h == 0 ? t : t + wstride) * 32;
-      const rsrc_t ndz = rsrc_rows(a.dz, rown, COUT * 2), ny = rsrc_rows(a.y, rown, COUT * 2);
+      const rsrc_t ndz = rsrc_rows(a.dz, rown, COUT * 2);
       const unsigned nso = (unsigned)((1 - h) * 16 * COUT * 2);
+      auto dy_rows = [&]() {
+        const rsrc_t ny = rsrc_rows(a.y, rown, COUT * 2);
 #pragma unroll
-      for (int j = 0; j < JN; ++j) {
-        const int r = rg + RG * j;
-        typename PbsVec<CW>::T o;
+        for (int j = 0; j < JN; ++j) {
+          const int r = rg + RG * j;
+          const bool rok = dact && (JN * RG == 16 || r < 16);
+          bf16_t* dp = Ds + (h * 16 + (rok ? r : 0)) * LDD + cc * CW;
+          VT yj4;
+          if constexpr (RC) yj4 = *(const VT*)dp;
+          else yj4 = yv[j];
+          typename PbsVec<CW>::T o;
 #pragma unroll
-        for (int e = 0; e < CW; ++e) {
-          const float yj = (float)yv[j][e];
-          const float z = fmaf(yj, sc[e], sh[e]);
-          const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
-          o[e] = (bf16_t)bn_bwd_apply1<bf16_t>(ca[e], gj, k1[e], k0[e], 0.f, yj);
+          for (int e = 0; e < CW; ++e) {
+            const float yj = (float)yj4[e];
+            const float z = fmaf(yj, sc[e], sh[e]);
+            const float gj = (float)dzv[j][e] * (z > 0.f ? (z < ghi ? 1.f : 0.f) : glo);
+            o[e] = (bf16_t)bn_bwd_apply1<bf16_t>(ca[e], gj, k1[e], k0[e], 0.f, yj);
+          }
+          dzv[j] = buf_ld<VT>(ndz, vdj(j), nso);
+          if constexpr (!RC) yv[j] = buf_ld<VT>(ny, vdj(j), nso);
+          if (rok) *(VT*)dp = o;
         }
-        dzv[j] = buf_ld<VT>(ndz, vdj(j), nso);
-        yv[j] = buf_ld<VT>(ny, vdj(j), nso);
-        if (dact && (JN * RG == 16 || r < 16)) *(VT*)(Ds + (h * 16 + r) * LDD + cc * CW) = o;
-      }
+      };
+      if constexpr (!RC) dy_rows();
       const bf16x8 xcur = xv;   // XG: the raw x of this half, for the sums at the dx write-back
       {
         bf16x8 v = xv;
@@ -480,6 +509,22 @@ __global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long nt
         if (xact) *(bf16x8*)(Xs + (h * 16 + xr) * LDX + xc * 8) = v;
       }
       __builtin_amdgcn_wave_barrier();
+      if constexpr (RC) {
+        // y^T tile by tile: A = W rows (16 channels x k), B = this half's x rows (k x 16 rows);
+        // lane (g, li) gets channels 16ct + 4g .. +3 of row li -> one 8-byte LDS write per tile
+        const bf16x8 zero8 = {};
+        const bf16x8 fb = 8 * g < CIN ? *(const bf16x8*)(Xs + (h * 16 + li) * LDX + 8 * g) : zero8;
+#pragma unroll
+        for (int ct = 0; ct < NCO; ++ct) {
+          const bf16x8 fw = 8 * g < CIN ? *(const bf16x8*)(Wf + (ct * 16 + li) * G::LDW + 8 * g) : zero8;
+          const f32x4 yt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          const bf16x4 yb = {(bf16_t)yt[0], (bf16_t)yt[1], (bf16_t)yt[2], (bf16_t)yt[3]};
+          *(bf16x4*)(Ds + (h * 16 + li) * LDD + ct * 16 + 4 * g) = yb;
+        }
+        __builtin_amdgcn_wave_barrier();
+        dy_rows();
+        __builtin_amdgcn_wave_barrier();
+      }
       if constexpr (DX) {
         // ---- dx = dy . W for the 16 rows of this half -> Cx -> 16-byte row segments ---------
         f32x4 accx[NCI];
@@ -629,7 +674,9 @@ struct PbgGeo {
 
 // FAST: the block's activations (linear output BatchNorm, ReLU6 input BatchNorm) at compile
 // time, channel pairs as packed fp32 ops; otherwise both activations at run time, per element
-template <int COUT, int NW, bool FAST>
+// DYP (rod_pw_bwd_gred_dyp): dy written by column group 0, dx not stored — a template argument so
+// the two entries are separate kernels in a trace / PMC pass (rod/roofline.py ENTRY_KERNELS)
+template <int COUT, int NW, bool FAST, bool DYP = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) pw_bwd_gred_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
   using G = PbgGeo<COUT, NW>;
   constexpr int CCH = G::CCH, RG = G::RG, JN = G::JN, KT = G::KT, LDD = G::LDD, NCO = G::NCO, XCH = G::XCH,
@@ -757,7 +804,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
         const rsrc_t ndz = rsrc_d(a.dz, rown), ny = rsrc_d(a.y, rown);
         const unsigned nso = (unsigned)((1 - h) * 16 * COUT * 2);
         // dyp (column group 0 only; other blocks and rows past M: the empty / range-checked resource)
-        const rsrc_t rdp = a.dyp && blockIdx.y == 0 ? rsrc_d(a.dyp, row0) : rod_rsrc(a.dz, 0u);
+        const rsrc_t rdp = DYP && blockIdx.y == 0 ? rsrc_d(a.dyp, row0) : rod_rsrc(a.dz, 0u);
         const unsigned dpso = (unsigned)(h * 16 * COUT * 2);
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
@@ -832,7 +879,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) p
 #pragma unroll
           for (int r = 0; r < 4; ++r) Cx[(4 * g + r) * LDX + j * 16 + li] = (bf16_t)accx[j][r];
         __builtin_amdgcn_wave_barrier();
-        const rsrc_t rdx = a.dx ? rsrc_x(a.dx, row0) : rod_rsrc(a.x, 0u);   // dyp form: dx not stored
+        const rsrc_t rdx = !DYP ? rsrc_x(a.dx, row0) : rod_rsrc(a.x, 0u);   // dyp form: dx not stored
         const unsigned so = (unsigned)(h * 16 * Cin * 2);
 #pragma unroll
         for (int j = 0; j < JX; ++j) {
@@ -1008,13 +1055,21 @@ size_t rod_pw_bwd_workspace(long M, int Cin, int Cout) {
   return blk * Cout * (Cin + 1) * sizeof(float) + 64;
 }
 
-int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
-               const float* beta, int act, const float* coef, const void* x, const float* xmean, const float* xrstd,
-               const float* xgamma, const float* xbeta, int xact, const void* wt1, void* dx, float* dw, float* db,
-               void* workspace, long M, int Cin, int Cout, int dtype, void* stream) {
+int rod_pw_bwd_rc_supported(long M, int Cin, int Cout, int dtype) {
+  return dtype == ROD_BF16 && M > 0 && pw_bwd_ok(Cin, Cout) && pw_bwd_stream_ok(Cin, Cout, false) ? 1 : 0;
+}
+
+static int pw_bwd_run(const void* dz, const void* y, const void* wt0, const float* mean, const float* rstd,
+                      const float* gamma, const float* beta, int act, const float* coef, const void* x,
+                      const float* xmean, const float* xrstd, const float* xgamma, const float* xbeta, int xact,
+                      const void* wt1, void* dx, float* dw, float* db, void* workspace, long M, int Cin, int Cout,
+                      int dtype, void* stream) {
   ROD_CHECK_ARG(dtype == ROD_BF16, "rod_pw_bwd: bf16 only");
   ROD_CHECK_ARG(M > 0 && pw_bwd_ok(Cin, Cout), "rod_pw_bwd: unsupported shape M=%ld Cin=%d Cout=%d", M, Cin, Cout);
-  ROD_CHECK_ARG(dz && y && mean && rstd && coef && x && dw && workspace, "rod_pw_bwd: NULL argument");
+  ROD_CHECK_ARG(dz && (y || wt0) && mean && rstd && coef && x && dw && workspace, "rod_pw_bwd: NULL argument");
+  ROD_CHECK_ARG(!wt0 || (!db && rod_pw_bwd_rc_supported(M, Cin, Cout, dtype)),
+                "rod_pw_bwd_rc: the recompute form takes the streaming shapes (16 -> 96, 24 -> 144) without bias");
+  ROD_CHECK_ARG((((uintptr_t)wt0) & 15) == 0, "rod_pw_bwd_rc: wt0 must be 16-byte aligned");
   ROD_CHECK_ARG(!dx || wt1, "rod_pw_bwd: dx needs wt1");
   ROD_CHECK_ARG(!xmean || xrstd, "rod_pw_bwd: bad input prologue");
   ROD_CHECK_ARG(((((uintptr_t)dz) | ((uintptr_t)y) | ((uintptr_t)x) | ((uintptr_t)wt1) | ((uintptr_t)dx)) & 15) == 0,
@@ -1026,15 +1081,21 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
   if (pw_bwd_stream_ok(Cin, Cout, db != nullptr)) {
     const int nblk = pw_bwd_stream_blocks(M);
     PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw, nullptr,
-                mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0};
+                mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0, 0, 0,
+                nullptr, (const bf16_t*)wt0};
     const long ntiles = cdivl(M, 32);
-#define PBS1(CI, CO, PR, DXF, XLN)                                                                           \
-  do {                                                                                                       \
-    const size_t lds = PbsGeo<CI, CO>::lds();                                                                \
-    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, PR, DXF, false, XLN>,                \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
-    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, PR, DXF, false, XLN>), dim3(nblk), dim3(256), lds, s, a, \
-                       ntiles, nullptr);                                                                     \
+#define PBS0(CI, CO, PR, DXF, XLN, RCF)                                                                         \
+  do {                                                                                                          \
+    const size_t lds = PbsGeo<CI, CO>::lds(RCF);                                                                \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, PR, DXF, false, XLN, RCF>,              \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
+    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, PR, DXF, false, XLN, RCF>), dim3(nblk), dim3(256), lds, s, \
+                       a, ntiles, nullptr);                                                                     \
+  } while (0)
+#define PBS1(CI, CO, PR, DXF, XLN)                  \
+  do {                                              \
+    if (wt0) PBS0(CI, CO, PR, DXF, XLN, true);      \
+    else PBS0(CI, CO, PR, DXF, XLN, false);         \
   } while (0)
 #define PBS(CI, CO, PR, DXF)                                      \
   do {                                                            \
@@ -1053,6 +1114,7 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
 #undef PBS2
 #undef PBS
 #undef PBS1
+#undef PBS0
     slab_sum(partw, dw, nblk, (long)Cout * Cin, s);
     return check_launch("rod_pw_bwd");
   }
@@ -1082,6 +1144,24 @@ int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rs
   return check_launch("rod_pw_bwd");
 }
 
+int rod_pw_bwd(const void* dz, const void* y, const float* mean, const float* rstd, const float* gamma,
+               const float* beta, int act, const float* coef, const void* x, const float* xmean, const float* xrstd,
+               const float* xgamma, const float* xbeta, int xact, const void* wt1, void* dx, float* dw, float* db,
+               void* workspace, long M, int Cin, int Cout, int dtype, void* stream) {
+  ROD_CHECK_ARG(y, "rod_pw_bwd: NULL y");
+  return pw_bwd_run(dz, y, nullptr, mean, rstd, gamma, beta, act, coef, x, xmean, xrstd, xgamma, xbeta, xact, wt1, dx,
+                    dw, db, workspace, M, Cin, Cout, dtype, stream);
+}
+
+int rod_pw_bwd_rc(const void* dz, const void* wt0, const float* mean, const float* rstd, const float* gamma,
+                  const float* beta, int act, const float* coef, const void* x, const float* xmean, const float* xrstd,
+                  const float* xgamma, const float* xbeta, int xact, const void* wt1, void* dx, float* dw,
+                  void* workspace, long M, int Cin, int Cout, int dtype, void* stream) {
+  ROD_CHECK_ARG(wt0, "rod_pw_bwd_rc: NULL wt0");
+  return pw_bwd_run(dz, nullptr, wt0, mean, rstd, gamma, beta, act, coef, x, xmean, xrstd, xgamma, xbeta, xact, wt1,
+                    dx, dw, nullptr, workspace, M, Cin, Cout, dtype, stream);
+}
+
 
 // expand shapes the gred entry takes (the streaming kernel with the input sums): 16 -> 96 only
 // (168 VGPRs, 3 waves / SIMD); 24 -> 144 would need 268 (1 wave), and its input is usually also a
@@ -1104,13 +1184,15 @@ static int pw_bwd_gred_run(const void* dz, const void* y, const float* mean, con
                            const float* beta, int act, const float* coef, const void* x, const float* xmean,
                            const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
                            void* dx, void* dyp, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout,
-                           int dtype, void* stream) {
+                           int dtype, void* stream, const void* wt0 = nullptr) {
   const bool sexp = dtype == ROD_BF16 && M > 0 && pw_bwd_xg_ok(Cin, Cout) && !dyp;
   const int nw = dtype == ROD_BF16 && M > 0 && !sexp ? pw_bwd_gred_nw(Cin, Cout) : 0;
   ROD_CHECK_ARG(nw || sexp, "rod_pw_bwd_gred: unsupported shape M=%ld Cin=%d Cout=%d dtype=%d", M, Cin, Cout,
                 dtype);
-  ROD_CHECK_ARG(dz && y && mean && rstd && coef && x && xmean && xrstd && dw && xparts && workspace,
+  ROD_CHECK_ARG(!wt0 || sexp, "rod_pw_bwd_gred_rc: the recompute form takes the 16 -> 96 expand only");
+  ROD_CHECK_ARG(dz && (y || wt0) && mean && rstd && coef && x && xmean && xrstd && dw && xparts && workspace,
                 "rod_pw_bwd_gred: NULL argument");
+  ROD_CHECK_ARG((((uintptr_t)wt0) & 15) == 0, "rod_pw_bwd_gred_rc: wt0 must be 16-byte aligned");
   ROD_CHECK_ARG((dx != nullptr) != (dyp != nullptr) && wt1,
                 "rod_pw_bwd_gred: wt1 and exactly one of dx / dyp required (the sums are over dx)");
   ROD_CHECK_ARG(((((uintptr_t)dz) | ((uintptr_t)y) | ((uintptr_t)x) | ((uintptr_t)wt1) | ((uintptr_t)dx) |
@@ -1123,15 +1205,20 @@ static int pw_bwd_gred_run(const void* dz, const void* y, const float* mean, con
     const int nb = pw_bwd_stream_blocks(M);
     PwBwdArgs a{(const bf16_t*)dz, (const bf16_t*)y, (const bf16_t*)x, (const bf16_t*)wt1, (bf16_t*)dx, partw,
                 nullptr, mean, rstd, gamma, beta, coef, xmean, xrstd, xgamma, xbeta, act, xact, M, 0, Cin, Cout, 0, 0,
-                0, 0};
+                0, 0, nullptr, (const bf16_t*)wt0};
     const long nt = cdivl(M, 32);
-#define PBX1(CI, CO, XLN)                                                                                 \
-  do {                                                                                                    \
-    const size_t lds = PbsGeo<CI, CO>::lds();                                                             \
-    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, true, true, true, XLN>,           \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                      \
-    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, true, true, true, XLN>), dim3(nb), dim3(256), lds, s, a, \
-                       nt, xparts);                                                                       \
+#define PBX0(CI, CO, XLN, RCF)                                                                                 \
+  do {                                                                                                         \
+    const size_t lds = PbsGeo<CI, CO>::lds(RCF);                                                               \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_stream_kernel<CI, CO, true, true, true, XLN, RCF>,           \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                           \
+    hipLaunchKernelGGL((pw_bwd_stream_kernel<CI, CO, true, true, true, XLN, RCF>), dim3(nb), dim3(256), lds, s, a, \
+                       nt, xparts);                                                                            \
+  } while (0)
+#define PBX1(CI, CO, XLN)                      \
+  do {                                         \
+    if (wt0) PBX0(CI, CO, XLN, true);          \
+    else PBX0(CI, CO, XLN, false);             \
   } while (0)
 #define PBX(CI, CO)                                          \
   if (Cin == CI) {                                           \
@@ -1141,6 +1228,7 @@ static int pw_bwd_gred_run(const void* dz, const void* y, const float* mean, con
     PBX(16, 96)
 #undef PBX
 #undef PBX1
+#undef PBX0
     slab_sum(partw, dw, nb, (long)Cout * Cin, s);
     return check_launch("rod_pw_bwd_gred");
   }
@@ -1154,12 +1242,17 @@ static int pw_bwd_gred_run(const void* dz, const void* y, const float* mean, con
   // 569 vs 433 us), so there the per-element form runs (ROD_PWB_GRED_FAST48=1: packed, A/B)
   static const bool fast48 = getenv("ROD_PWB_GRED_FAST48") && atoi(getenv("ROD_PWB_GRED_FAST48")) == 1;
   const bool fast = act == ROD_ACT_NONE && xact == ROD_ACT_RELU6 && (nw == 32 || fast48);
-#define PBG(CO, NW_, F)                                                                                         \
+#define PBGD(CO, NW_, F, D)                                                                                     \
   do {                                                                                                          \
     const size_t lds = PbgGeo<CO, NW_>::lds();                                                                  \
-    (void)hipFuncSetAttribute((const void*)pw_bwd_gred_kernel<CO, NW_, F>,                                      \
+    (void)hipFuncSetAttribute((const void*)pw_bwd_gred_kernel<CO, NW_, F, D>,                                   \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
-    hipLaunchKernelGGL((pw_bwd_gred_kernel<CO, NW_, F>), grid, dim3(256), lds, s, a, ntiles, xparts);           \
+    hipLaunchKernelGGL((pw_bwd_gred_kernel<CO, NW_, F, D>), grid, dim3(256), lds, s, a, ntiles, xparts);        \
+  } while (0)
+#define PBG(CO, NW_, F)                  \
+  do {                                   \
+    if (dyp) PBGD(CO, NW_, F, true);     \
+    else PBGD(CO, NW_, F, false);        \
   } while (0)
 #define PBG1(CO, NW_)                        \
   if (fast) PBG(CO, NW_, true);              \
@@ -1173,6 +1266,7 @@ static int pw_bwd_gred_run(const void* dz, const void* y, const float* mean, con
 #undef PBG2
 #undef PBG1
 #undef PBG
+#undef PBGD
   slab_sum(partw, dw, nblk, (long)Cout * Cin, s);
   return check_launch("rod_pw_bwd_gred");
 }
@@ -1195,6 +1289,16 @@ int rod_pw_bwd_gred_dyp(const void* dz, const void* y, const float* mean, const 
   ROD_CHECK_ARG(dyp, "rod_pw_bwd_gred_dyp: dyp required");
   return pw_bwd_gred_run(dz, y, mean, rstd, gamma, beta, act, coef, x, xmean, xrstd, xgamma, xbeta, xact, wt1,
                          nullptr, dyp, dw, xparts, workspace, M, Cin, Cout, dtype, stream);
+}
+
+int rod_pw_bwd_gred_rc(const void* dz, const void* wt0, const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, int act, const float* coef, const void* x, const float* xmean,
+                       const float* xrstd, const float* xgamma, const float* xbeta, int xact, const void* wt1,
+                       void* dx, float* dw, float* xparts, void* workspace, long M, int Cin, int Cout, int dtype,
+                       void* stream) {
+  ROD_CHECK_ARG(dx && wt0, "rod_pw_bwd_gred_rc: dx and wt0 required");
+  return pw_bwd_gred_run(dz, nullptr, mean, rstd, gamma, beta, act, coef, x, xmean, xrstd, xgamma, xbeta, xact, wt1,
+                         dx, nullptr, dw, xparts, workspace, M, Cin, Cout, dtype, stream, wt0);
 }
 
 }  // extern "C"

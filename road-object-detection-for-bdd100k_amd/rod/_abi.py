@@ -173,15 +173,17 @@ def _capturing():
 
 # entries whose parameter-gradient sums rod_slab_defer(1) may queue (include/rod.h, ABI 11)
 DEFERRING = frozenset(("rod_conv_wgrad", "rod_dw3x3_bwd_filter", "rod_dw3x3_bwd_filter_bn", "rod_pw_bwd",
-                       "rod_pw_bwd_gred", "rod_pw_bwd_gred_dyp", "rod_stem_wgrad_bn", "rod_dw3x3_bwd_fused",
+                       "rod_pw_bwd_rc", "rod_pw_bwd_gred", "rod_pw_bwd_gred_rc", "rod_pw_bwd_gred_dyp", "rod_stem_wgrad_bn", "rod_dw3x3_bwd_fused",
                        "rod_dw3x3_bwd_fused_pw"))
 # while sums are deferred: every tensor handed to such an entry (partial slabs, gradient outputs)
-# is kept referenced until rod_slab_flush has been enqueued (rod.ops.SlabDefer).  Any other entry
-# is checked against the queue length (rod_slab_pending) around the call: one that queued a sum
-# has its tensors kept too and its name recorded in DEFER_UNLISTED (a registry gap, which
-# tests/test_gpu_defer.py asserts never happens).
+# is kept referenced until rod_slab_flush has been enqueued (rod.ops.SlabDefer).  With WATCH_DEFER
+# (ROD_DEBUG_DEFER=1, or set by tests/test_gpu_defer.py) every other entry is checked against the
+# queue length (rod_slab_pending) around the call: one that queued a sum has its tensors kept too
+# and its name recorded in DEFER_UNLISTED (a registry gap, which the test asserts never happens
+# over REFINE / ALL / VGG steps).  Off on the production path: two extra ctypes calls per entry.
 KEEP = None
 DEFER_UNLISTED = set()
+WATCH_DEFER = os.environ.get("ROD_DEBUG_DEFER", "0") == "1"
 
 
 def call(name: str, *args):
@@ -195,7 +197,7 @@ def call(name: str, *args):
     if KEEP is not None:
         if name in DEFERRING:
             KEEP.extend(a for a in args if hasattr(a, "data_ptr"))
-        else:
+        elif WATCH_DEFER:
             watch = True
             pend0 = L.rod_slab_pending()
     conv = [(_ptr(a) if t == "ptr" else a) for (t, _), a in zip(argspec, args)]

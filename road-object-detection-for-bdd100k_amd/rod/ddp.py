@@ -25,10 +25,19 @@ xGMI note: 8 GPUs are fully connected point-to-point; a 22 MB (REFINE) / 35 MB (
 gradient in ~4 MB buckets gives RCCL messages large enough to run its multi-channel rings
 at link bandwidth while leaving room to overlap.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 _UID_KEY = 'rod_rccl_uid'
+# Buckets completed on a detector-head chain stream wait for the end of backward and launch from
+# the optimizer's stream.  ROD_DDP_CHAIN_DEFER=0 launches them where they complete instead (the
+# communication stream forked from the chain stream by an event, joined at the optimizer's stream):
+# that crashed hipStreamEndCapture (a segfault inside the HIP runtime) in round 6 too, on a 1-rank
+# group (gpurun_out/r6b_tests.log), although the communication stream is now joined at the
+# optimizer's stream — so the communication stream is never forked from a chain stream.
+CHAIN_DEFER = os.environ.get('ROD_DDP_CHAIN_DEFER', '1') == '1'
 
 
 def native_comm_init(rank, world, group=None):
@@ -68,17 +77,87 @@ def make_reducer(world, rank=None, group=None, bucket_mb=4.0):
     return GradReducer(world, bucket_mb, group)
 
 
+# Every collective a native reducer issues, in host order, when set to a list (tests): tuples
+# (entry, element count, dtype code, stream role).  The role is 'comm' when the call was enqueued
+# on the reducer's communication stream — the only stream a native collective may run on.
+TRACE = None
+
+
+class NativeComm(object):
+    """The library's communicator (include/rod.h ABI 16/19) driven from ONE stream.
+
+    RCCL requires every rank to issue a communicator's collectives in the same order, and two
+    streams driving one communicator concurrently may interleave differently on different ranks
+    (a cross-rank deadlock).  So every native collective of a step — the gradient buckets, the
+    SyncBatchNorm all-gathers, the hard-negative count / histogram sums — is enqueued here, on
+    this one communication stream, in host order: the stream first waits for everything the
+    calling stream has queued (an event), the collective runs, and a done event joins it back —
+    either right away (`run`: a collective whose result the calling stream consumes next) or
+    when the optimizer needs the sums (`launch`: a gradient bucket, overlapping backward).
+    Under HIP-graph capture the events are graph edges; no host synchronisation anywhere.
+
+    record=True (tests): the entries are logged in TRACE but not called, and an all-gather
+    replicates the local part (as if every rank held the same data) — so the collective
+    sequence of a real step can be compared across ranks that share one GPU."""
+
+    def __init__(self, record=False):
+        self.stream = None
+        self.record = bool(record)
+
+    def _enqueue(self, entry, args, count, code):
+        t = args[0]
+        if not t.is_cuda:          # record mode on CPU tensors (the gloo unit tests)
+            if TRACE is not None:
+                TRACE.append((entry, int(count), int(code), 'comm'))
+            if not self.record:
+                raise RuntimeError('native collectives need device tensors')
+            if entry == 'rod_allgather':
+                args[1].copy_(args[0].reshape(-1)[:count].repeat(args[1].numel() // count).view_as(args[1]))
+            return None, None
+        cur = torch.cuda.current_stream(t.device)
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=t.device)
+        comm = self.stream
+        ready = torch.cuda.Event()
+        ready.record(cur)            # the inputs are written
+        comm.wait_event(ready)
+        if TRACE is not None:
+            TRACE.append((entry, int(count), int(code), 'comm'))
+        if self.record:
+            if entry == 'rod_allgather':
+                with torch.cuda.stream(comm):
+                    n = args[1].numel() // count
+                    args[1].view(n, count).copy_(args[0].reshape(-1)[:count].expand(n, count))
+        else:
+            from . import _abi
+            _abi.call(entry, *args, comm.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(comm)
+        return done, cur
+
+    def run(self, entry, *args, count, code):
+        """A collective whose result the calling stream reads next: joined right away."""
+        done, cur = self._enqueue(entry, args, count, code)
+        if done is not None:
+            cur.wait_event(done)
+
+    def launch(self, entry, *args, count, code):
+        """A gradient bucket: returns the handle the optimizer's stream waits on."""
+        done, cur = self._enqueue(entry, args, count, code)
+        return _Done() if done is None else _Joined(done, cur)
+
+
 class GradReducer(object):
-    def __init__(self, world_size, bucket_mb=4.0, group=None, native=False):
+    def __init__(self, world_size, bucket_mb=4.0, group=None, native=False, record=False):
         self.world = world_size
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.group = group
-        # native=True: every collective goes through the library's own communicator
-        # (native_comm_init first): the buckets on a communication stream joined by events,
-        # the hard-negative sums and SyncBatchNorm gathers on the compute stream; otherwise
-        # torch.distributed (async work handles)
+        # native=True: every collective goes through the library's own communicator, all of
+        # them on ONE communication stream in host order (NativeComm): the buckets joined at
+        # the optimizer, the hard-negative sums and SyncBatchNorm gathers joined right away;
+        # otherwise torch.distributed (async work handles)
         self.native = bool(native)
-        self._comm = None      # the native communication stream (created on first use)
+        self.comm = NativeComm(record) if self.native else None
         self.store = None
         self.buckets = []
         # True while Trainer.step_graphed captures a 'split' step: the captured backward launches
@@ -139,17 +218,17 @@ class GradReducer(object):
             if st not in b['streams']:
                 b['streams'].append(st)
         b['pending'] -= 1
-        if b['pending'] == 0 and not self._on_chain_stream(p):
+        if b['pending'] == 0 and not (CHAIN_DEFER and self._on_chain_stream(p)):
             self._launch(b)
 
     @staticmethod
     def _on_chain_stream(p):
         """A gradient written on a detector-head chain stream (ops.LEVELS): a bucket completed
         there is launched after backward, from the stream that runs the optimizer (__call__).
-        Forking the communication stream from a chain stream crashed the end of a HIP-graph
+        Forking the communication stream from a chain stream crashes the end of a HIP-graph
         capture (hipStreamEndCapture, a segfault inside the runtime; tests/native_comm_worker.py
-        with ROD_HEAD_STREAMS=3), while the same step with the chains on the calling stream, or
-        with those buckets deferred, captures and replays bit-identically."""
+        and graph_dp_worker.py, rounds 5 and 6), while the same step with those buckets deferred
+        captures and replays bit-identically."""
         if not (torch.cuda.is_available() and p.is_cuda):
             return False
         from . import ops
@@ -188,26 +267,15 @@ class GradReducer(object):
     def _allreduce(self, view):
         if not self.native:
             return dist.all_reduce(view, group=self.group, async_op=True)
-        from . import _abi
-        cur = torch.cuda.current_stream(view.device)
-        if self._comm is None:
-            self._comm = torch.cuda.Stream(device=view.device)
-        ready = torch.cuda.Event()
-        ready.record(cur)                      # the bucket's gradients (and slab sums) are written
-        self._comm.wait_event(ready)
-        _abi.call('rod_allreduce_bucket', view, view.numel(), 0, self._comm.cuda_stream)
-        done = torch.cuda.Event()
-        done.record(self._comm)
-        return _Joined(done, cur)
+        return self.comm.launch('rod_allreduce_bucket', view, view.numel(), 0, count=view.numel(), code=0)
 
     def hnm_allreduce(self, tensors):
-        """In-place SUM of small device int32 tensors over the ranks, on the compute stream
-        (the hard-negative exchange of net_tools.det_clf_loss)."""
+        """In-place SUM of small device int32 tensors over the ranks (the hard-negative exchange
+        of net_tools.det_clf_loss); native: on the communication stream, joined right away."""
         if self.native:
-            from . import _abi, ops
             for t in tensors:
                 assert t.dtype == torch.int32 and t.is_contiguous()
-                _abi.call('rod_allreduce_bucket', t, t.numel(), 2, ops.stream())   # ROD_I32
+                self.comm.run('rod_allreduce_bucket', t, t.numel(), 2, count=t.numel(), code=2)   # ROD_I32
             return
         for t in tensors:
             dist.all_reduce(t, group=self.group)
@@ -215,7 +283,7 @@ class GradReducer(object):
     def bn_allgather(self, parts):
         """[world * nparts, ...] = every rank's BatchNorm partial statistics in rank order
         (SyncBatchNorm)."""
-        return allgather(parts, self.world, self.group, native=self.native)
+        return allgather(parts, self.world, self.group, comm=self.comm)
 
     def launched(self):
         return sum(1 for b in self.buckets if b['work'] is not None)
@@ -232,9 +300,9 @@ class _Joined(object):
     """A bucket summed on the communication stream: wait() makes the stream current at the
     wait — the one that runs the optimizer step — wait for it (an event edge: a graph
     dependency under capture), no host synchronisation.  Not the stream current at the launch:
-    a bucket is launched from inside backward, possibly on a detector-head chain stream
-    (ops.LEVELS) that nothing joins afterwards; joining the communication stream there left it
-    unjoined at the end of a HIP-graph capture (a crash in capture_end)."""
+    a bucket may be launched from inside backward on a detector-head chain stream (ops.LEVELS)
+    that nothing joins afterwards; joining the communication stream there left it unjoined at
+    the end of a HIP-graph capture (a crash in capture_end, round 5)."""
 
     def __init__(self, done, stream):
         self.done, self.device = done, stream.device
@@ -243,16 +311,15 @@ class _Joined(object):
         torch.cuda.current_stream(self.device).wait_event(self.done)
 
 
-def allgather(t, world, group=None, native=False):
-    """All-gather of a small device tensor into one [world * n, ...] buffer, rank-major, on the
-    compute stream (native: rod_allgather; RCCL all_gather_into_tensor; the list form for
-    gloo)."""
+def allgather(t, world, group=None, comm=None):
+    """All-gather of a small device tensor into one [world * n, ...] buffer, rank-major
+    (comm = a NativeComm: rod_allgather on its communication stream, joined right away; else
+    RCCL all_gather_into_tensor on the compute stream; the list form for gloo)."""
     t = t.contiguous()
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    if native:
-        from . import _abi, ops
+    if comm is not None:
         code = {torch.float32: 0, torch.bfloat16: 1, torch.int32: 2}[t.dtype]
-        _abi.call('rod_allgather', t, out, t.numel(), code, ops.stream())
+        comm.run('rod_allgather', t, out, t.numel(), code, count=t.numel(), code=code)
     elif dist.get_backend(group) == 'nccl':
         dist.all_gather_into_tensor(out, t, group=group)
     else:
@@ -270,10 +337,10 @@ class SyncBatchNorm(object):
     all-reduce adds up.  One all-gather of 3*C (forward) / 2*C (backward) floats per part and
     BatchNorm: a few KB to ~1 MB per layer, latency-bound on xGMI."""
 
-    def __init__(self, world, group=None, native=False):
+    def __init__(self, world, group=None, comm=None):
         self.world = world
         self.group = group
-        self.native = native
+        self.comm = comm   # the reducer's NativeComm (the one communication stream) or None
 
     def gather(self, parts):
-        return allgather(parts, self.world, self.group, native=self.native)
+        return allgather(parts, self.world, self.group, comm=self.comm)

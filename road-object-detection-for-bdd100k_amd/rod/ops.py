@@ -111,8 +111,10 @@ class LevelStreams:
         self.used = []
 
     def active(self, t):
-        # not under SyncBatchNorm: its statistics all-gathers would run on the chain streams
-        # concurrently, and one RCCL communicator must not be driven from several streams at once
+        # not under SyncBatchNorm: its statistics all-gathers would be issued from the chain
+        # streams — torch.distributed's would run there, several streams driving one
+        # communicator; the library's would fork its communication stream from a chain stream,
+        # which crashes the end of a HIP-graph capture (rod.ddp.GradReducer._on_chain_stream)
         return self.n > 0 and SYNC_BN is None and torch.is_tensor(t) and t.is_cuda
 
     def stream(self, i, device):
@@ -493,15 +495,28 @@ def pw_bwd_supported(Cin, Cout, dtype):
     return "pwbwd" not in _DISABLE and bool(_abi.lib().rod_pw_bwd_supported(int(Cin), int(Cout), _DT[dtype]))
 
 
-def pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, want_dx, dw, db):
-    """rod_pw_bwd: dx (or None), dw / db written in place (fp32 [Cout, Cin] / [Cout])."""
-    Cin, Cout = x.shape[-1], y.shape[-1]
-    M = y.numel() // Cout
+def pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, want_dx, dw, db, wt0=None):
+    """rod_pw_bwd: dx (or None), dw / db written in place (fp32 [Cout, Cin] / [Cout]).
+    wt0 (the forward operand): rod_pw_bwd_rc — y is recomputed from x in the kernel, not read."""
+    Cin, Cout = x.shape[-1], dz.shape[-1]
+    M = dz.numel() // Cout
     dx = torch.empty_like(x) if want_dx else None
-    ws = workspace(_abi.query("rod_pw_bwd_workspace", M, Cin, Cout), y.device)
+    ws = workspace(_abi.query("rod_pw_bwd_workspace", M, Cin, Cout), x.device)
+    if wt0 is not None:
+        assert db is None
+        _abi.call("rod_pw_bwd_rc", dz, wt0, mean, rstd, gamma, beta, act, coef, x, *_pro_args(xpro),
+                  wt1 if want_dx else None, dx, dw, ws, M, Cin, Cout, dtcode(x), stream())
+        return dx
     _abi.call("rod_pw_bwd", dz, y, mean, rstd, gamma, beta, act, coef, x, *_pro_args(xpro), wt1 if want_dx else None,
               dx, dw, db, ws, M, Cin, Cout, dtcode(y), stream())
     return dx
+
+
+def pw_bwd_rc_ok(M, Cin, Cout, dtype):
+    """The expand backward recomputes its pre-BatchNorm y from x (ABI 23, rod_pw_bwd_rc /
+    rod_pw_bwd_gred_rc) instead of reading it: ROD_DISABLE=rc turns it off (A/B)."""
+    return "rc" not in _DISABLE and dtype == torch.bfloat16 and \
+        bool(_abi.lib().rod_pw_bwd_rc_supported(int(M), int(Cin), int(Cout), _DT[dtype]))
 
 
 def pw_bwd_gred_parts(M, Cin, Cout, dtype):
@@ -511,16 +526,22 @@ def pw_bwd_gred_parts(M, Cin, Cout, dtype):
     return int(_abi.lib().rod_pw_bwd_gred_parts(int(M), int(Cin), int(Cout), _DT[dtype]))
 
 
-def pw_bwd_gred(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, dw, dyp=False):
+def pw_bwd_gred(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, dw, dyp=False, wt0=None):
     """rod_pw_bwd_gred: the project conv's backward through its BatchNorm (dx, dw written in
     place) plus the input BatchNorm's backward sums over (dx, x) -> (dx, [nparts, 2, Cin]).
-    dyp=True: rod_pw_bwd_gred_dyp — (dy [M, Cout], parts), dx not written (ABI 20)."""
-    Cin, Cout = x.shape[-1], y.shape[-1]
-    M = y.numel() // Cout
-    nparts = pw_bwd_gred_parts(M, Cin, Cout, y.dtype)
-    out = torch.empty((M, Cout), dtype=y.dtype, device=y.device) if dyp else torch.empty_like(x)
-    xparts = torch.empty((nparts, 2, Cin), dtype=torch.float32, device=y.device)
-    ws = workspace(_abi.query("rod_pw_bwd_gred_workspace", M, Cin, Cout), y.device)
+    dyp=True: rod_pw_bwd_gred_dyp — (dy [M, Cout], parts), dx not written (ABI 20).
+    wt0 (the forward operand; the 16 -> 96 expand): rod_pw_bwd_gred_rc — y recomputed, not read."""
+    Cin, Cout = x.shape[-1], dz.shape[-1]
+    M = dz.numel() // Cout
+    nparts = pw_bwd_gred_parts(M, Cin, Cout, x.dtype)
+    out = torch.empty((M, Cout), dtype=x.dtype, device=x.device) if dyp else torch.empty_like(x)
+    xparts = torch.empty((nparts, 2, Cin), dtype=torch.float32, device=x.device)
+    ws = workspace(_abi.query("rod_pw_bwd_gred_workspace", M, Cin, Cout), x.device)
+    if wt0 is not None:
+        assert not dyp
+        _abi.call("rod_pw_bwd_gred_rc", dz, wt0, mean, rstd, gamma, beta, act, coef, x, *_pro_args(xpro), wt1, out, dw,
+                  xparts, ws, M, Cin, Cout, dtcode(x), stream())
+        return out, xparts
     _abi.call("rod_pw_bwd_gred_dyp" if dyp else "rod_pw_bwd_gred", dz, y, mean, rstd, gamma, beta, act, coef, x,
               *_pro_args(xpro), wt1, out, dw, xparts, ws, M, Cin, Cout, dtcode(y), stream())
     return out, xparts
@@ -999,7 +1020,10 @@ class _ConvBN(torch.autograd.Function):
                 _put_dz_recipe(dx, (dyp, wt1, Cout))
                 _put_bn_parts(dx, xparts)
                 return dx, None, None, None, None, None
-            dx, xparts = pw_bwd_gred(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, grad_slot(w))
+            # the 16 -> 96 expand: its pre-BatchNorm y recomputed from x in the kernel (ABI 23)
+            wt0 = _prep(w, 0, x.dtype, Cout, Cin, 1) if pw_bwd_rc_ok(M, Cin, Cout, x.dtype) else None
+            dx, xparts = pw_bwd_gred(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, grad_slot(w),
+                                     wt0=wt0)
             _mark_written(w)
             _put_bn_parts(dx, xparts)
             return dx, None, None, None, None, None
@@ -1024,7 +1048,9 @@ class _ConvBN(torch.autograd.Function):
             gw = grad_slot(w) if _needs(w) else torch.empty((Cout, Cin), dtype=torch.float32, device=y.device)
             gb = grad_slot(b) if _needs(b) else None
             wt1 = _prep(w, 1, x.dtype, Cout, Cin, 1) if need_dx else None
-            dx = pw_bwd(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, need_dx, gw, gb)
+            # the streaming expand shapes (16 -> 96, 24 -> 144): y recomputed from x (ABI 23)
+            wt0 = _prep(w, 0, x.dtype, Cout, Cin, 1) if gb is None and pw_bwd_rc_ok(M, Cin, Cout, x.dtype) else None
+            dx = pw_bwd(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, need_dx, gw, gb, wt0=wt0)
             if _needs(w):
                 _mark_written(w)
             if _needs(b):

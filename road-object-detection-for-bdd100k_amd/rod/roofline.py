@@ -20,7 +20,9 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
                          never stored
   dw3x3_bwd_fused_pw   : the same algorithmic bytes (ABI 20: dz is recomputed from the cout-wide dy_p;
                          its reads of yd and dy_p are design traffic), flops + 2*N*H*W*C*cout
-  pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product
+  pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product;
+                         the _rc forms (ABI 23) recompute y = x.W^T instead of reading it:
+                         es*(M*Cout + M*Cin [+ M*Cin dx]) + 2W, + 2*M*Cin*Cout flops
   pw_bwd_gred (project): es*(2*M*Cout + 2*M*Cin) + W, 4*M*Cin*Cout + 10*M*Cout + 6*M*Cin (the
                          input BatchNorm's sums ride on the x it reads and the dx it writes);
                          the _dyp form writes the Cout-wide dy instead of dx: es*(3*M*Cout + M*Cin) + W
@@ -127,6 +129,17 @@ def cost(name, a):
         es = _ES[dt]
         return es * (2 * M * Cout + 2 * M * Cin) + Cout * Cin * (es + 4), \
             4 * M * Cin * Cout + 10 * M * Cout + 6 * M * Cin
+    if name == "rod_pw_bwd_rc":          # ABI 23: y recomputed from x (never read)
+        M, Cin, Cout, dt = a[18], a[19], a[20], a[21]
+        es = _ES[dt]
+        want_dx = a[15] is not None
+        byts = es * (M * Cout + M * Cin + (M * Cin if want_dx else 0)) + Cout * Cin * (2 * es + 4)
+        return byts, 2 * M * Cin * Cout * (3 if want_dx else 2) + 10 * M * Cout
+    if name == "rod_pw_bwd_gred_rc":
+        M, Cin, Cout, dt = a[19], a[20], a[21], a[22]
+        es = _ES[dt]
+        return es * (M * Cout + 2 * M * Cin) + Cout * Cin * (2 * es + 4), \
+            6 * M * Cin * Cout + 10 * M * Cout + 6 * M * Cin
     if name == "rod_pw_bwd_gred_dyp":
         M, Cin, Cout, dt = a[19], a[20], a[21], a[22]
         es = _ES[dt]
@@ -230,20 +243,35 @@ def kernel_match(name, pat):
 # recompute form (PW, ABI 20) and the backward-data BatchNorm prologue (BWD, ABI 22)
 _PW = ('2, 3, true>', 'Li2ELi3ELb1EE')
 _BWD = ('32, false, true>', 'Li32ELb0ELb1EE')
+# pw_bwd_stream_kernel<CIN, COUT, PRO, DX, XG, XL, RC> (round 6 names): XG = the input sums of
+# rod_pw_bwd_gred's expand form (PRO, DX, XG all true), RC = the recompute form (last argument);
+# pw_bwd_gred_kernel<COUT, NW, FAST, DYP>: DYP = rod_pw_bwd_gred_dyp (last argument)
+_XG = (', true, true, true, ', 'Lb1ELb1ELb1E')
+_LAST = ('true>(rod::PwBwdArgs', 'Lb1EEEvNS_9PwBwdArgs')
+
+
+def _forms(base, inc=(), exc=()):
+    """Demangled and mangled patterns of the template kernel rod::`base` with the (demangled,
+    mangled) pairs of inc / exc: each form's name prefix is part of it, so an exclusion written
+    for one form never lets the other form's name through."""
+    heads = ('rod::%s<' % base, '_ZN3rod%d%sI' % (len(base), base))
+    return tuple('&'.join([heads[i]] + [t[i] for t in inc]) + ''.join('!' + t[i] for t in exc) for i in (0, 1))
 
 # C-ABI entry -> (kernel patterns of which exactly one launches once per entry call, patterns
 # of every kernel the entry launches; kernel_match) for attributing rocprofv3 PMC counters
 # (tools/pmc_traffic.py); shared helper kernels (slab_sum, splitk_combine) are not attributed.
-# rod_pw_bwd_gred and _dyp run the same kernel (dyp is an argument): PMC cannot tell them apart
 ENTRY_KERNELS = {
     # rod_bn_bwd runs only on small tensors on the training path (ops.bn_bwd_dy): the one-launch kernel
     "rod_bn_bwd": (("bn_bwd_small_kernel",), ("bn_bwd_small_kernel",)),
     "rod_bn_apply": (("bn_apply_kernel",), ("bn_apply_kernel",)),
     "rod_bn_bwd_reduce": (("bn_bwd_reduce_kernel",), ("bn_bwd_reduce_kernel", "bn_bwd_finalize_kernel")),
     "rod_bn_bwd_apply": (("bn_bwd_apply_kernel",), ("bn_bwd_apply_kernel",)),
-    "rod_pw_bwd": (("pw_bwd_kernel", "pw_bwd_stream_kernel"), ("pw_bwd_kernel", "pw_bwd_stream_kernel")),
-    "rod_pw_bwd_gred": (("pw_bwd_gred_kernel",), ("pw_bwd_gred_kernel",)),
-    "rod_pw_bwd_gred_dyp": (("pw_bwd_gred_kernel",), ("pw_bwd_gred_kernel",)),
+    "rod_pw_bwd": (_forms("pw_bwd_kernel") + _forms("pw_bwd_stream_kernel", exc=(_XG, _LAST)),) * 2,
+    "rod_pw_bwd_rc": (_forms("pw_bwd_stream_kernel", inc=(_LAST,), exc=(_XG,)),) * 2,
+    "rod_pw_bwd_gred": (_forms("pw_bwd_gred_kernel", exc=(_LAST,)) +
+                        _forms("pw_bwd_stream_kernel", inc=(_XG,), exc=(_LAST,)),) * 2,
+    "rod_pw_bwd_gred_rc": (_forms("pw_bwd_stream_kernel", inc=(_XG, _LAST)),) * 2,
+    "rod_pw_bwd_gred_dyp": (_forms("pw_bwd_gred_kernel", inc=(_LAST,)),) * 2,
     "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),

@@ -71,7 +71,7 @@ class Trainer:
         if self.sync_bn:
             from rod.ddp import SyncBatchNorm
             ops.SYNC_BN = SyncBatchNorm(world_size, getattr(reducer, 'group', None),
-                                        native=bool(getattr(reducer, 'native', False)))
+                                        comm=getattr(reducer, 'comm', None))
         else:
             ops.SYNC_BN = None
         # weight gradients beside the backward-data chain (opt-in, ROD_ENABLE=side; single

@@ -97,6 +97,60 @@ def test_grad_reducer_gloo_world2():
     np.testing.assert_array_equal(out[0][2][1][1], out[1][2][1][1])
 
 
+def _order_worker(rank, world, port, q):
+    """The native reducer's collective sequence with the calls recorded, not made: buckets
+    launched from the gradient hooks, the hard-negative sums and SyncBatchNorm gathers issued
+    between them.  Every call must be on the one communication stream, and the (entry, count,
+    dtype) sequence must be the same on every rank."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from rod import ddp
+        st = _store()
+        st.params['frozen/w'].requires_grad_(False)
+        red = ddp.GradReducer(world, bucket_mb=2 * 64 * 8 * 4 / (1 << 20), native=True, record=True).attach(st)
+        sbn = ddp.SyncBatchNorm(world, comm=red.comm)
+        ddp.TRACE = []
+        names = [n for n in st.params if n != 'frozen/w']
+        for step in range(2):
+            red.hnm_allreduce([torch.zeros(2, dtype=torch.int32)])        # ALL mode: counts in the loss
+            for i, n in enumerate(reversed(names)):
+                p = st.params[n]
+                p._rod_grad.fill_(float(rank + i))
+                p._rod_on_grad(p)
+                if i % 3 == 1:       # a SyncBatchNorm backward gather between two gradient writes
+                    g = sbn.gather(torch.full((2, 2, 3 + i), float(rank)))
+                    assert g.shape == (2 * world, 2, 3 + i)
+            red(st.flat_grad)
+        q.put((rank, list(ddp.TRACE)))
+    finally:
+        ddp.TRACE = None
+        dist.destroy_process_group()
+
+
+def test_native_collective_order_identical_across_ranks():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_order_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    t0, t1 = out[0], out[1]
+    assert len(t0) > 10 and t0 == t1
+    assert {e[3] for e in t0} == {'comm'}
+    entries = [e[0] for e in t0]
+    assert 'rod_allgather' in entries and entries.count('rod_allreduce_bucket') > 4
+    # buckets launched from inside "backward", interleaved with the gathers, not all at the end
+    first_gather = entries.index('rod_allgather')
+    assert any(e == 'rod_allreduce_bucket' and c > 2 for e, c, _, _ in t0[:first_gather + 6])
+
+
 def test_cli_flag_surface():
     """train/evaluate/predict accept the reference's flag names and defaults."""
     import train

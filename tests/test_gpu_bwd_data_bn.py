@@ -16,7 +16,17 @@ bf16 = torch.bfloat16
 # ragged / multi-tile / split-K cases
 CASES = [(115200, 384, 64, ops.ROD_ACT_RELU6), (28800, 576, 96, ops.ROD_ACT_RELU6),
          (7360, 960, 160, ops.ROD_ACT_RELU6), (1920, 960, 160, ops.ROD_ACT_RELU6), (5003, 256, 24, ops.ROD_ACT_LEAKY),
-         (3001, 128, 264, ops.ROD_ACT_NONE), (640, 1280, 128, ops.ROD_ACT_LEAKY)]
+         (3001, 128, 264, ops.ROD_ACT_NONE), (640, 1280, 128, ops.ROD_ACT_LEAKY),
+         # the upper limit of rod_conv_bwd_data_bn_supported: the table's 4096 x 8 floats of
+         # dynamic LDS beside the static tiles fill gfx950's 160 KB per workgroup
+         (515, 4096, 64, ops.ROD_ACT_RELU6)]
+
+
+def test_bwd_data_bn_supported_bound(dev):
+    lib = _abi.lib()
+    code = ops.dtcode(torch.empty(1, dtype=bf16))
+    assert lib.rod_conv_bwd_data_bn_supported(4096, 64, code) == 1
+    assert lib.rod_conv_bwd_data_bn_supported(4104, 64, code) == 0
 
 
 @pytest.mark.parametrize('M,Cout,Cin,act', CASES)

@@ -27,7 +27,11 @@ def _run(train_range, dev, steps=2):
 def test_deferring_entries_listed_and_step_deterministic(train_range, dev):
     tr_range = getattr(config.train_range, train_range)
     _abi.DEFER_UNLISTED.clear()
-    f0, l0 = _run(tr_range, dev)
+    _abi.WATCH_DEFER = True     # the registry check (off on the production path)
+    try:
+        f0, l0 = _run(tr_range, dev)
+    finally:
+        _abi.WATCH_DEFER = False
     assert not _abi.DEFER_UNLISTED, sorted(_abi.DEFER_UNLISTED)
     f1, l1 = _run(tr_range, dev)
     assert torch.equal(l0, l1), (l0, l1)

@@ -73,3 +73,23 @@ def test_native_comm_one_rank(tmp_path, dev):
     d = torch.load(out, weights_only=True)
     print(d)
     assert d['ok'], d
+
+
+ORDER_WORKER = os.path.join(ROOT, 'tests', 'dp_order_worker.py')
+
+
+def test_native_collective_order_two_ranks(tmp_path, dev):
+    """Two ranks on one GPU (gloo rendezvous), the native reducer recording its collectives:
+    REFINE, ALL (fix_refine=False: the hard-negative exchange) and ALL + SyncBatchNorm issue the
+    same (entry, count, dtype) sequence on both ranks, eager and
+    under capture, every call on the one communication stream (rod.ddp.NativeComm)."""
+    out = str(tmp_path / 'o.pt')
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(_port()), ORDER_WORKER, '--out', out]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = torch.load(out, weights_only=True)
+    print({k: ({kk: vv for kk, vv in v.items() if kk != 'entries'} if isinstance(v, dict) else v)
+           for k, v in d.items()})
+    assert d['ok'], d

@@ -1,0 +1,125 @@
+"""The expanded tensor of an inverted-residual block recomputed instead of read (ABI 23; ref
+conv_blocks.py:263-270 expand -> 238-247 depthwise, mobilenet.py:417-420 BatchNorm).
+
+y = bf16(x_act . W^T) is what the expand conv's forward (rod_conv_fwd, the streaming 1x1 kernel)
+stores.  The recompute forms re-form it per tile from the narrow block input with the same MFMA and
+rounding, so every output must be bit-identical to the form that reads the stored y:
+  * rod_pw_bwd_rc vs rod_pw_bwd (the 24 -> 144 expands, plain input; 16 -> 96 with a prologue),
+  * rod_pw_bwd_gred_rc vs rod_pw_bwd_gred (block 1's 16 -> 96 expand whose input is block 0's
+    project output: linear input BatchNorm, its backward sums handed over),
+  * a REFINE training step with the recompute on / off (ROD_DISABLE=rc), eager and graphed."""
+import pytest
+import torch
+
+from rod import _abi, ops
+
+pytestmark = pytest.mark.gpu
+bf16 = torch.bfloat16
+
+
+def _bn(C, g, dev, mag=1.0):
+    return ((torch.randn(C, generator=g) * 0.2 * mag).to(dev), (torch.rand(C, generator=g) + 0.5).to(dev),
+            (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.2).to(dev))
+
+
+def _forward_y(x, w, xpro, M, Cin, Cout):
+    """The stored expand output: rod_conv_fwd exactly as _ConvBN.forward runs it."""
+    wt0 = ops._prep(w, 0, bf16, Cout, Cin, 1)
+    y = torch.empty((1, 1, M, Cout), dtype=bf16, device=x.device)
+    ops.conv_fwd_raw(x.view(1, 1, M, Cin), wt0, None, y, 1, 1, M, Cin, Cout, 1, None, xpro)
+    return y.view(M, Cout), wt0
+
+
+# (M, Cin, Cout, input prologue act or None): the step's streaming expand shapes (720p b8 has
+# 7,372,800 rows for 16 -> 96 and 1,843,200 for 24 -> 144) at sizes the streaming forward takes
+# (M >= 65536), ragged tails, and a tile-sized case
+RC_SHAPES = [(70001, 24, 144, None), (131072, 24, 144, ops.ROD_ACT_RELU6), (65536 + 17, 16, 96, ops.ROD_ACT_NONE),
+             (100003, 16, 96, ops.ROD_ACT_RELU6), (65600, 16, 96, None)]
+
+
+@pytest.mark.parametrize('M,Cin,Cout,xact', RC_SHAPES)
+def test_pw_bwd_rc_bit_identical(dev, M, Cin, Cout, xact):
+    assert ops.pw_bwd_rc_ok(M, Cin, Cout, bf16)
+    g = torch.Generator().manual_seed(M + 3 * Cin + Cout)
+    x = (torch.randn(M, Cin, generator=g) * 1.3 + 0.2).to(dev, bf16)
+    w = (torch.randn(Cout, 1, 1, Cin, generator=g) * 0.25).to(dev)
+    xpro = None
+    if xact is not None:
+        xm, xr, xg, xb = _bn(Cin, g, dev)
+        xpro = (xm, xr, xg, xb, xact)
+    y, wt0 = _forward_y(x, w, xpro, M, Cin, Cout)
+    dz = torch.randn(M, Cout, generator=g).to(dev, bf16)
+    mean = y.float().mean(0)
+    rstd = torch.rsqrt(y.float().var(0, unbiased=False) + 1e-3)
+    gamma = (torch.rand(Cout, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(Cout, generator=g) * 0.3).to(dev)
+    act = ops.ROD_ACT_RELU6
+    coef = ops.bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, False, False)
+    wt1 = ops._prep(w, 1, bf16, Cout, Cin, 1)
+    outs = []
+    for rc in (False, True):
+        dw = torch.zeros(Cout, Cin, device=dev)
+        dx = ops.pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, True, dw, None,
+                        wt0=wt0 if rc else None)
+        outs.append((dx, dw))
+    torch.cuda.synchronize()
+    (dx0, dw0), (dx1, dw1) = outs
+    assert torch.equal(dx0, dx1), float((dx0.float() - dx1.float()).abs().max())
+    assert torch.equal(dw0, dw1), float((dw0 - dw1).abs().max())
+
+
+@pytest.mark.parametrize('M', [65536 + 17, 262144 + 5])
+def test_pw_bwd_gred_rc_bit_identical(dev, M):
+    Cin, Cout = 16, 96
+    g = torch.Generator().manual_seed(M)
+    x = (torch.randn(M, Cin, generator=g) * 2.0 - 0.4).to(dev, bf16)
+    w = (torch.randn(Cout, 1, 1, Cin, generator=g) * 0.25).to(dev)
+    xm, xr, xg, xb = _bn(Cin, g, dev)
+    xpro = (xm, xr, xg, xb, ops.ROD_ACT_NONE)     # block 0's linear project BatchNorm
+    y, wt0 = _forward_y(x, w, xpro, M, Cin, Cout)
+    dz = torch.randn(M, Cout, generator=g).to(dev, bf16)
+    mean = y.float().mean(0)
+    rstd = torch.rsqrt(y.float().var(0, unbiased=False) + 1e-3)
+    gamma = (torch.rand(Cout, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(Cout, generator=g) * 0.3).to(dev)
+    act = ops.ROD_ACT_RELU6
+    coef = ops.bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, act, False, False)
+    wt1 = ops._prep(w, 1, bf16, Cout, Cin, 1)
+    outs = []
+    for rc in (False, True):
+        dw = torch.zeros(Cout, Cin, device=dev)
+        dx, parts = ops.pw_bwd_gred(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, dw,
+                                    wt0=wt0 if rc else None)
+        outs.append((dx, dw, parts))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), float((a.float() - b.float()).abs().max())
+
+
+@pytest.mark.parametrize('graphed', [False, True])
+def test_step_recompute_bit_identical(dev, graphed):
+    """REFINE step at 480x864 b2 (blocks 1-3 take the recompute forms) with ROD_DISABLE=rc and
+    without: losses and parameters bit-identical, and the recompute entries actually ran."""
+    from rod.data import synthetic_batch
+    from rod.trainer import Trainer
+    runs = []
+    for off in (True, False):
+        if off:
+            ops._DISABLE.add('rc')
+        try:
+            tr = Trainer((480, 864), 2, dtype=bf16, device=dev, seed=7)
+            batches = [synthetic_batch(2, 480, 864, dev, seed=50 + i) for i in range(2)]
+            step = tr.step_graphed if graphed else tr.step
+            _abi.PROBE.arm(['rod_pw_bwd_rc', 'rod_pw_bwd_gred_rc', 'rod_pw_bwd', 'rod_pw_bwd_gred'])
+            losses = [step(*batches[i % 2])[0].detach().clone() for i in range(3)]
+            torch.cuda.synchronize()
+            calls = _abi.PROBE.table()
+            _abi.PROBE.disarm()
+            runs.append((tr.net.store.flat.detach().clone(), torch.stack([l.reshape(()) for l in losses]), calls))
+        finally:
+            ops._DISABLE.discard('rc')
+    (f0, l0, c0), (f1, l1, c1) = runs
+    assert 'rod_pw_bwd_rc' not in c0 and 'rod_pw_bwd_gred_rc' not in c0
+    assert c1.get('rod_pw_bwd_gred_rc', (0,))[0] >= 1 and c1.get('rod_pw_bwd_rc', (0,))[0] >= 1, c1
+    assert torch.equal(l0, l1), (l0, l1)
+    assert torch.equal(f0, f1)
