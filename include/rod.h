@@ -100,6 +100,21 @@ int rod_dw3x3_fwd_stat_parts(int N, int Ho, int Wo, int C, int stride, int dtype
 int rod_dw3x3_fwd(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
                   const float* pro_beta, int pro_act, const float* w, void* y, float* stat_parts, int N, int H,
                   int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype, void* stream);
+/* The same forward with its input recomputed, not read (ABI 23; conv_blocks.py:263-270 expand +
+ * mobilenet.py:417-420 + 238-247): the depthwise input is ReLU6(BN_e(ye)) with ye =
+ * bf16(x_act . wt0^T) the expand conv's output, x [N,H,W,Cin] the block input (x_act: its pending
+ * BatchNorm prologue x_mean.. / x_act, or x itself when x_mean is NULL), wt0 = the expand's forward
+ * operand [C][Cin] bf16, e_* the expand BatchNorm (e_act ReLU6).  Each block forms ye for its input
+ * rows with the expand forward's MFMA and rounding, so y and stat_parts (same count,
+ * rod_dw3x3_fwd_stat_parts) are bit-identical to rod_dw3x3_fwd over the stored ye with that
+ * prologue, while the C-wide ye is never read (1.42 GB at 720p b8, block 1).  bf16, stride 1 / 2,
+ * Cin 16 / 24 / 32, TF-SAME pads; rod_dw3x3_fwd_rc_supported() tells which shapes. */
+int rod_dw3x3_fwd_rc_supported(int N, int H, int W, int C, int Cin, int stride, int dtype);
+int rod_dw3x3_fwd_rc(const void* x, const float* x_mean, const float* x_rstd, const float* x_gamma,
+                     const float* x_beta, int x_act, const void* wt0, int Cin, const float* e_mean,
+                     const float* e_rstd, const float* e_gamma, const float* e_beta, int e_act, const float* w,
+                     void* y, float* stat_parts, int N, int H, int W, int C, int stride, int pad_t, int pad_l,
+                     int Ho, int Wo, int dtype, void* stream);
 /* dx = d y / d x  (DepthwiseConv2dNativeBackpropInput).
  * gred_* (nullable, ABI 4): when x was read through a BatchNorm-apply prologue, dx is the
  * gradient of that BatchNorm's output and the kernel also reduces its backward partial

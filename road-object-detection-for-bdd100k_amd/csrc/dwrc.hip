@@ -1,0 +1,447 @@
+// dwrc.hip — depthwise 3x3 forward of an inverted-residual block whose expanded input is
+// recomputed from the narrow block input instead of read (ABI 23, rod_dw3x3_fwd_rc; reference
+// conv_blocks.py:263-270 expand + mobilenet.py:417-420 BatchNorm + conv_blocks.py:238-247
+// depthwise, in training).
+//
+// The depthwise input is xe = ReLU6(BN_e(ye)), ye = bf16(x_act . We^T) the expand conv's output
+// (x_act the block input x through its own pending BatchNorm).  rod_dw3x3_fwd reads ye (the
+// C-wide expanded tensor: 1.42 GB at 720p b8 for block 1's 16 -> 96) and applies BN_e + ReLU6 in
+// its load prologue.  Here a block reads its x rows instead (Cin = 16..32 channels: 6x fewer
+// bytes) and forms each input row of its tile with MFMA:
+//   * x rows go through a two-slot LDS ring (the input prologue applied, k zero-padded to 32);
+//   * ye^T tile by tile — A = We rows (16 channels x k, in registers), B = the row's x
+//     (k x 16 pixels) — v_mfma_f32_16x16x32_bf16, the expand forward's instruction with the
+//     operands swapped, so every ye value is the stored one bit for bit; BN_e + ReLU6 and the
+//     rounding in the epilogue, one 8-byte LDS write of 4 channels per lane and tile, into a
+//     two-slot [pixel][channel] tile (pixels outside the map / rows outside the strip: 0, the
+//     padding the reference convolves);
+//   * the depthwise part is rod_dw3x3_fwd's LDS-exchange engine with its exchange slot replaced
+//     by that tile: thread (p, cvb) reads its column (pair) and right neighbour from it, the same
+//     tap order, rounding, statistics and tile plan (dw_tile: the same part structure), so y and
+//     the BatchNorm parts are bit-identical to rod_dw3x3_fwd over the stored ye.
+// One barrier per input row: row q's tile is read, row q+1's formed, row q+2's x staged.
+#include "rod_common.h"
+#include "dw_common.h"
+
+namespace rod {
+
+typedef float rc_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 rc_b2 __attribute__((ext_vector_type(2)));
+
+struct DwRcArgs {
+  const bf16_t* x;      // [N, H, W, Cin] block input
+  BnPro xp;             // its pending BatchNorm (mean NULL: none)
+  const bf16_t* wt0;    // [C][Cin] expand forward operand
+  BnPro ep;             // the expand BatchNorm + ReLU6: the depthwise input
+  const float* w;       // [3][3][C]
+  bf16_t* y;            // [N, Ho, Wo, C]
+  float* parts;         // statistics parts or NULL
+  int H, W, C, pt, pl, Ho, Wo;
+};
+
+constexpr int RC_XLD = 40;   // x slot row: k 0..31 (zero past Cin) + 8 pad (bf16 elements)
+
+// LDS plan of one block (bytes): two x slots, two ye tiles, the two prologue tables
+struct DwRcLds {
+  int npt, nct, ldy;
+  size_t xs, ys, tabs, total;
+};
+inline DwRcLds dw_rc_lds(const DwTile& t, int S, int V, int Cin) {
+  DwRcLds l;
+  const int npix = S == 2 ? 2 * t.P : t.P;
+  const int Cc = t.CVb * V;
+  l.npt = (npix + 15) / 16;
+  l.nct = (Cc + 15) / 16;
+  l.ldy = l.nct * 16 + 8;
+  l.xs = (size_t)2 * l.npt * 16 * RC_XLD * 2;
+  l.ys = (size_t)2 * l.npt * 16 * l.ldy * 2;
+  l.tabs = (size_t)(2 * Cin + 2 * l.nct * 16) * 4;
+  const size_t stats = (size_t)(256 * (2 * V + 1) + 3 * 512) * 4;   // the epilogue merge (reuses the front)
+  l.total = std::max(l.xs + l.ys + l.tabs, stats);
+  return l;
+}
+
+template <int S, int V, int CIN, bool STATS>
+__global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl, int npt, int nct, int ldy) {
+  typedef bf16_t T;
+  typedef PackV<T, V> PK;
+  static_assert(CIN % 8 == 0 && CIN <= 32, "one k step");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int CVb = tl.CVb, P = tl.P;
+  const int p = tid / CVb, cvb = tid - (tid / CVb) * CVb;
+  int bx, strip, n;
+  xcd_block(bx, strip, n);
+  const int cg = bx % tl.cgroups, ct = bx / tl.cgroups;
+  const int Cc = CVb * V, cb = cg * Cc;
+  const int c = cb + cvb * V;
+  const int H = a.H, W = a.W, C = a.C, Ho = a.Ho, Wo = a.Wo;
+  const int wo0 = ct * tl.TWo;
+  const int ho0 = strip * tl.RB;
+  const int ho1 = ho0 + tl.RB < Ho ? ho0 + tl.RB : Ho;
+  constexpr int HL = S == 1 ? 1 : 0;
+  const int wo = wo0 + p - HL;
+  const bool comp = p >= HL && p <= P - 2 && wo < Wo;
+  const int npix = S == 2 ? 2 * P : P;                 // tile pixels (input columns) of the block
+  const int cbase = S == 2 ? 2 * wo0 - a.pl : wo0 - a.pl;   // input column of tile pixel 0
+  const int NPX = npt * 16;
+
+  bf16_t* xs = (bf16_t*)smem;                          // [2][NPX][RC_XLD]
+  bf16_t* ys = xs + 2 * NPX * RC_XLD;                  // [2][NPX][ldy]
+  float* xt = (float*)(ys + 2 * NPX * ldy);            // [CIN][2]: x prologue (scale, shift)
+  float* et = xt + 2 * CIN;                            // [nct*16][2]: BN_e (scale, shift)
+
+  // ---- set-up: tables, weights, zero k padding of the x slots --------------------------------
+  const bool xpro = a.xp.mean != nullptr;
+  if (tid < CIN) {
+    float sc = 1.f, sh = 0.f;
+    if (xpro) bn_pro_affine(a.xp, tid, sc, sh);
+    xt[2 * tid] = sc;
+    xt[2 * tid + 1] = sh;
+  }
+  for (int i = tid; i < nct * 16; i += 256) {
+    float sc = 0.f, sh = 0.f;
+    if (cb + i < C) bn_pro_affine(a.ep, cb + i, sc, sh);
+    et[2 * i] = sc;
+    et[2 * i + 1] = sh;
+  }
+  for (int i = tid; i < 2 * NPX * (RC_XLD - CIN) / 8; i += 256) {
+    const int row = i / ((RC_XLD - CIN) / 8), k8 = i - row * ((RC_XLD - CIN) / 8);
+    *(bf16x8*)(xs + row * RC_XLD + CIN + k8 * 8) = bf16x8{};
+  }
+  // this wave's channel tiles (ct2 = wave, wave + 4) and their We fragments
+  bf16x8 wf[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ctile = wave + 4 * j;
+    const int ch = cb + ctile * 16 + li;
+    wf[j] = bf16x8{};
+    if (ctile < nct && ch < C && 8 * g < CIN) wf[j] = *(const bf16x8*)(a.wt0 + (long)ch * CIN + 8 * g);
+  }
+  float wr[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) wr[k][v] = a.w[k * C + c + v];
+
+  // ---- x staging: thread u < NPX*CIN/8 owns chunk (pixel u / (CIN/8), k8 = u % (CIN/8)) -------
+  constexpr int KC = CIN / 8;
+  const int xpx = tid / KC, xk8 = tid - (tid / KC) * KC;
+  const bool xown = xpx < NPX;
+  const int xci = cbase + xpx;
+  const bool xcol = xown && xpx < npix && xci >= 0 && xci < W;
+  const T* xn = a.x + (long)n * H * W * CIN;
+  const int hi0 = S == 2 ? 2 * ho0 - a.pt : ho0 - a.pt;
+  const int nin = S == 2 ? 2 * (ho1 - ho0) + 1 : ho1 - ho0 + 2;
+  auto xload = [&](int q) -> bf16x8 {
+    const int hi = hi0 + q;
+    bf16x8 v = {};
+    if (xcol && q < nin && hi >= 0 && hi < H) v = *(const bf16x8*)(xn + ((long)hi * W + xci) * CIN + xk8 * 8);
+    return v;
+  };
+  auto xstage = [&](bf16x8 v, int slot) {   // the input prologue, rounded once (the forward's values)
+    if (!xown) return;
+    if (xpro) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = xk8 * 8 + e;
+        v[e] = (bf16_t)act_fwd(fmaf((float)v[e], xt[2 * k], xt[2 * k + 1]), a.xp.act);
+      }
+    }
+    *(bf16x8*)(xs + (slot * NPX + xpx) * RC_XLD + xk8 * 8) = v;
+  };
+  // ---- ye tile of input row q into slot q & 1 ------------------------------------------------
+  auto form = [&](int q) {
+    const int slot = q & 1;
+    const int hi = hi0 + q;
+    const bool rowok = q < nin && hi >= 0 && hi < H;
+    const bf16_t* xsl = xs + slot * NPX * RC_XLD;
+    bf16_t* ysl = ys + slot * NPX * ldy;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ctile = wave + 4 * j;
+      if (ctile >= nct) break;
+      const int c0 = ctile * 16 + 4 * g;                // local channel of this lane's first value
+      const f32x4 t0 = *(const f32x4*)(et + 2 * c0), t1 = *(const f32x4*)(et + 2 * c0 + 4);
+      for (int pt_ = 0; pt_ < npt; ++pt_) {
+        const int px = pt_ * 16 + li;
+        const bf16x8 fb = *(const bf16x8*)(xsl + px * RC_XLD + 8 * g);
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], fb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const int ci = cbase + px;
+        const bool ok = rowok && px < npix && ci >= 0 && ci < W;
+        // ye rounded to bf16 (the stored value), then BN_e + ReLU6 rounded (rod_dw3x3_fwd's prologue)
+        const rc_f2 y01 = __builtin_convertvector(__builtin_convertvector(rc_f2{acc[0], acc[1]}, rc_b2), rc_f2);
+        const rc_f2 y23 = __builtin_convertvector(__builtin_convertvector(rc_f2{acc[2], acc[3]}, rc_b2), rc_f2);
+        rc_f2 z01 = __builtin_elementwise_fma(y01, rc_f2{t0[0], t0[2]}, rc_f2{t0[1], t0[3]});
+        rc_f2 z23 = __builtin_elementwise_fma(y23, rc_f2{t1[0], t1[2]}, rc_f2{t1[1], t1[3]});
+        z01 = rc_f2{act_t<ROD_ACT_RELU6>(z01.x), act_t<ROD_ACT_RELU6>(z01.y)};
+        z23 = rc_f2{act_t<ROD_ACT_RELU6>(z23.x), act_t<ROD_ACT_RELU6>(z23.y)};
+        const rc_b2 b01 = __builtin_convertvector(z01, rc_b2), b23 = __builtin_convertvector(z23, rc_b2);
+        u32x2_t o;
+        o[0] = ok ? __builtin_bit_cast(unsigned, b01) : 0u;
+        o[1] = ok ? __builtin_bit_cast(unsigned, b23) : 0u;
+        *(u32x2_t*)(ysl + px * ldy + c0) = o;
+      }
+    }
+  };
+
+  // ---- outputs and statistics (dw_lx_body's) --------------------------------------------------
+  float piv[V], s1[V], s2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) piv[v] = s1[v] = s2[v] = 0.f;
+  const unsigned es = sizeof(T);
+  T* yn = a.y + (long)n * Ho * Wo * C + c;
+  const rsrc_t rys = rod_rsrc(yn - c, (unsigned)((long)Ho * Wo * C * es));
+  const rsrc_t rnull = rod_rsrc(yn - c, 0u);
+  const unsigned vy = comp ? (unsigned)(((long)wo * C + c) * es) : ROD_OOB;
+  const unsigned rsy = (unsigned)(Wo * C * es);
+  auto emit = [&](const float (&acc)[V], int ho, bool valid, bool first) {
+    PK o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) o.set(v, acc[v]);
+    if constexpr (STATS) {
+      if (valid) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float ov = o.get(v);
+          if (first) piv[v] = ov;
+          const float d = ov - piv[v];
+          s1[v] += d;
+          s2[v] = fmaf(d, d, s2[v]);
+        }
+      }
+    }
+    o.bstore(valid ? rys : rnull, vy, (unsigned)(valid ? ho : 0) * rsy);
+  };
+  // this thread's tile pixels: S=2 the column pair 2p, 2p+1 and the right neighbour 2p+2;
+  // S=1 p-1, p, p+1 (clamped into the tile: the clamped ones feed halo columns only)
+  const int pc = S == 2 ? 2 * p : p;
+  const int pa0 = S == 2 ? pc : (pc > 0 ? pc - 1 : 0);
+  const int pb0 = S == 2 ? pc + 1 : pc;
+  const int pr0 = pc + (S == 2 ? 2 : 1) < npix ? pc + (S == 2 ? 2 : 1) : npix - 1;
+  const int ia = (p < P ? pa0 : 0) * ldy + cvb * V, ib = (p < P ? pb0 : 0) * ldy + cvb * V,
+            ir = (p < P ? pr0 : 0) * ldy + cvb * V;
+  auto rd = [&](int slot, int off, float (&o)[V]) {
+    PK v;
+    v.load(ys + slot * NPX * ldy + off);
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = v.get(e);
+  };
+
+  // ---- prologue: x rows 0, 1 staged, row 2 in flight, ye of row 0 formed ----------------------
+  xstage(xload(0), 0);
+  xstage(xload(1), 1);
+  bf16x8 xr = xload(2);
+  __syncthreads();
+  form(0);
+  __syncthreads();
+  // one step: (a) row q's tile -> taps / outputs, (b) row q+1's tile, (c) row q+2's x staged and
+  // row q+3's loaded, (d) one barrier
+  auto advance = [&](int q) {
+    form(q + 1);
+    xstage(xr, q & 1);
+    xr = xload(q + 3);
+    __syncthreads();
+  };
+  if constexpr (S == 1) {
+    float acc[3][V];
+#pragma unroll
+    for (int s_ = 0; s_ < 3; ++s_)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[s_][v] = 0.f;
+    for (int q0 = 0; q0 < nin; q0 += 3) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int q = q0 + k;
+        if (q >= nin) break;
+        float L[V], cen[V], R[V];
+        rd(q & 1, ia, L);
+        rd(q & 1, ib, cen);
+        rd(q & 1, ir, R);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int sl = (k - i + 3) % 3;
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            float t = acc[sl][v];
+            t = fmaf(L[v], wr[i * 3][v], t);
+            t = fmaf(cen[v], wr[i * 3 + 1][v], t);
+            t = fmaf(R[v], wr[i * 3 + 2][v], t);
+            acc[sl][v] = t;
+          }
+        }
+        const int sd = (k + 1) % 3;
+        const int m = q - 2;
+        emit(acc[sd], ho0 + m, m >= 0 && ho0 + m < ho1, m == 0);
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
+        advance(q);
+      }
+    }
+  } else {
+    float acc[2][V];
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[s_][v] = 0.f;
+    for (int q0 = 0; q0 < nin; q0 += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = q0 + k;
+        if (q >= nin) break;
+        float c0v[V], c1v[V], R[V];
+        rd(k & 1, ia, c0v);
+        rd(k & 1, ib, c1v);
+        rd(k & 1, ir, R);
+        auto addrow = [&](int i, int sl) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            float t = acc[sl][v];
+            t = fmaf(c0v[v], wr[i * 3][v], t);
+            t = fmaf(c1v[v], wr[i * 3 + 1][v], t);
+            t = fmaf(R[v], wr[i * 3 + 2][v], t);
+            acc[sl][v] = t;
+          }
+        };
+        if ((k & 1) == 0) {
+          const int sn = k >> 1, sd = 1 - (k >> 1);
+          addrow(2, sd);
+          const int m = (q >> 1) - 1;
+          emit(acc[sd], ho0 + m, m >= 0 && ho0 + m < ho1, m == 0);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
+          addrow(0, sn);
+        } else {
+          addrow(1, k >> 1);
+        }
+        advance(q);
+      }
+    }
+  }
+
+  if constexpr (STATS) {
+    // dw_lx_body's merge: per thread (n, mean, M2), runs of 8 columns, then the runs -> part
+    __syncthreads();
+    float* sm = (float*)smem;
+    float* sq = sm + 256 * V;
+    float* sn = sq + 256 * V;
+    const int nr = comp ? ho1 - ho0 : 0;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float inv = nr > 0 ? 1.f / (float)nr : 0.f;
+      const float dm = s1[v] * inv;
+      sm[tid * V + v] = piv[v] + dm;
+      sq[tid * V + v] = nr > 0 ? fmaxf(s2[v] - s1[v] * dm, 0.f) : 0.f;
+    }
+    sn[tid] = (float)nr;
+    __syncthreads();
+    const int nrun = (P + 7) / 8;
+    float* l1n = sn + 256;
+    float* l1m = l1n + 512;
+    float* l1q = l1m + 512;
+    for (int e = tid; e < Cc * nrun; e += 256) {
+      const int ch = e % Cc, run = e / Cc;
+      const int cve = ch / V, v = ch - cve * V;
+      float pn = 0.f, pm = 0.f, pq = 0.f;
+      for (int pp = run * 8; pp < run * 8 + 8 && pp < P; ++pp) {
+        const int t2 = pp * CVb + cve;
+        chan_merge(pn, pm, pq, sn[t2], sm[t2 * V + v], sq[t2 * V + v]);
+      }
+      l1n[e] = pn;
+      l1m[e] = pm;
+      l1q[e] = pq;
+    }
+    __syncthreads();
+    const long part = ((long)n * tl.strips + strip) * tl.coltiles + ct;
+    for (int ch = tid; ch < Cc; ch += 256) {
+      float pn = 0.f, pm = 0.f, pq = 0.f;
+      for (int run = 0; run < nrun; ++run) chan_merge(pn, pm, pq, l1n[run * Cc + ch], l1m[run * Cc + ch], l1q[run * Cc + ch]);
+      store_stat_part(a.parts, C, part, cg * Cc + ch, pn, pm, pq);
+    }
+  }
+}
+
+// the plan rod_dw3x3_fwd would use for (x, y) 16-byte aligned, restricted to what the tile
+// holds: the V pack of dw_fwd_v, whole 16-channel tiles on <= 8 tiles (2 per wave), <= 4 pixel
+// tiles (64 input columns), Cin 16 / 24 / 32
+static bool dw_rc_plan(int N, int Ho, int Wo, int C, int S, int Cin, DwTile& t, int& V, DwRcLds& l) {
+  if (N <= 0 || Ho <= 0 || Wo <= 0 || C % 8 || (S != 1 && S != 2) || (Cin != 16 && Cin != 24 && Cin != 32))
+    return false;
+  V = dw_fwd_v(ROD_BF16, (long)N * Ho * Wo * S * S, C);
+  t = dw_tile(N, Ho, Wo, C, S, V);
+  l = dw_rc_lds(t, S, V, Cin);
+  return l.npt <= 4 && l.nct <= 8 && l.npt * 16 * (Cin / 8) <= 256 && l.total <= 64 * 1024;
+}
+
+}  // namespace rod
+
+using namespace rod;
+
+extern "C" {
+
+int rod_dw3x3_fwd_rc_supported(int N, int H, int W, int C, int Cin, int stride, int dtype) {
+  if (dtype != ROD_BF16 || H <= 0 || W <= 0) return 0;
+  const int Ho = (H + stride - 1) / stride, Wo = (W + stride - 1) / stride;
+  DwTile t;
+  int V;
+  DwRcLds l;
+  return dw_rc_plan(N, Ho, Wo, C, stride, Cin, t, V, l) ? 1 : 0;
+}
+
+int rod_dw3x3_fwd_rc(const void* x, const float* x_mean, const float* x_rstd, const float* x_gamma,
+                     const float* x_beta, int x_act, const void* wt0, int Cin, const float* e_mean,
+                     const float* e_rstd, const float* e_gamma, const float* e_beta, int e_act, const float* w,
+                     void* y, float* stat_parts, int N, int H, int W, int C, int stride, int pad_t, int pad_l,
+                     int Ho, int Wo, int dtype, void* stream) {
+  ROD_CHECK_ARG(x && wt0 && e_mean && e_rstd && w && y, "rod_dw3x3_fwd_rc: NULL argument");
+  ROD_CHECK_ARG(!x_mean || x_rstd, "rod_dw3x3_fwd_rc: the input prologue needs mean and rstd");
+  ROD_CHECK_ARG(e_act == ROD_ACT_RELU6, "rod_dw3x3_fwd_rc: the expand BatchNorm's activation must be ReLU6");
+  ROD_CHECK_ARG(x_act >= ROD_ACT_NONE && x_act <= ROD_ACT_RELU, "rod_dw3x3_fwd_rc: bad input act %d", x_act);
+  ROD_CHECK_ARG(rod_dw3x3_fwd_rc_supported(N, H, W, C, Cin, stride, dtype),
+                "rod_dw3x3_fwd_rc: unsupported N=%d H=%d W=%d C=%d Cin=%d stride=%d dtype=%d", N, H, W, C, Cin,
+                stride, dtype);
+  ROD_CHECK_ARG(Ho == (H + stride - 1) / stride && Wo == (W + stride - 1) / stride && pad_t >= 0 && pad_t <= 1 &&
+                    pad_l >= 0 && pad_l <= 1,
+                "rod_dw3x3_fwd_rc: output map / TF-SAME padding mismatch");
+  ROD_CHECK_ARG(((((uintptr_t)x) | ((uintptr_t)wt0) | ((uintptr_t)y)) & 15) == 0,
+                "rod_dw3x3_fwd_rc: x, wt0, y must be 16-byte aligned");
+  ROD_CHECK_ARG((long)Ho * Wo * C * 2 < (1L << 31), "rod_dw3x3_fwd_rc: image over 2 GiB");
+  DwTile t;
+  int V;
+  DwRcLds l;
+  dw_rc_plan(N, Ho, Wo, C, stride, Cin, t, V, l);
+  const DwRcArgs a{(const bf16_t*)x, BnPro{x_mean, x_rstd, x_gamma, x_beta, x_act}, (const bf16_t*)wt0,
+                   BnPro{e_mean, e_rstd, e_gamma, e_beta, e_act}, w, (bf16_t*)y, stat_parts, H, W, C, pad_t, pad_l,
+                   Ho, Wo};
+  const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
+  hipStream_t s = ROD_STREAM(stream);
+#define RCK(S_, V_, CI_)                                                                                        \
+  do {                                                                                                          \
+    if (stat_parts)                                                                                             \
+      hipLaunchKernelGGL((dw3x3_fwd_rc_kernel<S_, V_, CI_, true>), grid, dim3(256), l.total, s, a, t, l.npt,  \
+                         l.nct, l.ldy);                                                                         \
+    else                                                                                                        \
+      hipLaunchKernelGGL((dw3x3_fwd_rc_kernel<S_, V_, CI_, false>), grid, dim3(256), l.total, s, a, t, l.npt, \
+                         l.nct, l.ldy);                                                                         \
+  } while (0)
+#define RCV(S_, CI_)                   \
+  do {                                 \
+    if (V == 8) RCK(S_, 8, CI_);       \
+    else RCK(S_, 4, CI_);              \
+  } while (0)
+#define RCC(S_)                                    \
+  do {                                             \
+    if (Cin == 16) RCV(S_, 16);                    \
+    else if (Cin == 24) RCV(S_, 24);               \
+    else RCV(S_, 32);                              \
+  } while (0)
+  if (stride == 1) RCC(1);
+  else RCC(2);
+#undef RCC
+#undef RCV
+#undef RCK
+  return check_launch("rod_dw3x3_fwd_rc");
+}
+
+}  // extern "C"

@@ -514,9 +514,25 @@ def pw_bwd(dz, y, mean, rstd, gamma, beta, act, coef, x, xpro, wt1, want_dx, dw,
 
 def pw_bwd_rc_ok(M, Cin, Cout, dtype):
     """The expand backward recomputes its pre-BatchNorm y from x (ABI 23, rod_pw_bwd_rc /
-    rod_pw_bwd_gred_rc) instead of reading it: ROD_DISABLE=rc turns it off (A/B)."""
-    return "rc" not in _DISABLE and dtype == torch.bfloat16 and \
-        bool(_abi.lib().rod_pw_bwd_rc_supported(int(M), int(Cin), int(Cout), _DT[dtype]))
+    rod_pw_bwd_gred_rc) instead of reading it: ROD_DISABLE=rc turns it off (A/B).  Taken for
+    block 1's 16 -> 96 (720p b8: 683 -> 549 us); the 24 -> 144 form measured slower (266 -> 310 us
+    a call: one wave per SIMD, nothing hides the recompute's LDS round trip) and is opt-in
+    (ROD_ENABLE=rc144)."""
+    if "rc" in _DISABLE or dtype != torch.bfloat16 or (Cin != 16 and "rc144" not in _ENABLE):
+        return False
+    return bool(_abi.lib().rod_pw_bwd_rc_supported(int(M), int(Cin), int(Cout), _DT[dtype]))
+
+
+def dw_rc_ok(xe, N, H, W, C, stride):
+    """(x, x prologue, wt0, Cin) when the depthwise input xe is an expand conv's output that
+    rod_dw3x3_fwd_rc can recompute (ABI 23; ROD_DISABLE=rcdw: read the stored tensor), else None."""
+    src = getattr(xe, "_rod_expand", None)
+    if src is None or "rc" in _DISABLE or "rcdw" in _DISABLE or xe.dtype != torch.bfloat16:
+        return None
+    xin, xpro, wt0, Cin = src
+    if not _abi.lib().rod_dw3x3_fwd_rc_supported(N, H, W, C, int(Cin), int(stride), _DT[xe.dtype]):
+        return None
+    return src
 
 
 def pw_bwd_gred_parts(M, Cin, Cout, dtype):
@@ -975,6 +991,9 @@ class _ConvBN(torch.autograd.Function):
             x, ipro = xb, None
         ctx.src_dw = getattr(x, "_rod_dw", None)   # x is a depthwise output (_DWBN.forward)
         conv_fwd_raw(x, wt, b, y, N, H, W, Cin, Cout, ks, parts, ipro)
+        if ks == 1 and b is None and training and x.dtype == torch.bfloat16 and Cin <= 32:
+            # an expand conv: the consumer depthwise may recompute y from x (dw_rc_ok, ABI 23)
+            y._rod_expand = (x, ipro, wt, Cin)
         mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
         ctx.save_for_backward(x, w, b, y, mean, rstd)
         ctx.ks, ctx.ipro, ctx.gb, ctx.act, ctx.training = ks, ipro, (gamma, beta), act, training
@@ -1091,8 +1110,15 @@ class _DWBN(torch.autograd.Function):
         if training:
             nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C, stride, dtcode(x))
             parts = torch.empty((nparts, 3, C), dtype=torch.float32, device=x.device)
-        _abi.call("rod_dw3x3_fwd", x, *_pro_args(ipro), w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, dtcode(x),
-                  stream())
+        rc = dw_rc_ok(x, N, H, W, C, stride) if ipro is not None and ipro[4] == ROD_ACT_RELU6 else None
+        if rc is not None:
+            # the expanded input recomputed from the block input, never read (ABI 23)
+            xin, xpro, wt0, Cin = rc
+            _abi.call("rod_dw3x3_fwd_rc", xin, *_pro_args(xpro), wt0, Cin, *_pro_args(ipro), w, y, parts, N, H, W, C,
+                      stride, pt, pl, Ho, Wo, dtcode(x), stream())
+        else:
+            _abi.call("rod_dw3x3_fwd", x, *_pro_args(ipro), w, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo,
+                      dtcode(x), stream())
         y._rod_dw = (stride, ipro[4] if ipro is not None else -1)   # for the consumer's backward (dw_pw_ok)
         mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
         ctx.save_for_backward(x, w, y, mean, rstd)

@@ -2,6 +2,8 @@
 from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
 
   dw3x3 fwd / bwd_data : es*(in + out) + 9*C*4 bytes, 18*N*Ho*Wo*C flops
+  dw3x3 fwd_rc         : es*(x + out + We) + 9*C*4 (x the Cin-wide block input: the expanded input
+                         is recomputed, ABI 23), 2*N*H*W*Cin*C + 18*N*Ho*Wo*C
   dw3x3 bwd_filter     : es*(x + dy) + 9*C*4, 18*N*Ho*Wo*C
   conv fwd (1x1 / 3x3) : es*(M*Cin + M*Cout + Cout*K) (+4*Cout bias), 2*M*K*Cout; the _bnact form
                          (inference BatchNorm epilogue) + es*M*Cout for a residual
@@ -58,6 +60,11 @@ def cost(name, a):
         N, H, W, C, Ho, Wo, dt = a[9], a[10], a[11], a[12], a[16], a[17], a[18]
         es = _ES[dt]
         return es * (N * H * W * C + N * Ho * Wo * C) + 36 * C, 18 * N * Ho * Wo * C
+    if name == "rod_dw3x3_fwd_rc":        # ABI 23: the expanded input recomputed from the block input
+        N, H, W, C, Ho, Wo, dt, Cin = a[16], a[17], a[18], a[19], a[23], a[24], a[25], a[7]
+        es = _ES[dt]
+        return es * (N * H * W * Cin + N * Ho * Wo * C + C * Cin) + 36 * C, \
+            2 * N * H * W * Cin * C + 18 * N * Ho * Wo * C
     if name == "rod_dw3x3_bwd_data":
         N, H, W, C, Ho, Wo, dt = a[10], a[11], a[12], a[13], a[17], a[18], a[19]
         es = _ES[dt]
@@ -272,7 +279,8 @@ ENTRY_KERNELS = {
                         _forms("pw_bwd_stream_kernel", inc=(_XG,), exc=(_LAST,)),) * 2,
     "rod_pw_bwd_gred_rc": (_forms("pw_bwd_stream_kernel", inc=(_XG, _LAST)),) * 2,
     "rod_pw_bwd_gred_dyp": (_forms("pw_bwd_gred_kernel", inc=(_LAST,)),) * 2,
-    "rod_dw3x3_fwd": (("dw3x3_fwd_",), ("dw3x3_fwd_",)),
+    "rod_dw3x3_fwd": (("dw3x3_fwd_!dw3x3_fwd_rc",), ("dw3x3_fwd_!dw3x3_fwd_rc",)),
+    "rod_dw3x3_fwd_rc": (("dw3x3_fwd_rc_kernel",), ("dw3x3_fwd_rc_kernel",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),
     "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused!" + "!".join(_PW),), ("dw3x3_bwd_fused!" + "!".join(_PW),)),

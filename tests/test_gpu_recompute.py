@@ -7,6 +7,8 @@ rounding, so every output must be bit-identical to the form that reads the store
   * rod_pw_bwd_rc vs rod_pw_bwd (the 24 -> 144 expands, plain input; 16 -> 96 with a prologue),
   * rod_pw_bwd_gred_rc vs rod_pw_bwd_gred (block 1's 16 -> 96 expand whose input is block 0's
     project output: linear input BatchNorm, its backward sums handed over),
+  * rod_dw3x3_fwd_rc vs rod_dw3x3_fwd over the stored tensor with the BN_e + ReLU6 prologue: y and
+    the BatchNorm statistics parts (stride 2 and 1, both pack widths of the tile plan),
   * a REFINE training step with the recompute on / off (ROD_DISABLE=rc), eager and graphed."""
 import pytest
 import torch
@@ -39,7 +41,7 @@ RC_SHAPES = [(70001, 24, 144, None), (131072, 24, 144, ops.ROD_ACT_RELU6), (6553
 
 @pytest.mark.parametrize('M,Cin,Cout,xact', RC_SHAPES)
 def test_pw_bwd_rc_bit_identical(dev, M, Cin, Cout, xact):
-    assert ops.pw_bwd_rc_ok(M, Cin, Cout, bf16)
+    assert _abi.lib().rod_pw_bwd_rc_supported(M, Cin, Cout, ops.dtcode(torch.empty(1, dtype=bf16)))
     g = torch.Generator().manual_seed(M + 3 * Cin + Cout)
     x = (torch.randn(M, Cin, generator=g) * 1.3 + 0.2).to(dev, bf16)
     w = (torch.randn(Cout, 1, 1, Cin, generator=g) * 0.25).to(dev)
@@ -110,7 +112,8 @@ def test_step_recompute_bit_identical(dev, graphed):
             tr = Trainer((480, 864), 2, dtype=bf16, device=dev, seed=7)
             batches = [synthetic_batch(2, 480, 864, dev, seed=50 + i) for i in range(2)]
             step = tr.step_graphed if graphed else tr.step
-            _abi.PROBE.arm(['rod_pw_bwd_rc', 'rod_pw_bwd_gred_rc', 'rod_pw_bwd', 'rod_pw_bwd_gred'])
+            _abi.PROBE.arm(['rod_pw_bwd_rc', 'rod_pw_bwd_gred_rc', 'rod_pw_bwd', 'rod_pw_bwd_gred', 'rod_dw3x3_fwd_rc',
+                            'rod_dw3x3_fwd'])
             losses = [step(*batches[i % 2])[0].detach().clone() for i in range(3)]
             torch.cuda.synchronize()
             calls = _abi.PROBE.table()
@@ -119,7 +122,55 @@ def test_step_recompute_bit_identical(dev, graphed):
         finally:
             ops._DISABLE.discard('rc')
     (f0, l0, c0), (f1, l1, c1) = runs
-    assert 'rod_pw_bwd_rc' not in c0 and 'rod_pw_bwd_gred_rc' not in c0
-    assert c1.get('rod_pw_bwd_gred_rc', (0,))[0] >= 1 and c1.get('rod_pw_bwd_rc', (0,))[0] >= 1, c1
+    assert 'rod_pw_bwd_rc' not in c0 and 'rod_pw_bwd_gred_rc' not in c0 and 'rod_dw3x3_fwd_rc' not in c0
+    assert c1.get('rod_pw_bwd_gred_rc', (0,))[0] >= 1, c1
+    assert c1.get('rod_dw3x3_fwd_rc', (0,))[0] >= 1, c1
     assert torch.equal(l0, l1), (l0, l1)
     assert torch.equal(f0, f1)
+
+
+# (N, H, W, Cin, C, stride, input prologue act or None): block 1 (720p, 16 -> 96, stride 2, the
+# 16-byte pack plan) on 2 images, block 3 / block 2 shapes (24 -> 144 at 360x640, strides 2 / 1),
+# small maps on the 8-byte pack plan with odd sizes (TF-SAME pads 1 / 0), Cin 32
+DW_SHAPES = [(2, 720, 1280, 16, 96, 2, ops.ROD_ACT_NONE), (8, 360, 640, 24, 144, 2, None),
+             (5, 360, 640, 24, 144, 1, None), (2, 99, 171, 16, 96, 2, ops.ROD_ACT_RELU6),
+             (3, 57, 83, 24, 144, 1, ops.ROD_ACT_NONE), (2, 64, 96, 32, 192, 1, None), (1, 37, 45, 32, 192, 2, None)]
+
+
+@pytest.mark.parametrize('N,H,W,Cin,C,stride,xact', DW_SHAPES)
+def test_dw3x3_fwd_rc_bit_identical(dev, N, H, W, Cin, C, stride, xact):
+    code = ops.dtcode(torch.empty(1, dtype=bf16))
+    assert _abi.lib().rod_dw3x3_fwd_rc_supported(N, H, W, C, Cin, stride, code)
+    g = torch.Generator().manual_seed(N * H + W + C + stride)
+    M = N * H * W
+    x = (torch.randn(N, H, W, Cin, generator=g) * 1.4 + 0.1).to(dev, bf16)
+    w_e = (torch.randn(C, 1, 1, Cin, generator=g) * 0.3).to(dev)
+    xpro = None
+    if xact is not None:
+        xm, xr, xg, xb = _bn(Cin, g, dev)
+        xpro = (xm, xr, xg, xb, xact)
+    ye, wt0 = _forward_y(x.view(M, Cin), w_e, xpro, M, Cin, C)
+    ye = ye.view(N, H, W, C)
+    em = ye.float().mean((0, 1, 2)) + (torch.randn(C, generator=g) * 0.05).to(dev)
+    er = torch.rsqrt(ye.float().var((0, 1, 2), unbiased=False) + 1e-3)
+    eg, eb = (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.5 + 0.5).to(dev)
+    epro = (em, er, eg, eb, ops.ROD_ACT_RELU6)
+    wd = (torch.randn(3, 3, C, generator=g) * 0.3).to(dev)
+    Ho, pt = ops.same_pad(H, stride)
+    Wo, pl = ops.same_pad(W, stride)
+    nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C, stride, code)
+    outs = []
+    for rc in (False, True):
+        y = torch.empty((N, Ho, Wo, C), dtype=bf16, device=dev)
+        parts = torch.full((nparts, 3, C), -7.0, device=dev)
+        if rc:
+            _abi.call('rod_dw3x3_fwd_rc', x, *ops._pro_args(xpro), wt0, Cin, *ops._pro_args(epro), wd, y, parts, N, H,
+                      W, C, stride, pt, pl, Ho, Wo, code, ops.stream())
+        else:
+            _abi.call('rod_dw3x3_fwd', ye, *ops._pro_args(epro), wd, y, parts, N, H, W, C, stride, pt, pl, Ho, Wo, code,
+                      ops.stream())
+        outs.append((y, parts))
+    torch.cuda.synchronize()
+    (y0, p0), (y1, p1) = outs
+    assert torch.equal(y0, y1), float((y0.float() - y1.float()).abs().max())
+    assert torch.equal(p0, p1), float((p0 - p1).abs().max())
