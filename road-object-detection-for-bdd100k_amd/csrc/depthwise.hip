@@ -1631,10 +1631,6 @@ int rod_dw3x3_bwd_filter_bn(const void* x, const float* pro_mean, const float* p
 // order of the stride-1 rod_dw3x3_bwd_data kernel (dy rows ascending, taps L, C, R), so dx is
 // bit-identical to the unfused chain; dw and the BN_e sums are reassociated (column tiles).
 // =====================================================================================
-struct DwBwdBn {
-  const float *mean, *rstd, *gamma, *beta, *coef;  // BN_d and its backward coefficients [3][C]
-  int act;
-};
 
 template <typename T, int PACT, bool RED, int D = 3>
 __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restrict__ ye, const T* __restrict__ dz,
@@ -1840,26 +1836,6 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_fused_kernel(const T* __restric
   }
 }
 
-// Epilogue of the packed depthwise backward kernels: the per-block column sums of the nq staged
-// quantities (the 9 filter taps, then with the BatchNorm sums g and g*yhat; red = [nq][TB][V]
-// floats, halo lanes staged as 0) — every (quantity, channel) summed over the computing columns
-// 1 .. P-2 in column order by one thread, after ONE barrier for all quantities (the
-// one-quantity-at-a-time form took two barriers a quantity with Cc of the TB threads working;
-// the sums, and so the parts, are bit-identical).
-template <int V>
-__device__ __forceinline__ void dw_colsum_emit(const float* red, int q0, int nq, int TB, int Cc, int CVb, int P,
-                                               float* slab, float* gparts, long part, int C, int cg) {
-  for (int e = threadIdx.x; e < nq * Cc; e += TB) {
-    const int qs = e / Cc, ce = e - qs * Cc, qk = q0 + qs;
-    const int cve = ce / V, v = ce - cve * V;
-    const float* r = red + qs * TB * V;
-    float s = 0.f;
-    for (int pp = 1; pp <= P - 2; ++pp) s += r[(pp * CVb + cve) * V + v];
-    float* dst = qk < 9 ? slab + (part * 9 + qk) * C : gparts + (part * 2 + (qk - 9)) * C;
-    dst[cg * Cc + ce] = s;
-  }
-}
-
 // Issue-lean form of dw3x3_bwd_fused_kernel (the default; ROD_DWF_V1=1 selects the one above).
 // Same engine, same per-element arithmetic and accumulation order (dx bit-identical), cut for
 // the instruction stream (tools/dwfused_bench.py PMC: the step was ~230 VALU + ~90 SALU per
@@ -1873,40 +1849,6 @@ __device__ __forceinline__ void dw_colsum_emit(const float* red, int q0, int nq,
 //   * the activation gradients are specialised (ReLU6: one compare pair + select), and the
 //     BN_e gradient mask comes from the prologue's own z (the x element of the same row);
 //   * yhat_e = fma(ye, rstd, -mean * rstd) (the stride-2 kernel's form).
-typedef float dw_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ dw_f2 f2fma(dw_f2 a, dw_f2 b, dw_f2 c) { return __builtin_elementwise_fma(a, b, c); }
-template <int ACT>
-__device__ __forceinline__ float agrad(float z, int act) {
-  if constexpr (ACT == ROD_ACT_RELU6) return (z > 0.f && !(z >= 6.f)) ? 1.f : 0.f;  // == act_grad(z, RELU6)
-  else return act_grad(z, act);
-}
-template <typename T>
-__device__ __forceinline__ void unpack4(const PackV<T, 4>& p, dw_f2& a, dw_f2& b) {
-  a = dw_f2{p.get(0), p.get(1)};
-  b = dw_f2{p.get(2), p.get(3)};
-}
-template <typename T, int V>
-__device__ __forceinline__ void unpackv(const PackV<T, V>& p, dw_f2 (&o)[V / 2]) {
-#pragma unroll
-  for (int h = 0; h < V / 2; ++h) o[h] = dw_f2{p.get(2 * h), p.get(2 * h + 1)};
-}
-// one v_cvt_pk_bf16_f32 for the pair (RNE, as (bf16_t)x per element), unpacked by a shift / mask
-typedef __bf16 dw_b2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ dw_f2 round2(dw_f2 v, bf16_t) {
-  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(v, dw_b2));
-  return dw_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
-}
-// ReLU6 gradient gate (z > 0 && z < 6, NaN -> 0: agrad<ROD_ACT_RELU6>) as one unsigned compare
-// on the bits: positive floats order as integers, negative ones and NaN land above 6.0's bits
-__device__ __forceinline__ bool relu6_open(float z) {
-  return __builtin_bit_cast(unsigned, z) - 1u < 0x40BFFFFFu;
-}
-template <int ACT>
-__device__ __forceinline__ dw_f2 gate2(dw_f2 z, dw_f2 v, int act) {
-  if constexpr (ACT == ROD_ACT_RELU6) return dw_f2{relu6_open(z.x) ? v.x : 0.f, relu6_open(z.y) ? v.y : 0.f};
-  else return dw_f2{v.x * act_grad(z.x, act), v.y * act_grad(z.y, act)};
-}
-__device__ __forceinline__ dw_f2 round2(dw_f2 v, float) { return v; }
 
 // Project-gradient recompute (PW, ABI 20: rod_dw3x3_bwd_fused_pw).  In an inverted-residual block
 // dz — the gradient at act_d(BN_d(yd)), i.e. at the project conv's input — is dy_p . W_p with dy_p
@@ -2760,20 +2702,6 @@ __global__ void __launch_bounds__(1024 / V, V == 4 ? 2 : 1) dw3x3_bwd_fused_s2p_
   }
   __syncthreads();
   dw_colsum_emit<V>(red, 0, RED ? 11 : 9, TB, Cc, CVb, P, slab, gparts, part, C, cg);
-}
-
-// Both strides tile a map with one halo column each side (the S=1 plan geometry): stride 1
-// the output (= input) map, stride 2 the (A, B) map of dy positions that own a dx row / column.
-static bool dw_fused_geom(int N, int H, int W, int C, int S, int pt, int pl, int& A, int& B) {
-  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4) return false;
-  if (S == 1) {
-    if (pt != 1 || pl != 1) return false;
-    A = H, B = W;
-    return true;
-  }
-  if (S != 2 || pt < 0 || pt > 1 || pl < 0 || pl > 1) return false;
-  A = ((H - 1 + pt) >> 1) + 1, B = ((W - 1 + pl) >> 1) + 1;
-  return true;
 }
 
 extern "C" {

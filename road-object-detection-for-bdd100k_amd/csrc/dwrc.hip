@@ -50,7 +50,7 @@ inline DwRcLds dw_rc_lds(const DwTile& t, int S, int V, int Cin) {
   DwRcLds l;
   const int npix = S == 2 ? 2 * t.P : t.P;
   const int Cc = t.CVb * V;
-  l.npt = (npix + 15) / 16;
+  l.npt = std::max(2, (npix + 15) / 16);   // the kernel instantiates 2, 3 or 4 pixel tiles
   l.nct = (Cc + 15) / 16;
   l.ldy = l.nct * 16 + 8;
   l.xs = (size_t)2 * l.npt * 16 * RC_XLD * 2;
@@ -61,8 +61,9 @@ inline DwRcLds dw_rc_lds(const DwTile& t, int S, int V, int Cin) {
   return l;
 }
 
-template <int S, int V, int CIN, bool STATS>
-__global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl, int npt, int nct, int ldy) {
+template <int S, int V, int CIN, bool STATS, int NPT>
+__global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl, int nct, int ldy) {
+  constexpr int npt = NPT;
   typedef bf16_t T;
   typedef PackV<T, V> PK;
   static_assert(CIN % 8 == 0 && CIN <= 32, "one k step");
@@ -110,7 +111,8 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl
     const int row = i / ((RC_XLD - CIN) / 8), k8 = i - row * ((RC_XLD - CIN) / 8);
     *(bf16x8*)(xs + row * RC_XLD + CIN + k8 * 8) = bf16x8{};
   }
-  // this wave's channel tiles (ct2 = wave, wave + 4) and their We fragments
+  __syncthreads();   // the tables are read by every thread's first x staging below
+  // this wave's channel tiles (wave, wave + 4) and their We fragments
   bf16x8 wf[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -134,11 +136,15 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl
   const T* xn = a.x + (long)n * H * W * CIN;
   const int hi0 = S == 2 ? 2 * ho0 - a.pt : ho0 - a.pt;
   const int nin = S == 2 ? 2 * (ho1 - ho0) + 1 : ho1 - ho0 + 2;
+  // buffer loads, issued unconditionally (rod_common.h: a load under a branch makes the compiler
+  // drain the ring every step): the row clamped into the map (rows outside it are zeroed when the
+  // tile is formed), columns outside it at the out-of-range offset (they return 0)
+  const rsrc_t rx = rod_rsrc(xn, (unsigned)((long)H * W * CIN * 2));
+  const unsigned vx = xcol ? (unsigned)((xci * CIN + xk8 * 8) * 2) : ROD_OOB;
   auto xload = [&](int q) -> bf16x8 {
     const int hi = hi0 + q;
-    bf16x8 v = {};
-    if (xcol && q < nin && hi >= 0 && hi < H) v = *(const bf16x8*)(xn + ((long)hi * W + xci) * CIN + xk8 * 8);
-    return v;
+    const int hc = hi < 0 ? 0 : (hi >= H ? H - 1 : hi);
+    return buf_ld<bf16x8>(rx, vx, (unsigned)hc * (unsigned)(W * CIN * 2));
   };
   auto xstage = [&](bf16x8 v, int slot) {   // the input prologue, rounded once (the forward's values)
     if (!xown) return;
@@ -158,16 +164,22 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl
     const bool rowok = q < nin && hi >= 0 && hi < H;
     const bf16_t* xsl = xs + slot * NPX * RC_XLD;
     bf16_t* ysl = ys + slot * NPX * ldy;
+    // wave w forms channel tiles w and w + 4 for every pixel tile: the B fragments (x) read once
+    // per row, the A fragments (We) in registers.  (Dealing the units round-robin over the waves
+    // measured slower: 570 -> 703 us at 720p b8 block 1, a runtime unit loop and A from LDS.)
+    bf16x8 fb[npt];
+#pragma unroll
+    for (int pt_ = 0; pt_ < npt; ++pt_) fb[pt_] = *(const bf16x8*)(xsl + (pt_ * 16 + li) * RC_XLD + 8 * g);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int ctile = wave + 4 * j;
       if (ctile >= nct) break;
       const int c0 = ctile * 16 + 4 * g;                // local channel of this lane's first value
       const f32x4 t0 = *(const f32x4*)(et + 2 * c0), t1 = *(const f32x4*)(et + 2 * c0 + 4);
+#pragma unroll
       for (int pt_ = 0; pt_ < npt; ++pt_) {
         const int px = pt_ * 16 + li;
-        const bf16x8 fb = *(const bf16x8*)(xsl + px * RC_XLD + 8 * g);
-        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], fb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], fb[pt_], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         const int ci = cbase + px;
         const bool ok = rowok && px < npix && ci >= 0 && ci < W;
         // ye rounded to bf16 (the stored value), then BN_e + ReLU6 rounded (rod_dw3x3_fwd's prologue)
@@ -229,19 +241,24 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl
     for (int e = 0; e < V; ++e) o[e] = v.get(e);
   };
 
-  // ---- prologue: x rows 0, 1 staged, row 2 in flight, ye of row 0 formed ----------------------
+  // ---- prologue: x rows 0, 1 staged, rows 2 .. D+1 in flight, ye of row 0 formed ----------------
+  // x prefetch ring of D rows (the step loop's unroll: 3 for stride 1, 4 for stride 2): at step q
+  // row q+2 is staged from slot (q+2) % D and row q+2+D loaded into it, D steps of latency cover
+  constexpr int D = S == 1 ? 3 : 4;
+  bf16x8 xr[D];
   xstage(xload(0), 0);
   xstage(xload(1), 1);
-  bf16x8 xr = xload(2);
+#pragma unroll
+  for (int r = 2; r < 2 + D; ++r) xr[r % D] = xload(r);
   __syncthreads();
   form(0);
   __syncthreads();
-  // one step: (a) row q's tile -> taps / outputs, (b) row q+1's tile, (c) row q+2's x staged and
-  // row q+3's loaded, (d) one barrier
-  auto advance = [&](int q) {
+  // one step (k = q mod D): (a) row q's tile -> taps / outputs, (b) row q+1's tile, (c) row q+2's
+  // x staged and row q+2+D's loaded, (d) one barrier
+  auto advance = [&](int q, int k) {
     form(q + 1);
-    xstage(xr, q & 1);
-    xr = xload(q + 3);
+    xstage(xr[(k + 2) % D], q & 1);
+    xr[(k + 2) % D] = xload(q + 2 + D);
     __syncthreads();
   };
   if constexpr (S == 1) {
@@ -276,7 +293,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl
         emit(acc[sd], ho0 + m, m >= 0 && ho0 + m < ho1, m == 0);
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[sd][v] = 0.f;
-        advance(q);
+        advance(q, k);
       }
     }
   } else {
@@ -315,7 +332,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl
         } else {
           addrow(1, k >> 1);
         }
-        advance(q);
+        advance(q, k);
       }
     }
   }
@@ -416,14 +433,22 @@ int rod_dw3x3_fwd_rc(const void* x, const float* x_mean, const float* x_rstd, co
                    Ho, Wo};
   const dim3 grid(t.coltiles * t.cgroups, t.strips, N);
   hipStream_t s = ROD_STREAM(stream);
-#define RCK(S_, V_, CI_)                                                                                        \
-  do {                                                                                                          \
-    if (stat_parts)                                                                                             \
-      hipLaunchKernelGGL((dw3x3_fwd_rc_kernel<S_, V_, CI_, true>), grid, dim3(256), l.total, s, a, t, l.npt,  \
-                         l.nct, l.ldy);                                                                         \
-    else                                                                                                        \
-      hipLaunchKernelGGL((dw3x3_fwd_rc_kernel<S_, V_, CI_, false>), grid, dim3(256), l.total, s, a, t, l.npt, \
-                         l.nct, l.ldy);                                                                         \
+#define RCN(S_, V_, CI_, ST_)                                                                                  \
+  do {                                                                                                         \
+    if (l.npt <= 2)                                                                                            \
+      hipLaunchKernelGGL((dw3x3_fwd_rc_kernel<S_, V_, CI_, ST_, 2>), grid, dim3(256), l.total, s, a, t, l.nct, \
+                         l.ldy);                                                                               \
+    else if (l.npt == 3)                                                                                       \
+      hipLaunchKernelGGL((dw3x3_fwd_rc_kernel<S_, V_, CI_, ST_, 3>), grid, dim3(256), l.total, s, a, t, l.nct, \
+                         l.ldy);                                                                               \
+    else                                                                                                       \
+      hipLaunchKernelGGL((dw3x3_fwd_rc_kernel<S_, V_, CI_, ST_, 4>), grid, dim3(256), l.total, s, a, t, l.nct, \
+                         l.ldy);                                                                               \
+  } while (0)
+#define RCK(S_, V_, CI_)                         \
+  do {                                           \
+    if (stat_parts) RCN(S_, V_, CI_, true);      \
+    else RCN(S_, V_, CI_, false);                \
   } while (0)
 #define RCV(S_, CI_)                   \
   do {                                 \
@@ -441,6 +466,7 @@ int rod_dw3x3_fwd_rc(const void* x, const float* x_mean, const float* x_rstd, co
 #undef RCC
 #undef RCV
 #undef RCK
+#undef RCN
   return check_launch("rod_dw3x3_fwd_rc");
 }
 

@@ -525,9 +525,12 @@ def pw_bwd_rc_ok(M, Cin, Cout, dtype):
 
 def dw_rc_ok(xe, N, H, W, C, stride):
     """(x, x prologue, wt0, Cin) when the depthwise input xe is an expand conv's output that
-    rod_dw3x3_fwd_rc can recompute (ABI 23; ROD_DISABLE=rcdw: read the stored tensor), else None."""
+    rod_dw3x3_fwd_rc can recompute (ABI 23), else None.  Opt-in (ROD_ENABLE=rcdw): bit-identical,
+    but measured slower than reading the stored tensor at every 720p b8 block shape
+    (tools/rc_bench.py: block 1 378 -> 570 us, block 2 288 -> 357) — the per-row MFMA
+    and its epilogue sit on the barrier-synchronised row pipeline of a 4-wave block."""
     src = getattr(xe, "_rod_expand", None)
-    if src is None or "rc" in _DISABLE or "rcdw" in _DISABLE or xe.dtype != torch.bfloat16:
+    if src is None or "rc" in _DISABLE or "rcdw" not in _ENABLE or xe.dtype != torch.bfloat16:
         return None
     xin, xpro, wt0, Cin = src
     if not _abi.lib().rod_dw3x3_fwd_rc_supported(N, H, W, C, int(Cin), int(stride), _DT[xe.dtype]):

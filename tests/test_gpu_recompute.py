@@ -108,6 +108,8 @@ def test_step_recompute_bit_identical(dev, graphed):
     for off in (True, False):
         if off:
             ops._DISABLE.add('rc')
+        else:
+            ops._ENABLE.add('rcdw')   # the opt-in depthwise forward recompute too
         try:
             tr = Trainer((480, 864), 2, dtype=bf16, device=dev, seed=7)
             batches = [synthetic_batch(2, 480, 864, dev, seed=50 + i) for i in range(2)]
@@ -121,6 +123,7 @@ def test_step_recompute_bit_identical(dev, graphed):
             runs.append((tr.net.store.flat.detach().clone(), torch.stack([l.reshape(()) for l in losses]), calls))
         finally:
             ops._DISABLE.discard('rc')
+            ops._ENABLE.discard('rcdw')
     (f0, l0, c0), (f1, l1, c1) = runs
     assert 'rod_pw_bwd_rc' not in c0 and 'rod_pw_bwd_gred_rc' not in c0 and 'rod_dw3x3_fwd_rc' not in c0
     assert c1.get('rod_pw_bwd_gred_rc', (0,))[0] >= 1, c1
