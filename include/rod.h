@@ -155,6 +155,24 @@ int rod_dw3x3_bwd_fused(const void* ye, const float* pro_mean, const float* pro_
                         const float* coef, const float* w, void* dx, float* dw, float* gparts, void* workspace, int N,
                         int H, int W, int C, int stride, int pad_t, int pad_l, int Ho, int Wo, int dtype,
                         void* stream);
+/* The stride-2 fused backward with its input recomputed, not read (ABI 23; conv_blocks.py:263-270
+ * expand + mobilenet.py:417-420 + 238-247): rod_dw3x3_bwd_fused with ye (the expand conv's output,
+ * C-wide) replaced by the block input x [N,H,W,Cin] (x_mean.. / x_act: its pending BatchNorm
+ * prologue, NULL mean = none) and the expand's forward operand wt0 [C][Cin] bf16; e_* = the expand
+ * BatchNorm (the depthwise input prologue, pro_* of rod_dw3x3_bwd_fused; ReLU6).  Each block forms
+ * the ye values of its row steps in LDS with the expand forward's MFMA and rounding one step ahead,
+ * so dx, dw and gparts (required: the BN_e sums) are bit-identical to rod_dw3x3_bwd_fused over the
+ * stored ye, while ye is never read (1.42 GB at 720p b8, block 1).  bf16, stride 2, both BatchNorms
+ * ReLU6, Cin 16 / 24 / 32; parts / workspace: rod_dw3x3_bwd_fused_parts / _workspace. */
+int rod_dw3x3_bwd_fused_rc_supported(int N, int H, int W, int C, int Cin, int stride, int pad_t, int pad_l,
+                                     int dtype);
+int rod_dw3x3_bwd_fused_rc(const void* x, const float* x_mean, const float* x_rstd, const float* x_gamma,
+                           const float* x_beta, int x_act, const void* wt0, int Cin, const float* e_mean,
+                           const float* e_rstd, const float* e_gamma, const float* e_beta, int e_act, const void* dz,
+                           const void* yd, const float* bn_mean, const float* bn_rstd, const float* bn_gamma,
+                           const float* bn_beta, int bn_act, const float* coef, const float* w, void* dx, float* dw,
+                           float* gparts, void* workspace, int N, int H, int W, int C, int stride, int pad_t,
+                           int pad_l, int Ho, int Wo, int dtype, void* stream);
 /* The same stride-1 pass without a materialised dz (ABI 20): in the inverted-residual block dz is
  * the project conv's input gradient dy_p . W_p (conv_blocks.py:287-294 backward), so the kernel
  * reads the cout-wide dy_p ([N*H*W][cout] bf16: the project BatchNorm's backward output, written
@@ -340,6 +358,15 @@ int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, co
  * afterwards (the project conv's backward-data and the depthwise BatchNorm it feeds,
  * conv_blocks.py:287-294 -> 238-247); 0 otherwise.  M = N*H*W rows, K = Cin. */
 int rod_conv_fwd_stream_ok(long M, int K, int Cout, int dtype);
+/* Statistics only (ABI 23): the BatchNorm statistics parts of y = x_act . wt^T ([ceil(M/128)][3][Cout],
+ * the stat_parts contract of rod_conv_fwd, bit-identical to it) with y NOT written — the expand conv
+ * of an inverted-residual block whose consumers recompute y from x (rod_dw3x3_fwd_rc,
+ * rod_dw3x3_bwd_fused_rc, rod_pw_bwd(_gred)_rc): the C-wide expanded tensor never crosses HBM.
+ * 1x1, no bias, bf16, Cin <= 32 on the streaming kernel's shapes (rod_conv_fwd_stats_supported). */
+int rod_conv_fwd_stats_supported(long M, int Cin, int Cout, int dtype);
+int rod_conv_fwd_stats(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                       const float* pro_beta, int pro_act, const void* wt, float* stat_parts, long M, int Cin, int Cout,
+                       int dtype, void* stream);
 /* Inference conv + BatchNorm-apply epilogue (ABI 21): rod_conv_fwd whose output is
  *   z = act(fma(y, scale, offset)) (+ res),  y = the conv output rounded to bf16,
  *   scale = bn_rstd*bn_gamma, offset = bn_beta - bn_mean*scale (bn_affine),

@@ -786,6 +786,8 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const T* __restrict__ X, 
 // Streaming 1x1 GEMM (bf16, K <= 96, no bias / prologue): y[m, n0 .. n0 + 16*NT) = x[m, :K] *
 // wt[n0 .., :K]^T over N groups of 16*NT columns (blockIdx.y), with an optional epilogue:
 //   MODE 1: the BatchNorm statistics parts of y ([ceil(M/128)][3][Cout], the forward expand);
+//   MODE 3: those statistics only, y not written (ABI 23, rod_conv_fwd_stats: an expand whose
+//           consumers recompute y from x);
 //   MODE 2: "gred" — the BatchNorm-backward sums of y taken as dz against the pre-BatchNorm
 //           tensor gr.y at the same positions ([ceil(M/128)][2][Cout]: sum g, sum g*yhat,
 //           g = dz * act'(BN(gr.y))), for a backward-data whose output is the gradient of a
@@ -838,7 +840,7 @@ __global__ void __launch_bounds__(256, (PRO && KT >= 5) ? 4 : 1) pw_stream_kerne
   constexpr int CPR = NP / 8;       // 16-byte chunks per output row of the group
   constexpr int RG = 64 / CPR;      // gred: row groups of lanes (lanes >= RG*CPR idle)
   constexpr int JN = (16 + RG - 1) / RG;
-  constexpr bool STATS = MODE == 1, GRED = MODE == 2;
+  constexpr bool STATS = MODE == 1 || MODE == 3, GRED = MODE == 2, NOSTORE = MODE == 3;
   __shared__ __attribute__((aligned(16))) bf16_t Bs[NP * LDB];
   __shared__ __attribute__((aligned(16))) bf16_t Cs[PWS_WAVES][16 * LDC];
   constexpr bool PTAB = PRO && KT > 1;
@@ -1016,12 +1018,15 @@ __global__ void __launch_bounds__(256, (PRO && KT >= 5) ? 4 : 1) pw_stream_kerne
             }
           }
         }
+        if constexpr (!NOSTORE) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cs[(lg * 4 + r) * LDC + b * 16 + fr] = (bf16_t)v[r];
+          for (int r = 0; r < 4; ++r) cs[(lg * 4 + r) * LDC + b * 16 + fr] = (bf16_t)v[r];
+        }
       }
       __builtin_amdgcn_wave_barrier();
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      if constexpr (GRED) {
+      if constexpr (NOSTORE) {
+      } else if constexpr (GRED) {
         // fixed-chunk write-back + the BatchNorm-backward sums of the stored values
         if (gact) {
 #pragma unroll
@@ -1109,6 +1114,30 @@ static int pw_stream_groups(long M, int K, int Cout, int& nt, bool gred = false)
 }
 static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long M, int K, int Cout, int ldx, int ldy,
                              float* stats, const BnGred* gr, hipStream_t s, const BnPro* pro = nullptr) {
+  if (y == nullptr) {   // statistics only (rod_conv_fwd_stats): K <= 32, one k step
+    int nt = 0;
+    const int ng = pw_stream_groups(M, K, Cout, nt, false);
+    if (ng == 0 || !stats || gr || K > 32) return false;
+    const long ntiles = cdivl(M, 128);
+    const long maxw = cdivl(256L * 3 * PWS_WAVES, ng);
+    const long per = cdivl(ntiles, maxw);
+    const dim3 grid((unsigned)cdivl(cdivl(ntiles, per), PWS_WAVES), ng);
+    const BnGred g{};
+    const BnPro pv = pro ? *pro : BnPro{};
+#define PWN(NT_)                                                                                               \
+  if (nt == NT_) {                                                                                             \
+    if (pro)                                                                                                   \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, 1, 3, true>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, \
+                         ldy, stats, g, pv);                                                                   \
+    else                                                                                                       \
+      hipLaunchKernelGGL((pw_stream_kernel<NT_, 1, 3>), grid, dim3(256), 0, s, x, wt, y, M, K, Cout, ldx, ldy,  \
+                         stats, g);                                                                            \
+    return true;                                                                                               \
+  }
+    PWN(2) PWN(3) PWN(4) PWN(6) PWN(8) PWN(9) PWN(12)
+#undef PWN
+    return false;
+  }
   int nt = 0;
   const int ng = pw_stream_groups(M, K, Cout, nt, gr != nullptr);
   if (ng == 0 || (gr && (stats || ldy != Cout))) return false;
@@ -2319,6 +2348,28 @@ int rod_conv_fwd(const void* x, const float* pro_mean, const float* pro_rstd, co
                                               gred_parts ? &gr : nullptr, N, H, W, Cin, Cout, ksize, ldx, ldy,
                                               ROD_STREAM(stream)));
   return check_launch("rod_conv_fwd");
+}
+
+int rod_conv_fwd_stats_supported(long M, int Cin, int Cout, int dtype) {
+  int nt = 0;
+  return dtype == ROD_BF16 && Cin <= 32 && pw_stream_groups(M, Cin, Cout, nt, false) > 0 ? 1 : 0;
+}
+
+int rod_conv_fwd_stats(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,
+                       const float* pro_beta, int pro_act, const void* wt, float* stat_parts, long M, int Cin, int Cout,
+                       int dtype, void* stream) {
+  ROD_CHECK_ARG(rod_conv_fwd_stats_supported(M, Cin, Cout, dtype),
+                "rod_conv_fwd_stats: unsupported M=%ld Cin=%d Cout=%d dtype=%d", M, Cin, Cout, dtype);
+  ROD_CHECK_ARG(x && wt && stat_parts, "rod_conv_fwd_stats: NULL argument");
+  ROD_CHECK_ARG(!pro_mean || pro_rstd, "rod_conv_fwd_stats: bad BatchNorm prologue");
+  ROD_CHECK_ARG(((((uintptr_t)x) | ((uintptr_t)wt)) & 15) == 0, "rod_conv_fwd_stats: x, wt must be 16-byte aligned");
+  const BnPro pro{pro_mean, pro_rstd, pro_gamma, pro_beta, pro_act};
+  if (!pw_stream_launch((const bf16_t*)x, (const bf16_t*)wt, nullptr, M, Cin, Cout, Cin, Cout, stat_parts, nullptr,
+                        ROD_STREAM(stream), pro_mean ? &pro : nullptr)) {
+    set_error("rod_conv_fwd_stats: no statistics-only plan for M=%ld Cin=%d Cout=%d", M, Cin, Cout);
+    return ROD_EINVAL;
+  }
+  return check_launch("rod_conv_fwd_stats");
 }
 
 int rod_conv_fwd_bnact(const void* x, const float* pro_mean, const float* pro_rstd, const float* pro_gamma,

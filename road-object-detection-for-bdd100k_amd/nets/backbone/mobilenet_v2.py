@@ -90,9 +90,12 @@ class MobilenetV2:
         g, b, mm, mv = self._bn_args(name)
         return (*ops.eval_stats(mm, mv, BN_EPS), g, b)
 
-    def _conv_bn(self, x, w, ks, name, act, training):
-        """conv + BatchNorm(+act) as one node (ops.conv2d_bn), left Pending (owned)."""
-        return ops.conv2d_bn(x, w, None, ks, *self._bn_args(name), act, training, BN_DECAY, BN_EPS)
+    def _conv_bn(self, x, w, ks, name, act, training, dw_stride=0):
+        """conv + BatchNorm(+act) as one node (ops.conv2d_bn), left Pending (owned).  dw_stride: an
+        expand conv feeding a depthwise of that stride (stride 2: its output may stay unwritten, the
+        consumers recomputing it from x — ops._nostore_ok)."""
+        return ops.conv2d_bn(x, w, None, ks, *self._bn_args(name), act, training, BN_DECAY, BN_EPS,
+                             dw_stride=dw_stride)
 
     def __call__(self, x, is_training, final_endpoint=None, taps=None):
         """Returns the endpoint dict {'layer_1': ..., 'layer_24': ...} (mobilenet.py:275-281).
@@ -136,7 +139,7 @@ class MobilenetV2:
                     inp, x = graph.fork(x, 2)
                 if inner > cin:
                     x = keep(self._conv_bn(x, P[base + '/expand/weights'], 1, base + '/expand/BatchNorm',
-                                           ops.ROD_ACT_RELU6, is_training))
+                                           ops.ROD_ACT_RELU6, is_training, dw_stride=s))
                 x = keep(ops.dw3x3_bn(x, P[base + '/depthwise/depthwise_weights'], s,
                                       *self._bn_args(base + '/depthwise/BatchNorm'), ops.ROD_ACT_RELU6, is_training,
                                       BN_DECAY, BN_EPS))

@@ -174,16 +174,19 @@ def _capturing():
 # entries whose parameter-gradient sums rod_slab_defer(1) may queue (include/rod.h, ABI 11)
 DEFERRING = frozenset(("rod_conv_wgrad", "rod_dw3x3_bwd_filter", "rod_dw3x3_bwd_filter_bn", "rod_pw_bwd",
                        "rod_pw_bwd_rc", "rod_pw_bwd_gred", "rod_pw_bwd_gred_rc", "rod_pw_bwd_gred_dyp", "rod_stem_wgrad_bn", "rod_dw3x3_bwd_fused",
-                       "rod_dw3x3_bwd_fused_pw"))
+                       "rod_dw3x3_bwd_fused_pw", "rod_dw3x3_bwd_fused_rc"))
 # while sums are deferred: every tensor handed to such an entry (partial slabs, gradient outputs)
 # is kept referenced until rod_slab_flush has been enqueued (rod.ops.SlabDefer).  With WATCH_DEFER
-# (ROD_DEBUG_DEFER=1, or set by tests/test_gpu_defer.py) every other entry is checked against the
-# queue length (rod_slab_pending) around the call: one that queued a sum has its tensors kept too
-# and its name recorded in DEFER_UNLISTED (a registry gap, which the test asserts never happens
-# over REFINE / ALL / VGG steps).  Off on the production path: two extra ctypes calls per entry.
+# every other entry is checked against the queue length (rod_slab_pending) around the call: one
+# that queued a sum has its tensors kept too and its name recorded in DEFER_UNLISTED (a registry
+# gap, which tests/test_gpu_defer.py asserts never happens over REFINE / ALL steps).  On by default
+# (ROD_DEFER_WATCH=0 turns it off): it costs two ctypes calls per entry of an EAGER backward only —
+# a graph replay runs no Python — and a gap corrupts weight gradients silently (round 6 found one:
+# rod_dw3x3_bwd_fused_rc, its slab freed and reused before the deferred flush read it, caught as
+# run-to-run different steps by tools/rc_step_diag.py), while the watch keeps such a call correct.
 KEEP = None
 DEFER_UNLISTED = set()
-WATCH_DEFER = os.environ.get("ROD_DEBUG_DEFER", "0") == "1"
+WATCH_DEFER = os.environ.get("ROD_DEFER_WATCH", "1") != "0"
 
 
 def call(name: str, *args):

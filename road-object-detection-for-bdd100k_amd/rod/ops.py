@@ -538,6 +538,32 @@ def dw_rc_ok(xe, N, H, W, C, stride):
     return src
 
 
+def _nostore_ok(x, ipro, N, H, W, Cin, Cout, dw_stride):
+    """The expand conv of an inverted-residual block whose depthwise has stride 2 need not write its
+    output at all (ABI 23): every consumer of it can recompute it from the block input x — the
+    depthwise forward (rod_dw3x3_fwd_rc), the depthwise backward (rod_dw3x3_bwd_fused_rc) and the
+    expand's own backward (rod_pw_bwd_gred_rc for 16 -> 96 with the previous project's BatchNorm
+    pending, else rod_pw_bwd_rc) — and its BatchNorm statistics come from rod_conv_fwd_stats.  Taken
+    only when every one of those paths applies (no silent read of the unwritten tensor is possible:
+    _ConvBN / _DWBN raise if they end up elsewhere).  ROD_DISABLE=nostore or rc turns it off."""
+    if dw_stride != 2 or "nostore" in _DISABLE or "rc" in _DISABLE or "epistats" in _DISABLE or "bnpro" in _DISABLE or \
+            SYNC_BN is not None or x.dtype != torch.bfloat16:
+        return False
+    L = _abi.lib()
+    M = N * H * W
+    dt = _DT[x.dtype]
+    _, pt = same_pad(H, 2)
+    _, pl = same_pad(W, 2)
+    if not (L.rod_conv_fwd_stats_supported(M, Cin, Cout, dt) and L.rod_dw3x3_fwd_rc_supported(N, H, W, Cout, Cin, 2, dt)
+            and L.rod_dw3x3_bwd_fused_rc_supported(N, H, W, Cout, Cin, 2, pt, pl, dt)
+            and _dw_fused_ok(N, -(-H // 2), -(-W // 2), Cout, x.dtype, 2)):
+        return False
+    if not L.rod_pw_bwd_rc_supported(M, Cin, Cout, dt):
+        return False
+    gred = ipro is not None and M >= 65536 and pw_bwd_gred_parts(M, Cin, Cout, x.dtype) > 0
+    return gred or _pw_fused_ok(M, Cin, Cout, x.dtype)
+
+
 def pw_bwd_gred_parts(M, Cin, Cout, dtype):
     """Part count of rod_pw_bwd_gred for this project shape (0: not taken)."""
     if "pwgred" in _DISABLE:
@@ -849,6 +875,8 @@ def bn_pending(x, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, part
 
 def materialize(p, residual=None):
     """Write act(BatchNorm(y)) (+ residual after the activation) of a Pending."""
+    if isinstance(p, Pending) and getattr(p.y, "_rod_nostore", False):
+        raise RuntimeError("an unwritten expand output (ABI 23 recompute) cannot be materialised")
     if not isinstance(p, Pending):
         return p
     if p.owned:
@@ -973,12 +1001,29 @@ class _ConvBN(torch.autograd.Function):
     BatchNorm prologue (mean, rstd, gamma, beta, act) when the input is an owned Pending."""
 
     @staticmethod
-    def forward(ctx, x, w, b, ks, ipro, obn):
+    def forward(ctx, x, w, b, ks, ipro, obn, dw_stride=0):
         gamma, beta, mm, mv, act, training, decay, eps = obn
         N, H, W, Cin = x.shape
         Cout = w.shape[0]
         assert w.shape == (Cout, ks, ks, Cin), (tuple(w.shape), ks, Cin)
         wt = _prep(w, 0, x.dtype, Cout, Cin, ks)
+        ctx.nostore = training and ks == 1 and b is None and act == ROD_ACT_RELU6 and \
+            _nostore_ok(x, ipro, N, H, W, Cin, Cout, dw_stride)
+        if ctx.nostore:
+            # the expanded tensor is never written (ABI 23): a placeholder of its shape that no
+            # kernel reads (its consumers recompute it from x), the statistics from x alone
+            y = torch.empty(1, dtype=x.dtype, device=x.device).expand(N, H, W, Cout)
+            parts = torch.empty((-(-(N * H * W) // 128), 3, Cout), dtype=torch.float32, device=x.device)
+            _abi.call("rod_conv_fwd_stats", x, *_pro_args(ipro), wt, parts, N * H * W, Cin, Cout, dtcode(x), stream())
+            y._rod_expand = (x, ipro, wt, Cin)
+            y._rod_nostore = True
+            mean, rstd = bn_statistics(y, mm, mv, training, decay, eps, parts)
+            ctx.src_dw = None
+            ctx.save_for_backward(x, w, b, y, mean, rstd)
+            ctx.ks, ctx.ipro, ctx.gb, ctx.act, ctx.training = ks, ipro, (gamma, beta), act, training
+            ctx.mark_non_differentiable(mean, rstd)
+            ctx.set_materialize_grads(False)
+            return y, mean, rstd
         y = torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
         parts = None
         if training:
@@ -1007,7 +1052,7 @@ class _ConvBN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz, *_):
         if dz is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         if not ctx.training:
             raise RuntimeError("BatchNorm backward in inference mode is not part of the reference graph")
         x, w, b, y, mean, rstd = ctx.saved_tensors
@@ -1018,6 +1063,9 @@ class _ConvBN(torch.autograd.Function):
         dz = dz.contiguous()
         need_dx = ctx.needs_input_grad[0]
         parts = _take_bn_parts(dz)   # the BN sums a fused depthwise backward already formed
+        if ctx.nostore and parts is None:
+            raise RuntimeError("expand conv without a stored output: its BatchNorm-backward sums must come from the "
+                               "depthwise backward (rod_dw3x3_bwd_fused_rc)")
         if ctx.ks == 1 and b is None and ctx.ipro is not None and need_dx and _needs(w) and \
                 M >= 65536 and SYNC_BN is None and pw_bwd_gred_parts(M, Cin, Cout, y.dtype) > 0:
             # the project conv of an inverted-residual block (conv_blocks.py:287-294): one pass for
@@ -1041,14 +1089,16 @@ class _ConvBN(torch.autograd.Function):
                 dx = torch.empty(1, dtype=x.dtype, device=x.device).expand(x.shape)
                 _put_dz_recipe(dx, (dyp, wt1, Cout))
                 _put_bn_parts(dx, xparts)
-                return dx, None, None, None, None, None
+                return dx, None, None, None, None, None, None
             # the 16 -> 96 expand: its pre-BatchNorm y recomputed from x in the kernel (ABI 23)
-            wt0 = _prep(w, 0, x.dtype, Cout, Cin, 1) if pw_bwd_rc_ok(M, Cin, Cout, x.dtype) else None
+            wt0 = _prep(w, 0, x.dtype, Cout, Cin, 1) if ctx.nostore or pw_bwd_rc_ok(M, Cin, Cout, x.dtype) else None
             dx, xparts = pw_bwd_gred(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, grad_slot(w),
                                      wt0=wt0)
             _mark_written(w)
             _put_bn_parts(dx, xparts)
-            return dx, None, None, None, None, None
+            return dx, None, None, None, None, None, None
+        if ctx.nostore and not (ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w))):
+            raise RuntimeError("expand conv without a stored output reached a backward path that reads it")
         if ctx.ks == 3 and not need_dx and b is None and ctx.ipro is None and _needs(w) and \
                 "stembn" not in _DISABLE and _abi.lib().rod_stem_wgrad_bn_supported(Cin, Cout, 3, dtcode(y)):
             # the stem (mobilenet_v2.py:58 + its batch_norm): the weight gradient forms dy from the
@@ -1061,7 +1111,7 @@ class _ConvBN(torch.autograd.Function):
             _abi.call("rod_stem_wgrad_bn", x, dz, y, mean, rstd, gamma, beta, ctx.act, coef, grad_slot(w), ws, N, H,
                       W, Cin, Cout, 3, dtcode(y), stream())
             _mark_written(w)
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         if ctx.ks == 1 and _pw_fused_ok(M, Cin, Cout, y.dtype) and (need_dx or _needs(w) or _needs(b)):
             if parts is not None:
                 coef = bn_bwd_coef_from_parts(parts, M, Cout, rstd, gamma, beta, _needs(gamma), _needs(beta))
@@ -1071,7 +1121,8 @@ class _ConvBN(torch.autograd.Function):
             gb = grad_slot(b) if _needs(b) else None
             wt1 = _prep(w, 1, x.dtype, Cout, Cin, 1) if need_dx else None
             # the streaming expand shapes (16 -> 96, 24 -> 144): y recomputed from x (ABI 23)
-            wt0 = _prep(w, 0, x.dtype, Cout, Cin, 1) if gb is None and pw_bwd_rc_ok(M, Cin, Cout, x.dtype) else None
+            wt0 = _prep(w, 0, x.dtype, Cout, Cin, 1) \
+                if gb is None and (ctx.nostore or pw_bwd_rc_ok(M, Cin, Cout, x.dtype)) else None
             dx = pw_bwd(dz, y, mean, rstd, gamma, beta, ctx.act, coef, x, ctx.ipro, wt1, need_dx, gw, gb, wt0=wt0)
             if _needs(w):
                 _mark_written(w)
@@ -1095,7 +1146,7 @@ class _ConvBN(torch.autograd.Function):
             else:
                 dy = bn_bwd_dy(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
             dx = _conv_bwd_from_dy(x, w, b, ctx.ks, dy, ctx.ipro, need_dx)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
 class _DWBN(torch.autograd.Function):
@@ -1113,7 +1164,11 @@ class _DWBN(torch.autograd.Function):
         if training:
             nparts = _abi.lib().rod_dw3x3_fwd_stat_parts(N, Ho, Wo, C, stride, dtcode(x))
             parts = torch.empty((nparts, 3, C), dtype=torch.float32, device=x.device)
+        nostore = getattr(x, "_rod_nostore", False)
         rc = dw_rc_ok(x, N, H, W, C, stride) if ipro is not None and ipro[4] == ROD_ACT_RELU6 else None
+        if nostore:
+            rc = x._rod_expand   # the input was never written: recompute (checked by _nostore_ok)
+        ctx.rc_src = rc if nostore else None
         if rc is not None:
             # the expanded input recomputed from the block input, never read (ABI 23)
             xin, xpro, wt0, Cin = rc
@@ -1171,6 +1226,25 @@ class _DWBN(torch.autograd.Function):
             if parts is not None:
                 return bn_bwd_coef_from_parts(parts, N * Ho * Wo, C, rstd, gamma, beta, _needs(gamma), _needs(beta))
             return bn_bwd_reduce(dz, y, mean, rstd, gamma, beta, ctx.act, _needs(gamma), _needs(beta))
+        if ctx.rc_src is not None:
+            # the input (the expand's output) was never written: the stride-2 fused backward
+            # recomputes it from the block input (ABI 23)
+            if not (_needs(w) and ctx.needs_input_grad[0] and ctx.ipro is not None and s == 2):
+                raise RuntimeError("depthwise over an unwritten expand output needs the fused stride-2 backward")
+            xin, xpro, wt0, Cin = ctx.rc_src
+            dz = dz.contiguous()
+            coef = coef_d()
+            dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+            gparts = torch.empty((_abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C, s, pt, pl), 2, C),
+                                 dtype=torch.float32, device=x.device)
+            ws = workspace(_abi.query("rod_dw3x3_bwd_fused_workspace", N, H, W, C, s, pt, pl), x.device)
+            det = lambda t: None if t is None else t.detach()
+            _abi.call("rod_dw3x3_bwd_fused_rc", xin, *_pro_args(xpro), wt0, Cin, *_pro_args(ctx.ipro), dz, y, mean, rstd,
+                      det(gamma), det(beta), ctx.act, coef, w, dx, grad_slot(w), gparts, ws, N, H, W, C, s, pt, pl,
+                      Ho, Wo, dtcode(dz), stream())
+            _mark_written(w)
+            _put_bn_parts(dx, gparts)
+            return dx, None, None, None, None
         if _needs(w) and ctx.needs_input_grad[0] and _dw_fused_ok(N, Ho, Wo, C, x.dtype, s):
             # one pass: BN_d backward apply + backward-data + filter gradient (+ the input
             # BatchNorm's backward sums, handed to the producer) — rod_dw3x3_bwd_fused
@@ -1252,10 +1326,13 @@ def _in_pro(x):
     return x, None
 
 
-def conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3):
-    """slim.conv2d + slim.batch_norm(+act), left Pending (owned) for the consumer's prologue."""
+def conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, dw_stride=0):
+    """slim.conv2d + slim.batch_norm(+act), left Pending (owned) for the consumer's prologue.
+    dw_stride: the conv is an inverted-residual block's expand feeding a depthwise of that stride
+    (its output may then stay unwritten: _nostore_ok)."""
     xt, ipro = _in_pro(x)
-    y, mean, rstd = _ConvBN.apply(xt, w, b, ksize, ipro, (gamma, beta, mmean, mvar, act, training, decay, eps))
+    y, mean, rstd = _ConvBN.apply(xt, w, b, ksize, ipro, (gamma, beta, mmean, mvar, act, training, decay, eps),
+                                  dw_stride)
     return Pending(y, mean, rstd, gamma, beta, act, training, owned=True)
 
 

@@ -9,6 +9,7 @@ rounding, so every output must be bit-identical to the form that reads the store
     project output: linear input BatchNorm, its backward sums handed over),
   * rod_dw3x3_fwd_rc vs rod_dw3x3_fwd over the stored tensor with the BN_e + ReLU6 prologue: y and
     the BatchNorm statistics parts (stride 2 and 1, both pack widths of the tile plan),
+  * rod_dw3x3_bwd_fused_rc vs rod_dw3x3_bwd_fused (stride 2): dx, dw and the BN_e backward parts,
   * a REFINE training step with the recompute on / off (ROD_DISABLE=rc), eager and graphed."""
 import pytest
 import torch
@@ -100,22 +101,24 @@ def test_pw_bwd_gred_rc_bit_identical(dev, M):
 
 @pytest.mark.parametrize('graphed', [False, True])
 def test_step_recompute_bit_identical(dev, graphed):
-    """REFINE step at 480x864 b2 (blocks 1-3 take the recompute forms) with ROD_DISABLE=rc and
-    without: losses and parameters bit-identical, and the recompute entries actually ran."""
+    """REFINE step at 480x864 b2 with every recompute form off (ROD_DISABLE=rc: the expanded
+    tensors written and read) and with the defaults (blocks 1 and 3: the expand output never written
+    — rod_conv_fwd_stats, rod_dw3x3_fwd_rc, rod_dw3x3_bwd_fused_rc, rod_pw_bwd(_gred)_rc; block 1's
+    16 -> 96 backward recompute elsewhere too): losses and parameters bit-identical, eager and
+    graphed, and the recompute entries ran."""
     from rod.data import synthetic_batch
     from rod.trainer import Trainer
     runs = []
+    names = ['rod_pw_bwd_rc', 'rod_pw_bwd_gred_rc', 'rod_dw3x3_fwd_rc', 'rod_dw3x3_bwd_fused_rc', 'rod_conv_fwd_stats',
+             'rod_pw_bwd', 'rod_pw_bwd_gred', 'rod_dw3x3_fwd']
     for off in (True, False):
         if off:
             ops._DISABLE.add('rc')
-        else:
-            ops._ENABLE.add('rcdw')   # the opt-in depthwise forward recompute too
         try:
             tr = Trainer((480, 864), 2, dtype=bf16, device=dev, seed=7)
             batches = [synthetic_batch(2, 480, 864, dev, seed=50 + i) for i in range(2)]
             step = tr.step_graphed if graphed else tr.step
-            _abi.PROBE.arm(['rod_pw_bwd_rc', 'rod_pw_bwd_gred_rc', 'rod_pw_bwd', 'rod_pw_bwd_gred', 'rod_dw3x3_fwd_rc',
-                            'rod_dw3x3_fwd'])
+            _abi.PROBE.arm(names)
             losses = [step(*batches[i % 2])[0].detach().clone() for i in range(3)]
             torch.cuda.synchronize()
             calls = _abi.PROBE.table()
@@ -123,13 +126,35 @@ def test_step_recompute_bit_identical(dev, graphed):
             runs.append((tr.net.store.flat.detach().clone(), torch.stack([l.reshape(()) for l in losses]), calls))
         finally:
             ops._DISABLE.discard('rc')
-            ops._ENABLE.discard('rcdw')
     (f0, l0, c0), (f1, l1, c1) = runs
-    assert 'rod_pw_bwd_rc' not in c0 and 'rod_pw_bwd_gred_rc' not in c0 and 'rod_dw3x3_fwd_rc' not in c0
-    assert c1.get('rod_pw_bwd_gred_rc', (0,))[0] >= 1, c1
-    assert c1.get('rod_dw3x3_fwd_rc', (0,))[0] >= 1, c1
+    assert not any(n in c0 for n in names[:5]), c0
+    for n in ('rod_pw_bwd_gred_rc', 'rod_pw_bwd_rc', 'rod_dw3x3_fwd_rc', 'rod_dw3x3_bwd_fused_rc', 'rod_conv_fwd_stats'):
+        assert c1.get(n, (0,))[0] >= 1, (n, c1)
+    n_eager = 3 if not graphed else 1    # the probe does not see captured calls or replays
+    assert c1['rod_conv_fwd_stats'][0] == 2 * n_eager and c1['rod_dw3x3_bwd_fused_rc'][0] == 2 * n_eager, c1
     assert torch.equal(l0, l1), (l0, l1)
     assert torch.equal(f0, f1)
+
+
+def test_nostore_step_opt_in_dw_recompute(dev):
+    """The opt-in recompute of the stride-1 depthwise forwards (ROD_ENABLE=rcdw) on top of the
+    defaults: bit-identical step."""
+    from rod.data import synthetic_batch
+    from rod.trainer import Trainer
+    runs = []
+    for on in (False, True):
+        if on:
+            ops._ENABLE.add('rcdw')
+        try:
+            tr = Trainer((480, 864), 2, dtype=bf16, device=dev, seed=8)
+            b = synthetic_batch(2, 480, 864, dev, seed=77)
+            losses = [tr.step(*b)[0].detach().clone() for _ in range(2)]
+            torch.cuda.synchronize()
+            runs.append((tr.net.store.flat.detach().clone(), torch.stack([l.reshape(()) for l in losses])))
+        finally:
+            ops._ENABLE.discard('rcdw')
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][0], runs[1][0])
 
 
 # (N, H, W, Cin, C, stride, input prologue act or None): block 1 (720p, 16 -> 96, stride 2, the
@@ -177,3 +202,63 @@ def test_dw3x3_fwd_rc_bit_identical(dev, N, H, W, Cin, C, stride, xact):
     (y0, p0), (y1, p1) = outs
     assert torch.equal(y0, y1), float((y0.float() - y1.float()).abs().max())
     assert torch.equal(p0, p1), float((p0 - p1).abs().max())
+
+
+def _fused_bwd_inputs(N, H, W, Cin, C, xact, g, dev):
+    M = N * H * W
+    x = (torch.randn(N, H, W, Cin, generator=g) * 1.4 + 0.1).to(dev, bf16)
+    w_e = (torch.randn(C, 1, 1, Cin, generator=g) * 0.3).to(dev)
+    xpro = None
+    if xact is not None:
+        xm, xr, xg, xb = _bn(Cin, g, dev)
+        xpro = (xm, xr, xg, xb, xact)
+    ye, wt0 = _forward_y(x.view(M, Cin), w_e, xpro, M, Cin, C)
+    ye = ye.view(N, H, W, C)
+    em = ye.float().mean((0, 1, 2)) + (torch.randn(C, generator=g) * 0.05).to(dev)
+    er = torch.rsqrt(ye.float().var((0, 1, 2), unbiased=False) + 1e-3)
+    epro = (em, er, (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.5 + 0.5).to(dev),
+            ops.ROD_ACT_RELU6)
+    return x, xpro, wt0, ye, epro
+
+
+# (N, H, W, Cin, C, input prologue act): block 1 at 720p on 2 images, block 3 (24 -> 144 at
+# 360x640), odd sizes (TF-SAME pads 1 / 0), Cin 32
+BWD_SHAPES = [(2, 720, 1280, 16, 96, ops.ROD_ACT_NONE), (8, 360, 640, 24, 144, None), (2, 99, 171, 16, 96, None),
+              (3, 58, 81, 24, 144, ops.ROD_ACT_NONE), (1, 45, 64, 32, 192, None)]
+
+
+@pytest.mark.parametrize('N,H,W,Cin,C,xact', BWD_SHAPES)
+def test_dw3x3_bwd_fused_rc_bit_identical(dev, N, H, W, Cin, C, xact):
+    code = ops.dtcode(torch.empty(1, dtype=bf16))
+    Ho, pt = ops.same_pad(H, 2)
+    Wo, pl = ops.same_pad(W, 2)
+    assert _abi.lib().rod_dw3x3_bwd_fused_rc_supported(N, H, W, C, Cin, 2, pt, pl, code)
+    g = torch.Generator().manual_seed(N * H + W + C)
+    x, xpro, wt0, ye, epro = _fused_bwd_inputs(N, H, W, Cin, C, xact, g, dev)
+    wd = (torch.randn(3, 3, C, generator=g) * 0.3).to(dev)
+    yd = torch.empty((N, Ho, Wo, C), dtype=bf16, device=dev)
+    _abi.call('rod_dw3x3_fwd', ye, *ops._pro_args(epro), wd, yd, None, N, H, W, C, 2, pt, pl, Ho, Wo, code, ops.stream())
+    dz = torch.randn(N, Ho, Wo, C, generator=g).to(dev, bf16)
+    dm = yd.float().mean((0, 1, 2))
+    dr = torch.rsqrt(yd.float().var((0, 1, 2), unbiased=False) + 1e-3)
+    dgam, dbet = (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.3).to(dev)
+    coef = ops.bn_bwd_reduce(dz, yd, dm, dr, dgam, dbet, ops.ROD_ACT_RELU6, False, False)
+    nparts = _abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C, 2, pt, pl)
+    wsb = _abi.query('rod_dw3x3_bwd_fused_workspace', N, H, W, C, 2, pt, pl)
+    outs = []
+    for rc in (False, True):
+        dx = torch.empty_like(ye)
+        dw = torch.zeros(3, 3, C, device=dev)
+        gp = torch.full((nparts, 2, C), -7.0, device=dev)
+        ws = ops.workspace(wsb, dev)
+        if rc:
+            _abi.call('rod_dw3x3_bwd_fused_rc', x, *ops._pro_args(xpro), wt0, Cin, *ops._pro_args(epro), dz, yd, dm, dr,
+                      dgam, dbet, ops.ROD_ACT_RELU6, coef, wd, dx, dw, gp, ws, N, H, W, C, 2, pt, pl, Ho, Wo, code,
+                      ops.stream())
+        else:
+            _abi.call('rod_dw3x3_bwd_fused', ye, *ops._pro_args(epro), dz, yd, dm, dr, dgam, dbet, ops.ROD_ACT_RELU6,
+                      coef, wd, dx, dw, gp, ws, N, H, W, C, 2, pt, pl, Ho, Wo, code, ops.stream())
+        outs.append((dx, dw, gp))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), float((a.float() - b.float()).abs().max())

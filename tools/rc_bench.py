@@ -74,6 +74,28 @@ def main():
         t0, t1 = timeit(stored), timeit(rc)
         ok = torch.equal(y0, y1) and torch.equal(p0, p1)
         print('%-16s dwfwd stored %7.1f us   rc %7.1f us   equal %s' % (name, t0, t1, ok), flush=True)
+        if s == 2 and _abi.lib().rod_dw3x3_bwd_fused_rc_supported(N, H, W, C, Cin, s, pt, pl, code):
+            dz = torch.randn(N, Ho, Wo, C, generator=g).to(dev, bf16)
+            dm, dr = y0.float().mean((0, 1, 2)), torch.rsqrt(y0.float().var((0, 1, 2)) + 1e-3)
+            dg, db = (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.3).to(dev)
+            coef = ops.bn_bwd_reduce(dz, y0, dm, dr, dg, db, ops.ROD_ACT_RELU6, False, False)
+            nb = _abi.lib().rod_dw3x3_bwd_fused_parts(N, H, W, C, 2, pt, pl)
+            ws = ops.workspace(_abi.query('rod_dw3x3_bwd_fused_workspace', N, H, W, C, 2, pt, pl), dev)
+            dx0, dx1 = torch.empty_like(ye), torch.empty_like(ye)
+            dw0, dw1 = torch.zeros(3, 3, C, device=dev), torch.zeros(3, 3, C, device=dev)
+            g0, g1 = torch.empty((nb, 2, C), device=dev), torch.empty((nb, 2, C), device=dev)
+
+            def bstored():
+                _abi.call('rod_dw3x3_bwd_fused', ye, *ops._pro_args(epro), dz, y0, dm, dr, dg, db, ops.ROD_ACT_RELU6,
+                          coef, wd, dx0, dw0, g0, ws, N, H, W, C, 2, pt, pl, Ho, Wo, code, ops.stream())
+
+            def brc():
+                _abi.call('rod_dw3x3_bwd_fused_rc', x, *ops._pro_args(xpro), wt0, Cin, *ops._pro_args(epro), dz, y0,
+                          dm, dr, dg, db, ops.ROD_ACT_RELU6, coef, wd, dx1, dw1, g1, ws, N, H, W, C, 2, pt, pl, Ho, Wo,
+                          code, ops.stream())
+            t2, t3 = timeit(bstored), timeit(brc)
+            ok = torch.equal(dx0, dx1) and torch.equal(dw0, dw1) and torch.equal(g0, g1)
+            print('%-16s dwbwd stored %7.1f us   rc %7.1f us   equal %s' % (name, t2, t3, ok), flush=True)
         del ye
 
 
