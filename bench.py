@@ -57,7 +57,7 @@ def parse():
     ap.add_argument('--no-dp-leg', dest='dp_leg', action='store_false')
     ap.add_argument('--sync-bn', dest='sync_bn', action='store_true', default=False,
                     help='N>1: BatchNorm statistics over the global batch (rod.ddp.SyncBatchNorm; default per rank)')
-    ap.add_argument('--probe', default='rod_dw3x3_bwd_fused,rod_dw3x3_bwd_fused_pw',
+    ap.add_argument('--probe', default='rod_dw3x3_bwd_fused,rod_dw3x3_bwd_fused_pw,rod_dw3x3_bwd_fused_rc',
                     help='C-ABI entry (or comma list, aggregated as one kernel family) reported in "roofline": '
                          'default the fused depthwise backward, the largest entry of the graphed step '
                          '(profiles/r3_refine_bf16_b8_720p_graph_stats.txt); rounds 1-2 reported the '
@@ -379,9 +379,10 @@ def replicated(r, world, dev):
     return r
 
 
-NORTH_STAR = ('rod_dw3x3_fwd', 'rod_dw3x3_bwd_fused', 'rod_dw3x3_bwd_fused_pw', 'rod_dw3x3_bwd_data',
-              'rod_dw3x3_bwd_filter', 'rod_conv_fwd', 'rod_conv_wgrad', 'rod_pw_bwd', 'rod_pw_bwd_gred',
-              'rod_pw_bwd_gred_dyp', 'rod_bn_bwd_reduce', 'rod_bn_bwd_apply', 'rod_bn_bwd')
+NORTH_STAR = ('rod_dw3x3_fwd', 'rod_dw3x3_fwd_rc', 'rod_dw3x3_bwd_fused', 'rod_dw3x3_bwd_fused_pw',
+              'rod_dw3x3_bwd_fused_rc', 'rod_dw3x3_bwd_data', 'rod_dw3x3_bwd_filter', 'rod_conv_fwd',
+              'rod_conv_fwd_stats', 'rod_conv_wgrad', 'rod_pw_bwd', 'rod_pw_bwd_rc', 'rod_pw_bwd_gred',
+              'rod_pw_bwd_gred_rc', 'rod_pw_bwd_gred_dyp', 'rod_bn_bwd_reduce', 'rod_bn_bwd_apply', 'rod_bn_bwd')
 
 
 def gpu_head_start(ms=120):

@@ -20,6 +20,9 @@ from the call's own arguments — the per-unit figures of SURVEY.md §8(d):
                          input BatchNorm's sums).  Its reads of dz and y are the BatchNorm
                          backward's SECOND pass (as for bn_bwd_apply): design traffic; dy is
                          never stored
+  dw3x3_bwd_fused_rc   : es*(x + dx) with x the Cin-wide block input (ABI 23: ye recomputed),
+                         flops + 2*N*H*W*Cin*C
+  conv_fwd_stats       : es*(M*Cin + W) + the parts (ABI 23: y never written)
   dw3x3_bwd_fused_pw   : the same algorithmic bytes (ABI 20: dz is recomputed from the cout-wide dy_p;
                          its reads of yd and dy_p are design traffic), flops + 2*N*H*W*C*cout
   pw_bwd (fused 1x1)   : es*(2*M*Cout + M*Cin [+ M*Cin dx]) + W, 2*M*Cin*Cout per product;
@@ -79,6 +82,11 @@ def cost(name, a):
         es = _ES[dt]
         red = 6 * N * H * W * C if a[17] is not None else 0
         return es * 2 * N * H * W * C + 72 * C, 44 * N * Ho * Wo * C + red
+    if name == "rod_dw3x3_bwd_fused_rc":   # ABI 23: the expanded input recomputed from x (Cin wide)
+        Cin, N, H, W, C, Ho, Wo, dt = a[7], a[26], a[27], a[28], a[29], a[33], a[34], a[35]
+        es = _ES[dt]
+        return es * (N * H * W * Cin + N * H * W * C + C * Cin) + 72 * C, \
+            44 * N * Ho * Wo * C + 6 * N * H * W * C + 2 * N * H * W * Cin * C
     if name == "rod_dw3x3_bwd_fused_pw":
         N, H, W, C, dt, cout = a[21], a[22], a[23], a[24], a[25], a[8]
         es = _ES[dt]
@@ -91,6 +99,10 @@ def cost(name, a):
         K = ks * ks * Cin
         gred = es * M * Cout if a[17] is not None else 0   # the gred epilogue reads y
         return es * (M * Cin + M * Cout + Cout * K) + (4 * Cout if a[7] is not None else 0) + gred, 2 * M * K * Cout
+    if name == "rod_conv_fwd_stats":      # ABI 23: the statistics of y only, y never written
+        M, Cin, Cout, dt = a[8], a[9], a[10], a[11]
+        es = _ES[dt]
+        return es * (M * Cin + Cout * Cin) + 12 * -(-M // 128) * Cout, 2 * M * Cin * Cout + 3 * M * Cout
     if name == "rod_conv_fwd_bnact":      # conv + eval BatchNorm / act (+ residual) epilogue (ABI 21)
         N, H, W, Cin, Cout, ks, dt = a[17], a[18], a[19], a[20], a[21], a[22], a[25]
         es = _ES[dt]
@@ -233,6 +245,9 @@ def design_bytes(name, a):
     if name == "rod_dw3x3_bwd_fused":     # + the re-read of dz and y (BatchNorm backward pass 2)
         N, C, Ho, Wo, dt = a[19], a[22], a[26], a[27], a[28]
         return cost(name, a)[0] + _ES[dt] * 2 * N * Ho * Wo * C
+    if name == "rod_dw3x3_bwd_fused_rc":  # + the re-read of dz and y (BatchNorm backward pass 2)
+        N, C, Ho, Wo, dt = a[26], a[29], a[33], a[34], a[35]
+        return cost(name, a)[0] + _ES[dt] * 2 * N * Ho * Wo * C
     if name == "rod_dw3x3_bwd_fused_pw":  # + the reads of yd and the cout-wide dy_p
         N, H, W, C, dt, cout = a[21], a[22], a[23], a[24], a[25], a[8]
         return cost(name, a)[0] + _ES[dt] * N * H * W * (C + cout)
@@ -255,6 +270,8 @@ _BWD = ('32, false, true>', 'Li32ELb0ELb1EE')
 # pw_bwd_gred_kernel<COUT, NW, FAST, DYP>: DYP = rod_pw_bwd_gred_dyp (last argument)
 _XG = (', true, true, true, ', 'Lb1ELb1ELb1E')
 _LAST = ('true>(rod::PwBwdArgs', 'Lb1EEEvNS_9PwBwdArgs')
+# pw_stream_kernel<NT, KT, MODE, ...>: MODE 3 = statistics only (rod_conv_fwd_stats; KT is 1 there)
+_STATS_ONLY = (', 1, 3', 'ELi1ELi3E')
 
 
 def _forms(base, inc=(), exc=()):
@@ -283,11 +300,13 @@ ENTRY_KERNELS = {
     "rod_dw3x3_fwd_rc": (("dw3x3_fwd_rc_kernel",), ("dw3x3_fwd_rc_kernel",)),
     "rod_dw3x3_bwd_data": (("dw3x3_bwd_data",), ("dw3x3_bwd_data",)),
     "rod_dw3x3_bwd_filter": (("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel"), ("dw3x3_bwdw_lx", "dw3x3_bwd_filter_kernel")),
-    "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused!" + "!".join(_PW),), ("dw3x3_bwd_fused!" + "!".join(_PW),)),
+    "rod_dw3x3_bwd_fused": (("dw3x3_bwd_fused!dw3x3_bwd_fused_rc!" + "!".join(_PW),),) * 2,
+    "rod_dw3x3_bwd_fused_rc": (("dw3x3_bwd_fused_rc_kernel",),) * 2,
     "rod_dw3x3_bwd_fused_pw": tuple(tuple("dw3x3_bwd_fused2&" + t for t in _PW) for _ in range(2)),
     "rod_conv_wgrad": (("conv_wgrad_kernel",), ("conv_wgrad_kernel", "colsum_kernel")),
-    "rod_conv_fwd": (("conv_fwd_kernel!" + "!".join(_BWD), "stem_fwd_mfma_kernel", "pw_stream_kernel"),
-                     ("conv_fwd_kernel!" + "!".join(_BWD), "stem_fwd_mfma_kernel", "pw_stream_kernel")),
+    "rod_conv_fwd": (("conv_fwd_kernel!" + "!".join(_BWD), "stem_fwd_mfma_kernel") +
+                     _forms("pw_stream_kernel", exc=(_STATS_ONLY,)),) * 2,
+    "rod_conv_fwd_stats": (_forms("pw_stream_kernel", inc=(_STATS_ONLY,)),) * 2,
     "rod_conv_bwd_data_bn": tuple(tuple("conv_fwd_kernel&" + t for t in _BWD) for _ in range(2)),
     "rod_bn_finalize": (("bn_parts_merge_kernel",), ("bn_parts_merge_kernel",)),
     "rod_ir_block_fwd": (("ir_block_fwd_kernel",), ("ir_block_fwd_kernel",)),
