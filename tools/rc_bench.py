@@ -52,6 +52,14 @@ def main():
         wt0 = ops._prep(w_e, 0, bf16, C, Cin, 1)
         ye = torch.empty((N, H, W, C), dtype=bf16, device=dev)
         ops.conv_fwd_raw(x, wt0, None, ye, N, H, W, Cin, C, 1, None, xpro)
+        if _abi.lib().rod_conv_fwd_stats_supported(M, Cin, C, code):
+            sp0 = torch.empty((-(-M // 128), 3, C), device=dev)
+            sp1 = torch.empty_like(sp0)
+            ta = timeit(lambda: ops.conv_fwd_raw(x, wt0, None, ye, N, H, W, Cin, C, 1, sp0, xpro))
+            tb = timeit(lambda: _abi.call('rod_conv_fwd_stats', x, *ops._pro_args(xpro), wt0, sp1, M, Cin, C, code,
+                                          ops.stream()))
+            print('%-16s expand stored+stats %7.1f us   stats only %7.1f us   equal %s' %
+                  (name, ta, tb, torch.equal(sp0, sp1)), flush=True)
         epro = (ye.float().mean((0, 1, 2)), torch.rsqrt(ye.float().var((0, 1, 2)) + 1e-3),
                 (torch.rand(C, generator=g) + 0.5).to(dev), (torch.randn(C, generator=g) * 0.5).to(dev),
                 ops.ROD_ACT_RELU6)
