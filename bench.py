@@ -581,7 +581,7 @@ def main():
         else:
             rl = {'bound': 'mfma', 'achieved': round(achieved_tf, 2), 'peak': peak_tf, 'unit': 'TFLOP/s',
                   'frac': round(achieved_tf / peak_tf, 4)}
-        traffic, tsrc = None, None
+        traffic, tsrc, pmc_lps = None, None, None
         if args.traffic and os.path.exists(args.traffic):
             tj = json.load(open(args.traffic))
             tes = [tj.get('entries', {}).get(p) for p in probe_set]
@@ -591,7 +591,11 @@ def main():
                 traffic = round(sum(te['bytes_per_launch'] * te['launches'] for te in tes) /
                                 max(1, sum(te['launches'] for te in tes)))
                 tsrc = os.path.relpath(args.traffic, ROOT)
+                # the PMC run's launches of the family per profiled step: must equal the probe's
+                if all(te.get('launches_per_step') is not None for te in tes):
+                    pmc_lps = sum(te['launches_per_step'] for te in tes)
         rl.update({'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, PMC)', 'traffic_source': tsrc,
+                   'traffic_launches_per_step': pmc_lps,
                    'cost_model': roofline.COST_MODEL_VERSION,
                    'alg_bytes_per_launch': byts // max(n_launch, 1), 'kernel': args.probe.replace(',', ' + '),
                    'launches_per_step': n_launch // max(probe_steps, 1),
