@@ -581,7 +581,7 @@ def main():
         else:
             rl = {'bound': 'mfma', 'achieved': round(achieved_tf, 2), 'peak': peak_tf, 'unit': 'TFLOP/s',
                   'frac': round(achieved_tf / peak_tf, 4)}
-        traffic, tsrc, pmc_lps = None, None, None
+        traffic, tsrc, pmc_lps, tj = None, None, None, {}
         if args.traffic and os.path.exists(args.traffic):
             tj = json.load(open(args.traffic))
             tes = [tj.get('entries', {}).get(p) for p in probe_set]
@@ -617,6 +617,11 @@ def main():
                            alg_TFLOPs=round(step_totals['alg_flops_per_step'] / (elapsed / args.steps) / 1e12, 2),
                            note='sum of algorithmic bytes of every librod call of a step (rod.roofline) / the timed '
                                 'ms_per_step; probed over eager steps after the timed region')
+            if tsrc is not None and tj.get('all_bytes_per_step'):
+                # the PMC passes' whole-step HBM bytes (every kernel), and the part the entries claim
+                step_rl.update(pmc_bytes_per_step=round(tj['all_bytes_per_step']),
+                               pmc_attributed_bytes_per_step=round(tj['attributed_bytes_per_step']),
+                               pmc_over_alg=round(tj['all_bytes_per_step'] / max(step_totals['alg_bytes_per_step'], 1), 3))
         imgs = args.batch * world * args.steps
         out = {
             'metric': 'training images/sec at 1280x720 bf16' if dtype == torch.bfloat16 else

@@ -65,6 +65,11 @@ def main():
     out['attributed_bytes_per_step'] = total / steps if steps else None
     out['all_bytes_per_step'] = (sum(b for _, b in fetch.values()) * 2.0 + sum(b for _, b in write.values())) / steps \
         if steps else None
+    # the kernels no entry claims (torch's own copies / fills, the optimizer, the loss tail): with
+    # them the per-entry bytes add up to the passes' whole per-step total
+    if steps:
+        out['unattributed_bytes_per_step'] = out['all_bytes_per_step'] - out['attributed_bytes_per_step']
+        out['unattributed_kernels'] = sorted({k for k in fetch if k not in owners})
     json.dump(out, open(sys.argv[3], 'w'), indent=1)
     for k, v in out['entries'].items():
         print(f"{k:24s} {v['launches']:6d} {v['bytes_per_launch'] / 1e6:10.2f} MB/launch")
