@@ -27,6 +27,7 @@ summ() {  # dir marker iterations title
 }
 for step in "$@"; do
   case $step in
+    bnsmall) for v in 4 2 1; do run bnsmall_$v 200 env ROD_BN_SMALL_CVB=$v python tools/bn_bench.py --iters 20; done; grep -H -E "M= *(1920|480|120) |TOTAL" $OUT/${TAG}_bnsmall_*.log ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
     clitest) run clitest 400 python -m pytest tests/test_gpu_fullsize.py -m gpu -q -k cli --timeout=300 -p no:cacheprovider ;;
