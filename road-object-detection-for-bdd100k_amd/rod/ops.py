@@ -564,6 +564,19 @@ def _nostore_ok(x, ipro, N, H, W, Cin, Cout, dw_stride):
     return gred or _pw_fused_ok(M, Cin, Cout, x.dtype)
 
 
+def _nostore_eval_ok(x, N, H, W, Cin, Cout, dw_stride):
+    """Inference: the expand conv of a stride-2 inverted-residual block that the
+    fused block kernel does not take (ops.ir_block_preferred: the 24- and 32-channel inputs) need
+    not write its output either — the depthwise forward recomputes it from the block input
+    (rod_dw3x3_fwd_rc, the eval BatchNorm in its expand epilogue, no statistics), the same rounded
+    values the stored tensor would hold.  There is no backward.  ROD_DISABLE=rcinf (or nostore /
+    rc / bnpro) turns it off."""
+    if dw_stride not in ((1, 2) if "rcinf1" in _ENABLE else (2,)) or "rcinf" in _DISABLE or "nostore" in _DISABLE or "rc" in _DISABLE or "bnpro" in _DISABLE or \
+            x.dtype != torch.bfloat16 or torch.is_grad_enabled() and x.requires_grad:
+        return False
+    return bool(_abi.lib().rod_dw3x3_fwd_rc_supported(N, H, W, Cout, Cin, int(dw_stride), _DT[x.dtype]))
+
+
 def pw_bwd_gred_parts(M, Cin, Cout, dtype):
     """Part count of rod_pw_bwd_gred for this project shape (0: not taken)."""
     if "pwgred" in _DISABLE:
@@ -1009,6 +1022,16 @@ class _ConvBN(torch.autograd.Function):
         wt = _prep(w, 0, x.dtype, Cout, Cin, ks)
         ctx.nostore = training and ks == 1 and b is None and act == ROD_ACT_RELU6 and \
             _nostore_ok(x, ipro, N, H, W, Cin, Cout, dw_stride)
+        if not training and ks == 1 and b is None and act == ROD_ACT_RELU6 and \
+                _nostore_eval_ok(x, N, H, W, Cin, Cout, dw_stride):
+            # inference: nothing is computed here; the depthwise forms the values from x
+            y = torch.empty(1, dtype=x.dtype, device=x.device).expand(N, H, W, Cout)
+            y._rod_expand = (x, ipro, wt, Cin)
+            y._rod_nostore = True
+            mean, rstd = bn_statistics(y, mm, mv, False, decay, eps)
+            ctx.training = False
+            ctx.mark_non_differentiable(mean, rstd)
+            return y, mean, rstd
         if ctx.nostore:
             # the expanded tensor is never written (ABI 23): a placeholder of its shape that no
             # kernel reads (its consumers recompute it from x), the statistics from x alone

@@ -157,6 +157,43 @@ def test_nostore_step_opt_in_dw_recompute(dev):
     assert torch.equal(runs[0][0], runs[1][0])
 
 
+@pytest.mark.parametrize('graphed', [False, True])
+def test_predict_expand_recompute_bit_identical(dev, graphed):
+    """Inference (predict.py path, ALL network, 480x864 b2): the stride-2 blocks the fused block
+    kernel does not take (24 -> 144, 32 -> 192) leave their expand output unwritten and the depthwise
+    forward recomputes it (ops._nostore_eval_ok); against ROD_DISABLE=rcinf (written and read) the
+    head outputs and the detections are bit-identical, and rod_dw3x3_fwd_rc ran twice per batch."""
+    import predict
+    from rod.data import synthetic_batch
+    img = synthetic_batch(2, 480, 864, dev, seed=61)[0]
+    runs = []
+    for off in (True, False):
+        if off:
+            ops._DISABLE.add('rcinf')
+        try:
+            pr = predict.Predictor((480, 864), dev, bf16, seed=60)
+            pr.keep_intermediates = not graphed
+            _abi.PROBE.arm(['rod_dw3x3_fwd_rc', 'rod_ir_block_fwd'])
+            scores, boxes = pr(img)
+            if graphed:
+                scores, boxes = pr(img)   # a replay of the captured graph
+            torch.cuda.synchronize()
+            calls = _abi.PROBE.table()
+            _abi.PROBE.disarm()
+            inter = [t.clone() for t in pr.last] if not graphed else []
+            runs.append((inter, torch.stack([scores[c] for c in sorted(scores)]),
+                         torch.stack([boxes[c] for c in sorted(boxes)]), calls))
+        finally:
+            ops._DISABLE.discard('rcinf')
+    (i0, s0, b0, c0), (i1, s1, b1, c1) = runs
+    assert 'rod_dw3x3_fwd_rc' not in c0, c0
+    assert c1.get('rod_dw3x3_fwd_rc', (0,))[0] == 2, c1
+    assert c1.get('rod_ir_block_fwd', (0,))[0] == c0.get('rod_ir_block_fwd', (0,))[0]
+    for a, b in zip(i0, i1):
+        assert torch.equal(a, b)
+    assert torch.equal(s0, s1) and torch.equal(b0, b1)
+
+
 # (N, H, W, Cin, C, stride, input prologue act or None): block 1 (720p, 16 -> 96, stride 2, the
 # 16-byte pack plan) on 2 images, block 3 / block 2 shapes (24 -> 144 at 360x640, strides 2 / 1),
 # small maps on the 8-byte pack plan with odd sizes (TF-SAME pads 1 / 0), Cin 32
