@@ -564,15 +564,26 @@ def _nostore_ok(x, ipro, N, H, W, Cin, Cout, dw_stride):
     return gred or _pw_fused_ok(M, Cin, Cout, x.dtype)
 
 
+def rc_eval_ok(Cin, inner, stride, dtype):
+    """Inference: an inverted-residual block whose expand output the depthwise
+    forward can recompute from the block input (rod_dw3x3_fwd_rc: Cin 16 / 24 / 32) runs as the
+    unfused chain with that output never written, in preference to the fused block kernel
+    (ir_block_fwd).  Measured on one box, alternating (profiles/r6_rcinf_ab.txt): 1080p b8 893 / 890
+    (fused blocks 1, 2, 4, 5) -> 902 / 904 img/s, 720p b32 2162 / 2160 -> 2172 / 2183.
+    ROD_DISABLE=rcinf turns it off, rcinf1 keeps the stride-1 blocks on the fused kernel."""
+    if "rcinf" in _DISABLE or "nostore" in _DISABLE or "rc" in _DISABLE or "bnpro" in _DISABLE or \
+            dtype != torch.bfloat16 or inner <= Cin or Cin not in (16, 24, 32):
+        return False
+    return stride == 2 or "rcinf1" not in _DISABLE
+
+
 def _nostore_eval_ok(x, N, H, W, Cin, Cout, dw_stride):
-    """Inference: the expand conv of a stride-2 inverted-residual block that the
-    fused block kernel does not take (ops.ir_block_preferred: the 24- and 32-channel inputs) need
-    not write its output either — the depthwise forward recomputes it from the block input
-    (rod_dw3x3_fwd_rc, the eval BatchNorm in its expand epilogue, no statistics), the same rounded
-    values the stored tensor would hold.  There is no backward.  ROD_DISABLE=rcinf (or nostore /
-    rc / bnpro) turns it off."""
-    if dw_stride not in ((1, 2) if "rcinf1" in _ENABLE else (2,)) or "rcinf" in _DISABLE or "nostore" in _DISABLE or "rc" in _DISABLE or "bnpro" in _DISABLE or \
-            x.dtype != torch.bfloat16 or torch.is_grad_enabled() and x.requires_grad:
+    """Inference: the expand conv of a block rc_eval_ok takes need not write its output — the
+    depthwise forward recomputes it from the block input (rod_dw3x3_fwd_rc, the eval BatchNorm in
+    its expand epilogue, no statistics), the same rounded values the stored tensor would hold.
+    There is no backward."""
+    if dw_stride not in (1, 2) or not rc_eval_ok(Cin, Cout, dw_stride, x.dtype) or \
+            torch.is_grad_enabled() and x.requires_grad:
         return False
     return bool(_abi.lib().rod_dw3x3_fwd_rc_supported(N, H, W, Cout, Cin, int(dw_stride), _DT[x.dtype]))
 
@@ -1434,6 +1445,8 @@ def ir_block_preferred(Cin, inner, Cout, stride, residual, dtype):
     stride-2 24- and 32-channel blocks measure 1.03-1.14x fused at b8 but lose at the predict
     path's b32 (18.76 -> 18.88 ms per batch with them fused)."""
     if not ir_block_supported(Cin, inner, Cout, stride, residual, dtype):
+        return False
+    if rc_eval_ok(Cin, inner, stride, dtype):   # the chain with the expand output recomputed
         return False
     if "irblock_all" in _ENABLE:
         return True

@@ -53,9 +53,24 @@ def test_ir_block_policy_is_host_only():
     from nets.backbone.mobilenet_v2 import layer_plan
     from rod import ops
     bf16 = torch.bfloat16
-    picked = [idx for (idx, kind, s, cin, inner, cout, res, sc) in layer_plan()
-              if kind == 'ir' and inner > cin and ops.ir_block_preferred(cin, inner, cout, s, res, bf16)]
-    assert picked == [3, 4, 6, 7], picked
+
+    def picked():
+        return [idx for (idx, kind, s, cin, inner, cout, res, sc) in layer_plan()
+                if kind == 'ir' and inner > cin and ops.ir_block_preferred(cin, inner, cout, s, res, bf16)]
+    # by default the 16..32-channel blocks take the chain with the expand output recomputed
+    # (ops.rc_eval_ok, measured faster); without it the fused kernel takes the ones measured
+    # faster fused than the plain chain
+    assert picked() == [], picked()
+    ops._DISABLE.add('rcinf')
+    try:
+        assert picked() == [3, 4, 6, 7], picked()
+    finally:
+        ops._DISABLE.discard('rcinf')
+    ops._DISABLE.add('rcinf1')
+    try:
+        assert picked() == [4, 6, 7], picked()   # the stride-1 ones fused, block 1 (stride 2) recomputed
+    finally:
+        ops._DISABLE.discard('rcinf1')
     assert ops.ir_block_supported(64, 384, 64, 1, True, bf16)
     assert not _abi.lib().rod_ir_block_persistent(64, 384, 64, 1, 1, 1)    # parameters exceed LDS
     assert _abi.lib().rod_ir_block_persistent(32, 192, 32, 1, 1, 1)
