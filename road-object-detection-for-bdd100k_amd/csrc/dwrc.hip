@@ -62,7 +62,7 @@ inline DwRcLds dw_rc_lds(const DwTile& t, int S, int V, int Cin) {
 }
 
 template <int S, int V, int CIN, bool STATS, int NPT>
-__global__ void __launch_bounds__(256, V == 8 ? 3 : 4) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl, int nct, int ldy) {
+__global__ void __launch_bounds__(256) dw3x3_fwd_rc_kernel(DwRcArgs a, DwTile tl, int nct, int ldy) {
   constexpr int npt = NPT;
   typedef bf16_t T;
   typedef PackV<T, V> PK;

@@ -828,7 +828,7 @@ constexpr int PWS_WAVES = 4;
 // (KT >= 5 with the table prologue: at least 4 waves per SIMD, 128 VGPRs — unbounded the compiler
 // took 144-172 and 2 waves per SIMD)
 template <int NT, int KT, int MODE, bool PRO = false, int PACT = ROD_ACT_RELU6>
-__global__ void __launch_bounds__(256, (PRO && KT >= 5) ? 4 : (MODE == 3 ? (NT <= 3 ? 7 : 5) : 1)) pw_stream_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+__global__ void __launch_bounds__(256, (PRO && KT >= 5) ? 4 : (MODE == 3 ? 5 : 1)) pw_stream_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                                                         bf16_t* __restrict__ Y, long M, int K, int Cout, int ldx,
                                                         int ldy, float* __restrict__ part, BnGred gr,
                                                         BnPro pro = BnPro{}) {
@@ -1116,17 +1116,14 @@ static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long 
                              float* stats, const BnGred* gr, hipStream_t s, const BnPro* pro = nullptr) {
   if (y == nullptr) {   // statistics only (rod_conv_fwd_stats): K <= 32, one k step
     int nt = 0;
-    // ROD_STATS_NARROW=1 (measurement switch): narrow N groups (3 MFMA tiles, x read once per
-    // group) at up to 7 blocks per CU instead of the widest group at 5
-    static const bool narrow = getenv("ROD_STATS_NARROW") && atoi(getenv("ROD_STATS_NARROW")) == 1;
-    const int ng = pw_stream_groups(M, K, Cout, nt, narrow);
+    const int ng = pw_stream_groups(M, K, Cout, nt, false);
     if (ng == 0 || !stats || gr || K > 32) return false;
     // no store to stream behind: latency-bound on its A loads, so up to 5 blocks of 4 waves per CU
     // (<= 102 VGPRs: 5 waves per SIMD) instead of the storing kernel's 3.  (A dedicated kernel
     // with a 2- / 4-deep A ring and the sub-steps unrolled measured slower: 232 -> 280 us at 720p
     // b8 16 -> 96, its registers up to 144-220.)
     const long ntiles = cdivl(M, 128);
-    const long maxw = cdivl(256L * (nt <= 3 ? 7 : 5) * PWS_WAVES, ng);
+    const long maxw = cdivl(256L * 5 * PWS_WAVES, ng);
     const long per = cdivl(ntiles, maxw);
     const dim3 grid((unsigned)cdivl(cdivl(ntiles, per), PWS_WAVES), ng);
     const BnGred g{};
