@@ -35,6 +35,10 @@ for step in "$@"; do
          for i in 1 2; do run pr0_$i 200 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run pr1_$i 200 python tools/predict_bench.py --res 1080 --batch 8 --iters 30; done &&
          for i in 1 2; do run tr0_$i 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run tr1_$i 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done;
          grep -H "dwfwd\|expand" $OUT/${TAG}_rcb_*.log; grep -H ms_per_batch $OUT/${TAG}_pr*.log; grep -H -o '"value": [0-9.]*' $OUT/${TAG}_tr*.log ;;
+    rcv) run rcvtest 300 env ROD_DW_RC_V=4 python -u -m pytest tests/test_gpu_recompute.py -k predict -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider &&
+         for i in 1 2; do run pv8_$i 200 python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run pv4_$i 200 env ROD_DW_RC_V=4 python tools/predict_bench.py --res 1080 --batch 8 --iters 30; done &&
+         for i in 1 2; do run qv8_$i 200 python tools/predict_bench.py --res 720 --batch 32 --iters 20 && run qv4_$i 200 env ROD_DW_RC_V=4 python tools/predict_bench.py --res 720 --batch 32 --iters 20; done;
+         grep -H ms_per_batch $OUT/${TAG}_pv*.log $OUT/${TAG}_qv*.log ;;
     bnsmall) for v in 4 2 1; do run bnsmall_$v 200 env ROD_BN_SMALL_CVB=$v python tools/bn_bench.py --iters 20; done; grep -H -E "M= *(1920|480|120) |TOTAL" $OUT/${TAG}_bnsmall_*.log ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
