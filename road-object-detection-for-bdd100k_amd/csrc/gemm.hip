@@ -1119,15 +1119,18 @@ static bool pw_stream_launch(const bf16_t* x, const bf16_t* wt, bf16_t* y, long 
     const int ng = pw_stream_groups(M, K, Cout, nt, false);
     if (ng == 0 || !stats || gr || K > 32) return false;
     // no store to stream behind: latency-bound on its A loads, so up to 5 blocks of 4 waves per CU
-    // (<= 102 VGPRs: 5 waves per SIMD) instead of the storing kernel's 3.  (A dedicated kernel
-    // with a 2- / 4-deep A ring and the sub-steps unrolled measured slower: 232 -> 280 us at 720p
-    // b8 16 -> 96, its registers up to 144-220.)
+    // (<= 102 VGPRs: 5 waves per SIMD) instead of the storing kernel's 3.  (Measured slower: a
+    // dedicated kernel with a 2- / 4-deep A ring and the sub-steps unrolled, 232 -> 280 us at 720p
+    // b8 16 -> 96, its registers up to 144-220; one that loads the next whole 128-row tile (4 KB a
+    // wave) before computing the current one through a register queue, 158 VGPRs at 3 waves per
+    // SIMD, 227 -> 253 us (24 -> 144: 80 -> 90) — the sub-step's MFMA -> rounding -> statistics
+    // chain, not the loads, is what the waves wait on.)
     const long ntiles = cdivl(M, 128);
+    const BnPro pv = pro ? *pro : BnPro{};
     const long maxw = cdivl(256L * 5 * PWS_WAVES, ng);
     const long per = cdivl(ntiles, maxw);
     const dim3 grid((unsigned)cdivl(cdivl(ntiles, per), PWS_WAVES), ng);
     const BnGred g{};
-    const BnPro pv = pro ? *pro : BnPro{};
 #define PWN(NT_)                                                                                               \
   if (nt == NT_) {                                                                                             \
     if (pro)                                                                                                   \

@@ -40,6 +40,35 @@ RC_SHAPES = [(70001, 24, 144, None), (131072, 24, 144, ops.ROD_ACT_RELU6), (6553
              (100003, 16, 96, ops.ROD_ACT_RELU6), (65600, 16, 96, None)]
 
 
+# (M, Cin, Cout, input prologue act or None): every N-group width of the statistics-only forward
+# (Cout 32 / 48 / 64 / 96 / 144 / 192: 2 / 3 / 4 / 6 / 9 / 12 MFMA tiles; 12, and 9 with a
+# prologue, take MODE 3 of the streaming kernel), tails of 1, 5 and 127 rows, both prologue forms
+STATS_SHAPES = [(65536 + 1, 16, 96, ops.ROD_ACT_NONE), (65536 * 2 + 5, 24, 144, None), (70000 + 127, 32, 192, None),
+                (65536 + 40, 16, 32, ops.ROD_ACT_RELU6), (65536 * 3, 24, 48, ops.ROD_ACT_NONE), (99999, 32, 64, None),
+                (65536 + 3, 24, 144, ops.ROD_ACT_RELU6), (7372800 // 8, 16, 96, ops.ROD_ACT_NONE)]
+
+
+@pytest.mark.parametrize('M,Cin,Cout,xact', STATS_SHAPES)
+def test_conv_fwd_stats_bit_identical(dev, M, Cin, Cout, xact):
+    """rod_conv_fwd_stats (the expand's statistics with its output never written) against the
+    statistics parts the storing forward (rod_conv_fwd) writes beside y: bit-identical."""
+    g = torch.Generator().manual_seed(M + Cin + Cout)
+    x = (torch.randn(M, Cin, generator=g) * 1.5).to(dev, bf16)
+    w = (torch.randn(Cout, 1, 1, Cin, generator=g) * 0.3).to(dev)
+    xpro = None if xact is None else (*_bn(Cin, g, dev), xact)
+    code = ops.dtcode(x)
+    assert _abi.lib().rod_conv_fwd_stats_supported(M, Cin, Cout, code)
+    wt0 = ops._prep(w, 0, bf16, Cout, Cin, 1)
+    nparts = -(-M // 128)
+    p0 = torch.full((nparts, 3, Cout), -7.0, device=dev)
+    p1 = torch.full((nparts, 3, Cout), -9.0, device=dev)
+    y = torch.empty((1, 1, M, Cout), dtype=bf16, device=dev)
+    ops.conv_fwd_raw(x.view(1, 1, M, Cin), wt0, None, y, 1, 1, M, Cin, Cout, 1, p0, xpro)
+    _abi.call('rod_conv_fwd_stats', x, *ops._pro_args(xpro), wt0, p1, M, Cin, Cout, code, ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(p0, p1)
+
+
 @pytest.mark.parametrize('M,Cin,Cout,xact', RC_SHAPES)
 def test_pw_bwd_rc_bit_identical(dev, M, Cin, Cout, xact):
     assert _abi.lib().rod_pw_bwd_rc_supported(M, Cin, Cout, ops.dtcode(torch.empty(1, dtype=bf16)))

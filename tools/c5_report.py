@@ -32,7 +32,8 @@ sys.path.insert(0, os.path.join(ROOT, 'road-object-detection-for-bdd100k_amd'))
 FAMILIES = {'rod_ir_block_fwd': ('ir_block_fwd_kernel',),
             'rod_conv_fwd': ('conv_fwd_kernel', 'pw_stream_kernel', 'stem_fwd_mfma_kernel', 'stem_conv_fwd_kernel',
                              'splitk_combine_kernel'),
-            'rod_dw3x3_fwd': ('dw3x3_fwd',), 'rod_bn_apply': ('bn_apply_kernel',)}
+            'rod_dw3x3_fwd': ('dw3x3_fwd_kernel', 'dw3x3_fwd_lx_kernel'),
+            'rod_dw3x3_fwd_rc': ('dw3x3_fwd_rc_kernel',), 'rod_bn_apply': ('bn_apply_kernel',)}
 
 
 def probe(a):

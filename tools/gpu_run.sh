@@ -39,6 +39,10 @@ for step in "$@"; do
          for i in 1 2; do run pv8_$i 200 python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run pv4_$i 200 env ROD_DW_RC_V=4 python tools/predict_bench.py --res 1080 --batch 8 --iters 30; done &&
          for i in 1 2; do run qv8_$i 200 python tools/predict_bench.py --res 720 --batch 32 --iters 20 && run qv4_$i 200 env ROD_DW_RC_V=4 python tools/predict_bench.py --res 720 --batch 32 --iters 20; done;
          grep -H ms_per_batch $OUT/${TAG}_pv*.log $OUT/${TAG}_qv*.log ;;
+    statsab) run statstest 400 python -u -m pytest tests/test_gpu_recompute.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider &&
+         run stb0 200 env ROD_STATS_TILE=0 python tools/rc_bench.py b1 b3 && run stb1 200 python tools/rc_bench.py b1 b3 &&
+         for i in 1 2; do run st0_$i 300 env ROD_STATS_TILE=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run st1_$i 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done;
+         grep -H "expand" $OUT/${TAG}_stb*.log; grep -H -o '"value": [0-9.]*' $OUT/${TAG}_st?_*.log ;;
     bnsmall) for v in 4 2 1; do run bnsmall_$v 200 env ROD_BN_SMALL_CVB=$v python tools/bn_bench.py --iters 20; done; grep -H -E "M= *(1920|480|120) |TOTAL" $OUT/${TAG}_bnsmall_*.log ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
