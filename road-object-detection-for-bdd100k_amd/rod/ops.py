@@ -1370,6 +1370,22 @@ def conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, ep
     return Pending(y, mean, rstd, gamma, beta, act, training, owned=True)
 
 
+def _cinpad_weights(w, cp, dtype):
+    """GEMM operand of a [Cout, 3, 3, Cin] weight zero-padded to Cin = cp (inference): cached on the
+    weight, refreshed when the weight changes (its version counter)."""
+    key = (w._version, cp, dtype)
+    hit = getattr(w, "_rod_cinpad", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    Cout, k, _, Cin = w.shape
+    wp = torch.zeros((Cout, k, k, cp), dtype=torch.float32, device=w.device)
+    wp[..., :Cin] = w.detach()
+    wt = torch.empty((Cout, k * k * cp), dtype=dtype, device=w.device)
+    _abi.call("rod_conv_weight_prep", wp, wt, Cout, cp, k, 0, dtcode(wt), stream())
+    w._rod_cinpad = (key, wt)
+    return wt
+
+
 def conv2d_bn_act(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps=1e-3, residual=None):
     """conv2d_bn + materialize: act(BN(conv(x))) (+ residual) written out.  Inference in bf16:
     ONE launch, rod_conv_fwd_bnact (ABI 21) — the conv's epilogue applies the eval BatchNorm
@@ -1386,14 +1402,29 @@ def conv2d_bn_act(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay
             _abi.lib().rod_conv_fwd_stream_ok(N * H * W, Cin, Cout, dtcode(xt)):
         # the streaming 1x1 kernel (no epilogue form) beats the tiled GEMM with the epilogue here
         return materialize(conv2d_bn(x, w, b, ksize, gamma, beta, mmean, mvar, act, training, decay, eps), residual)
-    if ksize == 3 and ipro is not None and N * H * W >= 16384 and "pro3" not in _DISABLE:
+    cp = -(-Cin // 8) * 8
+    if ksize == 3 and ipro is not None and Cin != cp and "cinpad" not in _DISABLE:
+        # the heads' last 3x3 convs (Cin = classes x anchors: 99, 66, 36): act(BN(x)) written once
+        # into a zero-padded [.., Cin rounded up to 8] tensor and the weights zero-padded to match,
+        # so the implicit GEMM's rows are 16-byte aligned (1080p b8 99 -> 99 at 34x60: 124 us
+        # unpadded, 31 us for 128 -> 128 on the same map, tools/conv_bench.py).  The padded k
+        # columns add exact zeros; the k-chunking of the sum differs (a rounding-level change).
+        xb = torch.zeros((N, H, W, cp), dtype=xt.dtype, device=xt.device)
+        im, ir, ig, ib, ia = ipro
+        _abi.call("rod_bn_apply", xt, im, ir, ig, ib, None, xb, N * H * W, Cin, 0, 0, cp, ia, dtcode(xt), stream())
+        xt, ipro = xb, None
+        wt = _cinpad_weights(w, cp, xt.dtype)
+        Cin = cp
+    elif ksize == 3 and ipro is not None and N * H * W >= 16384 and "pro3" not in _DISABLE:
         # as _ConvBN.forward: a 3x3 gathers every input element 9 times, so act(BN(x)) is written
         # once instead of applied in the load prologue (the same rounded values)
         xb = torch.empty_like(xt)
         im, ir, ig, ib, ia = ipro
         _abi.call("rod_bn_apply", xt, im, ir, ig, ib, None, xb, N * H * W, Cin, 0, 0, 0, ia, dtcode(xt), stream())
         xt, ipro = xb, None
-    wt = _prep(w, 0, xt.dtype, Cout, Cin, ksize)
+        wt = _prep(w, 0, xt.dtype, Cout, Cin, ksize)
+    else:
+        wt = _prep(w, 0, xt.dtype, Cout, Cin, ksize)
     z = torch.empty((N, H, W, Cout), dtype=xt.dtype, device=xt.device)
     mean, rstd = bn_statistics(z, mmean, mvar, False, decay, eps)
     nb = 0 if "splitk" in _DISABLE else _abi.query("rod_conv_fwd_workspace", N, H, W, Cin, Cout, ksize)

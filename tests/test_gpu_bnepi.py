@@ -65,6 +65,7 @@ def test_predict_bnepi_bit_identical(dev):
     for off in (True, False):
         if off:
             ops._DISABLE.add('bnepi')
+        ops._DISABLE.add('cinpad')   # the padded head convs sum k in other chunks (test below)
         try:
             pr = predict.Predictor((160, 288), dev, bf16)
             _abi.PROBE.arm(['rod_conv_fwd_bnact', 'rod_bn_apply'])
@@ -76,7 +77,39 @@ def test_predict_bnepi_bit_identical(dev):
             outs.append(({k: v.clone() for k, v in scores.items()}, {k: v.clone() for k, v in boxes.items()}, calls))
         finally:
             ops._DISABLE.discard('bnepi')
+            ops._DISABLE.discard('cinpad')
     (s0, b0, c0), (s1, b1, c1) = outs
     assert 'rod_conv_fwd_bnact' not in c0 and c1['rod_conv_fwd_bnact'][0] >= 18, c1
     assert c1.get('rod_bn_apply', (0,))[0] < c0['rod_bn_apply'][0] - 18, (c0, c1)
     assert all(torch.equal(s0[k], s1[k]) for k in s0) and all(torch.equal(b0[k], b1[k]) for k in b0)
+
+
+@pytest.mark.parametrize('N,H,W,C', [(8, 34, 60, 99), (2, 17, 30, 99), (4, 68, 120, 66), (3, 23, 41, 36)])
+def test_head_conv_cinpad_matches(dev, N, H, W, C):
+    """The heads' last 3x3 conv in inference (Cin = Cout = classes x anchors, not a multiple of 8)
+    with its input and weights zero-padded to Cin rounded up to 8 (ops.conv2d_bn_act) against the
+    unpadded conv (ROD_DISABLE=cinpad): the same products, the k sum in other chunks — within one
+    bf16 rounding of each other, elementwise."""
+    g = torch.Generator().manual_seed(N * H + C)
+    x = (torch.randn(N, H, W, C, generator=g)).to(dev, bf16)
+    w = (torch.randn(C, 3, 3, C, generator=g) / (9 * C) ** 0.5).to(dev)
+    b = (torch.randn(C, generator=g) * 0.1).to(dev)
+    im, ir = (torch.randn(C, generator=g) * 0.1).to(dev), (torch.rand(C, generator=g) + 0.5).to(dev)
+    ib = (torch.randn(C, generator=g) * 0.1).to(dev)
+    mm, mv = (torch.randn(C, generator=g) * 0.1).to(dev), (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(C, generator=g) * 0.1).to(dev)
+    outs = []
+    for off in (True, False):
+        if off:
+            ops._DISABLE.add('cinpad')
+        try:
+            with torch.no_grad():
+                xp = ops.Pending(x, im, ir, None, ib, ops.ROD_ACT_LEAKY, False, owned=True)
+                outs.append(ops.conv2d_bn_act(xp, w, b, 3, None, beta, mm, mv, ops.ROD_ACT_LEAKY, False, 0.997, 1e-3))
+            torch.cuda.synchronize()
+        finally:
+            ops._DISABLE.discard('cinpad')
+    z0, z1 = (o.float() for o in outs)
+    assert torch.isfinite(z1).all()
+    tol = z0.abs() * 2.0 ** -7 + 1e-3 * float(z0.abs().max())
+    assert bool(((z0 - z1).abs() <= tol).all()), float((z0 - z1).abs().max())

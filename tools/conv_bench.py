@@ -24,7 +24,10 @@ SHAPES = [(8, 720, 1280, 16, 96, 1, 0), (8, 360, 640, 96, 24, 1, 1), (8, 360, 64
           # the heads' last 3x3 convs (Cin = Cout = k x anchors, not a multiple of 8)
           (8, 90, 160, 66, 66, 3, 2), (8, 45, 80, 99, 99, 3, 2), (8, 45, 80, 36, 36, 3, 2),
           # projects with the depthwise BatchNorm prologue: 720p block 1, 180x320 blocks
-          (8, 720, 1280, 32, 16, 1, 1), (8, 180, 320, 192, 32, 1, 1), (8, 180, 320, 144, 32, 1, 1)]
+          (8, 720, 1280, 32, 16, 1, 1), (8, 180, 320, 192, 32, 1, 1), (8, 180, 320, 144, 32, 1, 1),
+          # C5 (1080p) heads: the last 3x3 convs and a 128 -> 128 3x3 on the deep levels
+          (8, 34, 60, 99, 99, 3, 2), (8, 68, 120, 99, 99, 3, 2), (8, 135, 240, 66, 66, 3, 2), (8, 34, 60, 128, 128, 3, 2),
+          (8, 17, 30, 99, 99, 3, 2)]
 
 
 def main():

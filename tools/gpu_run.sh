@@ -43,6 +43,10 @@ for step in "$@"; do
          run stb0 200 env ROD_STATS_TILE=0 python tools/rc_bench.py b1 b3 && run stb1 200 python tools/rc_bench.py b1 b3 &&
          for i in 1 2; do run st0_$i 300 env ROD_STATS_TILE=0 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run st1_$i 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done;
          grep -H "expand" $OUT/${TAG}_stb*.log; grep -H -o '"value": [0-9.]*' $OUT/${TAG}_st?_*.log ;;
+    c5heads) run cbh0 200 python tools/conv_bench.py --shapes 19,20,21,22,23 --ops fwd_plain && run cbh1 200 env ROD_DISABLE=splitk python tools/conv_bench.py --shapes 19,20,21,22,23 --ops fwd_plain ;;
+    cinpad) run cptest 400 python -u -m pytest tests/test_gpu_bnepi.py tests/test_gpu_fullsize.py -k "bnepi or cinpad or 1080p" -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider &&
+         for i in 1 2; do run cp0_$i 200 env ROD_DISABLE=cinpad python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run cp1_$i 200 python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run cq0_$i 200 env ROD_DISABLE=cinpad python tools/predict_bench.py --res 720 --batch 32 --iters 20 && run cq1_$i 200 python tools/predict_bench.py --res 720 --batch 32 --iters 20; done;
+         grep -H ms_per_batch $OUT/${TAG}_cp?_*.log $OUT/${TAG}_cq?_*.log ;;
     bnsmall) for v in 4 2 1; do run bnsmall_$v 200 env ROD_BN_SMALL_CVB=$v python tools/bn_bench.py --iters 20; done; grep -H -E "M= *(1920|480|120) |TOTAL" $OUT/${TAG}_bnsmall_*.log ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
