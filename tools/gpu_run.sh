@@ -51,6 +51,8 @@ for step in "$@"; do
     slabab) run slabtest 400 env ROD_SLAB_POLICY=1 python -u -m pytest tests/test_gpu_defer.py tests/test_gpu_train.py -k "defer or refine" -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider &&
          for i in 1 2 3; do run sl0_$i 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run sl1_$i 300 env ROD_SLAB_POLICY=1 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done;
          grep -H -o '"value": [0-9.]*' $OUT/${TAG}_sl?_*.log ;;
+    predprev) for i in 1 2; do run pp0_$i 200 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run pp1_$i 200 python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run pq0_$i 200 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python tools/predict_bench.py --res 720 --batch 32 --iters 20 && run pq1_$i 200 python tools/predict_bench.py --res 720 --batch 32 --iters 20; done;
+         grep -H ms_per_batch $OUT/${TAG}_pp?_*.log $OUT/${TAG}_pq?_*.log ;;
     bnsmall) for v in 4 2 1; do run bnsmall_$v 200 env ROD_BN_SMALL_CVB=$v python tools/bn_bench.py --iters 20; done; grep -H -E "M= *(1920|480|120) |TOTAL" $OUT/${TAG}_bnsmall_*.log ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
