@@ -345,8 +345,12 @@ template <> struct PbsVec<8> { typedef bf16x8 T; };
 // It is written into the half's dy rows in LDS, where each lane reads its chunk and overwrites it
 // with dy in place (the same lane reads and writes an element).  Saves the M x COUT y stream (the
 // expanded tensor of an inverted-residual block: 1.42 GB at 720p b8 for 16 -> 96).
+// Occupancy: the 16 -> 96 forms at 3 waves per SIMD — 120-168 VGPRs and no AGPRs, no spills
+// (unbounded: 156 + 24 AGPRs, 2 waves), so the 768-block grid is resident at once: block 1's
+// recomputing gred form 568.5 -> 557.8 us; the 24 -> 144 forms (200-250 + 72-76 AGPRs, 1 wave)
+// measured slower at 2 waves (306 -> 321-327 us) and stay unbounded (profiles/r6_pwbwd_bounds_ab.txt).
 template <int CIN, int COUT, bool PRO, bool DX, bool XG = false, bool XL = false, bool RC = false>
-__global__ void __launch_bounds__(256) pw_bwd_stream_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
+__global__ void __launch_bounds__(256, CIN == 16 ? 3 : 1) pw_bwd_stream_kernel(PwBwdArgs a, long ntiles, float* __restrict__ xparts) {
   using G = PbsGeo<CIN, COUT>;
   static_assert(!XG || (PRO && DX), "the input sums need the prologue and dx");
   static_assert(!RC || CIN <= 32, "the recompute is one k step");

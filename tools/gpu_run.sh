@@ -53,6 +53,15 @@ for step in "$@"; do
          grep -H -o '"value": [0-9.]*' $OUT/${TAG}_sl?_*.log ;;
     predprev) for i in 1 2; do run pp0_$i 200 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run pp1_$i 200 python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run pq0_$i 200 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python tools/predict_bench.py --res 720 --batch 32 --iters 20 && run pq1_$i 200 python tools/predict_bench.py --res 720 --batch 32 --iters 20; done;
          grep -H ms_per_batch $OUT/${TAG}_pp?_*.log $OUT/${TAG}_pq?_*.log ;;
+    trprev) run trtest 400 python -u -m pytest tests/test_gpu_recompute.py tests/test_gpu_pwbwd.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
+         for i in 1 2 3; do run tp0_$i 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run tp1_$i 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done;
+         grep -H -o '"value": [0-9.]*' $OUT/${TAG}_tp?_*.log ;;
+    profab) run profa 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so rocprofv3 --kernel-trace --stats -d $OUT/profa_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 &&
+         run profb 300 rocprofv3 --kernel-trace --stats -d $OUT/profb_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 &&
+         rm -f $OUT/profa_$TAG/run_kernel_trace.csv $OUT/profb_$TAG/run_kernel_trace.csv ;;
+    trprev2) run trtest2 400 python -u -m pytest tests/test_gpu_recompute.py tests/test_gpu_pwbwd.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
+         for i in 1 2; do run tq0_$i 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run tq1_$i 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done;
+         grep -H -o '"value": [0-9.]*' $OUT/${TAG}_tq?_*.log ;;
     bnsmall) for v in 4 2 1; do run bnsmall_$v 200 env ROD_BN_SMALL_CVB=$v python tools/bn_bench.py --iters 20; done; grep -H -E "M= *(1920|480|120) |TOTAL" $OUT/${TAG}_bnsmall_*.log ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
