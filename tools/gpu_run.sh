@@ -62,6 +62,9 @@ for step in "$@"; do
     trprev2) run trtest2 400 python -u -m pytest tests/test_gpu_recompute.py tests/test_gpu_pwbwd.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
          for i in 1 2; do run tq0_$i 300 env ROD_LIB=road-object-detection-for-bdd100k_amd/lib/librod_prev.so python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0 && run tq1_$i 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-inference --no-fp32-leg --no-tfrecord-leg --no-dp-leg --kernel-steps 0; done;
          grep -H -o '"value": [0-9.]*' $OUT/${TAG}_tq?_*.log ;;
+    sepi) run sepitest 400 python -u -m pytest tests/test_gpu_bnepi.py tests/test_gpu_recompute.py -k "predict" -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider &&
+         for i in 1 2; do run se0_$i 200 env ROD_DISABLE=streamepi python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run se1_$i 200 python tools/predict_bench.py --res 1080 --batch 8 --iters 30 && run sf0_$i 200 env ROD_DISABLE=streamepi python tools/predict_bench.py --res 720 --batch 32 --iters 20 && run sf1_$i 200 python tools/predict_bench.py --res 720 --batch 32 --iters 20; done;
+         grep -H ms_per_batch $OUT/${TAG}_se?_*.log $OUT/${TAG}_sf?_*.log ;;
     bnsmall) for v in 4 2 1; do run bnsmall_$v 200 env ROD_BN_SMALL_CVB=$v python tools/bn_bench.py --iters 20; done; grep -H -E "M= *(1920|480|120) |TOTAL" $OUT/${TAG}_bnsmall_*.log ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider ;;
